@@ -1,0 +1,148 @@
+/*
+ * krr_amd.h — C ABI of the MI355X-native KRR SimpleStrategy hot path.
+ *
+ * The reference (KRR v1.0.0) computes, per Kubernetes object, a CPU "percentile"
+ * and a memory max over Prometheus range-query series, one object at a time in
+ * Python Decimal.  This ABI replaces that per-object work with fleet-wide
+ * segmented kernels over one CSR float64 buffer:
+ *
+ *   segment s  = one (object, resource) series: the concatenation of the
+ *                object's pods in K8sObjectData.pods order, each pod's samples
+ *                in timestamp order (reference core/integrations/prometheus.py:150-155).
+ *   values[]   = float64 samples of every segment, back to back.
+ *   offsets[]  = S+1 int64 offsets; segment s is values[offsets[s] .. offsets[s+1]).
+ *
+ * A NaN slot is an ABSENT sample when `gaps_are_nan` is set (dense layout
+ * with pods aligned on a time grid); otherwise NaN is a real sample value
+ * and follows the reference's NaN behaviour (see KRR_FLAG_NAN).
+ *
+ * Entry points and the reference interface each replaces:
+ *
+ *   krr_segmented_percentile  <- SimpleStrategySettings.calculate_cpu_proposal
+ *                                robusta_krr/strategies/simple.py:31-36
+ *   krr_segmented_max         <- SimpleStrategySettings.calculate_memory_proposal
+ *                                robusta_krr/strategies/simple.py:24-29 (the max;
+ *                                the x(1+b/100) buffer is exact-decimal host work)
+ *   krr_simple_run            <- SimpleStrategy.run robusta_krr/strategies/simple.py:42-49,
+ *                                batched over every object (the loop the reference
+ *                                runs in Runner._gather_objects_recommendations,
+ *                                robusta_krr/core/runner.py:88-120)
+ *   krr_simple_run_host       <- same, for callers holding host buffers (PCIe-inclusive)
+ *
+ * Ownership: the caller owns every buffer; no allocation crosses the ABI.
+ * Device pointers are HIP device pointers on the ctx's device; `stream` is a
+ * hipStream_t (NULL = default stream).  Calls are asynchronous on `stream`
+ * unless stated.  Functions return KRR_OK (0) or a negative krr_status and
+ * never throw; krr_last_error(ctx) returns the message of the last failure.
+ * A ctx is not shared between threads (one ctx per thread/device); there is
+ * no global mutable state, so distinct ctxs are reentrant.
+ */
+#ifndef KRR_AMD_H
+#define KRR_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KRR_ABI_VERSION 1
+
+typedef enum {
+    KRR_OK = 0,
+    KRR_E_INVALID = -1,     /* bad argument (null pointer, bad mode, p out of (0,100]) */
+    KRR_E_HIP = -2,         /* HIP runtime error (message in krr_last_error) */
+    KRR_E_CAPACITY = -3,    /* a segment needs more selection scratch than was provisioned */
+    KRR_E_UNSUPPORTED = -4  /* option combination not implemented */
+} krr_status;
+
+/* Percentile rule for the CPU recommendation.  All rules share n = number of
+ * present samples and, for the exact rules, k = floor((n-1) * p / 100)
+ * computed in exact rational arithmetic (reference simple.py:36 evaluates
+ * int((n-1) * p / 100) in Decimal, which is exact for p with <= 15 digits). */
+typedef enum {
+    KRR_PCT_REF_INDEX = 0,    /* X[k] of the UNSORTED pod-ordered concatenation (the
+                                 reference's actual rule, simple.py:36) */
+    KRR_PCT_SORTED_LOWER = 1, /* sorted(X)[k]  (stable sort, README.md:103 intent) */
+    KRR_PCT_LINEAR = 2        /* np.percentile(X, p, method="linear") bit-exact:
+                                 vidx=(n-1)*q in f64, numpy _lerp without FMA */
+} krr_percentile_mode;
+
+/* Per-segment flags written to out_flags. */
+#define KRR_FLAG_NAN 1u       /* a NaN sample was present (gaps_are_nan == 0): the
+                                 reference raises decimal.InvalidOperation for max()
+                                 and sorted(); numpy returns NaN */
+#define KRR_FLAG_CAPACITY 2u  /* internal selection bound violated (never expected) */
+#define KRR_FLAG_EMPTY 4u     /* n == 0: value is NaN (reference: Decimal('NaN'),
+                                 simple.py:26-27 and 33-34) */
+
+typedef struct {
+    const double* values;    /* device pointer, n_values float64 */
+    const int64_t* offsets;  /* device pointer, n_segments+1 int64, non-decreasing */
+    int64_t n_segments;
+    int64_t n_values;
+    int64_t max_segment_len; /* upper bound on offsets[s+1]-offsets[s]; 0 = compute it (syncs) */
+    int32_t gaps_are_nan;    /* 1: NaN slot = absent sample */
+    int32_t reserved;
+} krr_series;
+
+typedef struct {
+    int32_t mode;            /* krr_percentile_mode */
+    int32_t reserved;
+    int64_t p_num;           /* percentile p = p_num / p_den exactly, 0 < p <= 100 */
+    int64_t p_den;           /* positive; p_den <= 1e15 */
+    double q;                /* float64(p) / 100.0 as numpy computes it (LINEAR only) */
+} krr_percentile_params;
+
+typedef struct krr_ctx krr_ctx;
+
+int krr_abi_version(void);
+
+/* Create a context bound to HIP device `device` (a process may hold several). */
+int krr_create(int device, krr_ctx** out_ctx);
+int krr_destroy(krr_ctx* ctx);
+const char* krr_last_error(const krr_ctx* ctx);
+
+/* CPU proposal per segment.  out_value[s] = the selected f64 sample (bit-exact),
+ * out_count[s] = n (present samples), out_flags[s] = KRR_FLAG_*.  All outputs are
+ * device pointers with n_segments entries. */
+int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series,
+                             const krr_percentile_params* params, double* out_value,
+                             int64_t* out_count, uint32_t* out_flags, void* stream);
+
+/* Memory proposal per segment: out_value[s] = max(X) with Python max() tie rule
+ * (first maximal element, which only matters for -0.0 vs +0.0), out_count[s] = n. */
+int krr_segmented_max(krr_ctx* ctx, const krr_series* series, double* out_value,
+                      int64_t* out_count, uint32_t* out_flags, void* stream);
+
+/* SimpleStrategy.run over every object: cpu and mem each hold one segment per
+ * object (same n_segments).  Outputs are device pointers of n_segments entries. */
+int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
+                   const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
+                   uint32_t* cpu_flags, double* mem_value, int64_t* mem_count,
+                   uint32_t* mem_flags, void* stream);
+
+/* Same as krr_simple_run, but every pointer (inputs and outputs) is a HOST
+ * pointer; copies in, runs, copies out and synchronises.  Includes PCIe. */
+int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* cpu_offsets,
+                        const double* mem_values, const int64_t* mem_offsets,
+                        int64_t n_objects, int32_t gaps_are_nan,
+                        const krr_percentile_params* params, double* cpu_value,
+                        int64_t* cpu_count, uint32_t* cpu_flags, double* mem_value,
+                        int64_t* mem_count, uint32_t* mem_flags);
+
+/* Synthetic week-long series (bench/test data), generated on the device from a
+ * counter-based hash so that no host packing or PCIe is involved.
+ * kind 0 = CPU cores ~ Gamma(k=2, theta=0.05); kind 1 = memory bytes
+ * floor(Normal(2e8, 2e7)).  Segment s holds pods of pod_len slots (the last pod
+ * takes the remainder); with gaps != 0, each pod gets a late start with prob.
+ * 0.3 (>= 1440 samples kept), and gap runs in blocks of 30 slots with a per-pod
+ * gap fraction ~ U(0, 0.2); gap slots are NaN. */
+int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
+                   uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KRR_AMD_H */

@@ -1,0 +1,219 @@
+"""ctypes binding of libkrr_amd.so — the C ABI declared in include/krr_amd.h.
+
+This is the only way the product path reaches the GPU.  There is no CPU or
+eager-PyTorch fallback: if the shared library is missing, fails to load, or no
+HIP device is present, every entry point raises NativeUnavailable.
+
+PyTorch is used only as plumbing (device memory and the current HIP stream);
+it is imported BEFORE the library is loaded so that libkrr_amd.so binds to the
+HIP runtime torch already mapped (both carry the soname libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("KRR_AMD_LIB", os.path.join(_HERE, "lib", "libkrr_amd.so"))
+
+KRR_OK = 0
+KRR_E_INVALID = -1
+KRR_E_HIP = -2
+KRR_E_CAPACITY = -3
+KRR_E_UNSUPPORTED = -4
+
+KRR_PCT_REF_INDEX = 0
+KRR_PCT_SORTED_LOWER = 1
+KRR_PCT_LINEAR = 2
+
+KRR_FLAG_NAN = 1
+KRR_FLAG_CAPACITY = 2
+KRR_FLAG_EMPTY = 4
+
+# Every symbol include/krr_amd.h declares (tests/test_abi.py checks the export table).
+EXPORTED_SYMBOLS = (
+    "krr_abi_version",
+    "krr_create",
+    "krr_destroy",
+    "krr_last_error",
+    "krr_segmented_percentile",
+    "krr_segmented_max",
+    "krr_simple_run",
+    "krr_simple_run_host",
+    "krr_synth_fill",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP extension (libkrr_amd.so) or a HIP device is not available."""
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libkrr_amd error {code}: {message}")
+        self.code = code
+
+
+class KrrSeries(ctypes.Structure):
+    _fields_ = [
+        ("values", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("n_segments", ctypes.c_int64),
+        ("n_values", ctypes.c_int64),
+        ("max_segment_len", ctypes.c_int64),
+        ("gaps_are_nan", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class KrrPercentileParams(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("p_num", ctypes.c_int64),
+        ("p_den", ctypes.c_int64),
+        ("q", ctypes.c_double),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(require_torch: bool = True) -> ctypes.CDLL:
+    """Load libkrr_amd.so and declare every prototype.  Raises NativeUnavailable."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if require_torch:
+            import torch  # noqa: F401  (bind to torch's HIP runtime first)
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+        sp, pp = ctypes.POINTER(KrrSeries), ctypes.POINTER(KrrPercentileParams)
+        lib.krr_abi_version.argtypes = []
+        lib.krr_abi_version.restype = ctypes.c_int
+        lib.krr_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        lib.krr_create.restype = ctypes.c_int
+        lib.krr_destroy.argtypes = [vp]
+        lib.krr_destroy.restype = ctypes.c_int
+        lib.krr_last_error.argtypes = [vp]
+        lib.krr_last_error.restype = ctypes.c_char_p
+        lib.krr_segmented_percentile.argtypes = [vp, sp, pp, vp, vp, vp, vp]
+        lib.krr_segmented_percentile.restype = ctypes.c_int
+        lib.krr_segmented_max.argtypes = [vp, sp, vp, vp, vp, vp]
+        lib.krr_segmented_max.restype = ctypes.c_int
+        lib.krr_simple_run.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_simple_run.restype = ctypes.c_int
+        lib.krr_simple_run_host.argtypes = [vp, vp, vp, vp, vp, i64, i32, pp, vp, vp, vp, vp, vp, vp]
+        lib.krr_simple_run_host.restype = ctypes.c_int
+        lib.krr_synth_fill.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, vp]
+        lib.krr_synth_fill.restype = ctypes.c_int
+        if lib.krr_abi_version() != 1:
+            raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+class Context:
+    """One krr_ctx bound to one HIP device (not shared between threads)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise NativeUnavailable("no HIP device visible: the KRR hot path runs only on MI355X (gfx950)")
+        self._lib = load_library()
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        rc = self._lib.krr_create(self.device, ctypes.byref(h))
+        if rc != KRR_OK:
+            raise NativeError(rc, f"krr_create(device={device}) failed")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.krr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        if rc != KRR_OK:
+            msg = self._lib.krr_last_error(self._h)
+            raise NativeError(rc, msg.decode() if msg else "")
+
+    # --- helpers ---------------------------------------------------------
+    @staticmethod
+    def _stream(stream) -> Optional[int]:
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    @staticmethod
+    def series(values, offsets, max_segment_len: int = 0, gaps_are_nan: bool = False) -> KrrSeries:
+        _check_tensor(values, "float64")
+        _check_tensor(offsets, "int64")
+        return KrrSeries(values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, values.numel(),
+                         int(max_segment_len), int(bool(gaps_are_nan)), 0)
+
+    # --- entry points -----------------------------------------------------
+    def segmented_percentile(self, series: KrrSeries, params: KrrPercentileParams, out_value, out_count,
+                             out_flags, stream=None) -> None:
+        for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, series.n_segments)
+        self._check(self._lib.krr_segmented_percentile(
+            self._h, ctypes.byref(series), ctypes.byref(params), out_value.data_ptr(), out_count.data_ptr(),
+            out_flags.data_ptr(), self._stream(stream)))
+
+    def segmented_max(self, series: KrrSeries, out_value, out_count, out_flags, stream=None) -> None:
+        for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, series.n_segments)
+        self._check(self._lib.krr_segmented_max(
+            self._h, ctypes.byref(series), out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(),
+            self._stream(stream)))
+
+    def simple_run(self, cpu: KrrSeries, mem: KrrSeries, params: KrrPercentileParams, out: dict,
+                   stream=None) -> None:
+        """out: dict with cpu_value/cpu_count/cpu_flags/mem_value/mem_count/mem_flags tensors."""
+        n = cpu.n_segments
+        for k, dt in (("cpu_value", "float64"), ("cpu_count", "int64"), ("cpu_flags", "int32"),
+                      ("mem_value", "float64"), ("mem_count", "int64"), ("mem_flags", "int32")):
+            _check_tensor(out[k], dt, n)
+        self._check(self._lib.krr_simple_run(
+            self._h, ctypes.byref(cpu), ctypes.byref(mem), ctypes.byref(params),
+            out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
+            out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
+            self._stream(stream)))
+
+    def synth_fill(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, stream=None) -> None:
+        _check_tensor(values, "float64")
+        _check_tensor(offsets, "int64")
+        self._check(self._lib.krr_synth_fill(
+            self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
+            int(kind), int(pod_len), int(bool(gaps)), self._stream(stream)))
+
+
+def _check_tensor(t, dtype: str, numel: Optional[int] = None) -> None:
+    import torch
+
+    want = getattr(torch, dtype)
+    if not isinstance(t, torch.Tensor) or t.dtype != want or not t.is_cuda or not t.is_contiguous():
+        raise TypeError(f"expected a contiguous {dtype} HIP-device tensor, got "
+                        f"{getattr(t, 'dtype', type(t))} on {getattr(t, 'device', '?')}")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"output tensor has {t.numel()} elements, need {numel}")

@@ -1,0 +1,99 @@
+"""Multi-GPU fleet sharding and result collection (one process per GPU).
+
+Objects are independent (runner.py:110-112; simple.py:42-49 reads only its own
+object), so a fleet shards into contiguous object ranges with no data-path
+collective.  Each rank runs the kernels on its shard; the only exchange is the
+per-object result records (32 B each) gathered to rank 0 — over RCCL/xGMI when
+the process group is "nccl" (= RCCL on ROCm), over gloo in the CPU tests.
+
+Record layout (int64[4] per object, 32 B):
+  [0] cpu value bits (float64 bit pattern)   [1] mem value bits
+  [2] cpu count | cpu flags << 48            [3] mem count | mem flags << 48
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+
+RECORD_WORDS = 4
+_COUNT_MASK = (1 << 48) - 1
+
+
+def shard_bounds(samples_per_object: Sequence[int] | np.ndarray, world_size: int) -> list[tuple[int, int]]:
+    """Cut objects [0, S) into world_size contiguous ranges with ~equal sample counts.
+
+    Cuts fall on object boundaries: rank r gets the objects whose sample prefix
+    starts in [r*T/W, (r+1)*T/W).  Every object lands in exactly one shard.
+    """
+    w = np.asarray(samples_per_object, dtype=np.int64)
+    S = int(w.size)
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    if S == 0:
+        return [(0, 0)] * world_size
+    prefix = np.concatenate([[0], np.cumsum(w)])
+    total = int(prefix[-1])
+    if total == 0:  # no samples anywhere: split by object count
+        cuts = [(S * r) // world_size for r in range(world_size + 1)]
+    else:
+        targets = [(total * r) // world_size for r in range(world_size + 1)]
+        cuts = [int(np.searchsorted(prefix[:-1], t, side="left")) for t in targets]
+        cuts[0], cuts[-1] = 0, S
+        for r in range(1, world_size + 1):  # monotone
+            cuts[r] = max(cuts[r], cuts[r - 1])
+    return [(cuts[r], cuts[r + 1]) for r in range(world_size)]
+
+
+def pack_records(out: dict):
+    """Device tensors from SimpleEngine.run_device -> one int64 [S, 4] tensor."""
+    import torch
+
+    cv = out["cpu_value"].view(torch.int64)
+    mv = out["mem_value"].view(torch.int64)
+    cc = out["cpu_count"] | (out["cpu_flags"].to(torch.int64) << 48)
+    mc = out["mem_count"] | (out["mem_flags"].to(torch.int64) << 48)
+    return torch.stack([cv, mv, cc, mc], dim=1).contiguous()
+
+
+def unpack_records(rec) -> dict:
+    """int64 [S, 4] (tensor or array) -> host numpy arrays of the six result fields."""
+    a = rec.cpu().numpy() if hasattr(rec, "cpu") else np.asarray(rec)
+    a = np.ascontiguousarray(a, dtype=np.int64).reshape(-1, RECORD_WORDS)
+    return {
+        "cpu_value": a[:, 0].copy().view(np.float64),
+        "mem_value": a[:, 1].copy().view(np.float64),
+        "cpu_count": a[:, 2] & _COUNT_MASK,
+        "cpu_flags": (a[:, 2] >> 48).astype(np.uint32),
+        "mem_count": a[:, 3] & _COUNT_MASK,
+        "mem_flags": (a[:, 3] >> 48).astype(np.uint32),
+    }
+
+
+def gather_records(local, dst: int = 0, group=None) -> Optional[object]:
+    """Gather every rank's [n_r, 4] records to rank `dst`, concatenated in rank order.
+
+    Ranks may hold different n_r: counts are exchanged first (one all_gather of a
+    single int64), shards are padded to the max, gathered in ONE collective, and
+    trimmed on dst.  Returns the [sum n_r, 4] tensor on dst, None elsewhere.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = local.device
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    width = max(max(counts), 1)
+    padded = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
+    if local.shape[0]:
+        padded[: local.shape[0]] = local
+    if rank == dst:
+        bufs = [torch.empty_like(padded) for _ in range(world)]
+        dist.gather(padded, gather_list=bufs, dst=dst, group=group)
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    dist.gather(padded, gather_list=None, dst=dst, group=group)
+    return None

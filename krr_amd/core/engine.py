@@ -1,0 +1,130 @@
+"""Device engine: moves a PackedFleet to HBM, runs the SimpleStrategy kernels
+through the C ABI, and returns the raw per-object results.
+
+There is no CPU path: ``SimpleEngine`` raises NativeUnavailable when the HIP
+library or a device is missing.  One krr_ctx per (thread, device) keeps the
+ABI's "one ctx per thread" rule while the reference's runner calls strategies
+from a thread pool (runner.py:104-106).
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from decimal import Decimal
+from fractions import Fraction
+from typing import Optional
+
+import numpy as np
+
+from krr_amd import _native
+from krr_amd.core.packing import PackedFleet, PackedSeries
+
+MODE_CODES = {"ref_index": _native.KRR_PCT_REF_INDEX, "sorted_lower": _native.KRR_PCT_SORTED_LOWER,
+              "linear": _native.KRR_PCT_LINEAR}
+P_DEN_MAX = 10**15
+
+
+def percentile_params(percentile, mode: str) -> _native.KrrPercentileParams:
+    """Exact rational p for the index rule, float64 q = p/100 for numpy's LINEAR rule.
+
+    The reference evaluates int((n-1) * p / 100) in Decimal (CLI path, p a Decimal)
+    or int/float arithmetic (default path, p the int 99); both equal the exact
+    floor for p with <= 15 significant digits, which the kernel computes in
+    128-bit integers.
+    """
+    if mode not in MODE_CODES:
+        raise ValueError(f"unknown percentile mode {mode!r}; expected one of {sorted(MODE_CODES)}")
+    frac = Fraction(Decimal(percentile)) if not isinstance(percentile, Fraction) else percentile
+    if not (0 < frac <= 100):
+        raise ValueError(f"percentile must be in (0, 100], got {percentile}")
+    if frac.denominator > P_DEN_MAX or frac.numerator > 100 * P_DEN_MAX:
+        raise ValueError(f"percentile {percentile} needs more than 15 significant digits; "
+                         "the batched exact index rule supports p_den <= 1e15")
+    q = float(percentile) / 100.0
+    return _native.KrrPercentileParams(MODE_CODES[mode], 0, frac.numerator, frac.denominator, q)
+
+
+@dataclass
+class RawResults:
+    """Per-object raw proposals as the kernels return them (host numpy arrays)."""
+    cpu_value: np.ndarray
+    cpu_count: np.ndarray
+    cpu_flags: np.ndarray
+    mem_value: np.ndarray
+    mem_count: np.ndarray
+    mem_flags: np.ndarray
+
+
+class SimpleEngine:
+    def __init__(self, device: int = 0):
+        self.device = int(device)
+        self._tls = threading.local()
+
+    def context(self) -> _native.Context:
+        ctx = getattr(self._tls, "ctx", None)
+        if ctx is None:
+            ctx = _native.Context(self.device)
+            self._tls.ctx = ctx
+        return ctx
+
+    def _to_device(self, ps: PackedSeries):
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        vals = torch.from_numpy(np.ascontiguousarray(ps.values, dtype=np.float64)).to(dev, non_blocking=False)
+        offs = torch.from_numpy(np.ascontiguousarray(ps.offsets, dtype=np.int64)).to(dev, non_blocking=False)
+        return vals, offs
+
+    def run_device(self, cpu_vals, cpu_offs, mem_vals, mem_offs, params: _native.KrrPercentileParams,
+                   cpu_max_len: int = 0, mem_max_len: int = 0, gaps_are_nan: bool = False,
+                   out: Optional[dict] = None, stream=None) -> dict:
+        """All inputs already in HBM (torch tensors).  Returns the device output dict."""
+        import torch
+
+        ctx = self.context()
+        S = cpu_offs.numel() - 1
+        dev = cpu_vals.device
+        if out is None:
+            out = {
+                "cpu_value": torch.empty(S, dtype=torch.float64, device=dev),
+                "cpu_count": torch.empty(S, dtype=torch.int64, device=dev),
+                "cpu_flags": torch.empty(S, dtype=torch.int32, device=dev),
+                "mem_value": torch.empty(S, dtype=torch.float64, device=dev),
+                "mem_count": torch.empty(S, dtype=torch.int64, device=dev),
+                "mem_flags": torch.empty(S, dtype=torch.int32, device=dev),
+            }
+        cs = ctx.series(cpu_vals, cpu_offs, cpu_max_len, gaps_are_nan)
+        ms = ctx.series(mem_vals, mem_offs, mem_max_len, gaps_are_nan)
+        ctx.simple_run(cs, ms, params, out, stream=stream)
+        return out
+
+    def run_packed(self, fleet: PackedFleet, params: _native.KrrPercentileParams) -> RawResults:
+        import torch
+
+        if fleet.cpu.n_segments != fleet.mem.n_segments:
+            raise ValueError("cpu and memory need one segment per object each")
+        self.context()  # raises NativeUnavailable without the HIP library or a device
+        if fleet.n_objects == 0:
+            e = np.zeros(0)
+            return RawResults(e, e.astype(np.int64), e.astype(np.uint32), e, e.astype(np.int64),
+                              e.astype(np.uint32))
+        with torch.cuda.device(self.device):
+            cv, co = self._to_device(fleet.cpu)
+            mv, mo = self._to_device(fleet.mem)
+            out = self.run_device(cv, co, mv, mo, params, max(fleet.cpu.max_len, 1), max(fleet.mem.max_len, 1),
+                                  fleet.cpu.gaps_are_nan)
+            host = {k: v.cpu().numpy() for k, v in out.items()}  # synchronises the stream
+        return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"].view(np.uint32),
+                          host["mem_value"], host["mem_count"], host["mem_flags"].view(np.uint32))
+
+
+_default_engines: dict[int, SimpleEngine] = {}
+_engines_lock = threading.Lock()
+
+
+def default_engine(device: int = 0) -> SimpleEngine:
+    with _engines_lock:
+        eng = _default_engines.get(device)
+        if eng is None:
+            eng = _default_engines[device] = SimpleEngine(device)
+        return eng

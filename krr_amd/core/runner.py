@@ -1,0 +1,90 @@
+"""Batched runner: the fleet-wide replacement of the reference's per-object loop
+(Runner._calculate_object_recommendations / _gather_objects_recommendations,
+robusta_krr/core/runner.py:88-120).
+
+  1. gather every object's HistoryData (loader I/O, concurrently as the reference does);
+  2. strategies with ``run_batch`` (SimpleStrategy): pack once, ONE kernel pass;
+     any other BaseStrategy subclass: the reference's per-object ``run()`` loop;
+  3. exact-decimal rounding + minimum clamp (runner.py:49-86, krr_amd.core.rounding);
+  4. ResourceAllocations (NaN -> "?", allocations.py:40-41).
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime
+from typing import Optional, Protocol, Sequence
+
+from krr_amd.core.abstract.strategies import (
+    BaseStrategy,
+    HistoryData,
+    ResourceHistoryData,
+    RunResult,
+    run_each,
+    supports_batch,
+)
+from krr_amd.core.models.allocations import ResourceAllocations, ResourceType
+from krr_amd.core.models.objects import K8sObjectData
+from krr_amd.core.rounding import DEFAULT_CPU_MIN_VALUE, DEFAULT_MEMORY_MIN_VALUE, format_result
+
+
+class HistoryLoader(Protocol):
+    """What the reference's PrometheusLoader.gather_data provides (prometheus.py:108-155)."""
+
+    async def gather_data(self, object: K8sObjectData, resource: ResourceType, period: datetime.timedelta,
+                          *, timeframe: datetime.timedelta) -> ResourceHistoryData: ...
+
+
+class BatchedRunner:
+    def __init__(self, strategy: BaseStrategy, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
+                 memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE):
+        self.strategy = strategy
+        self.cpu_min_value = cpu_min_value
+        self.memory_min_value = memory_min_value
+
+    @classmethod
+    def from_config(cls, config) -> "BatchedRunner":
+        return cls(config.create_strategy(), config.cpu_min_value, config.memory_min_value)
+
+    def raw_results(self, objects: Sequence[K8sObjectData], histories: Sequence[HistoryData]) -> list[RunResult]:
+        if len(objects) != len(histories):
+            raise ValueError("one HistoryData per object")
+        if supports_batch(self.strategy):
+            return self.strategy.run_batch(histories, objects)  # type: ignore[attr-defined]
+        return run_each(self.strategy, histories, objects)
+
+    def recommend(self, objects: Sequence[K8sObjectData], histories: Sequence[HistoryData]) -> list[RunResult]:
+        """Rounded RunResults, one per object (what _calculate_object_recommendations returns)."""
+        return [format_result(r, self.cpu_min_value, self.memory_min_value)
+                for r in self.raw_results(objects, histories)]
+
+    def allocations(self, objects: Sequence[K8sObjectData],
+                    histories: Sequence[HistoryData]) -> list[ResourceAllocations]:
+        return [to_allocations(r) for r in self.recommend(objects, histories)]
+
+    async def gather_histories(self, objects: Sequence[K8sObjectData], loader: HistoryLoader) -> list[HistoryData]:
+        settings = self.strategy.settings
+
+        async def one(obj: K8sObjectData) -> HistoryData:
+            data = await asyncio.gather(*[
+                loader.gather_data(obj, resource, settings.history_timedelta, timeframe=settings.timeframe_timedelta)
+                for resource in ResourceType
+            ])
+            return dict(zip(ResourceType, data))
+
+        return list(await asyncio.gather(*[one(o) for o in objects]))
+
+    async def gather_objects_recommendations(self, objects: Sequence[K8sObjectData],
+                                             loader: HistoryLoader) -> list[ResourceAllocations]:
+        histories = await self.gather_histories(objects, loader)
+        # the kernel pass runs off the event loop, like the reference's to_thread (runner.py:106)
+        return await asyncio.to_thread(self.allocations, objects, histories)
+
+
+def to_allocations(result: RunResult) -> ResourceAllocations:
+    return ResourceAllocations(
+        requests={rt: result[rt].request for rt in ResourceType},
+        limits={rt: result[rt].limit for rt in ResourceType},
+    )
+
+
+__all__ = ["BatchedRunner", "HistoryLoader", "to_allocations"]

@@ -1,0 +1,82 @@
+// krr_plan.h — host+device planning shared by the ABI and the kernels.
+#pragma once
+
+#include <stdint.h>
+#include <math.h>
+
+#include "krr_amd.h"
+
+namespace krr {
+
+#if defined(__HIPCC__)
+#define KRR_HD __host__ __device__
+#else
+#define KRR_HD
+#endif
+
+// Exact floor((n-1) * p_num / (100 * p_den)), host side (device side: krr_device.h).
+KRR_HD inline int64_t exact_rank_hd(int64_t n, int64_t p_num, int64_t p_den) {
+    const uint64_t a = (uint64_t)(n - 1);
+    const uint64_t den = 100ull * (uint64_t)p_den;
+    const unsigned __int128 num = (unsigned __int128)a * (uint64_t)p_num;
+    uint64_t k = (uint64_t)((double)a * ((double)p_num / (double)den));
+    if (k > a) k = a;
+    while (k < a && (unsigned __int128)(k + 1) * den <= num) ++k;
+    while (k > 0 && (unsigned __int128)k * den > num) --k;
+    return (int64_t)k;
+}
+
+// Which extreme of a segment of L slots the selection keeps, and how many keys.
+// The kernel needs ranks r1 (and r1+1 for LINEAR) of the n <= L present samples.
+// Keeping the top T = L - k(L) + 2 keys (or the bottom k(L) + 4) covers every
+// n <= L, because n - k(n) and k(n) are non-decreasing in n; the +2/+4 margins
+// absorb the +-1 floor error of the float64 LINEAR index.
+struct SidePlan {
+    uint32_t tkeep;
+    uint32_t bottom;  // 1: keep the smallest keys (flip the order)
+};
+
+KRR_HD inline SidePlan plan_side(int64_t L, int32_t mode, int64_t p_num, int64_t p_den, double q) {
+    SidePlan sp;
+    if (L <= 0) {
+        sp.tkeep = 1;
+        sp.bottom = 0;
+        return sp;
+    }
+    int64_t k;
+    if (mode == KRR_PCT_LINEAR) {
+        double v = (double)(L - 1) * q;
+        k = (int64_t)floor(v);
+        if (k > L - 1) k = L - 1;
+        if (k < 0) k = 0;
+    } else {
+        k = exact_rank_hd(L, p_num, p_den);
+    }
+    int64_t top = L - k + 2;
+    int64_t bot = k + 4;
+    if (top > L) top = L;
+    if (bot > L) bot = L;
+    if (top <= bot) {
+        sp.tkeep = (uint32_t)top;
+        sp.bottom = 0;
+    } else {
+        sp.tkeep = (uint32_t)bot;
+        sp.bottom = 1;
+    }
+    return sp;
+}
+
+// Elements one streaming iteration can append (U double2 per lane, 64 lanes).
+constexpr int kUnroll = 8;
+constexpr uint32_t kChunkElems = 2u * kUnroll * 64u;
+
+// LDS key capacity for a launch whose largest segment keeps tkeep keys:
+// room for tkeep, the same again as compaction slack, and one full chunk.
+inline uint32_t capacity_for(uint32_t tkeep_max) {
+    uint64_t c = 2ull * tkeep_max + kChunkElems + 64;
+    if (c < 2048) c = 2048;
+    c = (c + 255) & ~255ull;
+    return (uint32_t)c;
+}
+
+}  // namespace krr

@@ -1,0 +1,138 @@
+"""SimpleStrategy on MI355X — the reference's default strategy
+(robusta_krr/strategies/simple.py:16-49) with its per-sample work moved to HIP.
+
+  CPU    = the sample at index k = floor((n-1) * p / 100) of the pods' samples
+           concatenated in pod order, UNSORTED (simple.py:31-36)       [ref_index]
+  Memory = max(samples) * Decimal(1 + b / 100)                     (simple.py:24-29)
+  empty  -> Decimal('NaN');  CPU limit None, memory limit = request (simple.py:42-49)
+
+``percentile_mode`` (build extension, default "ref_index" = reference parity):
+  "sorted_lower" - sorted(samples)[k], the README's stated "99th percentile";
+  "linear"       - np.percentile(samples, p) (numpy 2.2 method="linear"), bit-exact.
+
+The GPU returns the selected/maximal float64 sample; the host rebuilds its
+Decimal exactly as the reference parsed it (prom_decimal) and applies the
+memory buffer in the reference's decimal context.
+"""
+from __future__ import annotations
+
+import decimal
+import enum
+from decimal import Decimal
+from typing import Optional, Sequence
+
+import numpy as np
+import pydantic.v1 as pd
+
+from krr_amd import _native
+from krr_amd.core.abstract.strategies import (
+    BaseStrategy,
+    HistoryData,
+    K8sObjectData,
+    ResourceRecommendation,
+    ResourceType,
+    RunResult,
+    StrategySettings,
+)
+from krr_amd.core.engine import RawResults, default_engine, percentile_params
+from krr_amd.core.packing import PackedFleet, pack_histories, pack_resource
+from krr_amd.core.rounding import reference_context
+from krr_amd.utils.prom_decimal import prom_decimal
+
+
+class PercentileMode(str, enum.Enum):
+    REF_INDEX = "ref_index"
+    SORTED_LOWER = "sorted_lower"
+    LINEAR = "linear"
+
+
+class SimpleStrategySettings(StrategySettings):
+    cpu_percentile: Decimal = pd.Field(
+        99, gt=0, le=100, description="The percentile to use for the CPU recommendation."
+    )
+    memory_buffer_percentage: Decimal = pd.Field(
+        5, gt=0, description="The percentage of added buffer to the peak memory usage for memory recommendation."
+    )
+    percentile_mode: PercentileMode = pd.Field(
+        PercentileMode.REF_INDEX,
+        description="CPU percentile rule: ref_index (reference KRR 1.0.0), sorted_lower, or linear (numpy).",
+    )
+    device: int = pd.Field(0, ge=0, description="HIP device that runs the kernels.")
+
+    # --- the two proposal functions, same names and signatures as the reference ---
+    def calculate_memory_proposal(self, data: dict[str, list[Decimal]]) -> Decimal:
+        raw = self._run_single({ResourceType.CPU: {}, ResourceType.Memory: data})
+        return self.memory_from_raw(raw, 0)
+
+    def calculate_cpu_proposal(self, data: dict[str, list[Decimal]]) -> Decimal:
+        raw = self._run_single({ResourceType.CPU: data, ResourceType.Memory: {}})
+        return self.cpu_from_raw(raw, 0)
+
+    # --- batched helpers ---
+    def params(self) -> _native.KrrPercentileParams:
+        return percentile_params(self.cpu_percentile, PercentileMode(self.percentile_mode).value)
+
+    def memory_buffer(self) -> Decimal:
+        with decimal.localcontext(reference_context()):
+            return Decimal(1 + self.memory_buffer_percentage / 100)
+
+    def run_fleet(self, fleet: PackedFleet) -> RawResults:
+        return default_engine(self.device).run_packed(fleet, self.params())
+
+    def _run_single(self, history: HistoryData) -> RawResults:
+        return self.run_fleet(pack_histories([history]))
+
+    def cpu_from_raw(self, raw: RawResults, i: int) -> Decimal:
+        flags = int(raw.cpu_flags[i])
+        if flags & _native.KRR_FLAG_CAPACITY:
+            raise RuntimeError(f"object {i}: CPU selection bound violated (KRR_FLAG_CAPACITY)")
+        if flags & _native.KRR_FLAG_EMPTY:
+            return Decimal("NaN")
+        if flags & _native.KRR_FLAG_NAN:
+            # sorted() over Decimals compares with '<'; a NaN operand signals once any
+            # comparison happens, i.e. when n >= 2 (one sample is never compared).
+            if PercentileMode(self.percentile_mode) is PercentileMode.SORTED_LOWER and raw.cpu_count[i] >= 2:
+                raise decimal.InvalidOperation([decimal.InvalidOperation])
+            return Decimal("NaN")
+        return prom_decimal(float(raw.cpu_value[i]))
+
+    def memory_from_raw(self, raw: RawResults, i: int, buffer: Optional[Decimal] = None) -> Decimal:
+        flags = int(raw.mem_flags[i])
+        if flags & _native.KRR_FLAG_EMPTY:
+            return Decimal("NaN")
+        if flags & _native.KRR_FLAG_NAN:
+            # max() over Decimals compares with '>' and a NaN operand signals
+            # (simple.py:29) — unless n == 1, where nothing is compared and NaN passes.
+            if raw.mem_count[i] >= 2:
+                raise decimal.InvalidOperation([decimal.InvalidOperation])
+            return Decimal("NaN")
+        if buffer is None:
+            buffer = self.memory_buffer()
+        with decimal.localcontext(reference_context()):
+            return prom_decimal(float(raw.mem_value[i])) * buffer
+
+
+class SimpleStrategy(BaseStrategy[SimpleStrategySettings]):
+    __display_name__ = "simple"
+
+    def run(self, history_data: HistoryData, object_data: K8sObjectData) -> RunResult:
+        return self.run_batch([history_data], [object_data])[0]
+
+    def run_batch(self, histories: Sequence[HistoryData],
+                  objects: Optional[Sequence[K8sObjectData]] = None) -> list[RunResult]:
+        """One fleet-wide kernel pass for every object (the batched-runner hook)."""
+        fleet = PackedFleet(pack_resource(histories, ResourceType.CPU), pack_resource(histories, ResourceType.Memory))
+        return self.results_from_raw(self.settings.run_fleet(fleet))
+
+    def results_from_raw(self, raw: RawResults) -> list[RunResult]:
+        st = self.settings
+        buffer = st.memory_buffer()
+        out: list[RunResult] = []
+        for i in range(int(np.asarray(raw.cpu_value).size)):
+            cpu = st.cpu_from_raw(raw, i)
+            mem = st.memory_from_raw(raw, i, buffer)
+            out.append({
+                ResourceType.CPU: ResourceRecommendation(request=cpu, limit=None),
+                ResourceType.Memory: ResourceRecommendation(request=mem, limit=mem),
+            })
+        return out

@@ -1,0 +1,72 @@
+"""The C-ABI library builds, loads and exports every symbol include/krr_amd.h declares.
+
+No compute calls here (no GPU in the CPU suite): only argument validation paths
+that return before touching a device.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "krr_amd.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return set(re.findall(r"^(?:int|const char\*)\s+(krr_\w+)\(", text, flags=re.M))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as g
+
+    g.build()
+    from krr_amd import _native
+
+    return _native.load_library()
+
+
+def test_header_matches_binding_table():
+    from krr_amd import _native
+
+    assert _declared() == set(_native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from krr_amd import _native
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = _declared() - exported
+    assert not missing, f"missing exports: {missing}"
+    for name in _declared():
+        assert hasattr(lib, name)
+
+
+def test_library_is_gfx950_code_object(lib):
+    from krr_amd import _native
+
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", "--string-dump=.hip_fatbin",
+                          _native.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+def test_abi_version_and_null_handling(lib):
+    assert lib.krr_abi_version() == 1
+    assert lib.krr_last_error(None) == b"null krr_ctx"
+    assert lib.krr_segmented_percentile(None, None, None, None, None, None, None) == -1
+    assert lib.krr_segmented_max(None, None, None, None, None, None) == -1
+    assert lib.krr_destroy(None) == 0
+    h = ctypes.c_void_p()
+    assert lib.krr_create(0, None) == -1
+
+
+def test_struct_layouts_match_header():
+    from krr_amd import _native
+
+    assert ctypes.sizeof(_native.KrrSeries) == 8 * 5 + 4 * 2
+    assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 3

@@ -1,0 +1,190 @@
+"""GPU parity of the segmented kernels against the CPU oracle (bit-exact).
+
+Calls go through the C ABI (krr_amd._native -> libkrr_amd.so).  The oracle is
+pinned to the reference by tests/test_oracle_golden.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"ref_index": 0, "sorted_lower": 1, "linear": 2}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from krr_amd import _native
+
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+def _run_gpu(ctx, values, offsets, mode, p_num, p_den, gaps=False, maxlen=0):
+    import torch
+
+    from krr_amd import _native
+
+    dev = torch.device("cuda:0")
+    dv = torch.from_numpy(np.ascontiguousarray(values, np.float64)).to(dev)
+    do = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).to(dev)
+    S = offsets.size - 1
+    ov = torch.empty(S, dtype=torch.float64, device=dev)
+    on = torch.empty(S, dtype=torch.int64, device=dev)
+    of = torch.empty(S, dtype=torch.int32, device=dev)
+    ser = ctx.series(dv, do, maxlen, gaps)
+    if mode == "max":
+        ctx.segmented_max(ser, ov, on, of)
+    else:
+        q = float(p_num) / float(p_den) / 100.0
+        ctx.segmented_percentile(ser, _native.KrrPercentileParams(MODES[mode], 0, p_num, p_den, q), ov, on, of)
+    torch.cuda.synchronize()
+    return ov.cpu().numpy(), on.cpu().numpy(), of.cpu().numpy().astype(np.uint32)
+
+
+def _oracle(values, offsets, mode, p_num, p_den, gaps=False):
+    if mode == "max":
+        return oracle.seg_max(values, offsets, gaps)
+    q = float(p_num) / float(p_den) / 100.0
+    return oracle.percentile(values, offsets, MODES[mode], p_num, p_den, q, gaps)
+
+
+def _assert_same(got, want, mode, tag=""):
+    gv, gn, gf = got
+    wv, wn, wf = want
+    assert np.array_equal(gn, wn), f"{tag} counts differ at {np.nonzero(gn != wn)[0][:10]}"
+    assert np.array_equal(gf, wf), f"{tag} flags differ at {np.nonzero(gf != wf)[0][:10]}"
+    gb, wb = gv.view(np.uint64), wv.view(np.uint64)
+    nan_both = np.isnan(gv) & np.isnan(wv)
+    same = (gb == wb) | nan_both
+    if mode == "linear":  # sign of a zero result is unspecified (numpy's partition is unstable)
+        same |= (gv == 0) & (wv == 0)
+    bad = np.nonzero(~same)[0]
+    assert bad.size == 0, f"{tag} values differ at {bad[:10]}: got {gv[bad[:5]]} want {wv[bad[:5]]}"
+
+
+def _ragged(rng, nseg, lo, hi):
+    lens = rng.integers(lo, hi, size=nseg)
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+
+
+PCTS = [(99, 1), (50, 1), (1, 10), (100, 1), (999, 10), (75, 1), (1, 1)]
+
+
+@pytest.mark.parametrize("mode", ["ref_index", "sorted_lower", "linear", "max"])
+@pytest.mark.parametrize("pct", PCTS)
+def test_random_ragged(ctx, mode, pct):
+    if mode == "max" and pct != PCTS[0]:
+        pytest.skip("max has no percentile")
+    rng = np.random.default_rng(hash((mode, pct)) & 0xFFFF)
+    offs = _ragged(rng, 300, 0, 6000)
+    offs[1:] += 0  # keep
+    vals = rng.gamma(2.0, 0.05, size=int(offs[-1]))
+    got = _run_gpu(ctx, vals, offs, mode, *pct)
+    want = _oracle(vals, offs, mode, *pct)
+    _assert_same(got, want, mode, f"{mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["ref_index", "sorted_lower", "linear", "max"])
+def test_gapped_dense(ctx, mode):
+    rng = np.random.default_rng(11)
+    S, L = 64, 5 * 2016
+    vals = rng.gamma(2.0, 0.05, size=S * L)
+    mask = rng.random(S * L) < 0.15
+    vals[mask] = np.nan
+    vals[3 * L:4 * L] = np.nan  # an all-gap segment
+    offs = (np.arange(S + 1) * L).astype(np.int64)
+    for pct in [(99, 1), (50, 1), (1, 10)]:
+        got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=True)
+        want = _oracle(vals, offs, mode, *pct, gaps=True)
+        _assert_same(got, want, mode, f"gaps {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear", "max", "ref_index"])
+def test_ties_and_specials(ctx, mode):
+    rng = np.random.default_rng(5)
+    offs = _ragged(rng, 200, 0, 3000)
+    N = int(offs[-1])
+    vals = rng.integers(0, 3, size=N).astype(np.float64)  # heavy ties
+    special = rng.random(N)
+    vals[special < 0.02] = -0.0
+    vals[(special >= 0.02) & (special < 0.025)] = np.inf
+    vals[(special >= 0.025) & (special < 0.03)] = -np.inf
+    for pct in [(99, 1), (50, 1), (1, 10), (100, 1)]:
+        got = _run_gpu(ctx, vals, offs, mode, *pct)
+        want = _oracle(vals, offs, mode, *pct)
+        _assert_same(got, want, mode, f"ties {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_adversarial_order(ctx, mode):
+    """Monotone and sawtooth series force a compaction on nearly every chunk."""
+    L = 50400
+    inc = np.arange(L, dtype=np.float64) * 1e-3
+    dec = inc[::-1].copy()
+    saw = np.tile(np.arange(1000, dtype=np.float64), L // 1000 + 1)[:L]
+    const = np.full(L, 0.25)
+    vals = np.concatenate([inc, dec, saw, const])
+    offs = (np.arange(5) * L).astype(np.int64)
+    for pct in [(99, 1), (50, 1), (1, 10), (9999, 100)]:
+        got = _run_gpu(ctx, vals, offs, mode, *pct)
+        want = _oracle(vals, offs, mode, *pct)
+        _assert_same(got, want, mode, f"adversarial {mode} p={pct}")
+
+
+def test_signed_zero_rules(ctx):
+    """Python max() keeps the first of -0/+0; sorted() is stable for them."""
+    segs = [[-0.0, 0.0], [0.0, -0.0], [-1.0, -0.0, 0.0, -0.0], [0.0, -0.0, -0.0, 0.0, -2.0]]
+    vals = np.array([x for s in segs for x in s])
+    offs = np.concatenate([[0], np.cumsum([len(s) for s in segs])]).astype(np.int64)
+    for mode in ("max", "sorted_lower"):
+        for pct in [(99, 1), (50, 1), (1, 10), (100, 1)]:
+            got = _run_gpu(ctx, vals, offs, mode, *pct)
+            want = _oracle(vals, offs, mode, *pct)
+            _assert_same(got, want, mode, f"zeros {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["ref_index", "sorted_lower", "linear", "max"])
+def test_nan_values_compact(ctx, mode):
+    """Without gap masking a NaN is a sample: flags + NaN per the reference's rules."""
+    rng = np.random.default_rng(9)
+    offs = _ragged(rng, 50, 1, 500)
+    vals = rng.gamma(2.0, 0.05, size=int(offs[-1]))
+    vals[rng.random(vals.size) < 0.003] = np.nan
+    got = _run_gpu(ctx, vals, offs, mode, 99, 1)
+    want = _oracle(vals, offs, mode, 99, 1)
+    _assert_same(got, want, mode, f"nan {mode}")
+
+
+def test_unaligned_offsets(ctx):
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 2500, size=257) | 1  # odd lengths -> odd starts
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    vals = rng.normal(size=int(offs[-1]))
+    for mode in ("ref_index", "sorted_lower", "linear", "max"):
+        got = _run_gpu(ctx, vals, offs, mode, 99, 1)
+        want = _oracle(vals, offs, mode, 99, 1)
+        _assert_same(got, want, mode, f"unaligned {mode}")
+
+
+def test_large_candidate_set_uses_scratch(ctx):
+    """p=50 on 50,400-sample series keeps ~25k keys: the HBM-scratch variant."""
+    rng = np.random.default_rng(21)
+    S, L = 40, 50400
+    vals = rng.gamma(2.0, 0.05, size=S * L)
+    offs = (np.arange(S + 1) * L).astype(np.int64)
+    for mode in ("sorted_lower", "linear"):
+        got = _run_gpu(ctx, vals, offs, mode, 50, 1)
+        want = _oracle(vals, offs, mode, 50, 1)
+        _assert_same(got, want, mode, f"scratch {mode}")
+
+
+def test_maxlen_autodetect(ctx):
+    rng = np.random.default_rng(4)
+    offs = _ragged(rng, 100, 0, 3000)
+    vals = rng.gamma(2.0, 0.05, size=int(offs[-1]))
+    got = _run_gpu(ctx, vals, offs, "linear", 99, 1, maxlen=0)
+    want = _oracle(vals, offs, "linear", 99, 1)
+    _assert_same(got, want, "linear", "autodetect")
