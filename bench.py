@@ -1,0 +1,262 @@
+"""Throughput bench of the KRR SimpleStrategy hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--mode linear|sorted_lower|ref_index]
+
+One "step" = one pass of the hot path over the rank's whole synthetic fleet
+shard, inputs resident in HBM: the CPU-percentile kernel over every CPU series,
+the max+count kernel over every memory series, and (N > 1) the RCCL gather of
+the 32-B per-container result records to rank 0, whose D2H copy ends the step.
+
+Workloads (BASELINE.json configs):
+  2 (default) 10k containers x 5 pods x 10,080 slots (7d@1m) per rank, NaN-gapped dense layout
+  3           100k containers x 1 pod, windows of 1..14 days @1m (1,440-20,160 samples), compact CSR
+  4           1M containers x 10,080 samples (7d@1m) split across the ranks, compact CSR
+Data are generated on the device by krr_synth_fill (counter hash; no host packing, no PCIe).
+
+Prints ONE JSON line on rank 0 (contract in the task brief): value = containers of ALL
+ranks / max-over-ranks step time; roofline = the CPU-percentile kernel's algorithmic
+bytes / its average launch time (HIP events on the launch stream) against 8 TB/s;
+cpu_baseline = the C oracle (OpenMP) on a bounded sample copied from the device.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from decimal import Decimal
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "container-series/sec right-sized (7d@1m) + % of HBM BW, 1/2/4/8 MI355X"
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SLOTS_7D = 10080
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
+    ap.add_argument("--percentile", default="99")
+    ap.add_argument("--containers", type=int, default=0, help="override containers per rank (testing)")
+    ap.add_argument("--cpu-sample", type=int, default=400, help="containers in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def workload(cfg: int, rank: int, world: int, override: int):
+    """Per-rank (offsets numpy array, pod_len, gaps, description, containers_total)."""
+    if cfg == 2:
+        n = override or 10_000
+        L = 5 * SLOTS_7D
+        offs = np.arange(n + 1, dtype=np.int64) * L
+        return offs, SLOTS_7D, True, f"config2: {n} containers/rank x 5 pods x 10080 slots (7d@1m), NaN-gapped dense", n * world
+    if cfg == 3:
+        n = override or 100_000
+        rng = np.random.default_rng(3 + rank)
+        L = rng.integers(1, 15, size=n) * 1440
+        offs = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+        return offs, 0, False, f"config3: {n} containers/rank x 1 pod, 1..14 days @1m, compact CSR", n * world
+    total = override * world if override else 1_000_000
+    lo, hi = (total * rank) // world, (total * (rank + 1)) // world
+    n = hi - lo
+    offs = np.arange(n + 1, dtype=np.int64) * SLOTS_7D
+    return offs, 0, False, f"config4: {total} containers x 10080 samples (7d@1m) over {world} ranks, compact CSR", total
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from krr_amd import _native
+    from krr_amd.core.distributed import gather_records, pack_records
+    from krr_amd.core.engine import percentile_params
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers)
+    S = offs_np.size - 1
+    N = int(offs_np[-1])
+    maxlen = int(np.max(np.diff(offs_np))) if S else 0
+    ctx = _native.Context(local)
+    offs = torch.from_numpy(offs_np).to(dev)
+    cpu = torch.empty(N, dtype=torch.float64, device=dev)
+    mem = torch.empty(N, dtype=torch.float64, device=dev)
+    seed = 1000003 * (args.config + 1) + rank
+    ctx.synth_fill(cpu, offs, seed, 0, pod_len, gaps)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, pod_len, gaps)
+    torch.cuda.synchronize()
+
+    params = percentile_params(Decimal(args.percentile), args.mode)
+    cs = ctx.series(cpu, offs, maxlen, gaps)
+    ms = ctx.series(mem, offs, maxlen, gaps)
+    out = {
+        "cpu_value": torch.empty(S, dtype=torch.float64, device=dev),
+        "cpu_count": torch.empty(S, dtype=torch.int64, device=dev),
+        "cpu_flags": torch.empty(S, dtype=torch.int32, device=dev),
+        "mem_value": torch.empty(S, dtype=torch.float64, device=dev),
+        "mem_count": torch.empty(S, dtype=torch.int64, device=dev),
+        "mem_flags": torch.empty(S, dtype=torch.int32, device=dev),
+    }
+    stream = torch.cuda.current_stream()
+    host_rec = torch.empty((containers_total if rank == 0 else S, 4), dtype=torch.int64, pin_memory=True)
+
+    def step(events=None):
+        if events is not None:
+            events[0].record(stream)
+        ctx.segmented_percentile(cs, params, out["cpu_value"], out["cpu_count"], out["cpu_flags"], stream)
+        if events is not None:
+            events[1].record(stream)
+        ctx.segmented_max(ms, out["mem_value"], out["mem_count"], out["mem_flags"], stream)
+        if events is not None:
+            events[2].record(stream)
+        rec = pack_records(out)
+        if world > 1:
+            rec = gather_records(rec, dst=0)
+        if rank == 0 or world == 1:
+            host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    step_s = float(dt.item())
+    pct_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    max_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    # algorithmic bytes per launch: every stored slot once, offsets, outputs
+    pct_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S
+    max_bytes = pct_bytes
+    achieved = pct_bytes / (pct_ms * 1e-3)
+    step_bytes_all = (pct_bytes + max_bytes) * world
+    result = {
+        "metric": METRIC,
+        "value": containers_total / step_s,
+        "unit": "container-series/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak" if args.config != 4 else "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (device counter-hash: CPU ~ Gamma(2, 0.05) cores, memory ~ floor(N(2e8, 2e7)) bytes)",
+        "config": {
+            "workload": desc,
+            "percentile_mode": args.mode,
+            "cpu_percentile": args.percentile,
+            "memory_buffer": "max x 1.05 (exact decimal, host)",
+            "containers": containers_total,
+            "slots_per_rank": 2 * N,
+            "parallelism": f"shard{world} (contiguous container ranges, RCCL gather of 32-B records)",
+        },
+        "samples_per_s": 2 * N * world / step_s,
+        "hbm_frac_step": step_bytes_all / step_s / (HBM_PEAK * world),
+        "kernels_ms": {"percentile": pct_ms, "max": max_ms},
+        "roofline": {
+            "kernel": "k_select" if args.mode != "ref_index" else ("k_refindex_gaps" if gaps else "k_refindex_dense"),
+            "bound": "hbm",
+            "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": pct_bytes,
+        },
+    }
+    if args.mode == "ref_index" and not gaps:
+        result["roofline"]["note"] = "compact REF_INDEX is one gather per segment: bytes count every slot anyway"
+    # PMC-measured HBM bytes per launch of the same kernel/workload (profiles/pmc_traffic.json)
+    try:
+        with open(args.traffic) as fh:
+            tr = json.load(fh)
+        key = f"config{args.config}:{args.mode}:{result['roofline']['kernel']}"
+        if key in tr and int(tr[key].get("containers_per_rank", -1)) == S:
+            result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
+            result["roofline"]["traffic_source"] = tr[key].get("source")
+    except (OSError, ValueError):
+        pass
+
+    # parity of this very run on a sample + the CPU baseline (rank 0, N = 1 only)
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        from oracle import oracle
+
+        m = max(1, min(args.cpu_sample, S))
+        end = int(offs_np[m])
+        c_host = cpu[:end].cpu().numpy()
+        m_host = mem[:end].cpu().numpy()
+        o_host = offs_np[: m + 1].copy()
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t_a = time.perf_counter()
+        ov, on, of = oracle.percentile(c_host, o_host, params.mode, params.p_num, params.p_den, params.q, gaps,
+                                       threads)
+        mv, mn, mf = oracle.seg_max(m_host, o_host, gaps, threads)
+        t_b = time.perf_counter()
+        gv = out["cpu_value"][:m].cpu().numpy()
+        same = (gv.view(np.uint64) == ov.view(np.uint64)) | (np.isnan(gv) & np.isnan(ov))
+        if args.mode == "linear":
+            same |= (gv == 0) & (ov == 0)
+        parity = bool(same.all() and np.array_equal(out["cpu_count"][:m].cpu().numpy(), on)
+                      and np.array_equal(out["mem_value"][:m].cpu().numpy(), mv, equal_nan=True)
+                      and np.array_equal(out["mem_count"][:m].cpu().numpy(), mn))
+        cpu_model = ""
+        try:
+            with open("/proc/cpuinfo") as fh:
+                cpu_model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+        except OSError:
+            pass
+        result["cpu_baseline"] = {
+            "value": m / (t_b - t_a),
+            "unit": "container-series/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"first {m} containers of this run ({2 * end} slots) copied D2H; oracle/krr_oracle.c "
+                      f"{args.mode} + max, OpenMP {threads} threads on {cpu_model or platform.processor()}",
+        }
+        result["parity_vs_oracle_on_sample"] = parity
+        # the reference's own CPU path, measured in the build container only (cannot travel):
+        result["reference_cpu_measured_in_build_container"] = {
+            "value": 492.0, "unit": "container-series/s", "cores": 1,
+            "source": "BASELINE.md (SimpleStrategy.run + _format_result, config 1)"}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
