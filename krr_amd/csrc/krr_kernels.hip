@@ -25,14 +25,30 @@
 #include "krr_device.h"
 #include "krr_plan.h"
 
+#ifndef KRR_STREAM_DEPTH
+#define KRR_STREAM_DEPTH 3  // chunks in flight per wave
+#endif
+#ifndef KRR_SELECT_WAVES_PER_SIMD
+#define KRR_SELECT_WAVES_PER_SIMD 2  // __launch_bounds__ occupancy hint for k_select
+#endif
+
 namespace krr {
 
 // ---------------------------------------------------------------------------
-// Streaming skeleton: one wave walks values[beg, end) with 16-byte loads,
-// U double2 per lane per chunk, next chunk prefetched while this one is
-// processed.  proc.prepare(k) is called wave-uniformly before a batch that
-// may append up to k candidates; proc.elem(bits, in_range) once per element.
+// Streaming skeleton.  One wave walks values[beg, end): the 16-byte aligned
+// body in chunks of kUnroll x 16 B per lane (8 KiB per wave), three chunks in
+// flight; the unaligned head/tail elements and the partial last chunk go
+// through ONE guarded chunk call (the partial chunk never fills its last slot,
+// so the head and tail elements ride in it).  A processor implements
+//   template <bool GUARD> void chunk(const double2 (&c)[kUnroll], uint32_t vmask)
+// where, with GUARD, bit (2u + h) of vmask says slot c[u].x (h=0) / .y (h=1)
+// of this lane holds a sample.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_chunk(double2 (&c)[kUnroll], const double2* __restrict__ p) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) c[u] = p[u * kWave];
+}
+
 template <class Proc>
 __device__ __forceinline__ void stream_segment(const double* __restrict__ vals, int64_t beg,
                                                int64_t end, Proc& proc, int lane) {
@@ -40,11 +56,6 @@ __device__ __forceinline__ void stream_segment(const double* __restrict__ vals, 
     if (a0 > end) a0 = end;
     int64_t a1 = end & ~(int64_t)1;
     if (a1 < a0) a1 = a0;
-    if (a0 > beg) {  // one leading element before the 16-byte aligned body
-        proc.prepare(64);
-        uint64_t u = lane == 0 ? dbits(vals[beg]) : 0;
-        proc.elem(u, lane == 0);
-    }
     const double2* __restrict__ v2 = reinterpret_cast<const double2*>(vals);
     const int64_t i0 = a0 >> 1;
     const int64_t nunits = (a1 >> 1) - i0;
@@ -52,48 +63,70 @@ __device__ __forceinline__ void stream_segment(const double* __restrict__ vals, 
     const int64_t nfull = nunits / CH;
     if (nfull > 0) {
         const double2* __restrict__ p = v2 + i0 + lane;
-        double2 cur[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) cur[u] = p[u * kWave];
-        for (int64_t c = 0; c < nfull; ++c) {
-            const int64_t cn = (c + 1 < nfull) ? c + 1 : c;
-            const double2* __restrict__ pn = p + cn * CH;
-            double2 nxt[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) nxt[u] = pn[u * kWave];
-            proc.prepare(2 * CH);
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                proc.elem(dbits(cur[u].x), true);
-                proc.elem(dbits(cur[u].y), true);
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+        const int64_t last = nfull - 1;
+        auto at = [&](int64_t c) { return p + (c < last ? c : last) * CH; };  // clamp: re-read, never overrun
+#if KRR_STREAM_DEPTH == 2
+        double2 b0[kUnroll], b1[kUnroll];
+        load_chunk(b0, at(0));
+        load_chunk(b1, at(1));
+        for (int64_t c = 0; c < nfull; c += 2) {
+            proc.template chunk<false>(b0, 0u);
+            load_chunk(b0, at(c + 2));
+            if (c + 1 < nfull) proc.template chunk<false>(b1, 0u);
+            load_chunk(b1, at(c + 3));
         }
+#else
+        double2 b0[kUnroll], b1[kUnroll], b2[kUnroll];
+        load_chunk(b0, at(0));
+        load_chunk(b1, at(1));
+        load_chunk(b2, at(2));
+        for (int64_t c = 0; c < nfull; c += 3) {
+            proc.template chunk<false>(b0, 0u);
+            load_chunk(b0, at(c + 3));
+            if (c + 1 < nfull) proc.template chunk<false>(b1, 0u);
+            load_chunk(b1, at(c + 4));
+            if (c + 2 < nfull) proc.template chunk<false>(b2, 0u);
+            load_chunk(b2, at(c + 5));
+        }
+#endif
     }
     const int64_t r0 = nfull * CH;
-    if (r0 < nunits) {  // one guarded partial chunk
+    const bool head = a0 > beg, tail = a1 < end;
+    if (r0 < nunits || head || tail) {
         double2 cur[kUnroll];
-        bool inr[kUnroll];
+        uint32_t vmask = 0;
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t j = r0 + u * kWave + lane;
-            inr[u] = j < nunits;
-            cur[u] = inr[u] ? v2[i0 + j] : make_double2(0.0, 0.0);
+            const bool in = j < nunits;
+            cur[u] = in ? v2[i0 + j] : make_double2(0.0, 0.0);
+            vmask |= in ? (3u << (2 * u)) : 0u;
         }
-        proc.prepare(2 * CH);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            proc.elem(dbits(cur[u].x), inr[u]);
-            proc.elem(dbits(cur[u].y), inr[u]);
+        // nunits - r0 < CH, so the last slot (u = kUnroll-1, lane 63) is free
+        if (lane == kWave - 1) {
+            if (head) {
+                cur[kUnroll - 1].x = vals[beg];
+                vmask |= 1u << (2 * (kUnroll - 1));
+            }
+            if (tail) {
+                cur[kUnroll - 1].y = vals[a1];
+                vmask |= 2u << (2 * (kUnroll - 1));
+            }
         }
-    }
-    if (a1 < end) {  // one trailing element
-        proc.prepare(64);
-        uint64_t u = lane == 0 ? dbits(vals[a1]) : 0;
-        proc.elem(u, lane == 0);
+        proc.template chunk<true>(cur, vmask);
     }
 }
+
+template <bool GUARD>
+__device__ __forceinline__ bool slot_in(uint32_t vmask, int j) {
+    return GUARD ? ((vmask >> j) & 1u) != 0 : true;
+}
+
+__device__ __forceinline__ double slot_val(const double2 (&c)[kUnroll], int j) {
+    return (j & 1) ? c[j >> 1].y : c[j >> 1].x;
+}
+
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll((long long)m); }
 
 // ---------------------------------------------------------------------------
 // MSD radix select over M = buf[0..cnt) U {xk repeated xc times}, in LDS or
@@ -103,6 +136,8 @@ __device__ __forceinline__ void stream_segment(const double* __restrict__ vals, 
 // (good enough for a compaction threshold).  The first digit starts at the
 // highest bit where min(M) and max(M) differ, so clustered keys (all samples
 // in one binade) still split on their first level; <= 8 bits per level.
+// Out of line: it is the rare fallback, and inlining it into every chunk call
+// site costs registers and I-cache on the hot path.
 // ---------------------------------------------------------------------------
 struct SelHit {
     uint64_t key;
@@ -111,10 +146,9 @@ struct SelHit {
     uint32_t ok;
 };
 
-__device__ __forceinline__ SelHit select_desc(const uint64_t* buf, uint32_t cnt, uint64_t xk,
-                                              uint32_t xc, uint32_t R, bool early,
-                                              uint64_t floor_key, uint32_t stop,
-                                              uint32_t* hist, int lane) {
+__device__ __noinline__ SelHit select_desc(const uint64_t* buf, uint32_t cnt, uint64_t xk, uint32_t xc,
+                                           uint32_t R, bool early, uint64_t floor_key, uint32_t stop,
+                                           uint32_t* hist, int lane) {
     SelHit out;
     out.ok = 1;
     uint64_t mn = ~0ull, mx = 0;
@@ -196,94 +230,297 @@ __device__ __forceinline__ SelHit select_desc(const uint64_t* buf, uint32_t cnt,
     return out;
 }
 
+// Find the digit bin holding the R-th largest (1-based) of a 256-bin histogram
+// (bins ordered by key), given `above0` elements already known to be larger.
+struct BinHit {
+    uint32_t b;      // bin index
+    uint32_t above;  // elements in higher bins (+ above0)
+    uint32_t cnt;    // elements in bin b
+    uint32_t found;
+};
+
+__device__ __forceinline__ BinHit find_bin_desc(const uint32_t* hist, uint32_t R, uint32_t above0, int lane) {
+    uint32_t hb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hb[j] = hist[4 * lane + j];
+    const uint32_t t = hb[0] + hb[1] + hb[2] + hb[3];
+    const uint32_t incl = wave_suffix_incl(t, lane);
+    uint32_t run = above0 + (incl - t);
+    int fb = -1;
+    uint32_t fab = 0, fcb = 0;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+        if (fb < 0 && run < R && run + hb[j] >= R) {
+            fb = 4 * lane + j;
+            fab = run;
+            fcb = hb[j];
+        }
+        run += hb[j];
+    }
+    const uint64_t m = ballot(fb >= 0);
+    BinHit h;
+    h.found = m != 0;
+    const int src = m ? __ffsll((long long)m) - 1 : 0;
+    h.b = uni32((uint32_t)__shfl(fb, src));
+    h.above = uni32((uint32_t)__shfl((int)fab, src));
+    h.cnt = uni32((uint32_t)__shfl((int)fcb, src));
+    return h;
+}
+
 // ---------------------------------------------------------------------------
 // Threshold-filtered candidate buffer (one wave per segment).
 //
 // Invariant over the present non-NaN samples seen so far, in (possibly
-// flipped) key order:  buf holds exactly those with key > thr, `eq` counts
+// flipped) key order:  buf holds exactly those with key > thr, `eqs` counts
 // those with key == thr, every other one is < thr ("below", implied by n).
-// Whenever a chunk might overflow buf, compact() raises thr so that at least
-// tkeep keys stay >= thr and at most tstop stay > thr; since the segment's
-// needed ranks lie in its top tkeep keys (krr_plan.h), they are never dropped.
+// Before a chunk is inserted, its candidates are COUNTED (classify: a few VALU
+// per sample, no branches, counts via ballot popcounts); if they do not fit,
+// compact() raises thr so that at least tkeep keys stay >= thr and at most
+// tstop = cap - kChunkElems stay > thr, then the chunk is re-classified and
+// always fits.  The segment's needed ranks lie in its top tkeep keys
+// (krr_plan.h), so they are never dropped.
+//
+// Fast path: once thr is a non-negative number t (top side), "key > thr" for a
+// sample with bits x is the single unsigned range test
+//   x - (bits(t)+1) < bits(+inf) - bits(t)
+// which also rejects every NaN and every negative number.
+//
+// H is a 256-bin histogram of buf kept up to date on every insert (bins of
+// width 2^hsh from hbase = thr + 1; bin 255 also takes everything above).  A
+// compaction reads the new threshold off H and needs one filter pass over buf,
+// which rebuilds H for the new range; select_desc is only the fallback when
+// the cut falls into the overflow bin or a crowded bin.  The final rank
+// queries use H the same way: locate the bin, gather its few members, rank
+// them in registers.
 // ---------------------------------------------------------------------------
 struct SelectProc {
     uint64_t* buf;
-    uint32_t* hist;
+    uint32_t* H;      // maintained histogram of buf
+    uint32_t* scr;    // select_desc scratch histogram
+    uint64_t* small;  // 64-key gather area
     int lane;
     uint32_t cap, tkeep, tstop;
     uint64_t flip;
-    int gaps;
     uint64_t thr;
-    uint32_t cnt, eqs;
-    uint32_t nvalid, nanc, eqc;  // per lane
+    uint32_t cnt, eqs, nnan;
+    uint64_t hbase;
+    uint32_t hsh, hvalid;
+    uint32_t fast;              // thr is a non-negative finite number or +0, top side
+    uint64_t tbits, tb1, tlim;  // fast-path constants
+    uint64_t mxk;               // per lane: largest key ever inserted
     uint32_t bad;
 
-    __device__ __forceinline__ void prepare(uint32_t max_new) {
-        if (cnt + max_new > cap) compact();
+    __device__ __forceinline__ void set_thr(uint64_t t) {
+        thr = uni64(t);
+        fast = (!flip && (thr & kSignBit) && (thr ^ kSignBit) <= 0x7FF0000000000000ull) ? 1u : 0u;
+        tbits = thr ^ kSignBit;
+        tb1 = tbits + 1;
+        tlim = 0x7FF0000000000000ull - tbits;
     }
 
-    __device__ __forceinline__ void elem(uint64_t u, bool inr) {
-        const bool nan = is_nan_bits(u);
-        nvalid += (inr && !(gaps && nan)) ? 1u : 0u;
-        nanc += (inr && nan) ? 1u : 0u;
-        const bool ok = inr && !nan;
-        const uint64_t k = okey(u) ^ flip;
-        eqc += (ok && k == thr) ? 1u : 0u;
-        const bool cand = ok && k > thr;
-        const uint64_t m = ballot(cand);
-        if (m) {
-            if (cand) buf[cnt + lane_prefix(m)] = k;
-            cnt = uni32(cnt + (uint32_t)__popcll((long long)m));
+    __device__ __forceinline__ uint32_t bin(uint64_t k) const {
+        const uint64_t d = (k - hbase) >> hsh;
+        return d > 255 ? 255u : (uint32_t)d;
+    }
+
+    template <bool GUARD, bool FAST>
+    __device__ __forceinline__ bool is_cand(double d, uint32_t vmask, int j, uint64_t& key) const {
+        const uint64_t x = dbits(d);
+        if (FAST) {
+            key = x | kSignBit;
+            return slot_in<GUARD>(vmask, j) && (x - tb1) < tlim;
+        }
+        key = okey(x) ^ flip;
+        return slot_in<GUARD>(vmask, j) && !__builtin_isnan(d) && key > thr;
+    }
+
+    // Count this chunk's candidates (C), ties with thr (E) and NaN slots (NN);
+    // jm = bit j set if slot j has a candidate in some lane.
+    template <bool GUARD, bool FAST>
+    __device__ __forceinline__ void classify(const double2 (&c)[kUnroll], uint32_t vmask, uint32_t& C,
+                                             uint32_t& E, uint32_t& NN, uint32_t& jm) const {
+        C = E = NN = jm = 0;
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double d = slot_val(c, j);
+            uint64_t key;
+            const bool cand = is_cand<GUARD, FAST>(d, vmask, j, key);
+            const bool in = slot_in<GUARD>(vmask, j);
+            const bool eq = FAST ? (in && dbits(d) == tbits) : (in && !__builtin_isnan(d) && key == thr);
+            const uint64_t m = ballot(cand);
+            C += popc64(m);
+            jm |= m ? (1u << j) : 0u;
+            E += popc64(ballot(eq));
+            NN += popc64(ballot(in && __builtin_isnan(d)));
         }
     }
 
-    __device__ __forceinline__ void compact() {
+    template <bool GUARD, bool FAST>
+    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], uint32_t vmask, uint32_t jm) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            if ((jm >> j) & 1u) {
+                uint64_t key;
+                const bool cand = is_cand<GUARD, FAST>(slot_val(c, j), vmask, j, key);
+                const uint64_t m = ballot(cand);
+                if (cand) {
+                    buf[cnt + lane_prefix(m)] = key;
+                    mxk = key > mxk ? key : mxk;
+                    if (hvalid) atomicAdd(&H[bin(key)], 1u);
+                }
+                cnt = uni32(cnt + popc64(m));
+            }
+        }
+    }
+
+    template <bool GUARD>
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+        uint32_t C, E, NN, jm;
+        if (fast) classify<GUARD, true>(c, vmask, C, E, NN, jm);
+        else classify<GUARD, false>(c, vmask, C, E, NN, jm);
+        if (cnt + C > cap) {
+            compact();
+            if (fast) classify<GUARD, true>(c, vmask, C, E, NN, jm);
+            else classify<GUARD, false>(c, vmask, C, E, NN, jm);
+            if (cnt + C > cap) {  // compaction failed (flagged): drop, never overrun
+                bad = 1;
+                return;
+            }
+        }
+        eqs += E;
+        nnan += NN;
+        if (jm) {
+            if (fast) insert<GUARD, true>(c, vmask, jm);
+            else insert<GUARD, false>(c, vmask, jm);
+        }
+    }
+
+    // Raise thr to nt and filter buf to keys > nt (counting keys == nt into eqs),
+    // rebuilding H over (nt, mx].
+    __device__ __forceinline__ void filter_rebuild(uint64_t nt, uint64_t mx) {
+        hbase = uni64(nt + 1);
+        const uint64_t range = mx > nt ? mx - hbase : 0ull;
+        const int bits = range ? 64 - __clzll((long long)range) : 0;
+        hsh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
+        for (uint32_t i = lane; i < 256; i += kWave) H[i] = 0;
         __syncthreads();
-        const uint32_t eqt = uni32(eqs + wave_sum_u32(eqc));
-        eqc = 0;
-        SelHit hit = select_desc(buf, cnt, thr, eqt, tkeep, true, thr, tstop, hist, lane);
-        uint64_t nt = hit.key;
-        if (!hit.ok || nt <= thr) {  // cannot happen while cnt > tstop; keep going, flag it
-            bad = 1;
-            eqs = eqt;
-            return;
-        }
         uint32_t w = 0, e = 0;
         for (uint32_t base = 0; base < cnt; base += kWave) {
             const uint32_t i = base + lane;
             const bool in = i < cnt;
             const uint64_t x = in ? buf[i] : 0ull;
             const bool keep = in && x > nt;
-            e += (in && x == nt) ? 1u : 0u;
+            e += popc64(ballot(in && x == nt));
             const uint64_t m = ballot(keep);
-            if (keep) buf[w + lane_prefix(m)] = x;
-            w += (uint32_t)__popcll((long long)m);
+            if (keep) {
+                buf[w + lane_prefix(m)] = x;
+                atomicAdd(&H[bin(x)], 1u);
+            }
+            w += popc64(m);
         }
         cnt = uni32(w);
-        eqs = wave_sum_u32(e);
-        thr = uni64(nt);
+        eqs = uni32(e);
+        hvalid = 1;
+        set_thr(nt);
+    }
+
+    __device__ __forceinline__ void compact() {
+        __syncthreads();
+        uint64_t nt = 0;
+        bool have = false;
+        if (hvalid) {
+            const BinHit bh = find_bin_desc(H, tkeep, 0, lane);
+            if (bh.found && bh.b < 255 && bh.above + bh.cnt <= tstop) {
+                nt = uni64(hbase + ((uint64_t)bh.b << hsh));  // >= hbase > thr
+                have = true;
+            }
+        }
+        if (!have) {
+            const SelHit hit = select_desc(buf, cnt, thr, eqs, tkeep, true, thr, tstop, scr, lane);
+            nt = uni64(hit.key);
+            if (!hit.ok || nt <= thr) {  // cannot happen while cnt > tstop; flag it
+                bad = 1;
+                return;
+            }
+        }
+        filter_rebuild(nt, wave_max_u64(mxk));
         __syncthreads();
     }
 
+    // The R-th largest key (1-based) of buf.
+    __device__ __forceinline__ uint64_t kth_largest(uint32_t R) {
+        if (hvalid) {
+            const BinHit bh = find_bin_desc(H, R, 0, lane);
+            if (bh.found && bh.b < 255 && bh.cnt <= kWave) {
+                const uint64_t lo = hbase + ((uint64_t)bh.b << hsh);
+                const uint64_t hi = lo + ((1ull << hsh) - 1);
+                uint32_t w = 0;
+                for (uint32_t base = 0; base < cnt; base += kWave) {
+                    const uint32_t i = base + lane;
+                    const bool in = i < cnt;
+                    const uint64_t x = in ? buf[i] : 0ull;
+                    const bool inb = in && x >= lo && x <= hi;
+                    const uint64_t m = ballot(inb);
+                    if (inb) small[w + lane_prefix(m)] = x;
+                    w += popc64(m);
+                }
+                __syncthreads();
+                const uint32_t R2 = R - bh.above;
+                const uint64_t v = (uint32_t)lane < w ? small[lane] : 0ull;
+                uint32_t gt = 0, ge = 0;
+                for (uint32_t j = 0; j < w; ++j) {
+                    const uint64_t y = small[j];
+                    gt += y > v ? 1u : 0u;
+                    ge += y >= v ? 1u : 0u;
+                }
+                const uint64_t sel = ballot((uint32_t)lane < w && gt < R2 && R2 <= ge);
+                __syncthreads();
+                if (sel) return uni64((uint64_t)__shfl((unsigned long long)v, __ffsll((long long)sel) - 1));
+                bad = 1;
+            }
+        }
+        const SelHit h = select_desc(buf, cnt, 0, 0, R, false, 0, 0, scr, lane);
+        if (!h.ok) bad = 1;
+        return h.key;
+    }
+
+    // Build H over the whole buffer (once at the end when no compaction ran).
+    __device__ __forceinline__ void build_hist() {
+        uint64_t mn = ~0ull, mx = 0;
+        for (uint32_t i = lane; i < cnt; i += kWave) {
+            const uint64_t x = buf[i];
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
+        mn = wave_min_u64(mn);
+        mx = wave_max_u64(mx);
+        hbase = mn;
+        const uint64_t range = mx - mn;
+        const int bits = range ? 64 - __clzll((long long)range) : 0;
+        hsh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
+        for (uint32_t i = lane; i < 256; i += kWave) H[i] = 0;
+        __syncthreads();
+        for (uint32_t i = lane; i < cnt; i += kWave) atomicAdd(&H[bin(buf[i])], 1u);
+        __syncthreads();
+        hvalid = 1;
+    }
+
     // Key of the element with ascending rank r (0-based) among nsel present samples.
-    __device__ uint64_t rank_key(uint64_t r, uint64_t nsel, uint64_t eqt) {
+    __device__ __forceinline__ uint64_t rank_key(uint64_t r, uint64_t nsel) {
         const uint64_t rr = flip ? (nsel - 1 - r) : r;
-        const uint64_t below = nsel - cnt - eqt;
+        const uint64_t below = nsel - cnt - eqs;
         if (rr < below) {
             bad = 1;
             return 0;
         }
-        if (rr < below + eqt) return thr;
-        const uint32_t idx = (uint32_t)(rr - below - eqt);
-        SelHit h = select_desc(buf, cnt, 0, 0, cnt - idx, false, 0, 0, hist, lane);
-        if (!h.ok) bad = 1;
-        return h.key;
+        if (rr < below + eqs) return thr;
+        const uint32_t idx = (uint32_t)(rr - below - eqs);
+        return kth_largest(cnt - idx);
     }
 };
 
 // Count present, numerically negative samples (x < -0.0) of [beg, end).
-__device__ uint64_t count_negative(const double* __restrict__ vals, int64_t beg, int64_t end,
-                                   int lane) {
+__device__ uint64_t count_negative(const double* __restrict__ vals, int64_t beg, int64_t end, int lane) {
     uint32_t c = 0;
     for (int64_t base = beg; base < end; base += kWave) {
         const int64_t i = base + lane;
@@ -296,8 +533,8 @@ __device__ uint64_t count_negative(const double* __restrict__ vals, int64_t beg,
 }
 
 // Bits of the j-th (0-based, position order) sample equal to +-0.0 in [beg, end).
-__device__ uint64_t nth_zero_bits(const double* __restrict__ vals, int64_t beg, int64_t end,
-                                  uint64_t j, int lane) {
+__device__ uint64_t nth_zero_bits(const double* __restrict__ vals, int64_t beg, int64_t end, uint64_t j,
+                                  int lane) {
     uint64_t run = 0;
     for (int64_t base = beg; base < end; base += kWave) {
         const int64_t i = base + lane;
@@ -305,7 +542,7 @@ __device__ uint64_t nth_zero_bits(const double* __restrict__ vals, int64_t beg, 
         const uint64_t u = in ? dbits(vals[i]) : 1ull;
         const bool z = in && is_zero_bits(u);
         const uint64_t m = ballot(z);
-        const uint32_t c = (uint32_t)__popcll((long long)m);
+        const uint32_t c = popc64(m);
         if (run + c > j) {
             const uint32_t want = (uint32_t)(j - run);
             const uint64_t sel = ballot(z && lane_prefix(m) == want);
@@ -340,11 +577,19 @@ struct SelectArgs {
     uint32_t* out_f;
 };
 
-__global__ __launch_bounds__(64) void k_select(SelectArgs A) {
+// GBUF selects where candidate buffers live at COMPILE time, so the LDS variant
+// emits ds_* (lgkmcnt) and never flat_* stores, which would force vmcnt(0)
+// waits and serialise the prefetch pipeline.
+template <bool GBUF>
+__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
+    // LDS: [H 1 KiB][select scratch 1 KiB][gather 512 B][candidate keys cap x 8 B]
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* hist = reinterpret_cast<uint32_t*>(smem);  // 256 x u32
-    uint64_t* buf = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.cap
-                               : reinterpret_cast<uint64_t*>(smem + 1024);
+    uint64_t* buf;
+    if constexpr (GBUF) {
+        buf = A.gscratch + (size_t)blockIdx.x * A.cap;
+    } else {
+        buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+    }
     const int lane = threadIdx.x;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
@@ -352,26 +597,29 @@ __global__ __launch_bounds__(64) void k_select(SelectArgs A) {
         const SidePlan sp = plan_side(L, A.mode, A.p_num, A.p_den, A.q);
         SelectProc P;
         P.buf = buf;
-        P.hist = hist;
+        P.H = reinterpret_cast<uint32_t*>(smem);
+        P.scr = reinterpret_cast<uint32_t*>(smem + 1024);
+        P.small = reinterpret_cast<uint64_t*>(smem + 2048);
         P.lane = lane;
         P.cap = A.cap;
         P.tkeep = sp.tkeep;
-        P.tstop = sp.tkeep + (A.cap - kChunkElems - sp.tkeep) / 2;
+        P.tstop = A.cap - kChunkElems;
         P.flip = sp.bottom ? ~0ull : 0ull;
-        P.gaps = A.gaps;
-        P.thr = 0;
         P.cnt = 0;
         P.eqs = 0;
-        P.nvalid = 0;
-        P.nanc = 0;
-        P.eqc = 0;
+        P.nnan = 0;
         P.bad = 0;
+        P.hbase = 0;
+        P.hsh = 0;
+        P.hvalid = 0;
+        P.mxk = 0;
+        P.set_thr(0);
         stream_segment(A.vals, beg, end, P, lane);
         __syncthreads();
+        if (!P.hvalid && P.cnt > kWave) P.build_hist();
 
-        const uint64_t n = wave_sum_u32(P.nvalid);
-        const uint64_t nnan = wave_sum_u32(P.nanc);
-        const uint64_t eqt = P.eqs + wave_sum_u32(P.eqc);
+        const uint64_t nnan = P.nnan;
+        const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
         uint32_t flags = 0;
         double result;
         if (n == 0) {
@@ -382,7 +630,7 @@ __global__ __launch_bounds__(64) void k_select(SelectArgs A) {
             flags |= KRR_FLAG_NAN;
         } else if (A.mode == KRR_PCT_SORTED_LOWER) {
             const int64_t r = exact_rank(n, A.p_num, A.p_den);
-            uint64_t bits = okey_inv(P.rank_key(r, n, eqt) ^ P.flip);
+            uint64_t bits = okey_inv(P.rank_key(r, n) ^ P.flip);
             if (is_zero_bits(bits)) {
                 // Python sorted() is stable and -0 == +0: the zero at rank r is the
                 // (r - #negatives)-th zero in position order.
@@ -403,8 +651,8 @@ __global__ __launch_bounds__(64) void k_select(SelectArgs A) {
                 next = prev + 1;
                 gamma = __dsub_rn(vidx, fl);
             }
-            const double a = bitsd(okey_inv(P.rank_key(prev, n, eqt) ^ P.flip));
-            const double b = (next == prev) ? a : bitsd(okey_inv(P.rank_key(next, n, eqt) ^ P.flip));
+            const double a = bitsd(okey_inv(P.rank_key(prev, n) ^ P.flip));
+            const double b = (next == prev) ? a : bitsd(okey_inv(P.rank_key(next, n) ^ P.flip));
             result = np_lerp(a, b, gamma);
         }
         if (P.bad) flags |= KRR_FLAG_CAPACITY;
@@ -418,10 +666,14 @@ __global__ __launch_bounds__(64) void k_select(SelectArgs A) {
 }
 
 // --------------------------- REF_INDEX ------------------------------------
-struct CountProc {
-    uint32_t n;
-    __device__ __forceinline__ void prepare(uint32_t) {}
-    __device__ __forceinline__ void elem(uint64_t u, bool inr) { n += (inr && !is_nan_bits(u)) ? 1u : 0u; }
+struct NanCountProc {
+    uint32_t nn;
+    template <bool GUARD>
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j)
+            nn += popc64(ballot(slot_in<GUARD>(vmask, j) && __builtin_isnan(slot_val(c, j))));
+    }
 };
 
 struct RefArgs {
@@ -439,9 +691,9 @@ __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
     const int lane = threadIdx.x;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
-        CountProc C{0};
+        NanCountProc C{0};
         stream_segment(A.vals, beg, end, C, lane);
-        const uint64_t n = wave_sum_u32(C.n);
+        const uint64_t n = (uint64_t)(end - beg) - C.nn;
         double result = bitsd(kQuietNaN);
         uint32_t flags = 0;
         if (n == 0) {
@@ -458,7 +710,7 @@ __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
                     const uint64_t u = in ? dbits(A.vals[i]) : kQuietNaN;
                     const bool p = in && !is_nan_bits(u);
                     const uint64_t m = ballot(p);
-                    const uint32_t c = (uint32_t)__popcll((long long)m);
+                    const uint32_t c = popc64(m);
                     if (run + c > j) {
                         const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(j - run));
                         found = uni64((uint64_t)__shfl((unsigned long long)u, __ffsll((long long)sel) - 1));
@@ -473,7 +725,7 @@ __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
                     const uint64_t u = in ? dbits(A.vals[i]) : kQuietNaN;
                     const bool p = in && !is_nan_bits(u);
                     const uint64_t m = ballot(p);
-                    const uint32_t c = (uint32_t)__popcll((long long)m);
+                    const uint32_t c = popc64(m);
                     if (run + c > k) {
                         const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(k - run));
                         found = uni64((uint64_t)__shfl((unsigned long long)u, __ffsll((long long)sel) - 1));
@@ -511,19 +763,28 @@ __global__ __launch_bounds__(256) void k_refindex_dense(RefArgs A) {
 }
 
 // ------------------------------- MAX --------------------------------------
+// v_max_f64 returns the non-NaN operand, so NaN slots (gaps or padding) drop
+// out of the running max for free; one VALU per sample plus one NaN test.
 struct MaxProc {
-    uint32_t nvalid, nanc;
-    uint64_t mk;
-    int gaps;
-    __device__ __forceinline__ void prepare(uint32_t) {}
-    __device__ __forceinline__ void elem(uint64_t u, bool inr) {
-        const bool nan = is_nan_bits(u);
-        nvalid += (inr && !(gaps && nan)) ? 1u : 0u;
-        nanc += (inr && nan) ? 1u : 0u;
-        const uint64_t k = (inr && !nan) ? okey(u) : 0ull;
-        mk = k > mk ? k : mk;
+    double mx;
+    uint32_t nn;
+    template <bool GUARD>
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double d = slot_val(c, j);
+            const bool in = slot_in<GUARD>(vmask, j);
+            mx = fmax(mx, in ? d : __builtin_nan(""));
+            nn += popc64(ballot(in && __builtin_isnan(d)));
+        }
     }
 };
+
+__device__ __forceinline__ double wave_max_f64(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
+    return x;
+}
 
 struct MaxArgs {
     const double* vals;
@@ -539,19 +800,19 @@ __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
     const int lane = threadIdx.x;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
-        MaxProc M{0, 0, 0ull, A.gaps};
+        MaxProc M{__builtin_nan(""), 0u};
         stream_segment(A.vals, beg, end, M, lane);
-        const uint64_t n = wave_sum_u32(M.nvalid);
-        const uint64_t nnan = wave_sum_u32(M.nanc);
-        const uint64_t mk = wave_max_u64(M.mk);
+        const uint64_t L = (uint64_t)(end - beg);
+        const uint64_t n = A.gaps ? L - M.nn : L;
+        const double mx = wave_max_f64(M.mx);
         double result = bitsd(kQuietNaN);
         uint32_t flags = 0;
         if (n == 0) {
             flags = KRR_FLAG_EMPTY;
-        } else if (nnan && !A.gaps) {
+        } else if (M.nn && !A.gaps) {
             flags = KRR_FLAG_NAN;
         } else {
-            uint64_t bits = okey_inv(mk);
+            uint64_t bits = uni64(dbits(mx));
             // Python max() keeps the FIRST maximal element; only +-0 compare equal
             // with different bits.
             if (is_zero_bits(bits)) bits = nth_zero_bits(A.vals, beg, end, 0, lane);
@@ -748,7 +1009,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
         delete c;
         return KRR_E_HIP;
     }
-    (void)hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -809,9 +1070,9 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
     A.out_v = out_value;
     A.out_n = out_count;
     A.out_f = out_flags;
-    const size_t lds = 1024 + (size_t)cap * 8;
+    const size_t lds = kSelectLdsFixed + (size_t)cap * 8;
     if (lds <= ctx->max_lds) {
-        hipLaunchKernelGGL(k_select, dim3(grid_for(S)), dim3(64), lds, st, A);
+        hipLaunchKernelGGL(k_select<false>, dim3(grid_for(S)), dim3(64), lds, st, A);
     } else {
         // Candidate buffers too large for LDS (e.g. p near 50 on very long series):
         // same algorithm with per-block buffers in HBM scratch, persistent grid.
@@ -826,7 +1087,7 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
             ctx->scratch_bytes = need;
         }
         A.gscratch = ctx->scratch;
-        hipLaunchKernelGGL(k_select, dim3((unsigned)grid), dim3(64), 1024, st, A);
+        hipLaunchKernelGGL(k_select<true>, dim3((unsigned)grid), dim3(64), kSelectLdsFixed, st, A);
     }
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;

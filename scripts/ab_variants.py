@@ -1,0 +1,109 @@
+"""A/B timing of libkrr_amd build variants in ONE process (interleaved rounds).
+
+Each variant is a separately built .so (different -D flags); all are loaded side by
+side with ctypes and fed the same device-resident synthetic workload.
+usage: python scripts/ab_variants.py lib1.so lib2.so ... [--mode linear] [--rounds 5]
+"""
+import argparse
+import ctypes
+import os
+import sys
+from decimal import Decimal
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--mode", default="linear")
+    ap.add_argument("--percentile", default="99")
+    ap.add_argument("--containers", type=int, default=10000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+    from oracle import oracle
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.init()
+    base = _native.load_library()
+    libs = []
+    for path in a.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        for name in ("krr_create", "krr_segmented_percentile", "krr_segmented_max", "krr_synth_fill"):
+            getattr(lib, name).argtypes = getattr(base, name).argtypes
+            getattr(lib, name).restype = ctypes.c_int
+        h = ctypes.c_void_p()
+        assert lib.krr_create(0, ctypes.byref(h)) == 0
+        libs.append((os.path.basename(path), lib, h))
+    n = a.containers
+    if a.config == 2:
+        L, pod_len, gaps = 5 * 10080, 10080, True
+        offs_np = np.arange(n + 1, dtype=np.int64) * L
+    else:
+        rng = np.random.default_rng(3)
+        offs_np = np.concatenate([[0], np.cumsum(rng.integers(1, 15, size=n) * 1440)]).astype(np.int64)
+        pod_len, gaps = 0, False
+    offs = torch.from_numpy(offs_np).to(dev)
+    N = int(offs_np[-1])
+    cpu = torch.empty(N, dtype=torch.float64, device=dev)
+    mem = torch.empty(N, dtype=torch.float64, device=dev)
+    ctx = _native.Context(0)
+    ctx.synth_fill(cpu, offs, 7, 0, pod_len, gaps)
+    ctx.synth_fill(mem, offs, 8, 1, pod_len, gaps)
+    maxlen = int(np.max(np.diff(offs_np)))
+    cs = ctx.series(cpu, offs, maxlen, gaps)
+    ms = ctx.series(mem, offs, maxlen, gaps)
+    params = percentile_params(Decimal(a.percentile), a.mode)
+    S = n
+    outs = {}
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    times = {name: {"pct": [], "max": []} for name, _, _ in libs}
+    for r in range(a.rounds):
+        for name, lib, h in libs:
+            ov = torch.empty(S, dtype=torch.float64, device=dev)
+            on = torch.empty(S, dtype=torch.int64, device=dev)
+            of = torch.empty(S, dtype=torch.int32, device=dev)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(stream)
+            rc = lib.krr_segmented_percentile(h, ctypes.byref(cs), ctypes.byref(params), ov.data_ptr(),
+                                              on.data_ptr(), of.data_ptr(), sp)
+            e[1].record(stream)
+            rc |= lib.krr_segmented_max(h, ctypes.byref(ms), ov.data_ptr() if False else torch.empty(
+                S, dtype=torch.float64, device=dev).data_ptr(), on.data_ptr(), of.data_ptr(), sp)
+            e[2].record(stream)
+            torch.cuda.synchronize()
+            assert rc == 0
+            times[name]["pct"].append(e[0].elapsed_time(e[1]))
+            times[name]["max"].append(e[1].elapsed_time(e[2]))
+            if r == 0:
+                # percentile outputs are overwritten by the count of max? keep a separate check run
+                ov2 = torch.empty(S, dtype=torch.float64, device=dev)
+                lib.krr_segmented_percentile(h, ctypes.byref(cs), ctypes.byref(params), ov2.data_ptr(),
+                                             on.data_ptr(), of.data_ptr(), sp)
+                torch.cuda.synchronize()
+                outs[name] = ov2.cpu().numpy()
+    # parity on a sample vs the oracle
+    m = min(200, S)
+    end = int(offs_np[m])
+    ov, _, _ = oracle.percentile(cpu[:end].cpu().numpy(), offs_np[: m + 1], params.mode, params.p_num,
+                                 params.p_den, params.q, gaps, 16)
+    bytes_pct = 8 * N + 8 * (S + 1) + 20 * S
+    for name, _, _ in libs:
+        t = np.array(times[name]["pct"])
+        tm = np.array(times[name]["max"])
+        got = outs[name][:m]
+        ok = bool(np.all((got.view(np.uint64) == ov.view(np.uint64)) | ((got == 0) & (ov == 0))))
+        print(f"{name:28s} pct median {np.median(t):.4f} ms min {t.min():.4f} -> {bytes_pct / np.median(t) / 1e9:.0f} GB/s"
+              f" | max median {np.median(tm):.4f} ms | parity {ok}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+"""Minimal driver for rocprofv3 passes: generate one workload on the device, then
+run the percentile and max kernels `--reps` times (nothing else on the GPU)."""
+import argparse
+import os
+import sys
+from decimal import Decimal
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="linear")
+    ap.add_argument("--percentile", default="99")
+    ap.add_argument("--containers", type=int, default=10000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+
+    dev = torch.device("cuda", 0)
+    ctx = _native.Context(0)
+    n = a.containers
+    if a.config == 2:
+        L, pod_len, gaps = 5 * 10080, 10080, True
+        offs_np = np.arange(n + 1, dtype=np.int64) * L
+    else:
+        rng = np.random.default_rng(3)
+        Ls = rng.integers(1, 15, size=n) * 1440
+        offs_np = np.concatenate([[0], np.cumsum(Ls)]).astype(np.int64)
+        pod_len, gaps = 0, False
+    offs = torch.from_numpy(offs_np).to(dev)
+    N = int(offs_np[-1])
+    cpu = torch.empty(N, dtype=torch.float64, device=dev)
+    mem = torch.empty(N, dtype=torch.float64, device=dev)
+    ctx.synth_fill(cpu, offs, 7, 0, pod_len, gaps)
+    ctx.synth_fill(mem, offs, 8, 1, pod_len, gaps)
+    S = n
+    maxlen = int(np.max(np.diff(offs_np)))
+    cs = ctx.series(cpu, offs, maxlen, gaps)
+    ms = ctx.series(mem, offs, maxlen, gaps)
+    ov = torch.empty(S, dtype=torch.float64, device=dev)
+    on = torch.empty(S, dtype=torch.int64, device=dev)
+    of = torch.empty(S, dtype=torch.int32, device=dev)
+    params = percentile_params(Decimal(a.percentile), a.mode)
+    for _ in range(a.reps):
+        ctx.segmented_percentile(cs, params, ov, on, of)
+        ctx.segmented_max(ms, ov, on, of)
+    torch.cuda.synchronize()
+    print("done", S, N)
+
+
+if __name__ == "__main__":
+    main()

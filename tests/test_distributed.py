@@ -1,0 +1,110 @@
+"""Multi-rank path on CPU: sharding + RCCL-style result gather, world_size 2 over gloo.
+
+The per-rank compute is stood in for by the CPU oracle (test infrastructure);
+what is under test is shard_bounds / pack_records / gather_records /
+unpack_records — the N > 1 path bench.py runs over RCCL on the GPU box.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from krr_amd.core.distributed import gather_records, pack_records, shard_bounds, unpack_records
+from oracle import oracle
+
+
+def test_shard_bounds_cover_and_balance():
+    rng = np.random.default_rng(0)
+    w = rng.integers(0, 20000, size=1001)
+    for world in (1, 2, 3, 8, 16):
+        b = shard_bounds(w, world)
+        assert b[0][0] == 0 and b[-1][1] == w.size
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        loads = [int(w[lo:hi].sum()) for lo, hi in b]
+        assert max(loads) - min(loads) <= 2 * int(w.max()) + 1
+    assert shard_bounds([], 4) == [(0, 0)] * 4
+    assert shard_bounds([0, 0, 0, 0], 2) == [(0, 2), (2, 4)]
+
+
+def _fleet(seed=1):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, size=57)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    cpu = rng.gamma(2.0, 0.05, size=int(offs[-1]))
+    mem = np.floor(rng.normal(2e8, 2e7, size=int(offs[-1])))
+    return offs, cpu, mem
+
+
+def _compute(offs, cpu, mem, lo, hi):
+    o = offs[lo:hi + 1] - offs[lo]
+    c = cpu[offs[lo]:offs[hi]]
+    m = mem[offs[lo]:offs[hi]]
+    cv, cn, cf = oracle.percentile(c, o, 2, 99, 1, 0.99)
+    mv, mn, mf = oracle.seg_max(m, o)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dt)
+    return {"cpu_value": t(cv, torch.float64), "cpu_count": t(cn, torch.int64),
+            "cpu_flags": t(cf.astype(np.int32), torch.int32), "mem_value": t(mv, torch.float64),
+            "mem_count": t(mn, torch.int64), "mem_flags": t(mf.astype(np.int32), torch.int32)}
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        offs, cpu, mem = _fleet()
+        lo, hi = shard_bounds(np.diff(offs), world)[rank]
+        rec = pack_records(_compute(offs, cpu, mem, lo, hi))
+        out = gather_records(rec, dst=0)
+        if rank == 0:
+            q.put(unpack_records(out))
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_reassembles_fleet_in_order(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    offs, cpu, mem = _fleet()
+    want = _compute(offs, cpu, mem, 0, offs.size - 1)
+    for k, v in want.items():
+        w = v.numpy()
+        g = got[k]
+        if w.dtype == np.float64:
+            assert np.array_equal(g.view(np.uint64), w.view(np.uint64)) or np.array_equal(g, w, equal_nan=True), k
+        else:
+            assert np.array_equal(g.astype(np.int64), w.astype(np.int64)), k
+
+
+def test_record_roundtrip_keeps_bits_and_flags():
+    d = {"cpu_value": torch.tensor([float("nan"), -0.0, 1.5], dtype=torch.float64),
+         "cpu_count": torch.tensor([0, 3, 2**40], dtype=torch.int64),
+         "cpu_flags": torch.tensor([4, 0, 1], dtype=torch.int32),
+         "mem_value": torch.tensor([2e8, float("inf"), 0.0], dtype=torch.float64),
+         "mem_count": torch.tensor([1, 2, 3], dtype=torch.int64),
+         "mem_flags": torch.tensor([0, 2, 4], dtype=torch.int32)}
+    u = unpack_records(pack_records(d))
+    assert np.signbit(u["cpu_value"][1]) and np.isnan(u["cpu_value"][0])
+    assert u["cpu_count"].tolist() == [0, 3, 2**40] and u["cpu_flags"].tolist() == [4, 0, 1]
+    assert u["mem_flags"].tolist() == [0, 2, 4] and np.isinf(u["mem_value"][1])
