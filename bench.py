@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=400, help="containers in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--separate", action="store_true", help="two launches (percentile, max) instead of the fused one")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -121,10 +122,15 @@ def main():
     def step(events=None):
         if events is not None:
             events[0].record(stream)
-        ctx.segmented_percentile(cs, params, out["cpu_value"], out["cpu_count"], out["cpu_flags"], stream)
-        if events is not None:
-            events[1].record(stream)
-        ctx.segmented_max(ms, out["mem_value"], out["mem_count"], out["mem_flags"], stream)
+        if args.separate:
+            ctx.segmented_percentile(cs, params, out["cpu_value"], out["cpu_count"], out["cpu_flags"], stream)
+            if events is not None:
+                events[1].record(stream)
+            ctx.segmented_max(ms, out["mem_value"], out["mem_count"], out["mem_flags"], stream)
+        else:  # one fused launch: CPU percentile + memory max for every container
+            ctx.simple_run(cs, ms, params, out, stream)
+            if events is not None:
+                events[1].record(stream)
         if events is not None:
             events[2].record(stream)
         rec = pack_records(out)
@@ -151,14 +157,21 @@ def main():
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())
-    pct_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    max_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
-    # algorithmic bytes per launch (DESIGN.md §Roofline): every stored slot once, offsets, outputs
-    pct_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S
-    max_bytes = pct_bytes
-    achieved = pct_bytes / (pct_ms * 1e-3)
-    step_bytes_all = (pct_bytes + max_bytes) * world
+    # algorithmic bytes per launch (DESIGN.md §2): every stored slot once, offsets, outputs
+    seg_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S  # one resource
+    if args.separate:
+        kname = "k_select" if args.mode != "ref_index" else ("k_refindex_gaps" if gaps else "k_refindex_dense")
+        kbytes, kms = seg_bytes, k1_ms
+        kernels = {kname: k1_ms, "k_max": k2_ms}
+    else:
+        kname = "k_simple" if not (args.mode == "ref_index" and not gaps) else "k_refindex_dense+k_max"
+        kbytes, kms = 2 * seg_bytes, k1_ms
+        kernels = {kname: k1_ms}
+    achieved = kbytes / (kms * 1e-3)
+    step_bytes_all = 2 * seg_bytes * world
     result = {
         "metric": METRIC,
         "value": containers_total / step_s,
@@ -183,16 +196,16 @@ def main():
         },
         "samples_per_s": 2 * N * world / step_s,
         "hbm_frac_step": step_bytes_all / step_s / (HBM_PEAK * world),
-        "kernels_ms": {"percentile": pct_ms, "max": max_ms},
+        "kernels_ms": kernels,
         "roofline": {
-            "kernel": "k_select" if args.mode != "ref_index" else ("k_refindex_gaps" if gaps else "k_refindex_dense"),
+            "kernel": kname,
             "bound": "hbm",
             "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
             "traffic": None,
-            "algorithmic_bytes_per_launch": pct_bytes,
+            "algorithmic_bytes_per_launch": kbytes,
         },
     }
     if args.mode == "ref_index" and not gaps:

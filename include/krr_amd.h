@@ -73,6 +73,7 @@ typedef enum {
                                  reference raises decimal.InvalidOperation for max()
                                  and sorted(); numpy returns NaN */
 #define KRR_FLAG_CAPACITY 2u  /* internal selection bound violated (never expected) */
+/* bits 8..15 of a KRR_FLAG_CAPACITY result carry an internal reason code (diagnostic) */
 #define KRR_FLAG_EMPTY 4u     /* n == 0: value is NaN (reference: Decimal('NaN'),
                                  simple.py:26-27 and 33-34) */
 

@@ -26,32 +26,48 @@
 #include "krr_plan.h"
 
 #ifndef KRR_STREAM_DEPTH
-#define KRR_STREAM_DEPTH 3  // chunks in flight per wave
+#define KRR_STREAM_DEPTH 2  // chunks in flight per wave
 #endif
 #ifndef KRR_SELECT_WAVES_PER_SIMD
-#define KRR_SELECT_WAVES_PER_SIMD 2  // __launch_bounds__ occupancy hint for k_select
+#define KRR_SELECT_WAVES_PER_SIMD 3  // __launch_bounds__ occupancy hint for k_select
 #endif
 
 namespace krr {
 
+// Diagnostic build (-DKRR_DIAG): per-segment cycle and event counters written
+// to a buffer attached with krr_diag_attach(); never compiled into the product.
+#ifdef KRR_DIAG
+__device__ unsigned long long* g_diag = nullptr;
+enum { D_TOTAL, D_COMPACT, D_FINAL, D_NCOMPACT, D_NFALLBACK, D_ACTIVE_SLOTS, D_INSERTED, D_CHUNKS, D_WORDS };
+#define KRR_DIAG_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define KRR_DIAG_ADD(field, val) \
+    do { diag[field] += (val); } while (0)
+#else
+#define KRR_DIAG_T0(v)
+#define KRR_DIAG_ADD(field, val) \
+    do {                          \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Streaming skeleton.  One wave walks values[beg, end): the 16-byte aligned
-// body in chunks of kUnroll x 16 B per lane (8 KiB per wave), three chunks in
-// flight; the unaligned head/tail elements and the partial last chunk go
-// through ONE guarded chunk call (the partial chunk never fills its last slot,
-// so the head and tail elements ride in it).  A processor implements
-//   template <bool GUARD> void chunk(const double2 (&c)[kUnroll], uint32_t vmask)
-// where, with GUARD, bit (2u + h) of vmask says slot c[u].x (h=0) / .y (h=1)
-// of this lane holds a sample.
+// body in chunks of kUnroll x 16 B per lane (8 KiB per wave), the next chunk
+// in flight while this one is processed.  The partial last chunk is padded
+// with NaN and carries the unaligned head/tail elements in its last slot
+// (lane 63, which a partial chunk never fills), so every chunk goes through
+// the same `proc.chunk(c)` body: a NaN is never a candidate, never a tie and is
+// ignored by fmax, and the padding count is returned so NaN counts can be
+// corrected.  ONE_SITE keeps a single inlined chunk body (register rotation,
+// one 64-bit move per slot) for processors whose body is large.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void load_chunk(double2 (&c)[kUnroll], const double2* __restrict__ p) {
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) c[u] = p[u * kWave];
 }
 
-template <class Proc>
-__device__ __forceinline__ void stream_segment(const double* __restrict__ vals, int64_t beg,
-                                               int64_t end, Proc& proc, int lane) {
+template <bool ONE_SITE, class Proc>
+__device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ vals, int64_t beg,
+                                                   int64_t end, Proc& proc, int lane) {
     int64_t a0 = (beg + 1) & ~(int64_t)1;
     if (a0 > end) a0 = end;
     int64_t a1 = end & ~(int64_t)1;
@@ -61,65 +77,50 @@ __device__ __forceinline__ void stream_segment(const double* __restrict__ vals, 
     const int64_t nunits = (a1 >> 1) - i0;
     constexpr int CH = kUnroll * kWave;  // double2 units per chunk
     const int64_t nfull = nunits / CH;
-    if (nfull > 0) {
-        const double2* __restrict__ p = v2 + i0 + lane;
-        const int64_t last = nfull - 1;
-        auto at = [&](int64_t c) { return p + (c < last ? c : last) * CH; };  // clamp: re-read, never overrun
-#if KRR_STREAM_DEPTH == 2
-        double2 b0[kUnroll], b1[kUnroll];
-        load_chunk(b0, at(0));
-        load_chunk(b1, at(1));
-        for (int64_t c = 0; c < nfull; c += 2) {
-            proc.template chunk<false>(b0, 0u);
-            load_chunk(b0, at(c + 2));
-            if (c + 1 < nfull) proc.template chunk<false>(b1, 0u);
-            load_chunk(b1, at(c + 3));
-        }
-#else
-        double2 b0[kUnroll], b1[kUnroll], b2[kUnroll];
-        load_chunk(b0, at(0));
-        load_chunk(b1, at(1));
-        load_chunk(b2, at(2));
-        for (int64_t c = 0; c < nfull; c += 3) {
-            proc.template chunk<false>(b0, 0u);
-            load_chunk(b0, at(c + 3));
-            if (c + 1 < nfull) proc.template chunk<false>(b1, 0u);
-            load_chunk(b1, at(c + 4));
-            if (c + 2 < nfull) proc.template chunk<false>(b2, 0u);
-            load_chunk(b2, at(c + 5));
-        }
-#endif
-    }
-    const int64_t r0 = nfull * CH;
+    const int64_t rem = nunits - nfull * CH;
     const bool head = a0 > beg, tail = a1 < end;
-    if (r0 < nunits || head || tail) {
-        double2 cur[kUnroll];
-        uint32_t vmask = 0;
+    const bool partial = rem > 0 || head || tail;
+    const int64_t nch = nfull + (partial ? 1 : 0);
+    if (nch == 0) return 0;
+    const double2* __restrict__ p = v2 + i0 + lane;
+    const double qnan = __builtin_nan("");
+    auto fill = [&](double2 (&c)[kUnroll], int64_t ci) {
+        if (ci < nfull) {
+            load_chunk(c, p + ci * CH);
+        } else {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const int64_t j = r0 + u * kWave + lane;
-            const bool in = j < nunits;
-            cur[u] = in ? v2[i0 + j] : make_double2(0.0, 0.0);
-            vmask |= in ? (3u << (2 * u)) : 0u;
-        }
-        // nunits - r0 < CH, so the last slot (u = kUnroll-1, lane 63) is free
-        if (lane == kWave - 1) {
-            if (head) {
-                cur[kUnroll - 1].x = vals[beg];
-                vmask |= 1u << (2 * (kUnroll - 1));
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t j = ci * CH + u * kWave + lane;
+                c[u] = j < nunits ? v2[i0 + j] : make_double2(qnan, qnan);
             }
-            if (tail) {
-                cur[kUnroll - 1].y = vals[a1];
-                vmask |= 2u << (2 * (kUnroll - 1));
+            if (lane == kWave - 1) {
+                if (head) c[kUnroll - 1].x = vals[beg];
+                if (tail) c[kUnroll - 1].y = vals[a1];
             }
         }
-        proc.template chunk<true>(cur, vmask);
+    };
+    if constexpr (ONE_SITE) {
+        double2 cur[kUnroll], nxt[kUnroll];
+        fill(cur, 0);
+#pragma unroll 1
+        for (int64_t ci = 0; ci < nch; ++ci) {
+            if (ci + 1 < nch) fill(nxt, ci + 1);
+            proc.chunk(cur);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+        }
+    } else {
+        double2 b0[kUnroll], b1[kUnroll];
+        fill(b0, 0);
+        if (nch > 1) fill(b1, 1);
+        for (int64_t ci = 0; ci < nch; ci += 2) {
+            proc.chunk(b0);
+            if (ci + 2 < nch) fill(b0, ci + 2);
+            if (ci + 1 < nch) proc.chunk(b1);
+            if (ci + 3 < nch) fill(b1, ci + 3);
+        }
     }
-}
-
-template <bool GUARD>
-__device__ __forceinline__ bool slot_in(uint32_t vmask, int j) {
-    return GUARD ? ((vmask >> j) & 1u) != 0 : true;
+    return partial ? (uint32_t)(2 * CH - 2 * rem - (head ? 1 : 0) - (tail ? 1 : 0)) : 0u;
 }
 
 __device__ __forceinline__ double slot_val(const double2 (&c)[kUnroll], int j) {
@@ -127,108 +128,6 @@ __device__ __forceinline__ double slot_val(const double2 (&c)[kUnroll], int j) {
 }
 
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll((long long)m); }
-
-// ---------------------------------------------------------------------------
-// MSD radix select over M = buf[0..cnt) U {xk repeated xc times}, in LDS or
-// global scratch, by one wave.  Finds the R-th largest key (1-based):
-// v with count(M > v) < R <= count(M >= v).  With `early`, it may stop at a
-// digit-bin edge e > floor_key with count(M >= e) >= R and count(M > e) <= stop
-// (good enough for a compaction threshold).  The first digit starts at the
-// highest bit where min(M) and max(M) differ, so clustered keys (all samples
-// in one binade) still split on their first level; <= 8 bits per level.
-// Out of line: it is the rare fallback, and inlining it into every chunk call
-// site costs registers and I-cache on the hot path.
-// ---------------------------------------------------------------------------
-struct SelHit {
-    uint64_t key;
-    uint32_t above;  // count(M > key)   (exact when !early)
-    uint32_t ge;     // count(M >= key)  (upper bound when early-stopped)
-    uint32_t ok;
-};
-
-__device__ __noinline__ SelHit select_desc(const uint64_t* buf, uint32_t cnt, uint64_t xk, uint32_t xc,
-                                           uint32_t R, bool early, uint64_t floor_key, uint32_t stop,
-                                           uint32_t* hist, int lane) {
-    SelHit out;
-    out.ok = 1;
-    uint64_t mn = ~0ull, mx = 0;
-    for (uint32_t i = lane; i < cnt; i += kWave) {
-        const uint64_t x = buf[i];
-        mn = x < mn ? x : mn;
-        mx = x > mx ? x : mx;
-    }
-    mn = wave_min_u64(mn);
-    mx = wave_max_u64(mx);
-    if (xc) {
-        mn = xk < mn ? xk : mn;
-        mx = xk > mx ? xk : mx;
-    }
-    const uint32_t total = cnt + xc;
-    if (R == 0 || R > total) {
-        out.key = mx;
-        out.above = 0;
-        out.ge = total;
-        out.ok = 0;
-        return out;
-    }
-    uint64_t lo = mn, hi = mx;
-    uint32_t above = 0, ge = total;
-    while (lo != hi) {
-        const int h = 63 - __clzll((long long)(lo ^ hi));
-        const int s = h >= 7 ? h - 7 : 0;
-        const uint32_t nb = 1u << (h - s + 1);
-        const uint64_t pre = (h == 63) ? 0ull : ((lo >> (h + 1)) << (h + 1));
-        for (uint32_t i = lane; i < 256; i += kWave) hist[i] = 0;
-        __syncthreads();
-        for (uint32_t i = lane; i < cnt; i += kWave) {
-            const uint64_t x = buf[i];
-            if (x >= lo && x <= hi) atomicAdd(&hist[(uint32_t)(x >> s) & (nb - 1)], 1u);
-        }
-        if (lane == 0 && xc && xk >= lo && xk <= hi) atomicAdd(&hist[(uint32_t)(xk >> s) & (nb - 1)], xc);
-        __syncthreads();
-        uint32_t hb[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hb[j] = hist[4 * lane + j];
-        const uint32_t t = hb[0] + hb[1] + hb[2] + hb[3];
-        const uint32_t incl = wave_suffix_incl(t, lane);
-        uint32_t run = above + (incl - t);
-        int fb = -1;
-        uint32_t fab = 0, fcb = 0;
-#pragma unroll
-        for (int j = 3; j >= 0; --j) {
-            if (fb < 0 && run < R && run + hb[j] >= R) {
-                fb = 4 * lane + j;
-                fab = run;
-                fcb = hb[j];
-            }
-            run += hb[j];
-        }
-        const uint64_t m = ballot(fb >= 0);
-        const int src = __ffsll((long long)m) - 1;
-        const int b = __shfl(fb, src);
-        const uint32_t ab = uni32((uint32_t)__shfl((int)fab, src));
-        const uint32_t cb = uni32((uint32_t)__shfl((int)fcb, src));
-        const uint64_t blo = pre | ((uint64_t)(uint32_t)b << s);
-        const uint64_t bhi = blo | (s == 0 ? 0ull : ((1ull << s) - 1));
-        const uint64_t nlo = uni64(blo > lo ? blo : lo);
-        const uint64_t nhi = uni64(bhi < hi ? bhi : hi);
-        __syncthreads();  // histogram reads done before the next level clears it
-        if (early && nlo > floor_key && ab + cb <= stop) {
-            out.key = nlo;
-            out.above = ab;
-            out.ge = ab + cb;
-            return out;
-        }
-        lo = nlo;
-        hi = nhi;
-        above = ab;
-        ge = ab + cb;
-    }
-    out.key = lo;
-    out.above = above;
-    out.ge = ge;
-    return out;
-}
 
 // Find the digit bin holding the R-th largest (1-based) of a 256-bin histogram
 // (bins ordered by key), given `above0` elements already known to be larger.
@@ -285,30 +184,29 @@ __device__ __forceinline__ BinHit find_bin_desc(const uint32_t* hist, uint32_t R
 //   x - (bits(t)+1) < bits(+inf) - bits(t)
 // which also rejects every NaN and every negative number.
 //
-// H is a 256-bin histogram of buf kept up to date on every insert (bins of
-// width 2^hsh from hbase = thr + 1; bin 255 also takes everything above).  A
-// compaction reads the new threshold off H and needs one filter pass over buf,
-// which rebuilds H for the new range; select_desc is only the fallback when
-// the cut falls into the overflow bin or a crowded bin.  The final rank
-// queries use H the same way: locate the bin, gather its few members, rank
-// them in registers.
+// Insertion is kept minimal (ballot + mbcnt position + one ds_write): with a
+// ~1-3% candidate rate nearly every 64-wide slot has a candidate, so every
+// VALU spent per insert is spent on most slots.  A compaction instead builds a
+// 256-bin histogram of the buffer over [min, max] and reads the cut off it,
+// re-histogramming a crowded bin's range if needed (locate), then filters
+// once.  The final rank queries locate the rank the same way down to <= 64
+// keys, gather them and rank them in registers.
 // ---------------------------------------------------------------------------
 struct SelectProc {
     uint64_t* buf;
-    uint32_t* H;      // maintained histogram of buf
-    uint32_t* scr;    // select_desc scratch histogram
+    uint32_t* H;      // 256-bin histogram of buf (also select_desc's scratch)
     uint64_t* small;  // 64-key gather area
     int lane;
     uint32_t cap, tkeep, tstop;
     uint64_t flip;
     uint64_t thr;
     uint32_t cnt, eqs, nnan;
-    uint64_t hbase;
-    uint32_t hsh, hvalid;
     uint32_t fast;              // thr is a non-negative finite number or +0, top side
     uint64_t tbits, tb1, tlim;  // fast-path constants
-    uint64_t mxk;               // per lane: largest key ever inserted
     uint32_t bad;
+#ifdef KRR_DIAG
+    unsigned long long diag[D_WORDS];
+#endif
 
     __device__ __forceinline__ void set_thr(uint64_t t) {
         thr = uni64(t);
@@ -318,204 +216,289 @@ struct SelectProc {
         tlim = 0x7FF0000000000000ull - tbits;
     }
 
-    __device__ __forceinline__ uint32_t bin(uint64_t k) const {
-        const uint64_t d = (k - hbase) >> hsh;
-        return d > 255 ? 255u : (uint32_t)d;
-    }
-
-    template <bool GUARD, bool FAST>
-    __device__ __forceinline__ bool is_cand(double d, uint32_t vmask, int j, uint64_t& key) const {
+    template <bool FAST>
+    __device__ __forceinline__ bool is_cand(double d, uint64_t& key) const {
         const uint64_t x = dbits(d);
         if (FAST) {
             key = x | kSignBit;
-            return slot_in<GUARD>(vmask, j) && (x - tb1) < tlim;
+            return (x - tb1) < tlim;
         }
         key = okey(x) ^ flip;
-        return slot_in<GUARD>(vmask, j) && !__builtin_isnan(d) && key > thr;
+        return !__builtin_isnan(d) && key > thr;
     }
 
-    // Count this chunk's candidates (C), ties with thr (E) and NaN slots (NN);
-    // jm = bit j set if slot j has a candidate in some lane.
-    template <bool GUARD, bool FAST>
-    __device__ __forceinline__ void classify(const double2 (&c)[kUnroll], uint32_t vmask, uint32_t& C,
+    // Count candidates (C), ties with thr (E) and NaN slots (NN) among the slots
+    // in smask; jm = bit j set if slot j has a candidate in some lane.
+    template <bool FAST>
+    __device__ __forceinline__ void classify(const double2 (&c)[kUnroll], uint32_t smask, uint32_t& C,
                                              uint32_t& E, uint32_t& NN, uint32_t& jm) const {
         C = E = NN = jm = 0;
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
-            const double d = slot_val(c, j);
-            uint64_t key;
-            const bool cand = is_cand<GUARD, FAST>(d, vmask, j, key);
-            const bool in = slot_in<GUARD>(vmask, j);
-            const bool eq = FAST ? (in && dbits(d) == tbits) : (in && !__builtin_isnan(d) && key == thr);
-            const uint64_t m = ballot(cand);
-            C += popc64(m);
-            jm |= m ? (1u << j) : 0u;
-            E += popc64(ballot(eq));
-            NN += popc64(ballot(in && __builtin_isnan(d)));
+            if ((smask >> j) & 1u) {  // wave-uniform
+                const double d = slot_val(c, j);
+                uint64_t key;
+                const bool cand = is_cand<FAST>(d, key);
+                const bool eq = FAST ? (dbits(d) == tbits) : (!__builtin_isnan(d) && key == thr);
+                const uint64_t m = ballot(cand);
+                C += popc64(m);
+                jm |= m ? (1u << j) : 0u;
+                E += popc64(ballot(eq));
+                NN += popc64(ballot(__builtin_isnan(d)));
+            }
         }
     }
 
-    template <bool GUARD, bool FAST>
-    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], uint32_t vmask, uint32_t jm) {
+    template <bool FAST>
+    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], uint32_t jm) {
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             if ((jm >> j) & 1u) {
+                // Opaque copy: recompute the test here instead of letting the
+                // compiler keep classify's 16 keys/masks alive across compact().
+                double d = slot_val(c, j);
+                asm volatile("" : "+v"(d));
                 uint64_t key;
-                const bool cand = is_cand<GUARD, FAST>(slot_val(c, j), vmask, j, key);
+                const bool cand = is_cand<FAST>(d, key);
                 const uint64_t m = ballot(cand);
-                if (cand) {
-                    buf[cnt + lane_prefix(m)] = key;
-                    mxk = key > mxk ? key : mxk;
-                    if (hvalid) atomicAdd(&H[bin(key)], 1u);
-                }
+                if (cand) buf[cnt + lane_prefix(m)] = key;
                 cnt = uni32(cnt + popc64(m));
             }
         }
     }
 
-    template <bool GUARD>
-    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+    // Classify the slots in smask, compact once if needed, insert.  Returns false
+    // (nothing inserted, nothing counted) if the candidates still do not fit.
+    __device__ __forceinline__ bool try_slots(const double2 (&c)[kUnroll], uint32_t smask) {
         uint32_t C, E, NN, jm;
-        if (fast) classify<GUARD, true>(c, vmask, C, E, NN, jm);
-        else classify<GUARD, false>(c, vmask, C, E, NN, jm);
+        if (uni32(fast)) classify<true>(c, smask, C, E, NN, jm);
+        else classify<false>(c, smask, C, E, NN, jm);
         if (cnt + C > cap) {
             compact();
-            if (fast) classify<GUARD, true>(c, vmask, C, E, NN, jm);
-            else classify<GUARD, false>(c, vmask, C, E, NN, jm);
-            if (cnt + C > cap) {  // compaction failed (flagged): drop, never overrun
-                bad = 1;
-                return;
-            }
+            if (uni32(fast)) classify<true>(c, smask, C, E, NN, jm);
+            else classify<false>(c, smask, C, E, NN, jm);
+            if (cnt + C > cap) return false;
         }
         eqs += E;
         nnan += NN;
+        KRR_DIAG_ADD(D_ACTIVE_SLOTS, __popc(jm));
+        KRR_DIAG_ADD(D_INSERTED, C);
         if (jm) {
-            if (fast) insert<GUARD, true>(c, vmask, jm);
-            else insert<GUARD, false>(c, vmask, jm);
+            if (uni32(fast)) insert<true>(c, jm);
+            else insert<false>(c, jm);
+        }
+        return true;
+    }
+
+    // After a compaction at most tstop = cap - kChunkElems/2 keys remain, so half a
+    // chunk always fits: a chunk with more candidates than the free space (the
+    // first chunks of a segment, or a monotone series) goes in as two halves.
+    // The halves run through the same inlined body (a 3-iteration loop).
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+        KRR_DIAG_ADD(D_CHUNKS, 1);
+        uint32_t smask = 0xFFFFu;
+#pragma unroll 1
+        for (int step = 0; step < 3; ++step) {
+            if (try_slots(c, smask)) {
+                if (smask != 0x00FFu) return;  // whole chunk, or second half done
+                smask = 0xFF00u;
+                continue;
+            }
+            if (smask != 0xFFFFu) {
+                bad |= 2u;
+                return;
+            }
+            smask = 0x00FFu;
         }
     }
 
-    // Raise thr to nt and filter buf to keys > nt (counting keys == nt into eqs),
-    // rebuilding H over (nt, mx].
-    __device__ __forceinline__ void filter_rebuild(uint64_t nt, uint64_t mx) {
-        hbase = uni64(nt + 1);
-        const uint64_t range = mx > nt ? mx - hbase : 0ull;
+    // min and max key of buf; four LDS reads in flight per lane.
+    __device__ __forceinline__ void buf_minmax(uint64_t& mn_out, uint64_t& mx_out) const {
+        uint64_t mn = ~0ull, mx = 0;
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : buf[0];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                mn = x[t] < mn ? x[t] : mn;
+                mx = x[t] > mx ? x[t] : mx;
+            }
+        }
+        mn_out = wave_min_u64(mn);
+        mx_out = wave_max_u64(mx);
+    }
+
+    // Histogram of the keys of buf inside [lo, hi] (256 bins of width 2^hsh from
+    // lo; the range always fits 256 bins), four LDS reads in flight per lane.
+    __device__ __forceinline__ uint32_t hist_range(uint64_t lo, uint64_t hi) {
+        const uint64_t range = hi - lo;
         const int bits = range ? 64 - __clzll((long long)range) : 0;
-        hsh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
+        const uint32_t sh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
         for (uint32_t i = lane; i < 256; i += kWave) H[i] = 0;
         __syncthreads();
-        uint32_t w = 0, e = 0;
-        for (uint32_t base = 0; base < cnt; base += kWave) {
-            const uint32_t i = base + lane;
-            const bool in = i < cnt;
-            const uint64_t x = in ? buf[i] : 0ull;
-            const bool keep = in && x > nt;
-            e += popc64(ballot(in && x == nt));
-            const uint64_t m = ballot(keep);
-            if (keep) {
-                buf[w + lane_prefix(m)] = x;
-                atomicAdd(&H[bin(x)], 1u);
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : 0ull;
             }
-            w += popc64(m);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (base + t * kWave + lane < cnt && x[t] >= lo && x[t] <= hi)
+                    atomicAdd(&H[(uint32_t)((x[t] - lo) >> sh)], 1u);
+        }
+        __syncthreads();
+        return sh;
+    }
+
+    // Locate the R-th largest key of buf (all keys in [mn, mx]) to a key range
+    // [lo, hi] holding `cnt` keys with `above` larger ones: histogram, pick the
+    // bin, re-histogram that bin's range, until `good(above, cnt)` or the range
+    // is a single key.  Each level is one pass over buf (an MSD radix select
+    // whose digits adapt to the remaining range).
+    struct Cut {
+        uint64_t lo, hi;
+        uint32_t above, cnt, ok;
+    };
+    template <class Good>
+    __device__ __forceinline__ Cut locate(uint32_t R, uint64_t mn, uint64_t mx, Good good) {
+        Cut c;
+        c.lo = mn;
+        c.hi = mx;
+        c.above = 0;
+        c.cnt = cnt;
+        c.ok = 1;
+#pragma unroll 1
+        for (int level = 0; level < 9; ++level) {
+            const uint32_t sh = hist_range(c.lo, c.hi);
+            const BinHit bh = find_bin_desc(H, R, c.above, lane);
+            __syncthreads();
+            if (!bh.found) {
+                c.ok = 0;
+                return c;
+            }
+            const uint64_t blo = uni64(c.lo + ((uint64_t)bh.b << sh));
+            const uint64_t span = (1ull << sh) - 1;
+            const uint64_t bhi = uni64(c.hi - blo <= span ? c.hi : blo + span);
+            c.lo = blo;
+            c.hi = bhi;
+            c.above = bh.above;
+            c.cnt = bh.cnt;
+            if (good(c.above, c.cnt) || blo == bhi) return c;
+        }
+        return c;
+    }
+
+    // Raise thr to nt: keep keys > nt in buf (in place), count keys == nt into eqs.
+    // A block of 4 x 64 keys is read before any of its survivors is written, and
+    // survivors land at or below the block start, so nothing unread is overwritten.
+    __device__ __forceinline__ void filter(uint64_t nt) {
+        uint32_t w = 0, e = 0;
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bool in = base + t * kWave + lane < cnt;
+                const bool keep = in && x[t] > nt;
+                e += popc64(ballot(in && x[t] == nt));
+                const uint64_t m = ballot(keep);
+                if (keep) buf[w + lane_prefix(m)] = x[t];
+                w += popc64(m);
+            }
         }
         cnt = uni32(w);
         eqs = uni32(e);
-        hvalid = 1;
         set_thr(nt);
     }
 
+    // Every key in buf is > thr.  Cut at the low edge of the key range holding
+    // the tkeep-th largest so that <= tstop keys stay above it (or at that key
+    // when one key is crowded: then fewer than tkeep stay above).  With
+    // cnt <= tstop there is nothing to gain; the caller inserts in halves.
     __device__ __forceinline__ void compact() {
+        if (cnt <= tstop) return;
+        KRR_DIAG_T0(t0);
         __syncthreads();
-        uint64_t nt = 0;
-        bool have = false;
-        if (hvalid) {
-            const BinHit bh = find_bin_desc(H, tkeep, 0, lane);
-            if (bh.found && bh.b < 255 && bh.above + bh.cnt <= tstop) {
-                nt = uni64(hbase + ((uint64_t)bh.b << hsh));  // >= hbase > thr
-                have = true;
-            }
+        uint64_t mn, mx;
+        buf_minmax(mn, mx);
+        const uint32_t ts = tstop;
+        const Cut ct = locate(tkeep, mn, mx, [ts](uint32_t above, uint32_t c) { return above + c <= ts; });
+        if (!ct.ok || ct.lo <= thr) {  // cannot happen while cnt > tstop >= tkeep; flag it
+            bad |= 1u;
+            return;
         }
-        if (!have) {
-            const SelHit hit = select_desc(buf, cnt, thr, eqs, tkeep, true, thr, tstop, scr, lane);
-            nt = uni64(hit.key);
-            if (!hit.ok || nt <= thr) {  // cannot happen while cnt > tstop; flag it
-                bad = 1;
-                return;
-            }
-        }
-        filter_rebuild(nt, wave_max_u64(mxk));
+        filter(ct.lo);
         __syncthreads();
+        KRR_DIAG_ADD(D_NCOMPACT, 1);
+#ifdef KRR_DIAG
+        KRR_DIAG_ADD(D_COMPACT, __builtin_amdgcn_s_memtime() - t0);
+#endif
     }
 
-    // The R-th largest key (1-based) of buf.
-    __device__ __forceinline__ uint64_t kth_largest(uint32_t R) {
-        if (hvalid) {
-            const BinHit bh = find_bin_desc(H, R, 0, lane);
-            if (bh.found && bh.b < 255 && bh.cnt <= kWave) {
-                const uint64_t lo = hbase + ((uint64_t)bh.b << hsh);
-                const uint64_t hi = lo + ((1ull << hsh) - 1);
-                uint32_t w = 0;
-                for (uint32_t base = 0; base < cnt; base += kWave) {
-                    const uint32_t i = base + lane;
-                    const bool in = i < cnt;
-                    const uint64_t x = in ? buf[i] : 0ull;
-                    const bool inb = in && x >= lo && x <= hi;
-                    const uint64_t m = ballot(inb);
-                    if (inb) small[w + lane_prefix(m)] = x;
-                    w += popc64(m);
-                }
-                __syncthreads();
-                const uint32_t R2 = R - bh.above;
-                const uint64_t v = (uint32_t)lane < w ? small[lane] : 0ull;
-                uint32_t gt = 0, ge = 0;
-                for (uint32_t j = 0; j < w; ++j) {
-                    const uint64_t y = small[j];
-                    gt += y > v ? 1u : 0u;
-                    ge += y >= v ? 1u : 0u;
-                }
-                const uint64_t sel = ballot((uint32_t)lane < w && gt < R2 && R2 <= ge);
-                __syncthreads();
-                if (sel) return uni64((uint64_t)__shfl((unsigned long long)v, __ffsll((long long)sel) - 1));
-                bad = 1;
+    // The R-th largest key (1-based) of buf: locate it to a range of <= 64 keys
+    // (or one key), gather those, rank them in registers.
+    __device__ __forceinline__ uint64_t kth_largest(uint32_t R, uint64_t mn, uint64_t mx) {
+        const Cut ct = locate(R, mn, mx, [](uint32_t, uint32_t c) { return c <= (uint32_t)kWave; });
+        if (!ct.ok) {
+            bad |= 16u;
+            return 0;
+        }
+        if (ct.lo == ct.hi) return ct.lo;
+        uint32_t w = 0;
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bool inb = base + t * kWave + lane < cnt && x[t] >= ct.lo && x[t] <= ct.hi;
+                const uint64_t m = ballot(inb);
+                if (inb) small[w + lane_prefix(m)] = x[t];
+                w += popc64(m);
             }
         }
-        const SelHit h = select_desc(buf, cnt, 0, 0, R, false, 0, 0, scr, lane);
-        if (!h.ok) bad = 1;
-        return h.key;
-    }
-
-    // Build H over the whole buffer (once at the end when no compaction ran).
-    __device__ __forceinline__ void build_hist() {
-        uint64_t mn = ~0ull, mx = 0;
-        for (uint32_t i = lane; i < cnt; i += kWave) {
-            const uint64_t x = buf[i];
-            mn = x < mn ? x : mn;
-            mx = x > mx ? x : mx;
+        __syncthreads();
+        const uint32_t R2 = R - ct.above;
+        const uint64_t v = (uint32_t)lane < w ? small[lane] : 0ull;
+        uint32_t gt = 0, ge = 0;
+        for (uint32_t j = 0; j < w; ++j) {
+            const uint64_t y = small[j];
+            gt += y > v ? 1u : 0u;
+            ge += y >= v ? 1u : 0u;
         }
-        mn = wave_min_u64(mn);
-        mx = wave_max_u64(mx);
-        hbase = mn;
-        const uint64_t range = mx - mn;
-        const int bits = range ? 64 - __clzll((long long)range) : 0;
-        hsh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
-        for (uint32_t i = lane; i < 256; i += kWave) H[i] = 0;
+        const uint64_t sel = ballot((uint32_t)lane < w && gt < R2 && R2 <= ge);
         __syncthreads();
-        for (uint32_t i = lane; i < cnt; i += kWave) atomicAdd(&H[bin(buf[i])], 1u);
-        __syncthreads();
-        hvalid = 1;
+        if (!sel) {
+            bad |= 8u;
+            return 0;
+        }
+        return uni64((uint64_t)__shfl((unsigned long long)v, __ffsll((long long)sel) - 1));
     }
 
     // Key of the element with ascending rank r (0-based) among nsel present samples.
-    __device__ __forceinline__ uint64_t rank_key(uint64_t r, uint64_t nsel) {
+    __device__ __forceinline__ uint64_t rank_key(uint64_t r, uint64_t nsel, uint64_t mn, uint64_t mx) {
         const uint64_t rr = flip ? (nsel - 1 - r) : r;
         const uint64_t below = nsel - cnt - eqs;
         if (rr < below) {
-            bad = 1;
+            bad |= 4u;
             return 0;
         }
         if (rr < below + eqs) return thr;
         const uint32_t idx = (uint32_t)(rr - below - eqs);
-        return kth_largest(cnt - idx);
+        return kth_largest(cnt - idx, mn, mx);
     }
 };
 
@@ -577,46 +560,39 @@ struct SelectArgs {
     uint32_t* out_f;
 };
 
-// GBUF selects where candidate buffers live at COMPILE time, so the LDS variant
-// emits ds_* (lgkmcnt) and never flat_* stores, which would force vmcnt(0)
-// waits and serialise the prefetch pipeline.
-template <bool GBUF>
-__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
-    // LDS: [H 1 KiB][select scratch 1 KiB][gather 512 B][candidate keys cap x 8 B]
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* buf;
-    if constexpr (GBUF) {
-        buf = A.gscratch + (size_t)blockIdx.x * A.cap;
-    } else {
-        buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
-    }
-    const int lane = threadIdx.x;
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+// One CPU segment (SORTED_LOWER / LINEAR) by one wave.
+// LDS (smem): [H 1 KiB][gather 512 B][candidate keys cap x 8 B] unless buf is HBM scratch.
+__device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem,
+                                               uint64_t* buf, int lane) {
+    {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t L = end - beg;
         const SidePlan sp = plan_side(L, A.mode, A.p_num, A.p_den, A.q);
         SelectProc P;
         P.buf = buf;
         P.H = reinterpret_cast<uint32_t*>(smem);
-        P.scr = reinterpret_cast<uint32_t*>(smem + 1024);
-        P.small = reinterpret_cast<uint64_t*>(smem + 2048);
+        P.small = reinterpret_cast<uint64_t*>(smem + 1024);
         P.lane = lane;
         P.cap = A.cap;
         P.tkeep = sp.tkeep;
-        P.tstop = A.cap - kChunkElems;
+        P.tstop = A.cap - kChunkElems / 2;
         P.flip = sp.bottom ? ~0ull : 0ull;
         P.cnt = 0;
         P.eqs = 0;
         P.nnan = 0;
         P.bad = 0;
-        P.hbase = 0;
-        P.hsh = 0;
-        P.hvalid = 0;
-        P.mxk = 0;
         P.set_thr(0);
-        stream_segment(A.vals, beg, end, P, lane);
+#ifdef KRR_DIAG
+        for (int d = 0; d < D_WORDS; ++d) P.diag[d] = 0;
+        KRR_DIAG_T0(t_begin);
+#endif
+        P.nnan -= stream_segment<true>(A.vals, beg, end, P, lane);  // drop the NaN padding
         __syncthreads();
-        if (!P.hvalid && P.cnt > kWave) P.build_hist();
+#ifdef KRR_DIAG
+        KRR_DIAG_T0(t_final);
+#endif
+        uint64_t bmn = 0, bmx = 0;
+        if (P.cnt) P.buf_minmax(bmn, bmx);
 
         const uint64_t nnan = P.nnan;
         const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
@@ -628,34 +604,58 @@ __global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(Select
         } else if (nnan && !A.gaps) {
             result = bitsd(kQuietNaN);
             flags |= KRR_FLAG_NAN;
-        } else if (A.mode == KRR_PCT_SORTED_LOWER) {
-            const int64_t r = exact_rank(n, A.p_num, A.p_den);
-            uint64_t bits = okey_inv(P.rank_key(r, n) ^ P.flip);
-            if (is_zero_bits(bits)) {
-                // Python sorted() is stable and -0 == +0: the zero at rank r is the
-                // (r - #negatives)-th zero in position order.
-                const uint64_t neg = count_negative(A.vals, beg, end, lane);
-                bits = nth_zero_bits(A.vals, beg, end, (uint64_t)r - neg, lane);
+        } else {
+            // ranks needed: SORTED_LOWER r0; LINEAR numpy prev/next.  One rank-query
+            // body serves both (a 1-2 iteration loop keeps it inlined once).
+            int64_t r0, r1;
+            double gamma = 0.0;
+            if (A.mode == KRR_PCT_SORTED_LOWER) {
+                r0 = r1 = exact_rank(n, A.p_num, A.p_den);
+            } else {  // KRR_PCT_LINEAR, numpy method="linear"
+                const double vidx = __dmul_rn((double)(n - 1), A.q);
+                if (vidx >= (double)(n - 1)) {
+                    r0 = r1 = (int64_t)n - 1;
+                    gamma = __dsub_rn(vidx, -1.0);  // numpy subtracts the clipped index -1
+                } else {
+                    const double fl = floor(vidx);
+                    r0 = (int64_t)fl;
+                    r1 = r0 + 1;
+                    gamma = __dsub_rn(vidx, fl);
+                }
             }
-            result = bitsd(bits);
-        } else {  // KRR_PCT_LINEAR, numpy method="linear"
-            const double vidx = __dmul_rn((double)(n - 1), A.q);
-            int64_t prev, next;
-            double gamma;
-            if (vidx >= (double)(n - 1)) {
-                prev = next = (int64_t)n - 1;
-                gamma = __dsub_rn(vidx, -1.0);  // numpy subtracts the clipped index -1
+            uint64_t k0 = 0, k1 = 0;
+            const int nq = r1 != r0 ? 2 : 1;
+#pragma unroll 1
+            for (int qi = 0; qi < nq; ++qi) {
+                const uint64_t kq = P.rank_key((uint64_t)(qi ? r1 : r0), n, bmn, bmx);
+                if (qi) k1 = kq;
+                else k0 = kq;
+            }
+            const double a = bitsd(okey_inv(k0 ^ P.flip));
+            if (A.mode == KRR_PCT_SORTED_LOWER) {
+                uint64_t bits = dbits(a);
+                if (is_zero_bits(bits)) {
+                    // Python sorted() is stable and -0 == +0: the zero at rank r is the
+                    // (r - #negatives)-th zero in position order.
+                    const uint64_t neg = count_negative(A.vals, beg, end, lane);
+                    bits = nth_zero_bits(A.vals, beg, end, (uint64_t)r0 - neg, lane);
+                }
+                result = bitsd(bits);
             } else {
-                const double fl = floor(vidx);
-                prev = (int64_t)fl;
-                next = prev + 1;
-                gamma = __dsub_rn(vidx, fl);
+                const double b = nq == 2 ? bitsd(okey_inv(k1 ^ P.flip)) : a;
+                result = np_lerp(a, b, gamma);
             }
-            const double a = bitsd(okey_inv(P.rank_key(prev, n) ^ P.flip));
-            const double b = (next == prev) ? a : bitsd(okey_inv(P.rank_key(next, n) ^ P.flip));
-            result = np_lerp(a, b, gamma);
         }
-        if (P.bad) flags |= KRR_FLAG_CAPACITY;
+        if (P.bad) flags |= KRR_FLAG_CAPACITY | (P.bad << 8);  // reason bits (diagnostic)
+#ifdef KRR_DIAG
+        {
+            const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+            P.diag[D_TOTAL] = t_end - t_begin;
+            P.diag[D_FINAL] = t_end - t_final;
+            if (lane == 0 && g_diag)
+                for (int d = 0; d < D_WORDS; ++d) g_diag[(size_t)s * D_WORDS + d] = P.diag[d];
+        }
+#endif
         if (lane == 0) {
             A.out_v[s] = result;
             A.out_n[s] = (int64_t)n;
@@ -665,14 +665,28 @@ __global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(Select
     }
 }
 
+// GBUF selects where candidate buffers live at COMPILE time, so the LDS variant
+// emits ds_* (lgkmcnt) and never flat_* stores, which would force vmcnt(0)
+// waits and serialise the prefetch pipeline.
+template <bool GBUF>
+__device__ __forceinline__ uint64_t* select_buffer(const SelectArgs& A, unsigned char* smem) {
+    if constexpr (GBUF) return A.gscratch + (size_t)blockIdx.x * A.cap;
+    else return reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+}
+
+template <bool GBUF>
+__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* buf = select_buffer<GBUF>(A, smem);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) select_segment(A, s, smem, buf, threadIdx.x);
+}
+
 // --------------------------- REF_INDEX ------------------------------------
 struct NanCountProc {
     uint32_t nn;
-    template <bool GUARD>
-    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
 #pragma unroll
-        for (int j = 0; j < 2 * kUnroll; ++j)
-            nn += popc64(ballot(slot_in<GUARD>(vmask, j) && __builtin_isnan(slot_val(c, j))));
+        for (int j = 0; j < 2 * kUnroll; ++j) nn += popc64(ballot(__builtin_isnan(slot_val(c, j))));
     }
 };
 
@@ -687,12 +701,11 @@ struct RefArgs {
 };
 
 // NaN-gapped layout: the k-th PRESENT sample in position order.
-__global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
-    const int lane = threadIdx.x;
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+__device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t s, int lane) {
+    {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         NanCountProc C{0};
-        stream_segment(A.vals, beg, end, C, lane);
+        C.nn -= stream_segment<false>(A.vals, beg, end, C, lane);
         const uint64_t n = (uint64_t)(end - beg) - C.nn;
         double result = bitsd(kQuietNaN);
         uint32_t flags = 0;
@@ -744,6 +757,10 @@ __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
     }
 }
 
+__global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment(A, s, threadIdx.x);
+}
+
 // Compact CSR (every slot is a sample, NaN included): X[k] is one gather.
 __global__ __launch_bounds__(256) void k_refindex_dense(RefArgs A) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -768,14 +785,12 @@ __global__ __launch_bounds__(256) void k_refindex_dense(RefArgs A) {
 struct MaxProc {
     double mx;
     uint32_t nn;
-    template <bool GUARD>
-    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll], uint32_t vmask) {
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             const double d = slot_val(c, j);
-            const bool in = slot_in<GUARD>(vmask, j);
-            mx = fmax(mx, in ? d : __builtin_nan(""));
-            nn += popc64(ballot(in && __builtin_isnan(d)));
+            mx = fmax(mx, d);
+            nn += popc64(ballot(__builtin_isnan(d)));
         }
     }
 };
@@ -796,12 +811,12 @@ struct MaxArgs {
     uint32_t* out_f;
 };
 
-__global__ __launch_bounds__(64) void k_max(MaxArgs A) {
-    const int lane = threadIdx.x;
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+template <bool ONE_SITE>
+__device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lane) {
+    {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         MaxProc M{__builtin_nan(""), 0u};
-        stream_segment(A.vals, beg, end, M, lane);
+        M.nn -= stream_segment<ONE_SITE>(A.vals, beg, end, M, lane);
         const uint64_t L = (uint64_t)(end - beg);
         const uint64_t n = A.gaps ? L - M.nn : L;
         const double mx = wave_max_f64(M.mx);
@@ -822,6 +837,33 @@ __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
             A.out_v[s] = result;
             A.out_n[s] = (int64_t)n;
             A.out_f[s] = flags;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_max(MaxArgs A) {
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) max_segment<false>(A, s, threadIdx.x);
+}
+
+// ------------------------------ FUSED --------------------------------------
+// SimpleStrategy.run for the whole fleet in ONE launch: work item b < S_cpu is
+// CPU segment b (select or REF_INDEX-on-gaps), the rest are memory segments.
+// The dispatcher hands out blocks in order, so the shorter memory-max blocks
+// fill CUs as the CPU blocks drain instead of leaving a partly idle last round
+// per kernel; one launch is also one roofline for the whole step.
+enum { CPU_SELECT = 0, CPU_REF_GAPS = 1 };
+
+template <bool GBUF, int CPU_KIND>
+__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t S_cpu = CPU_KIND == CPU_SELECT ? A.S : R.S;
+    const int64_t total = S_cpu + M.S;
+    for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+        if (b < S_cpu) {
+            if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, b, smem, select_buffer<GBUF>(A, smem), threadIdx.x);
+            else refindex_gaps_segment(R, b, threadIdx.x);
+        } else {
+            max_segment<true>(M, b - S_cpu, threadIdx.x);
         }
     }
 }
@@ -964,6 +1006,52 @@ int check_series(krr_ctx* ctx, const krr_series* s) {
     return KRR_OK;
 }
 
+// Plan a SORTED_LOWER / LINEAR launch: candidate capacity from the longest
+// segment, LDS bytes, and (when the buffers do not fit LDS) the HBM scratch
+// for a persistent grid of `*grid` blocks.  `extra_blocks` = work items after
+// the CPU segments in the same launch (the fused kernel's memory segments).
+int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_params* params,
+                hipStream_t st, int64_t extra_blocks, double* ov, int64_t* on, uint32_t* of,
+                SelectArgs* A, size_t* lds, int64_t* grid) {
+    int64_t Lmax = 0;
+    int rc = resolve_maxlen(ctx, series, st, &Lmax);
+    if (rc) return rc;
+    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
+    const uint32_t cap = capacity_for(sp.tkeep);
+    *A = SelectArgs{};
+    A->vals = series->values;
+    A->offs = series->offsets;
+    A->S = series->n_segments;
+    A->mode = params->mode;
+    A->gaps = series->gaps_are_nan;
+    A->p_num = params->p_num;
+    A->p_den = params->p_den;
+    A->q = params->q;
+    A->cap = cap;
+    A->gscratch = nullptr;
+    A->out_v = ov;
+    A->out_n = on;
+    A->out_f = of;
+    const int64_t items = series->n_segments + extra_blocks;
+    *lds = kSelectLdsFixed + (size_t)cap * 8;
+    *grid = items;
+    if (*lds <= ctx->max_lds) return KRR_OK;
+    // Candidate buffers too large for LDS (e.g. p near 50 on very long series):
+    // same algorithm with per-block buffers in HBM scratch, persistent grid.
+    *lds = kSelectLdsFixed;
+    *grid = (int64_t)ctx->num_cus * 8 < items ? (int64_t)ctx->num_cus * 8 : items;
+    const size_t need = (size_t)*grid * cap * 8;
+    if (need > ctx->scratch_bytes) {
+        if (ctx->scratch) KRR_HIP(ctx, hipFree(ctx->scratch));
+        ctx->scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        KRR_HIP(ctx, hipMalloc(&ctx->scratch, need));
+        ctx->scratch_bytes = need;
+    }
+    A->gscratch = ctx->scratch;
+    return KRR_OK;
+}
+
 int check_params(krr_ctx* ctx, const krr_percentile_params* p) {
     if (!p) return set_err(ctx, KRR_E_INVALID, "null params%s", "");
     if (p->mode < KRR_PCT_REF_INDEX || p->mode > KRR_PCT_LINEAR)
@@ -1011,6 +1099,8 @@ int krr_create(int device, krr_ctx** out_ctx) {
     }
     (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
+    (void)hipFuncSetAttribute((const void*)k_simple<false, CPU_SELECT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
 }
@@ -1051,44 +1141,13 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
         return KRR_OK;
     }
 
-    int64_t Lmax = 0;
-    rc = resolve_maxlen(ctx, series, st, &Lmax);
+    SelectArgs A;
+    size_t lds = 0;
+    int64_t grid = 0;
+    rc = plan_select(ctx, series, params, st, 0, out_value, out_count, out_flags, &A, &lds, &grid);
     if (rc) return rc;
-    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
-    const uint32_t cap = capacity_for(sp.tkeep);
-    SelectArgs A{};
-    A.vals = series->values;
-    A.offs = series->offsets;
-    A.S = S;
-    A.mode = params->mode;
-    A.gaps = series->gaps_are_nan;
-    A.p_num = params->p_num;
-    A.p_den = params->p_den;
-    A.q = params->q;
-    A.cap = cap;
-    A.gscratch = nullptr;
-    A.out_v = out_value;
-    A.out_n = out_count;
-    A.out_f = out_flags;
-    const size_t lds = kSelectLdsFixed + (size_t)cap * 8;
-    if (lds <= ctx->max_lds) {
-        hipLaunchKernelGGL(k_select<false>, dim3(grid_for(S)), dim3(64), lds, st, A);
-    } else {
-        // Candidate buffers too large for LDS (e.g. p near 50 on very long series):
-        // same algorithm with per-block buffers in HBM scratch, persistent grid.
-        int64_t grid = (int64_t)ctx->num_cus * 8;
-        if (grid > S) grid = S;
-        const size_t need = (size_t)grid * cap * 8;
-        if (need > ctx->scratch_bytes) {
-            if (ctx->scratch) KRR_HIP(ctx, hipFree(ctx->scratch));
-            ctx->scratch = nullptr;
-            ctx->scratch_bytes = 0;
-            KRR_HIP(ctx, hipMalloc(&ctx->scratch, need));
-            ctx->scratch_bytes = need;
-        }
-        A.gscratch = ctx->scratch;
-        hipLaunchKernelGGL(k_select<true>, dim3((unsigned)grid), dim3(64), kSelectLdsFixed, st, A);
-    }
+    if (A.gscratch) hipLaunchKernelGGL(k_select<true>, dim3((unsigned)grid), dim3(64), lds, st, A);
+    else hipLaunchKernelGGL(k_select<false>, dim3(grid_for(grid)), dim3(64), lds, st, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
@@ -1117,9 +1176,40 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
     if (!cpu || !mem) return set_err(ctx, KRR_E_INVALID, "null series%s", "");
     if (cpu->n_segments != mem->n_segments)
         return set_err(ctx, KRR_E_INVALID, "cpu and mem need one segment per object each%s", "");
-    int rc = krr_segmented_percentile(ctx, cpu, params, cpu_value, cpu_count, cpu_flags, stream);
+    int rc = check_series(ctx, cpu);
+    if (!rc) rc = check_series(ctx, mem);
+    if (!rc) rc = check_params(ctx, params);
     if (rc) return rc;
-    return krr_segmented_max(ctx, mem, mem_value, mem_count, mem_flags, stream);
+    const int64_t S = cpu->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!cpu_value || !cpu_count || !cpu_flags || !mem_value || !mem_count || !mem_flags)
+        return set_err(ctx, KRR_E_INVALID, "null outputs%s", "");
+    if (params->mode == KRR_PCT_REF_INDEX && !cpu->gaps_are_nan) {
+        // compact REF_INDEX is one gather per segment: nothing to fuse with
+        rc = krr_segmented_percentile(ctx, cpu, params, cpu_value, cpu_count, cpu_flags, stream);
+        if (rc) return rc;
+        return krr_segmented_max(ctx, mem, mem_value, mem_count, mem_flags, stream);
+    }
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipStream_t st = (hipStream_t)stream;
+    MaxArgs M{mem->values, mem->offsets, S, mem->gaps_are_nan, mem_value, mem_count, mem_flags};
+    RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags};
+    SelectArgs A{};
+    if (params->mode == KRR_PCT_REF_INDEX) {
+        hipLaunchKernelGGL((k_simple<false, CPU_REF_GAPS>), dim3(grid_for(2 * S)), dim3(64), 0, st, A, R, M);
+    } else {
+        size_t lds = 0;
+        int64_t grid = 0;
+        rc = plan_select(ctx, cpu, params, st, S, cpu_value, cpu_count, cpu_flags, &A, &lds, &grid);
+        if (rc) return rc;
+        if (A.gscratch)
+            hipLaunchKernelGGL((k_simple<true, CPU_SELECT>), dim3((unsigned)grid), dim3(64), lds, st, A, R, M);
+        else
+            hipLaunchKernelGGL((k_simple<false, CPU_SELECT>), dim3(grid_for(grid)), dim3(64), lds, st, A, R, M);
+    }
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
 }
 
 int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* cpu_offsets,
@@ -1194,6 +1284,12 @@ int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* c
     (void)hipFree(d);
     return rc;
 }
+
+#ifdef KRR_DIAG
+int krr_diag_attach(void* dev_buffer) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(krr::g_diag), &dev_buffer, sizeof(void*)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
                    int32_t kind, int64_t pod_len, int32_t gaps, void* stream) {

@@ -66,21 +66,22 @@ KRR_HD inline SidePlan plan_side(int64_t L, int32_t mode, int64_t p_num, int64_t
     return sp;
 }
 
-// Fixed LDS of the select kernel ahead of the candidate keys: maintained
-// histogram (1 KiB), fallback-select scratch histogram (1 KiB), 64-key gather.
-constexpr uint32_t kSelectLdsFixed = 2560;
+// Fixed LDS of the select kernel ahead of the candidate keys: 256-bin
+// histogram (1 KiB) and the 64-key gather area (512 B).
+constexpr uint32_t kSelectLdsFixed = 1536;
 
 // Elements one streaming iteration can append (U double2 per lane, 64 lanes).
 constexpr int kUnroll = 8;
 constexpr uint32_t kChunkElems = 2u * kUnroll * 64u;
 
 // LDS key capacity for a launch whose largest segment keeps tkeep keys.
-// After a compaction at most tstop = cap - kChunkElems keys remain, so the next
+// After a compaction at most tstop = cap - kChunkElems/2 keys remain, so half a
 // chunk always fits; the 128-key margin above tkeep is what a histogram cut may
-// keep beyond tkeep before the exact fallback is needed.
+// keep beyond tkeep before the exact fallback is needed.  The first chunk of a
+// segment (every sample a candidate) must fit an empty buffer.
 inline uint32_t capacity_for(uint32_t tkeep_max) {
-    uint64_t c = (uint64_t)tkeep_max + kChunkElems + 128;
-    if (c < 1280) c = 1280;
+    uint64_t c = (uint64_t)tkeep_max + kChunkElems / 2 + 128;
+    if (c < kChunkElems + 64) c = kChunkElems + 64;
     c = (c + 63) & ~63ull;
     return (uint32_t)c;
 }
