@@ -87,10 +87,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("KRR_BENCH_BACKEND", "nccl") != "nccl":
+        local %= max(torch.cuda.device_count(), 1)  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # RCCL ("nccl") over xGMI in production; KRR_BENCH_BACKEND=gloo rehearses the
+    # N>1 path with several ranks on ONE GPU (RCCL refuses duplicate devices).
+    backend = os.environ.get("KRR_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers)
     S = offs_np.size - 1
@@ -135,7 +144,7 @@ def main():
             events[2].record(stream)
         rec = pack_records(out)
         if world > 1:
-            rec = gather_records(rec, dst=0)
+            rec = gather_records(rec.to(coll_dev), dst=0)
         if rank == 0 or world == 1:
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
 
@@ -153,7 +162,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=dev)
+    dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--containers", type=int, default=10000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--separate", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -48,9 +49,15 @@ def main():
     on = torch.empty(S, dtype=torch.int64, device=dev)
     of = torch.empty(S, dtype=torch.int32, device=dev)
     params = percentile_params(Decimal(a.percentile), a.mode)
+    out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+           (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+            ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
     for _ in range(a.reps):
-        ctx.segmented_percentile(cs, params, ov, on, of)
-        ctx.segmented_max(ms, ov, on, of)
+        if a.separate:
+            ctx.segmented_percentile(cs, params, ov, on, of)
+            ctx.segmented_max(ms, ov, on, of)
+        else:
+            ctx.simple_run(cs, ms, params, out)
     torch.cuda.synchronize()
     print("done", S, N)
 
