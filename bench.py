@@ -81,7 +81,7 @@ def main():
     import torch.distributed as dist
 
     from krr_amd import _native
-    from krr_amd.core.distributed import gather_records, pack_records
+    from krr_amd.core.distributed import gather_records
     from krr_amd.core.engine import percentile_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +127,7 @@ def main():
     }
     stream = torch.cuda.current_stream()
     host_rec = torch.empty((containers_total if rank == 0 else S, 4), dtype=torch.int64, pin_memory=True)
+    dev_rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
 
     def step(events=None):
         if events is not None:
@@ -142,7 +143,8 @@ def main():
                 events[1].record(stream)
         if events is not None:
             events[2].record(stream)
-        rec = pack_records(out)
+        ctx.pack_records(out, dev_rec, stream)  # one launch: 32-B records
+        rec = dev_rec
         if world > 1:
             rec = gather_records(rec.to(coll_dev), dst=0)
         if rank == 0 or world == 1:

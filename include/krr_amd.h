@@ -132,6 +132,14 @@ int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* c
                         int64_t* cpu_count, uint32_t* cpu_flags, double* mem_value,
                         int64_t* mem_count, uint32_t* mem_flags);
 
+/* Multi-GPU result records: int64[4] per object (32 B) = cpu value bits, mem value
+ * bits, cpu count | cpu flags << 48, mem count | mem flags << 48.  Device pointers;
+ * records has 4 * n_objects entries.  (What a rank sends to rank 0 over RCCL.) */
+int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value,
+                     const int64_t* cpu_count, const uint32_t* cpu_flags, const double* mem_value,
+                     const int64_t* mem_count, const uint32_t* mem_flags, int64_t* records,
+                     void* stream);
+
 /* Synthetic week-long series (bench/test data), generated on the device from a
  * counter-based hash so that no host packing or PCIe is involved.
  * kind 0 = CPU cores ~ Gamma(k=2, theta=0.05); kind 1 = memory bytes

@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "krr_segmented_max",
     "krr_simple_run",
     "krr_simple_run_host",
+    "krr_pack_records",
     "krr_synth_fill",
 )
 
@@ -115,6 +116,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_simple_run.restype = ctypes.c_int
         lib.krr_simple_run_host.argtypes = [vp, vp, vp, vp, vp, i64, i32, pp, vp, vp, vp, vp, vp, vp]
         lib.krr_simple_run_host.restype = ctypes.c_int
+        lib.krr_pack_records.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_pack_records.restype = ctypes.c_int
         lib.krr_synth_fill.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, vp]
         lib.krr_synth_fill.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
@@ -166,10 +169,14 @@ class Context:
 
     @staticmethod
     def series(values, offsets, max_segment_len: int = 0, gaps_are_nan: bool = False) -> KrrSeries:
+        """Describe device tensors as a krr_series.  The struct keeps references to
+        both tensors, so their memory cannot be freed and reused while it is alive."""
         _check_tensor(values, "float64")
         _check_tensor(offsets, "int64")
-        return KrrSeries(values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, values.numel(),
-                         int(max_segment_len), int(bool(gaps_are_nan)), 0)
+        ser = KrrSeries(values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, values.numel(),
+                        int(max_segment_len), int(bool(gaps_are_nan)), 0)
+        ser._keep = (values, offsets)
+        return ser
 
     # --- entry points -----------------------------------------------------
     def segmented_percentile(self, series: KrrSeries, params: KrrPercentileParams, out_value, out_count,
@@ -199,6 +206,15 @@ class Context:
             out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
             out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
             self._stream(stream)))
+
+    def pack_records(self, out: dict, records, stream=None) -> None:
+        """out: the six result tensors; records: int64 [S, 4] device tensor."""
+        n = out["cpu_value"].numel()
+        _check_tensor(records, "int64", 4 * n)
+        self._check(self._lib.krr_pack_records(
+            self._h, n, out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
+            out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
+            records.data_ptr(), self._stream(stream)))
 
     def synth_fill(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, stream=None) -> None:
         _check_tensor(values, "float64")

@@ -868,6 +868,26 @@ __global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_simple(Select
     }
 }
 
+// 32-byte result records for the multi-GPU gather (int64[4] per object):
+// cpu bits, mem bits, cpu count | cpu flags << 48, mem count | mem flags << 48.
+__global__ __launch_bounds__(256) void k_pack_records(int64_t S, const double* __restrict__ cv,
+                                                      const int64_t* __restrict__ cn,
+                                                      const uint32_t* __restrict__ cf,
+                                                      const double* __restrict__ mv,
+                                                      const int64_t* __restrict__ mn,
+                                                      const uint32_t* __restrict__ mf,
+                                                      int64_t* __restrict__ rec) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    longlong2 a, b;
+    a.x = (long long)dbits(cv[s]);
+    a.y = (long long)dbits(mv[s]);
+    b.x = (long long)((uint64_t)cn[s] | ((uint64_t)cf[s] << 48));
+    b.y = (long long)((uint64_t)mn[s] | ((uint64_t)mf[s] << 48));
+    reinterpret_cast<longlong2*>(rec)[2 * s] = a;
+    reinterpret_cast<longlong2*>(rec)[2 * s + 1] = b;
+}
+
 // Largest segment length (for planning when the caller did not pass it).
 __global__ void k_maxlen(const int64_t* __restrict__ offs, int64_t S, unsigned long long* out) {
     uint64_t m = 0;
@@ -1283,6 +1303,23 @@ int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* c
     }
     (void)hipFree(d);
     return rc;
+}
+
+int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value, const int64_t* cpu_count,
+                     const uint32_t* cpu_flags, const double* mem_value, const int64_t* mem_count,
+                     const uint32_t* mem_flags, int64_t* records, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (n_objects < 0 || (n_objects > 0 && (!cpu_value || !cpu_count || !cpu_flags || !mem_value ||
+                                            !mem_count || !mem_flags || !records)))
+        return set_err(ctx, KRR_E_INVALID, "bad pack_records arguments%s", "");
+    if (n_objects == 0) return KRR_OK;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_pack_records, dim3((unsigned)((n_objects + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, n_objects, cpu_value, cpu_count, cpu_flags, mem_value, mem_count,
+                       mem_flags, records);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
 }
 
 #ifdef KRR_DIAG
