@@ -60,9 +60,27 @@ enum { D_TOTAL, D_COMPACT, D_FINAL, D_NCOMPACT, D_NFALLBACK, D_ACTIVE_SLOTS, D_I
 // corrected.  ONE_SITE keeps a single inlined chunk body (register rotation,
 // one 64-bit move per slot) for processors whose body is large.
 // ---------------------------------------------------------------------------
+#ifndef KRR_NT_LOADS
+#define KRR_NT_LOADS 1  // nontemporal (streaming) policy on the once-read value stream (0: default policy)
+#endif
+typedef double v2f64 __attribute__((ext_vector_type(2)));
+
+// A chunk of zeros: the target of the prefetch loads that have no real slot
+// (partial chunk lanes, the prefetch past a segment's last chunk).  L2-resident.
+__device__ double2 g_zero_chunk[kUnroll * kWave];
+
+__device__ __forceinline__ double2 load16(const double2* p) {
+    if constexpr (KRR_NT_LOADS) {
+        const v2f64 v = __builtin_nontemporal_load(reinterpret_cast<const v2f64*>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *p;
+    }
+}
+
 __device__ __forceinline__ void load_chunk(double2 (&c)[kUnroll], const double2* __restrict__ p) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) c[u] = p[u * kWave];
+    for (int u = 0; u < kUnroll; ++u) c[u] = load16(p + u * kWave);
 }
 
 template <bool ONE_SITE, class Proc>
@@ -100,11 +118,52 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
         }
     };
     if constexpr (ONE_SITE) {
+        // Every in-loop fill issues exactly kUnroll 16-byte loads, unconditionally
+        // (partial-chunk lanes and the prefetch past the last chunk read the
+        // zero chunk instead, and are then replaced by NaN), so the compiler's
+        // wait before proc.chunk(cur) is vmcnt(kUnroll) — the next chunk stays
+        // in flight while this one is processed — instead of vmcnt(0).
+        double hv = qnan, tv = qnan;
+        if (head) hv = vals[beg];
+        if (tail) tv = vals[a1];
+        const double2* __restrict__ zp = g_zero_chunk + lane;
+        auto fill_u = [&](double2 (&c)[kUnroll], int64_t ci) {
+            if (ci < nfull) {
+                load_chunk(c, p + ci * CH);
+            } else {
+                const double2* q[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const int64_t j = ci * CH + u * kWave + lane;
+                    q[u] = (ci < nch && j < nunits) ? v2 + i0 + j : zp + u * kWave;
+                }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) c[u] = load16(q[u]);
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const int64_t j = ci * CH + u * kWave + lane;
+                    if (j >= nunits) c[u] = make_double2(qnan, qnan);
+                }
+                if (lane == kWave - 1) {
+                    c[kUnroll - 1].x = hv;
+                    c[kUnroll - 1].y = tv;
+                }
+            }
+        };
+        // cur only ever receives register copies of nxt (here and at the bottom of
+        // the loop), so on every path into proc.chunk(cur) the only loads in
+        // flight are nxt's and the wait the compiler places is for nothing.
         double2 cur[kUnroll], nxt[kUnroll];
-        fill(cur, 0);
+        fill_u(nxt, 0);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            double x = nxt[u].x, y = nxt[u].y;
+            asm volatile("" : "+v"(x), "+v"(y));
+            cur[u] = make_double2(x, y);
+        }
 #pragma unroll 1
         for (int64_t ci = 0; ci < nch; ++ci) {
-            if (ci + 1 < nch) fill(nxt, ci + 1);
+            fill_u(nxt, ci + 1);
             proc.chunk(cur);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
@@ -170,19 +229,24 @@ __device__ __forceinline__ BinHit find_bin_desc(const uint32_t* hist, uint32_t R
 // Threshold-filtered candidate buffer (one wave per segment).
 //
 // Invariant over the present non-NaN samples seen so far, in (possibly
-// flipped) key order:  buf holds exactly those with key > thr, `eqs` counts
-// those with key == thr, every other one is < thr ("below", implied by n).
-// Before a chunk is inserted, its candidates are COUNTED (classify: a few VALU
-// per sample, no branches, counts via ballot popcounts); if they do not fit,
-// compact() raises thr so that at least tkeep keys stay >= thr and at most
-// tstop = cap - kChunkElems stay > thr, then the chunk is re-classified and
-// always fits.  The segment's needed ranks lie in its top tkeep keys
+// flipped) key order, in one of two modes:
+//   inclusive (incl = 1): buf holds exactly those with key >= thr; every other
+//                         one is < thr ("below", implied by n);
+//   strict    (incl = 0): buf holds exactly those with key > thr, `eqs` counts
+//                         those with key == thr, the rest are below.
+// A segment starts inclusive at thr = 0 (every key).  Strict mode is entered
+// only when one key value is so crowded that cutting at it inclusively would
+// keep too many (e.g. a mostly-zero series); the next cut returns to inclusive.
+// When a chunk's candidates do not fit, compact() raises thr so that at least
+// tkeep keys stay in buf (+ ties) and at most tstop stay in buf, then the chunk
+// is re-classified.  The segment's needed ranks lie in its top tkeep keys
 // (krr_plan.h), so they are never dropped.
 //
-// Fast path: once thr is a non-negative number t (top side), "key > thr" for a
-// sample with bits x is the single unsigned range test
-//   x - (bits(t)+1) < bits(+inf) - bits(t)
-// which also rejects every NaN and every negative number.
+// Fast path (inclusive, top side, thr = key of a non-negative number t): "key >=
+// thr" for a sample with bits x is the single unsigned range test
+//   x - bits(t) < bits(+inf) - bits(t) + 1
+// which also rejects every NaN and every negative number, and no tie count is
+// needed.  NaN slots are counted for every chunk up front (independent of thr).
 //
 // Insertion is kept minimal (ballot + mbcnt position + one ds_write): with a
 // ~1-3% candidate rate nearly every 64-wide slot has a candidate, so every
@@ -200,20 +264,22 @@ struct SelectProc {
     uint32_t cap, tkeep, tstop;
     uint64_t flip;
     uint64_t thr;
-    uint32_t cnt, eqs, nnan;
-    uint32_t fast;              // thr is a non-negative finite number or +0, top side
-    uint64_t tbits, tb1, tlim;  // fast-path constants
+    uint32_t incl;             // 1: inclusive mode (buf = keys >= thr), 0: strict
+    uint32_t cnt, eqs;
+    uint32_t nnan_lane;        // this lane's NaN slots (reduced at the end)
+    uint32_t fast;             // inclusive, top side, thr = key of a number in [+0, +inf]
+    uint64_t tb, tlim;         // fast-path constants
     uint32_t bad;
 #ifdef KRR_DIAG
     unsigned long long diag[D_WORDS];
 #endif
 
-    __device__ __forceinline__ void set_thr(uint64_t t) {
+    __device__ __forceinline__ void set_thr(uint64_t t, uint32_t inclusive) {
         thr = uni64(t);
-        fast = (!flip && (thr & kSignBit) && (thr ^ kSignBit) <= 0x7FF0000000000000ull) ? 1u : 0u;
-        tbits = thr ^ kSignBit;
-        tb1 = tbits + 1;
-        tlim = 0x7FF0000000000000ull - tbits;
+        incl = uni32(inclusive);
+        fast = (incl && !flip && (thr & kSignBit) && (thr ^ kSignBit) <= 0x7FF0000000000000ull) ? 1u : 0u;
+        tb = thr ^ kSignBit;
+        tlim = 0x7FF0000000000001ull - tb;
     }
 
     template <bool FAST>
@@ -221,30 +287,38 @@ struct SelectProc {
         const uint64_t x = dbits(d);
         if (FAST) {
             key = x | kSignBit;
-            return (x - tb1) < tlim;
+            return (x - tb) < tlim;
         }
         key = okey(x) ^ flip;
-        return !__builtin_isnan(d) && key > thr;
+        return !__builtin_isnan(d) && (incl ? key >= thr : key > thr);
     }
 
-    // Count candidates (C), ties with thr (E) and NaN slots (NN) among the slots
+    // NaN slots of a whole chunk (absent samples in the gapped layout), counted
+    // per lane in a VGPR (no 16 live lane masks); reduced once per segment.
+    __device__ __forceinline__ void count_nan(const double2 (&c)[kUnroll]) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) nnan_lane += __builtin_isnan(slot_val(c, j)) ? 1u : 0u;
+    }
+
+    // Count candidates (C) and, in strict mode, ties with thr (E) among the slots
     // in smask; jm = bit j set if slot j has a candidate in some lane.
-    template <bool FAST>
+    // OPAQUE: re-materialise each slot value (general path inside the step loop),
+    // so the compiler cannot hoist 16 slots' keys and masks out of that loop.
+    template <bool FAST, bool OPAQUE = true>
     __device__ __forceinline__ void classify(const double2 (&c)[kUnroll], uint32_t smask, uint32_t& C,
-                                             uint32_t& E, uint32_t& NN, uint32_t& jm) const {
-        C = E = NN = jm = 0;
+                                             uint32_t& E, uint32_t& jm) const {
+        C = E = jm = 0;
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             if ((smask >> j) & 1u) {  // wave-uniform
-                const double d = slot_val(c, j);
+                double d = slot_val(c, j);
+                if (OPAQUE) asm volatile("" : "+v"(d));
                 uint64_t key;
                 const bool cand = is_cand<FAST>(d, key);
-                const bool eq = FAST ? (dbits(d) == tbits) : (!__builtin_isnan(d) && key == thr);
                 const uint64_t m = ballot(cand);
                 C += popc64(m);
                 jm |= m ? (1u << j) : 0u;
-                E += popc64(ballot(eq));
-                NN += popc64(ballot(__builtin_isnan(d)));
+                if (!FAST && !incl) E += popc64(ballot(!__builtin_isnan(d) && key == thr));
             }
         }
     }
@@ -270,17 +344,16 @@ struct SelectProc {
     // Classify the slots in smask, compact once if needed, insert.  Returns false
     // (nothing inserted, nothing counted) if the candidates still do not fit.
     __device__ __forceinline__ bool try_slots(const double2 (&c)[kUnroll], uint32_t smask) {
-        uint32_t C, E, NN, jm;
-        if (uni32(fast)) classify<true>(c, smask, C, E, NN, jm);
-        else classify<false>(c, smask, C, E, NN, jm);
+        uint32_t C, E, jm;
+        if (uni32(fast)) classify<true>(c, smask, C, E, jm);
+        else classify<false>(c, smask, C, E, jm);
         if (cnt + C > cap) {
             compact();
-            if (uni32(fast)) classify<true>(c, smask, C, E, NN, jm);
-            else classify<false>(c, smask, C, E, NN, jm);
+            if (uni32(fast)) classify<true>(c, smask, C, E, jm);
+            else classify<false>(c, smask, C, E, jm);
             if (cnt + C > cap) return false;
         }
         eqs += E;
-        nnan += NN;
         KRR_DIAG_ADD(D_ACTIVE_SLOTS, __popc(jm));
         KRR_DIAG_ADD(D_INSERTED, C);
         if (jm) {
@@ -290,12 +363,29 @@ struct SelectProc {
         return true;
     }
 
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+        KRR_DIAG_ADD(D_CHUNKS, 1);
+        count_nan(c);
+        // Steady state: fast inclusive threshold, the whole chunk fits.
+        if (uni32(fast)) {
+            uint32_t C, E, jm;
+            classify<true, false>(c, 0xFFFFu, C, E, jm);
+            if (cnt + C <= cap) {
+                KRR_DIAG_ADD(D_ACTIVE_SLOTS, __popc(jm));
+                KRR_DIAG_ADD(D_INSERTED, C);
+                if (jm) insert<true>(c, jm);
+                return;
+            }
+        }
+        chunk_general(c);
+    }
+
+    // Compaction, general (slow) threshold test, insertion in halves.
     // After a compaction at most tstop = cap - kChunkElems/2 keys remain, so half a
     // chunk always fits: a chunk with more candidates than the free space (the
     // first chunks of a segment, or a monotone series) goes in as two halves.
     // The halves run through the same inlined body (a 3-iteration loop).
-    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
-        KRR_DIAG_ADD(D_CHUNKS, 1);
+    __device__ __forceinline__ void chunk_general(const double2 (&c)[kUnroll]) {
         uint32_t smask = 0xFFFFu;
 #pragma unroll 1
         for (int step = 0; step < 3; ++step) {
@@ -394,10 +484,11 @@ struct SelectProc {
         return c;
     }
 
-    // Raise thr to nt: keep keys > nt in buf (in place), count keys == nt into eqs.
-    // A block of 4 x 64 keys is read before any of its survivors is written, and
-    // survivors land at or below the block start, so nothing unread is overwritten.
-    __device__ __forceinline__ void filter(uint64_t nt) {
+    // Raise thr to nt: keep keys >= nt (inclusive) or keys > nt (strict; keys == nt
+    // are counted into eqs) in buf, in place.  A block of 4 x 64 keys is read
+    // before any of its survivors is written, and survivors land at or below the
+    // block start, so nothing unread is overwritten.
+    __device__ __forceinline__ void filter(uint64_t nt, uint32_t inclusive) {
         uint32_t w = 0, e = 0;
         for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
             uint64_t x[4];
@@ -409,7 +500,7 @@ struct SelectProc {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const bool in = base + t * kWave + lane < cnt;
-                const bool keep = in && x[t] > nt;
+                const bool keep = in && (inclusive ? x[t] >= nt : x[t] > nt);
                 e += popc64(ballot(in && x[t] == nt));
                 const uint64_t m = ballot(keep);
                 if (keep) buf[w + lane_prefix(m)] = x[t];
@@ -417,14 +508,15 @@ struct SelectProc {
             }
         }
         cnt = uni32(w);
-        eqs = uni32(e);
-        set_thr(nt);
+        eqs = inclusive ? 0u : uni32(e);
+        set_thr(nt, inclusive);
     }
 
-    // Every key in buf is > thr.  Cut at the low edge of the key range holding
-    // the tkeep-th largest so that <= tstop keys stay above it (or at that key
-    // when one key is crowded: then fewer than tkeep stay above).  With
-    // cnt <= tstop there is nothing to gain; the caller inserts in halves.
+    // Cut at the low edge lo of the key range holding the tkeep-th largest, so
+    // that >= tkeep and <= tstop keys stay >= lo (inclusive), or, when that range
+    // is one crowded key, strictly above it with its copies counted in eqs (then
+    // fewer than tkeep stay in buf).  With cnt <= tstop there is nothing to gain;
+    // the caller inserts in halves.
     __device__ __forceinline__ void compact() {
         if (cnt <= tstop) return;
         KRR_DIAG_T0(t0);
@@ -433,11 +525,13 @@ struct SelectProc {
         buf_minmax(mn, mx);
         const uint32_t ts = tstop;
         const Cut ct = locate(tkeep, mn, mx, [ts](uint32_t above, uint32_t c) { return above + c <= ts; });
-        if (!ct.ok || ct.lo <= thr) {  // cannot happen while cnt > tstop >= tkeep; flag it
+        const uint32_t inclusive = ct.above + ct.cnt <= ts ? 1u : 0u;
+        // progress (cannot fail while cnt > tstop >= tkeep; flagged if it does)
+        if (!ct.ok || !(ct.lo > thr || (incl && !inclusive && ct.lo == thr))) {
             bad |= 1u;
             return;
         }
-        filter(ct.lo);
+        filter(ct.lo, inclusive);
         __syncthreads();
         KRR_DIAG_ADD(D_NCOMPACT, 1);
 #ifdef KRR_DIAG
@@ -491,13 +585,14 @@ struct SelectProc {
     // Key of the element with ascending rank r (0-based) among nsel present samples.
     __device__ __forceinline__ uint64_t rank_key(uint64_t r, uint64_t nsel, uint64_t mn, uint64_t mx) {
         const uint64_t rr = flip ? (nsel - 1 - r) : r;
-        const uint64_t below = nsel - cnt - eqs;
+        const uint64_t ties = incl ? 0u : eqs;
+        const uint64_t below = nsel - cnt - ties;
         if (rr < below) {
             bad |= 4u;
             return 0;
         }
-        if (rr < below + eqs) return thr;
-        const uint32_t idx = (uint32_t)(rr - below - eqs);
+        if (rr < below + ties) return thr;
+        const uint32_t idx = (uint32_t)(rr - below - ties);
         return kth_largest(cnt - idx, mn, mx);
     }
 };
@@ -579,14 +674,14 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
         P.flip = sp.bottom ? ~0ull : 0ull;
         P.cnt = 0;
         P.eqs = 0;
-        P.nnan = 0;
+        P.nnan_lane = 0;
         P.bad = 0;
-        P.set_thr(0);
+        P.set_thr(0, 1u);  // inclusive at the lowest key: every sample is a candidate
 #ifdef KRR_DIAG
         for (int d = 0; d < D_WORDS; ++d) P.diag[d] = 0;
         KRR_DIAG_T0(t_begin);
 #endif
-        P.nnan -= stream_segment<true>(A.vals, beg, end, P, lane);  // drop the NaN padding
+        const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);  // NaN padding slots
         __syncthreads();
 #ifdef KRR_DIAG
         KRR_DIAG_T0(t_final);
@@ -594,7 +689,7 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
         uint64_t bmn = 0, bmx = 0;
         if (P.cnt) P.buf_minmax(bmn, bmx);
 
-        const uint64_t nnan = P.nnan;
+        const uint64_t nnan = wave_sum_u32(P.nnan_lane) - pad;
         const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
         uint32_t flags = 0;
         double result;

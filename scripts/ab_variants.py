@@ -1,7 +1,8 @@
 """A/B timing of libkrr_amd build variants in ONE process (interleaved rounds).
 
 Each variant is a separately built .so (different -D flags); all are loaded side by
-side with ctypes and fed the same device-resident synthetic workload.
+side with ctypes and fed the same device-resident synthetic workload.  Times the
+percentile kernel, the max kernel and the fused krr_simple_run launch per variant.
 usage: python scripts/ab_variants.py lib1.so lib2.so ... [--mode linear] [--rounds 5]
 """
 import argparse
@@ -33,10 +34,11 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.init()
     base = _native.load_library()
+    names = ("krr_create", "krr_segmented_percentile", "krr_segmented_max", "krr_simple_run")
     libs = []
     for path in a.libs:
         lib = ctypes.CDLL(os.path.abspath(path))
-        for name in ("krr_create", "krr_segmented_percentile", "krr_segmented_max", "krr_synth_fill"):
+        for name in names:
             getattr(lib, name).argtypes = getattr(base, name).argtypes
             getattr(lib, name).restype = ctypes.c_int
         h = ctypes.c_void_p()
@@ -62,47 +64,50 @@ def main():
     ms = ctx.series(mem, offs, maxlen, gaps)
     params = percentile_params(Decimal(a.percentile), a.mode)
     S = n
-    outs = {}
     stream = torch.cuda.current_stream()
     sp = ctypes.c_void_p(stream.cuda_stream)
-    times = {name: {"pct": [], "max": []} for name, _, _ in libs}
+
+    def outs():
+        return [torch.empty(S, dtype=dt, device=dev) for dt in
+                (torch.float64, torch.int64, torch.int32, torch.float64, torch.int64, torch.int32)]
+
+    o = {name: outs() for name, _, _ in libs}
+    times = {name: {"pct": [], "max": [], "fused": []} for name, _, _ in libs}
     for r in range(a.rounds):
         for name, lib, h in libs:
-            ov = torch.empty(S, dtype=torch.float64, device=dev)
-            on = torch.empty(S, dtype=torch.int64, device=dev)
-            of = torch.empty(S, dtype=torch.int32, device=dev)
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            cv, cn, cf, mv, mn, mf = o[name]
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             e[0].record(stream)
-            rc = lib.krr_segmented_percentile(h, ctypes.byref(cs), ctypes.byref(params), ov.data_ptr(),
-                                              on.data_ptr(), of.data_ptr(), sp)
+            rc = lib.krr_segmented_percentile(h, ctypes.byref(cs), ctypes.byref(params), cv.data_ptr(),
+                                              cn.data_ptr(), cf.data_ptr(), sp)
             e[1].record(stream)
-            rc |= lib.krr_segmented_max(h, ctypes.byref(ms), ov.data_ptr() if False else torch.empty(
-                S, dtype=torch.float64, device=dev).data_ptr(), on.data_ptr(), of.data_ptr(), sp)
+            rc |= lib.krr_segmented_max(h, ctypes.byref(ms), mv.data_ptr(), mn.data_ptr(), mf.data_ptr(), sp)
             e[2].record(stream)
+            rc |= lib.krr_simple_run(h, ctypes.byref(cs), ctypes.byref(ms), ctypes.byref(params),
+                                     cv.data_ptr(), cn.data_ptr(), cf.data_ptr(), mv.data_ptr(), mn.data_ptr(),
+                                     mf.data_ptr(), sp)
+            e[3].record(stream)
             torch.cuda.synchronize()
             assert rc == 0
             times[name]["pct"].append(e[0].elapsed_time(e[1]))
             times[name]["max"].append(e[1].elapsed_time(e[2]))
-            if r == 0:
-                # percentile outputs are overwritten by the count of max? keep a separate check run
-                ov2 = torch.empty(S, dtype=torch.float64, device=dev)
-                lib.krr_segmented_percentile(h, ctypes.byref(cs), ctypes.byref(params), ov2.data_ptr(),
-                                             on.data_ptr(), of.data_ptr(), sp)
-                torch.cuda.synchronize()
-                outs[name] = ov2.cpu().numpy()
-    # parity on a sample vs the oracle
+            times[name]["fused"].append(e[2].elapsed_time(e[3]))
+    # parity on a sample vs the oracle (outputs of the last fused launch)
     m = min(200, S)
     end = int(offs_np[m])
     ov, _, _ = oracle.percentile(cpu[:end].cpu().numpy(), offs_np[: m + 1], params.mode, params.p_num,
                                  params.p_den, params.q, gaps, 16)
-    bytes_pct = 8 * N + 8 * (S + 1) + 20 * S
+    mvo, _, _ = oracle.seg_max(mem[:end].cpu().numpy(), offs_np[: m + 1], gaps, 16)
+    seg_bytes = 8 * N + 8 * (S + 1) + 20 * S
     for name, _, _ in libs:
-        t = np.array(times[name]["pct"])
-        tm = np.array(times[name]["max"])
-        got = outs[name][:m]
-        ok = bool(np.all((got.view(np.uint64) == ov.view(np.uint64)) | ((got == 0) & (ov == 0))))
-        print(f"{name:28s} pct median {np.median(t):.4f} ms min {t.min():.4f} -> {bytes_pct / np.median(t) / 1e9:.0f} GB/s"
-              f" | max median {np.median(tm):.4f} ms | parity {ok}")
+        t = {k: np.median(np.array(v)) for k, v in times[name].items()}
+        got = o[name][0][:m].cpu().numpy()
+        gm = o[name][3][:m].cpu().numpy()
+        ok = bool(np.all((got.view(np.uint64) == ov.view(np.uint64)) | ((got == 0) & (ov == 0)))
+                  and np.array_equal(gm, mvo, equal_nan=True))
+        print(f"{name:28s} pct {t['pct']:.4f} ms ({seg_bytes / t['pct'] / 1e6:.0f} GB/s) | "
+              f"max {t['max']:.4f} ms ({seg_bytes / t['max'] / 1e6:.0f} GB/s) | "
+              f"fused {t['fused']:.4f} ms ({2 * seg_bytes / t['fused'] / 1e6:.0f} GB/s) | parity {ok}", flush=True)
 
 
 if __name__ == "__main__":
