@@ -22,7 +22,12 @@ __device__ __forceinline__ bool is_nan_bits(uint64_t u) { return (u << 1) > 0xFF
 __device__ __forceinline__ bool is_zero_bits(uint64_t u) { return (u << 1) == 0; }
 
 // Order-preserving key: for non-NaN a, b:  a <_IEEE b  <=>  okey(a) < okey(b), with -0 < +0.
-__device__ __forceinline__ uint64_t okey(uint64_t u) { return (u & kSignBit) ? ~u : (u | kSignBit); }
+__device__ __forceinline__ uint64_t okey(uint64_t u) {
+    // x ^ (sign ? all ones : sign bit only): one arithmetic shift, one or, two xors
+    const uint32_t hi = (uint32_t)(u >> 32);
+    const uint32_t m = (uint32_t)((int32_t)hi >> 31);
+    return ((uint64_t)(hi ^ (m | 0x80000000u)) << 32) | (uint32_t)((uint32_t)u ^ m);
+}
 __device__ __forceinline__ uint64_t okey_inv(uint64_t k) { return (k & kSignBit) ? (k ^ kSignBit) : ~k; }
 
 // Force a value the program knows is wave-uniform into scalar registers.
@@ -40,35 +45,82 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// ---- wave64 DPP primitives -------------------------------------------------
+// Inclusive scans run on DPP row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast15 / row_bcast31 carry row totals across rows (GFX9-family DPP, which
+// gfx950 keeps); broadcasts from a uniform lane are v_readlane.  Nothing here
+// needs a ds_bpermute address register, so no lane-address VGPRs get hoisted
+// into the kernels' loops.
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp32(uint32_t ident, uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)x, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t ident, uint64_t x) {
+    const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)ident, (uint32_t)x);
+    const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(ident >> 32), (uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct OpAdd32 {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+struct OpMinU64 {
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return b < a ? b : a; }
+};
+struct OpMaxU64 {
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return b > a ? b : a; }
+};
+
+// Inclusive scan over lanes 0..63 (lane l gets op over lanes 0..l).
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan32(uint32_t x, uint32_t ident, Op op) {
+    x = op(x, dpp32<kDppRowShr1, 0xF>(ident, x));
+    x = op(x, dpp32<kDppRowShr2, 0xF>(ident, x));
+    x = op(x, dpp32<kDppRowShr4, 0xF>(ident, x));
+    x = op(x, dpp32<kDppRowShr8, 0xF>(ident, x));
+    x = op(x, dpp32<kDppRowBcast15, 0xA>(ident, x));
+    x = op(x, dpp32<kDppRowBcast31, 0xC>(ident, x));
+    return x;
+}
+template <class Op>
+__device__ __forceinline__ uint64_t wave_scan64(uint64_t x, uint64_t ident, Op op) {
+    x = op(x, dpp64<kDppRowShr1, 0xF>(ident, x));
+    x = op(x, dpp64<kDppRowShr2, 0xF>(ident, x));
+    x = op(x, dpp64<kDppRowShr4, 0xF>(ident, x));
+    x = op(x, dpp64<kDppRowShr8, 0xF>(ident, x));
+    x = op(x, dpp64<kDppRowBcast15, 0xA>(ident, x));
+    x = op(x, dpp64<kDppRowBcast31, 0xC>(ident, x));
+    return x;
+}
+
+// Value of x in (wave-uniform) lane src, as a scalar.
+__device__ __forceinline__ uint32_t lane_bcast32(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, src);
+}
+__device__ __forceinline__ uint64_t lane_bcast64(uint64_t x, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
-    return uni32(x);
+    return lane_bcast32(wave_scan32(x, 0u, OpAdd32{}), kWave - 1);
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
-        x = y > x ? y : x;
-    }
-    return uni64(x);
+    return lane_bcast64(wave_scan64(x, 0ull, OpMaxU64{}), kWave - 1);
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
-        x = y < x ? y : x;
-    }
-    return uni64(x);
+    return lane_bcast64(wave_scan64(x, ~0ull, OpMinU64{}), kWave - 1);
 }
 // Inclusive suffix sum over lanes: lane l gets sum_{m >= l} x_m.
 __device__ __forceinline__ uint32_t wave_suffix_incl(uint32_t x, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t y = (uint32_t)__shfl_down((int)x, d);
-        if (lane + d < kWave) x += y;
-    }
-    return x;
+    (void)lane;
+    const uint32_t incl = wave_scan32(x, 0u, OpAdd32{});
+    return lane_bcast32(incl, kWave - 1) - incl + x;
 }
 
 // k = floor((n-1) * p_num / (100 * p_den)) exactly (n >= 1, 0 < p <= 100, p_den <= 1e15).

@@ -29,7 +29,10 @@
 #define KRR_STREAM_DEPTH 2  // chunks in flight per wave
 #endif
 #ifndef KRR_SELECT_WAVES_PER_SIMD
-#define KRR_SELECT_WAVES_PER_SIMD 3  // __launch_bounds__ occupancy hint for k_select
+#define KRR_SELECT_WAVES_PER_SIMD 3  // __launch_bounds__ occupancy hint for the single-pass select
+#endif
+#ifndef KRR_HSEL_WAVES_PER_SIMD
+#define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
 
 namespace krr {
@@ -219,9 +222,9 @@ __device__ __forceinline__ BinHit find_bin_desc(const uint32_t* hist, uint32_t R
     BinHit h;
     h.found = m != 0;
     const int src = m ? __ffsll((long long)m) - 1 : 0;
-    h.b = uni32((uint32_t)__shfl(fb, src));
-    h.above = uni32((uint32_t)__shfl((int)fab, src));
-    h.cnt = uni32((uint32_t)__shfl((int)fcb, src));
+    h.b = lane_bcast32((uint32_t)fb, src);
+    h.above = lane_bcast32(fab, src);
+    h.cnt = lane_bcast32(fcb, src);
     return h;
 }
 
@@ -579,7 +582,7 @@ struct SelectProc {
             bad |= 8u;
             return 0;
         }
-        return uni64((uint64_t)__shfl((unsigned long long)v, __ffsll((long long)sel) - 1));
+        return lane_bcast64(v, __ffsll((long long)sel) - 1);
     }
 
     // Key of the element with ascending rank r (0-based) among nsel present samples.
@@ -625,7 +628,7 @@ __device__ uint64_t nth_zero_bits(const double* __restrict__ vals, int64_t beg, 
             const uint32_t want = (uint32_t)(j - run);
             const uint64_t sel = ballot(z && lane_prefix(m) == want);
             const int src = __ffsll((long long)sel) - 1;
-            return uni64((uint64_t)__shfl((unsigned long long)u, src));
+            return lane_bcast64(u, src);
         }
         run += c;
     }
@@ -648,23 +651,78 @@ struct SelectArgs {
     int32_t gaps;
     int64_t p_num, p_den;
     double q;
-    uint32_t cap;
-    uint64_t* gscratch;  // non-null: candidate buffers live in HBM scratch, cap keys per block
+    uint32_t cap;        // single-pass candidate capacity (keys); longer segments use hselect
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
 };
 
-// One CPU segment (SORTED_LOWER / LINEAR) by one wave.
-// LDS (smem): [H 1 KiB][gather 512 B][candidate keys cap x 8 B] unless buf is HBM scratch.
-__device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem,
-                                               uint64_t* buf, int lane) {
+// Ranks a SORTED_LOWER / LINEAR result needs among n present samples (ascending,
+// 0-based): SORTED_LOWER r0 = r1 = k; LINEAR numpy's prev/next with its gamma.
+struct Ranks {
+    int64_t r0, r1;
+    double gamma;
+};
+
+__device__ __forceinline__ Ranks ranks_for(const SelectArgs& A, uint64_t n) {
+    Ranks R;
+    R.gamma = 0.0;
+    if (A.mode == KRR_PCT_SORTED_LOWER) {
+        R.r0 = R.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+    } else {  // KRR_PCT_LINEAR, numpy method="linear"
+        const double vidx = __dmul_rn((double)(n - 1), A.q);
+        if (vidx >= (double)(n - 1)) {
+            R.r0 = R.r1 = (int64_t)n - 1;
+            R.gamma = __dsub_rn(vidx, -1.0);  // numpy subtracts the clipped index -1
+        } else {
+            const double fl = floor(vidx);
+            R.r0 = (int64_t)fl;
+            R.r1 = R.r0 + 1;
+            R.gamma = __dsub_rn(vidx, fl);
+        }
+    }
+    return R;
+}
+
+// Result from the ascending keys k0 (rank r0) and k1 (rank r1).
+__device__ __forceinline__ double finish_value(const SelectArgs& A, const Ranks& R, uint64_t k0, uint64_t k1,
+                                               int64_t beg, int64_t end, int lane) {
+    const double a = bitsd(okey_inv(k0));
+    if (A.mode == KRR_PCT_SORTED_LOWER) {
+        uint64_t bits = dbits(a);
+        if (is_zero_bits(bits)) {
+            // Python sorted() is stable and -0 == +0: the zero at rank r is the
+            // (r - #negatives)-th zero in position order.
+            const uint64_t neg = count_negative(A.vals, beg, end, lane);
+            bits = nth_zero_bits(A.vals, beg, end, (uint64_t)R.r0 - neg, lane);
+        }
+        return bitsd(bits);
+    }
+    const double b = R.r1 != R.r0 ? bitsd(okey_inv(k1)) : a;
+    return np_lerp(a, b, R.gamma);
+}
+
+__device__ __forceinline__ void write_result(const SelectArgs& A, int64_t s, double v, uint64_t n, uint32_t flags,
+                                             int lane) {
+    if (lane == 0) {
+        A.out_v[s] = v;
+        A.out_n[s] = (int64_t)n;
+        A.out_f[s] = flags;
+    }
+}
+
+// LDS of the select kernels: [H 1 KiB][gather 512 B] then, from kSelectLdsFixed,
+// either the single-pass candidate keys (cap x 8 B) or hselect's histogram
+// (kHistBins x 4 B) + collect buffer (kCollectCap x 8 B).
+
+// One CPU segment (SORTED_LOWER / LINEAR) by one wave, single HBM pass.
+__device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t L = end - beg;
         const SidePlan sp = plan_side(L, A.mode, A.p_num, A.p_den, A.q);
         SelectProc P;
-        P.buf = buf;
+        P.buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
         P.H = reinterpret_cast<uint32_t*>(smem);
         P.small = reinterpret_cast<uint64_t*>(smem + 1024);
         P.lane = lane;
@@ -692,54 +750,23 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
         const uint64_t nnan = wave_sum_u32(P.nnan_lane) - pad;
         const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
         uint32_t flags = 0;
-        double result;
+        double result = bitsd(kQuietNaN);
         if (n == 0) {
-            result = bitsd(kQuietNaN);
             flags |= KRR_FLAG_EMPTY;
         } else if (nnan && !A.gaps) {
-            result = bitsd(kQuietNaN);
             flags |= KRR_FLAG_NAN;
         } else {
-            // ranks needed: SORTED_LOWER r0; LINEAR numpy prev/next.  One rank-query
-            // body serves both (a 1-2 iteration loop keeps it inlined once).
-            int64_t r0, r1;
-            double gamma = 0.0;
-            if (A.mode == KRR_PCT_SORTED_LOWER) {
-                r0 = r1 = exact_rank(n, A.p_num, A.p_den);
-            } else {  // KRR_PCT_LINEAR, numpy method="linear"
-                const double vidx = __dmul_rn((double)(n - 1), A.q);
-                if (vidx >= (double)(n - 1)) {
-                    r0 = r1 = (int64_t)n - 1;
-                    gamma = __dsub_rn(vidx, -1.0);  // numpy subtracts the clipped index -1
-                } else {
-                    const double fl = floor(vidx);
-                    r0 = (int64_t)fl;
-                    r1 = r0 + 1;
-                    gamma = __dsub_rn(vidx, fl);
-                }
-            }
+            const Ranks R = ranks_for(A, n);
             uint64_t k0 = 0, k1 = 0;
-            const int nq = r1 != r0 ? 2 : 1;
+            // one rank-query body serves both ranks (a 1-2 iteration loop keeps it inlined once)
+            const int nq = R.r1 != R.r0 ? 2 : 1;
 #pragma unroll 1
             for (int qi = 0; qi < nq; ++qi) {
-                const uint64_t kq = P.rank_key((uint64_t)(qi ? r1 : r0), n, bmn, bmx);
+                const uint64_t kq = P.rank_key((uint64_t)(qi ? R.r1 : R.r0), n, bmn, bmx) ^ P.flip;
                 if (qi) k1 = kq;
                 else k0 = kq;
             }
-            const double a = bitsd(okey_inv(k0 ^ P.flip));
-            if (A.mode == KRR_PCT_SORTED_LOWER) {
-                uint64_t bits = dbits(a);
-                if (is_zero_bits(bits)) {
-                    // Python sorted() is stable and -0 == +0: the zero at rank r is the
-                    // (r - #negatives)-th zero in position order.
-                    const uint64_t neg = count_negative(A.vals, beg, end, lane);
-                    bits = nth_zero_bits(A.vals, beg, end, (uint64_t)r0 - neg, lane);
-                }
-                result = bitsd(bits);
-            } else {
-                const double b = nq == 2 ? bitsd(okey_inv(k1 ^ P.flip)) : a;
-                result = np_lerp(a, b, gamma);
-            }
+            result = finish_value(A, R, k0, k1, beg, end, lane);
         }
         if (P.bad) flags |= KRR_FLAG_CAPACITY | (P.bad << 8);  // reason bits (diagnostic)
 #ifdef KRR_DIAG
@@ -751,29 +778,338 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
                 for (int d = 0; d < D_WORDS; ++d) g_diag[(size_t)s * D_WORDS + d] = P.diag[d];
         }
 #endif
-        if (lane == 0) {
-            A.out_v[s] = result;
-            A.out_n[s] = (int64_t)n;
-            A.out_f[s] = flags;
-        }
+        write_result(A, s, result, n, flags, lane);
         __syncthreads();
     }
 }
 
-// GBUF selects where candidate buffers live at COMPILE time, so the LDS variant
-// emits ds_* (lgkmcnt) and never flat_* stores, which would force vmcnt(0)
-// waits and serialise the prefetch pipeline.
-template <bool GBUF>
-__device__ __forceinline__ uint64_t* select_buffer(const SelectArgs& A, unsigned char* smem) {
-    if constexpr (GBUF) return A.gscratch + (size_t)blockIdx.x * A.cap;
-    else return reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+// ---------------------------------------------------------------------------
+// hselect: exact order statistics of a segment whose candidate set would not
+// fit LDS (mid percentiles of long series: p50 of 50,400 samples needs 25k
+// keys).  A streaming histogram pass over a key range [lo, hi] (kHistBins
+// bins, LDS atomics) locates the bin holding the needed ranks, counting the
+// keys below lo; a second streaming pass collects that bin's keys (expected
+// ~100) into LDS, where the ranks are selected exactly.  The first range comes
+// from a 64-sample strided probe of the segment widened 16x each way in value
+// (4 exponents in key space), so two HBM passes are the common case; a rank
+// that falls outside [lo, hi] or into a bin with more than kCollectCap keys
+// refines the range and repeats (bounded).  Zeros are counted apart when they
+// lie below lo, so a mostly-zero series resolves in the first pass.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kKeyNegInf = 0x000FFFFFFFFFFFFFull;  // okey(-inf)
+constexpr uint64_t kKeyPosInf = 0xFFF0000000000000ull;  // okey(+inf)
+constexpr uint64_t kKeyNegZero = 0x7FFFFFFFFFFFFFFFull; // okey(-0)
+constexpr uint64_t kKeyPosZero = 0x8000000000000000ull; // okey(+0)
+
+template <bool FIRST, bool ZSPLIT>
+struct HistProc {
+    uint32_t* hist;
+    uint64_t lo, span;
+    uint32_t sh;
+    uint32_t below_l, zb_l, z0_l, nan_l, nneg_l;  // per-lane counters
+
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double d = slot_val(c, j);
+            const uint64_t x = dbits(d);
+            const uint64_t key = okey(x);
+            below_l += key < lo ? 1u : 0u;  // + negative NaNs (key < okey(-inf)); removed later
+            if (ZSPLIT) {
+                zb_l += key <= kKeyPosZero ? 1u : 0u;  // negatives, -0, +0 (+ negative NaNs)
+                z0_l += x == 0 ? 1u : 0u;
+            }
+            if (FIRST) {
+                const bool nan = __builtin_isnan(d);
+                nan_l += nan ? 1u : 0u;
+                nneg_l += (nan && (x & kSignBit)) ? 1u : 0u;
+            }
+            const uint64_t t = key - lo;
+            if (t <= span) atomicAdd(&hist[(uint32_t)(t >> sh)], 1u);
+            // one slot at a time: nothing of this slot stays live into the next
+            asm volatile("" ::: "memory");
+        }
+    }
+};
+
+struct HistCounts {
+    uint32_t pad, below_l, zb_l, z0_l, nan_l, nneg_l;
+};
+
+template <bool FIRST, bool ZSPLIT>
+__device__ __forceinline__ HistCounts hist_pass(const double* vals, int64_t beg, int64_t end, uint32_t* hist,
+                                                uint64_t lo, uint64_t span, uint32_t sh, int lane) {
+    HistProc<FIRST, ZSPLIT> HP;
+    HP.hist = hist;
+    HP.lo = lo;
+    HP.span = span;
+    HP.sh = sh;
+    HP.below_l = HP.zb_l = HP.z0_l = HP.nan_l = HP.nneg_l = 0;
+    HistCounts hc;
+    hc.pad = stream_segment<true>(vals, beg, end, HP, lane);
+    hc.below_l = HP.below_l;
+    hc.zb_l = HP.zb_l;
+    hc.z0_l = HP.z0_l;
+    hc.nan_l = HP.nan_l;
+    hc.nneg_l = HP.nneg_l;
+    return hc;
 }
 
-template <bool GBUF>
-__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
+struct CollectProc {
+    uint64_t* buf;
+    uint64_t lo, span;
+    uint32_t cnt;
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const uint64_t key = okey(dbits(slot_val(c, j)));
+            const bool in = key - lo <= span;  // NaN keys lie outside [okey(-inf), okey(+inf)]
+            const uint64_t m = ballot(in);
+            if (m) {
+                if (in) buf[cnt + lane_prefix(m)] = key;
+                cnt = uni32(cnt + popc64(m));
+            }
+        }
+    }
+};
+
+// Lane l's share of the histogram is bins [32 l, 32 l + 32): its total and the
+// inclusive prefix of the totals over lanes.
+struct HistScan {
+    uint32_t t, incl, total;
+};
+
+__device__ __forceinline__ HistScan hist_scan(const uint32_t* hist, int lane) {
+    constexpr uint32_t per = kHistBins / kWave;
+    static_assert(per % 4 == 0, "bins per lane");
+    const uint4* h4 = reinterpret_cast<const uint4*>(hist + (uint32_t)lane * per);
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < per / 4; ++j) {
+        const uint4 v = h4[j];
+        t += v.x + v.y + v.z + v.w;
+    }
+    const uint32_t incl = wave_scan32(t, 0u, OpAdd32{});
+    HistScan hs;
+    hs.t = t;
+    hs.incl = incl;
+    hs.total = lane_bcast32(incl, kWave - 1);
+    return hs;
+}
+
+// Bin holding ascending rank r (0-based, r < total, relative to the histogram's
+// first key): bin index, keys in earlier bins, keys in the bin.
+__device__ __forceinline__ void hist_find(const uint32_t* hist, const HistScan& hs, uint64_t r, int lane,
+                                          uint32_t& b, uint64_t& before, uint32_t& cnt) {
+    constexpr uint32_t per = kHistBins / kWave;
+    const uint32_t rr = (uint32_t)r;
+    const uint64_t m = ballot(rr < hs.incl);
+    const int src = __ffsll((long long)m) - 1;
+    const uint32_t base = lane_bcast32(hs.incl - hs.t, src);
+    // second level: lane j < per looks at bin src * per + j
+    const uint32_t h = (uint32_t)lane < per ? hist[(uint32_t)src * per + (uint32_t)lane] : 0u;
+    const uint32_t incl = wave_scan32(h, 0u, OpAdd32{});
+    const uint64_t m2 = ballot((uint32_t)lane < per && rr - base < incl);
+    const int sel = __ffsll((long long)m2) - 1;
+    b = (uint32_t)src * per + (uint32_t)sel;
+    cnt = lane_bcast32(h, sel);
+    before = base + lane_bcast32(incl - h, sel);
+}
+
+// A resolved rank: either an exact key or a key range [lo, hi] holding `count`
+// keys with `below` keys smaller than lo.
+struct RankLoc {
+    uint64_t lo, hi, below, count;
+    uint32_t exact;
+};
+
+__device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
+    {
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        const int64_t L = end - beg;
+        uint32_t* hist = reinterpret_cast<uint32_t*>(smem + kSelectLdsFixed);
+        uint64_t* cbuf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed + kHistBins * 4);
+        uint32_t bad = 0;
+
+        // 64-sample strided probe -> first key range
+        uint64_t kmn = ~0ull, kmx = 0;
+        if (L > 0) {
+            const int64_t i = L >= kWave ? ((int64_t)lane * L) / kWave : (lane < L ? lane : 0);
+            const uint64_t x = dbits(A.vals[beg + i]);
+            const bool ok = !is_nan_bits(x) && !is_zero_bits(x);
+            const uint64_t k = okey(x);
+            kmn = ok ? k : ~0ull;
+            kmx = ok ? k : 0ull;
+        }
+        kmn = wave_min_u64(kmn);
+        kmx = wave_max_u64(kmx);
+        constexpr uint64_t kWiden = 4ull << 52;  // 16x in value
+        uint64_t lo = kKeyNegInf, hi = kKeyPosInf;
+        if (kmn <= kmx) {
+            lo = kmn >= kKeyNegInf + kWiden ? kmn - kWiden : kKeyNegInf;
+            hi = kmx <= kKeyPosInf - kWiden ? kmx + kWiden : kKeyPosInf;
+        }
+
+        uint64_t n = 0, nneg = 0;
+        uint32_t flags = 0;
+        double result = bitsd(kQuietNaN);
+        Ranks R;
+        R.r0 = R.r1 = 0;
+        R.gamma = 0.0;
+        RankLoc loc[2];
+        uint32_t done = 0;
+#pragma unroll 1
+        for (int pass = 0; pass < 10 && !done; ++pass) {
+            // ---- histogram pass over [lo, hi]
+            const uint64_t span = hi - lo;
+            const int bits = span ? 64 - __clzll((long long)span) : 0;
+            const uint32_t sh = bits > kHistBits ? (uint32_t)(bits - kHistBits) : 0u;
+            for (uint32_t i = lane; i < kHistBins; i += kWave) hist[i] = 0;
+            __syncthreads();
+            const uint32_t zsplit = lo > kKeyPosZero ? 1u : 0u;
+            HistCounts HP;
+            if (pass == 0) {
+                if (zsplit) HP = hist_pass<true, true>(A.vals, beg, end, hist, lo, span, sh, lane);
+                else HP = hist_pass<true, false>(A.vals, beg, end, hist, lo, span, sh, lane);
+            } else {
+                if (zsplit) HP = hist_pass<false, true>(A.vals, beg, end, hist, lo, span, sh, lane);
+                else HP = hist_pass<false, false>(A.vals, beg, end, hist, lo, span, sh, lane);
+            }
+            const uint32_t pad = HP.pad;
+            __syncthreads();
+            if (pass == 0) {
+                const uint64_t nnan = wave_sum_u32(HP.nan_l) - pad;
+                nneg = wave_sum_u32(HP.nneg_l);
+                n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;
+                if (n == 0) {
+                    flags |= KRR_FLAG_EMPTY;
+                    break;
+                }
+                if (nnan && !A.gaps) {
+                    flags |= KRR_FLAG_NAN;
+                    break;
+                }
+                R = ranks_for(A, n);
+            }
+            const uint64_t below = wave_sum_u32(HP.below_l) - nneg;
+            const uint64_t zb = zsplit ? wave_sum_u32(HP.zb_l) - nneg : 0;
+            const uint64_t z0 = zsplit ? wave_sum_u32(HP.z0_l) : 0;
+            const HistScan hs = hist_scan(hist, lane);
+            const uint64_t inr = hs.total;
+            // locate both ranks
+#pragma unroll 1
+            for (int qi = 0; qi < 2; ++qi) {
+                const uint64_t r = (uint64_t)(qi ? R.r1 : R.r0);
+                RankLoc& l = loc[qi];
+                l.exact = 0;
+                if (r < below) {
+                    if (zsplit && r >= zb - z0 && r < zb) {
+                        l.exact = 1;
+                        l.lo = l.hi = kKeyPosZero;
+                    } else if (zsplit && r < zb) {
+                        l.lo = kKeyNegInf;
+                        l.hi = kKeyNegZero;
+                        l.below = 0;
+                        l.count = zb - z0;
+                    } else if (zsplit) {
+                        l.lo = kKeyPosZero + 1;
+                        l.hi = lo - 1;
+                        l.below = zb;
+                        l.count = below - zb;
+                    } else {
+                        l.lo = kKeyNegInf;
+                        l.hi = lo - 1;
+                        l.below = 0;
+                        l.count = below;
+                    }
+                } else if (r < below + inr) {
+                    uint32_t b, c;
+                    uint64_t before;
+                    hist_find(hist, hs, r - below, lane, b, before, c);
+                    l.lo = lo + ((uint64_t)b << sh);
+                    const uint64_t w = (1ull << sh) - 1;
+                    l.hi = hi - l.lo <= w ? hi : l.lo + w;
+                    l.below = below + before;
+                    l.count = c;
+                } else {
+                    l.lo = hi + 1;
+                    l.hi = kKeyPosInf;
+                    l.below = below + inr;
+                    l.count = n - below - inr;
+                }
+                if (!l.exact && l.lo == l.hi) l.exact = 1;
+            }
+            __syncthreads();
+            if (loc[0].exact && loc[1].exact) {
+                done = 1;
+                break;
+            }
+            // the key range still to resolve (one range, or the union of two)
+            RankLoc u = loc[0].exact ? loc[1] : loc[0];
+            if (!loc[0].exact && !loc[1].exact && (loc[1].lo != loc[0].lo || loc[1].hi != loc[0].hi)) {
+                u.lo = loc[0].lo;
+                u.hi = loc[1].hi;
+                u.below = loc[0].below;
+                u.count = loc[1].below + loc[1].count - loc[0].below;
+            }
+            if (u.count <= kCollectCap) {
+                // ---- collect pass: the range's keys into LDS, select there
+                CollectProc CP;
+                CP.buf = cbuf;
+                CP.lo = u.lo;
+                CP.span = u.hi - u.lo;
+                CP.cnt = 0;
+                stream_segment<true>(A.vals, beg, end, CP, lane);
+                __syncthreads();
+                if (CP.cnt != (uint32_t)u.count) {
+                    bad |= 32u;
+                    break;
+                }
+                SelectProc P;
+                P.buf = cbuf;
+                P.H = reinterpret_cast<uint32_t*>(smem);
+                P.small = reinterpret_cast<uint64_t*>(smem + 1024);
+                P.lane = lane;
+                P.cnt = CP.cnt;
+                P.bad = 0;
+                uint64_t mn, mx;
+                P.buf_minmax(mn, mx);
+#pragma unroll 1
+                for (int qi = 0; qi < 2; ++qi) {
+                    if (loc[qi].exact) continue;
+                    const uint64_t r = (uint64_t)(qi ? R.r1 : R.r0);
+                    const uint64_t idx = r - u.below;  // ascending index in the range
+                    loc[qi].lo = P.kth_largest((uint32_t)(u.count - idx), mn, mx);
+                    loc[qi].exact = 1;
+                }
+                bad |= P.bad;
+                done = 1;
+                break;
+            }
+            // ---- refine: histogram the range again
+            lo = u.lo;
+            hi = u.hi;
+        }
+        if (n && !(flags & (KRR_FLAG_EMPTY | KRR_FLAG_NAN))) {
+            if (done) result = finish_value(A, R, loc[0].lo, loc[1].lo, beg, end, lane);
+            else bad |= 64u;
+        }
+        if (bad) flags |= KRR_FLAG_CAPACITY | (bad << 8);
+        write_result(A, s, result, n, flags, lane);
+        __syncthreads();
+    }
+}
+
+// k_select<false>: every segment in one pass (the launch's longest segment fits
+// A.cap keys); k_select<true>: every segment through hselect.  Separate kernels
+// keep each one's register allocation to its own path.
+template <bool HSEL>
+__global__ __launch_bounds__(64, HSEL ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* buf = select_buffer<GBUF>(A, smem);
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) select_segment(A, s, smem, buf, threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        if constexpr (HSEL) hselect_segment(A, s, smem, threadIdx.x);
+        else select_segment(A, s, smem, threadIdx.x);
+    }
 }
 
 // --------------------------- REF_INDEX ------------------------------------
@@ -821,7 +1157,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
                     const uint32_t c = popc64(m);
                     if (run + c > j) {
                         const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(j - run));
-                        found = uni64((uint64_t)__shfl((unsigned long long)u, __ffsll((long long)sel) - 1));
+                        found = lane_bcast64(u, __ffsll((long long)sel) - 1);
                         break;
                     }
                     run += c;
@@ -836,7 +1172,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
                     const uint32_t c = popc64(m);
                     if (run + c > k) {
                         const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(k - run));
-                        found = uni64((uint64_t)__shfl((unsigned long long)u, __ffsll((long long)sel) - 1));
+                        found = lane_bcast64(u, __ffsll((long long)sel) - 1);
                         break;
                     }
                     run += c;
@@ -890,10 +1226,11 @@ struct MaxProc {
     }
 };
 
+struct OpMaxF64Bits {  // fmax on f64 bit patterns: the non-NaN operand wins
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return dbits(fmax(bitsd(a), bitsd(b))); }
+};
 __device__ __forceinline__ double wave_max_f64(double x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
-    return x;
+    return bitsd(lane_bcast64(wave_scan64(dbits(x), kQuietNaN, OpMaxF64Bits{}), kWave - 1));
 }
 
 struct MaxArgs {
@@ -946,16 +1283,17 @@ __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
 // The dispatcher hands out blocks in order, so the shorter memory-max blocks
 // fill CUs as the CPU blocks drain instead of leaving a partly idle last round
 // per kernel; one launch is also one roofline for the whole step.
-enum { CPU_SELECT = 0, CPU_REF_GAPS = 1 };
+enum { CPU_SELECT = 0, CPU_REF_GAPS = 1, CPU_HSELECT = 2 };
 
-template <bool GBUF, int CPU_KIND>
-__global__ __launch_bounds__(64, KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
+template <int CPU_KIND>
+__global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int64_t S_cpu = CPU_KIND == CPU_SELECT ? A.S : R.S;
+    const int64_t S_cpu = CPU_KIND == CPU_REF_GAPS ? R.S : A.S;
     const int64_t total = S_cpu + M.S;
     for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
         if (b < S_cpu) {
-            if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, b, smem, select_buffer<GBUF>(A, smem), threadIdx.x);
+            if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, b, smem, threadIdx.x);
+            else if constexpr (CPU_KIND == CPU_HSELECT) hselect_segment(A, b, smem, threadIdx.x);
             else refindex_gaps_segment(R, b, threadIdx.x);
         } else {
             max_segment<true>(M, b - S_cpu, threadIdx.x);
@@ -1056,8 +1394,6 @@ struct krr_ctx {
     int device;
     int num_cus;
     size_t max_lds;
-    uint64_t* scratch;
-    size_t scratch_bytes;
     unsigned long long* d_tmp;
     char err[512];
 };
@@ -1121,18 +1457,18 @@ int check_series(krr_ctx* ctx, const krr_series* s) {
     return KRR_OK;
 }
 
-// Plan a SORTED_LOWER / LINEAR launch: candidate capacity from the longest
-// segment, LDS bytes, and (when the buffers do not fit LDS) the HBM scratch
-// for a persistent grid of `*grid` blocks.  `extra_blocks` = work items after
-// the CPU segments in the same launch (the fused kernel's memory segments).
+// Plan a SORTED_LOWER / LINEAR launch: single-pass candidate capacity from the
+// longest segment, or (when that exceeds kSingleCapMax keys) the hselect path
+// for every segment (A->cap = 0), and the LDS bytes.
 int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_params* params,
-                hipStream_t st, int64_t extra_blocks, double* ov, int64_t* on, uint32_t* of,
-                SelectArgs* A, size_t* lds, int64_t* grid) {
+                hipStream_t st, double* ov, int64_t* on, uint32_t* of, SelectArgs* A, size_t* lds) {
     int64_t Lmax = 0;
     int rc = resolve_maxlen(ctx, series, st, &Lmax);
     if (rc) return rc;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
-    const uint32_t cap = capacity_for(sp.tkeep);
+    const uint32_t need = capacity_for(sp.tkeep);
+    const bool hsel = need > kSingleCapMax;  // every segment of the launch through hselect
+    const uint32_t cap = hsel ? 0u : need;
     *A = SelectArgs{};
     A->vals = series->values;
     A->offs = series->offsets;
@@ -1143,27 +1479,11 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->p_den = params->p_den;
     A->q = params->q;
     A->cap = cap;
-    A->gscratch = nullptr;
     A->out_v = ov;
     A->out_n = on;
     A->out_f = of;
-    const int64_t items = series->n_segments + extra_blocks;
-    *lds = kSelectLdsFixed + (size_t)cap * 8;
-    *grid = items;
-    if (*lds <= ctx->max_lds) return KRR_OK;
-    // Candidate buffers too large for LDS (e.g. p near 50 on very long series):
-    // same algorithm with per-block buffers in HBM scratch, persistent grid.
-    *lds = kSelectLdsFixed;
-    *grid = (int64_t)ctx->num_cus * 8 < items ? (int64_t)ctx->num_cus * 8 : items;
-    const size_t need = (size_t)*grid * cap * 8;
-    if (need > ctx->scratch_bytes) {
-        if (ctx->scratch) KRR_HIP(ctx, hipFree(ctx->scratch));
-        ctx->scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        KRR_HIP(ctx, hipMalloc(&ctx->scratch, need));
-        ctx->scratch_bytes = need;
-    }
-    A->gscratch = ctx->scratch;
+    *lds = kSelectLdsFixed + (hsel ? kHselectLds : (size_t)cap * 8);
+    if (*lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "select needs %s%lld B of LDS", "", (long long)*lds);
     return KRR_OK;
 }
 
@@ -1190,8 +1510,6 @@ int krr_create(int device, krr_ctx** out_ctx) {
     krr_ctx* c = new (std::nothrow) krr_ctx();
     if (!c) return KRR_E_INVALID;
     c->device = device;
-    c->scratch = nullptr;
-    c->scratch_bytes = 0;
     c->d_tmp = nullptr;
     c->err[0] = 0;
     int ndev = 0;
@@ -1214,7 +1532,11 @@ int krr_create(int device, krr_ctx** out_ctx) {
     }
     (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
-    (void)hipFuncSetAttribute((const void*)k_simple<false, CPU_SELECT>,
+    (void)hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)c->max_lds);
+    (void)hipFuncSetAttribute((const void*)k_simple<CPU_SELECT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
+    (void)hipFuncSetAttribute((const void*)k_simple<CPU_HSELECT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -1223,7 +1545,6 @@ int krr_create(int device, krr_ctx** out_ctx) {
 int krr_destroy(krr_ctx* ctx) {
     if (!ctx) return KRR_OK;
     DeviceGuard g(ctx->device);
-    if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
     delete ctx;
     return KRR_OK;
@@ -1258,11 +1579,10 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
 
     SelectArgs A;
     size_t lds = 0;
-    int64_t grid = 0;
-    rc = plan_select(ctx, series, params, st, 0, out_value, out_count, out_flags, &A, &lds, &grid);
+    rc = plan_select(ctx, series, params, st, out_value, out_count, out_flags, &A, &lds);
     if (rc) return rc;
-    if (A.gscratch) hipLaunchKernelGGL(k_select<true>, dim3((unsigned)grid), dim3(64), lds, st, A);
-    else hipLaunchKernelGGL(k_select<false>, dim3(grid_for(grid)), dim3(64), lds, st, A);
+    if (A.cap) hipLaunchKernelGGL(k_select<false>, dim3(grid_for(S)), dim3(64), lds, st, A);
+    else hipLaunchKernelGGL(k_select<true>, dim3(grid_for(S)), dim3(64), lds, st, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
@@ -1312,16 +1632,13 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
     RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags};
     SelectArgs A{};
     if (params->mode == KRR_PCT_REF_INDEX) {
-        hipLaunchKernelGGL((k_simple<false, CPU_REF_GAPS>), dim3(grid_for(2 * S)), dim3(64), 0, st, A, R, M);
+        hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(2 * S)), dim3(64), 0, st, A, R, M);
     } else {
         size_t lds = 0;
-        int64_t grid = 0;
-        rc = plan_select(ctx, cpu, params, st, S, cpu_value, cpu_count, cpu_flags, &A, &lds, &grid);
+        rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds);
         if (rc) return rc;
-        if (A.gscratch)
-            hipLaunchKernelGGL((k_simple<true, CPU_SELECT>), dim3((unsigned)grid), dim3(64), lds, st, A, R, M);
-        else
-            hipLaunchKernelGGL((k_simple<false, CPU_SELECT>), dim3(grid_for(grid)), dim3(64), lds, st, A, R, M);
+        if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
+        else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
     }
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;

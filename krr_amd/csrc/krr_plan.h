@@ -79,11 +79,24 @@ constexpr uint32_t kChunkElems = 2u * kUnroll * 64u;
 // chunk always fits; the 128-key margin above tkeep is what a histogram cut may
 // keep beyond tkeep before the exact fallback is needed.  The first chunk of a
 // segment (every sample a candidate) must fit an empty buffer.
-inline uint32_t capacity_for(uint32_t tkeep_max) {
+KRR_HD inline uint32_t capacity_for(uint32_t tkeep_max) {
     uint64_t c = (uint64_t)tkeep_max + kChunkElems / 2 + 128;
     if (c < kChunkElems + 64) c = kChunkElems + 64;
     c = (c + 63) & ~63ull;
     return (uint32_t)c;
 }
+
+// Largest single-pass candidate capacity (keys); a segment needing more is
+// selected by hselect (histogram pass + collect pass) instead.
+#ifndef KRR_SINGLE_CAP_MAX
+#define KRR_SINGLE_CAP_MAX 2048
+#endif
+constexpr uint32_t kSingleCapMax = KRR_SINGLE_CAP_MAX;
+
+// hselect LDS after kSelectLdsFixed: histogram + collect buffer.
+constexpr int kHistBits = 11;
+constexpr uint32_t kHistBins = 1u << kHistBits;
+constexpr uint32_t kCollectCap = 1024;
+constexpr size_t kHselectLds = (size_t)kHistBins * 4 + (size_t)kCollectCap * 8;
 
 }  // namespace krr

@@ -169,8 +169,8 @@ def test_unaligned_offsets(ctx):
         _assert_same(got, want, mode, f"unaligned {mode}")
 
 
-def test_large_candidate_set_uses_scratch(ctx):
-    """p=50 on 50,400-sample series keeps ~25k keys: the HBM-scratch variant."""
+def test_large_candidate_set_uses_hselect(ctx):
+    """p=50 on 50,400-sample series would keep ~25k keys: the histogram + collect path."""
     rng = np.random.default_rng(21)
     S, L = 40, 50400
     vals = rng.gamma(2.0, 0.05, size=S * L)
@@ -178,7 +178,79 @@ def test_large_candidate_set_uses_scratch(ctx):
     for mode in ("sorted_lower", "linear"):
         got = _run_gpu(ctx, vals, offs, mode, 50, 1)
         want = _oracle(vals, offs, mode, 50, 1)
-        _assert_same(got, want, mode, f"scratch {mode}")
+        _assert_same(got, want, mode, f"hselect {mode}")
+
+
+def _hselect_segments(L, rng):
+    """Series that stress hselect's range estimate, refinement and zero handling."""
+    segs = {}
+    segs["gamma"] = rng.gamma(2.0, 0.05, size=L)
+    z = rng.gamma(2.0, 0.05, size=L)
+    z[rng.random(L) < 0.7] = 0.0
+    segs["mostly_zero"] = z
+    m = rng.random(L) * 1e-9  # the strided probe sees only 1.0: ranks fall below its range
+    m[(np.arange(64) * L) // 64] = 1.0
+    segs["probe_misled_low"] = m
+    h = 1.0 + rng.random(L) * 1e-3
+    h[(np.arange(64) * L) // 64] = 1e-6  # ... and above it
+    h[rng.random(L) < 0.4] = 1e12
+    segs["probe_misled_high"] = h
+    c = rng.gamma(2.0, 0.05, size=L)
+    c[rng.random(L) < 0.6] = 0.5  # one crowded value in the middle
+    segs["crowded_middle"] = c
+    segs["normal_signed"] = rng.normal(size=L)
+    sp = rng.normal(size=L)
+    u = rng.random(L)
+    sp[u < 0.2] = -0.0
+    sp[(u >= 0.2) & (u < 0.4)] = 0.0
+    sp[(u >= 0.4) & (u < 0.45)] = np.inf
+    sp[(u >= 0.45) & (u < 0.5)] = -np.inf
+    segs["signed_zero_inf"] = sp
+    segs["log_uniform"] = np.exp(rng.uniform(-690, 690, size=L)) * np.where(rng.random(L) < 0.3, -1.0, 1.0)
+    segs["increasing"] = np.arange(L, dtype=np.float64)
+    segs["decreasing"] = np.arange(L, dtype=np.float64)[::-1].copy()
+    segs["constant"] = np.full(L, 3.25)
+    segs["two_values"] = np.where(rng.random(L) < 0.5, 1.0, 2.0)
+    return segs
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_hselect_adversarial(ctx, mode):
+    rng = np.random.default_rng(77)
+    L = 50400
+    segs = _hselect_segments(L, rng)
+    names = list(segs)
+    vals = np.concatenate([segs[k] for k in names])
+    offs = (np.arange(len(names) + 1) * L).astype(np.int64)
+    for pct in [(50, 1), (75, 1), (90, 1), (25, 1), (10, 1), (95, 1), (333, 10)]:
+        got = _run_gpu(ctx, vals, offs, mode, *pct)
+        want = _oracle(vals, offs, mode, *pct)
+        for i, nm in enumerate(names):
+            one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
+            _assert_same(one[0], one[1], mode, f"hselect {nm} {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_hselect_gapped_and_ragged(ctx, mode):
+    """Mixed single-pass / hselect segments in one launch, NaN gaps (incl. negative NaN)."""
+    rng = np.random.default_rng(78)
+    offs = _ragged(rng, 120, 0, 30000)
+    N = int(offs[-1])
+    vals = rng.gamma(2.0, 0.05, size=N)
+    vals[rng.random(N) < 0.2] = np.nan
+    neg_nan = np.frombuffer(np.uint64(0xFFF8000000000001).tobytes(), dtype=np.float64)[0]
+    vals[rng.random(N) < 0.01] = neg_nan
+    vals[rng.random(N) < 0.1] = 0.0
+    for pct in [(50, 1), (80, 1), (20, 1), (99, 1)]:
+        got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=True)
+        want = _oracle(vals, offs, mode, *pct, gaps=True)
+        _assert_same(got, want, mode, f"hselect gapped {mode} p={pct}")
+    vals_c = np.nan_to_num(vals, nan=0.25)
+    vals_c[rng.random(N) < 0.00005] = neg_nan  # a few real NaN samples: flagged
+    for pct in [(50, 1), (65, 1)]:
+        got = _run_gpu(ctx, vals_c, offs, mode, *pct)
+        want = _oracle(vals_c, offs, mode, *pct)
+        _assert_same(got, want, mode, f"hselect compact {mode} p={pct}")
 
 
 def test_maxlen_autodetect(ctx):
