@@ -11,6 +11,9 @@ Workloads (BASELINE.json configs):
   2 (default) 10k containers x 5 pods x 10,080 slots (7d@1m) per rank, NaN-gapped dense layout
   3           100k containers x 1 pod, windows of 1..14 days @1m (1,440-20,160 samples), compact CSR
   4           1M containers x 10,080 samples (7d@1m) split across the ranks, compact CSR
+  5           sketch mode: 100k CPU series x 172,800 samples (30d@15s) TIME-sharded across the
+              ranks (rank r holds the r-th time slice of every series); per-slice log-linear
+              sketches merged by one reduce-scatter, rank error vs the exact path reported
 Data are generated on the device by krr_synth_fill (counter hash; no host packing, no PCIe).
 
 Prints ONE JSON line on rank 0 (contract in the task brief): value = containers of ALL
@@ -43,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--sketch-bits", type=int, default=5, help="config 5: log-linear bins per octave = 2^bits")
+    ap.add_argument("--error-sample", type=int, default=256, help="config 5: series checked against the exact path")
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
     ap.add_argument("--containers", type=int, default=0, help="override containers per rank (testing)")
@@ -100,6 +105,8 @@ def main():
         else:
             dist.init_process_group(backend)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
+    if args.config == 5:
+        return run_config5(args, world, rank, local, dev, coll_dev)
 
     offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers)
     S = offs_np.size - 1
@@ -280,6 +287,176 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
+
+
+SLOTS_30D_15S = 30 * 24 * 60 * 4  # 172,800
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        return platform.processor()
+
+
+def run_config5(args, world, rank, local, dev, coll_dev):
+    """Config 5: time-sharded 30d@15s series, sketch mode (see krr_amd/core/sketch.py).
+
+    step = per-slice sketch build (one HBM pass) -> reduce-scatter of the sketches
+    (RCCL, N > 1) -> query of this rank's owner block -> results gathered to rank 0.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from krr_amd import _native
+    from krr_amd.core import sketch
+    from krr_amd.core.distributed import gather_records
+    from krr_amd.core.engine import percentile_params
+
+    S = args.containers or 100_000
+    T = SLOTS_30D_15S
+    t0, t1 = (T * rank) // world, (T * (rank + 1)) // world
+    Lr = t1 - t0
+    ctx = _native.Context(local)
+    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * Lr
+    cpu = torch.empty(S * Lr, dtype=torch.float64, device=dev)
+    seed = 1000003 * 6
+    ctx.synth_fill_window(cpu, offs, seed, 0, 0, False, t0, T)
+    torch.cuda.synchronize()
+    ser = ctx.series(cpu, offs, Lr, False)
+    cfg = sketch.SketchConfig(mantissa_bits=args.sketch_bits)
+    params = percentile_params(Decimal(args.percentile), params_mode(args))
+    stream = torch.cuda.current_stream()
+    host_rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
+    state = {}
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        sk = sketch.build(ctx, ser, cfg, stream)
+        if ev is not None:
+            ev[1].record(stream)
+        merged = sketch.merge_time_sharded(sk)
+        res = sketch.query(ctx, merged, cfg, params, stream)
+        rec = torch.stack([res["value"].view(torch.int64), res["count"] | (res["flags"].to(torch.int64) << 48),
+                           torch.zeros_like(res["count"]), torch.zeros_like(res["count"])], dim=1)
+        if world > 1:
+            rec = gather_records(rec.to(coll_dev), dst=0)
+        if rank == 0:
+            host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+        state["merged"] = merged
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    t_a = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_b = time.perf_counter()
+    dt = torch.tensor([(t_b - t_a) / args.steps], dtype=torch.float64, device=coll_dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    step_s = float(dt.item())
+    kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    N = S * Lr
+    kbytes = 8 * N + 8 * (S + 1) + S * (4 * cfg.width + 8 + 8 + 4)
+    result = {
+        "metric": METRIC,
+        "value": S / step_s,
+        "unit": "cpu-series/s (30d@15s, sketch mode)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (device counter-hash: CPU ~ Gamma(2, 0.05) cores), generated per time slice",
+        "config": {
+            "workload": f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
+                        f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave",
+            "percentile_mode": params_mode(args), "cpu_percentile": args.percentile,
+            "series": S, "slots_per_rank": N,
+            "parallelism": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
+        },
+        "samples_per_s": S * T / step_s,
+        "kernels_ms": {"k_sketch_build": kms},
+        "roofline": {"kernel": "k_sketch_build", "bound": "hbm", "achieved": kbytes / (kms * 1e-3) / 1e9,
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kbytes / (kms * 1e-3) / HBM_PEAK,
+                     "traffic": None, "algorithmic_bytes_per_launch": kbytes},
+    }
+    # rank error of the sketch answers against the exact path on a sample of series
+    m = max(1, min(args.error_sample, S))
+    piece = cpu.view(S, Lr)[:m].contiguous()
+    if world > 1:
+        width = (T + world - 1) // world
+        pad = torch.full((m, width), float("nan"), dtype=torch.float64, device=dev)
+        pad[:, :Lr] = piece
+        bufs = [torch.empty_like(pad, device=coll_dev) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad.to(coll_dev), gather_list=bufs, dst=0)
+        if rank == 0:
+            full = torch.cat([b[:, : ((T * (r + 1)) // world - (T * r) // world)].to(dev)
+                              for r, b in enumerate(bufs)], dim=1).contiguous()
+    else:
+        full = piece
+    sk_vals = None
+    if rank == 0:
+        rec = host_rec[:m].numpy()
+        sk_vals = rec[:, 0].copy().view(np.float64)
+        fo = torch.arange(m + 1, dtype=torch.int64, device=dev) * T
+        fser = ctx.series(full.view(-1), fo, T, False)
+        ev_ = torch.empty(m, dtype=torch.float64, device=dev)
+        en_ = torch.empty(m, dtype=torch.int64, device=dev)
+        ef_ = torch.empty(m, dtype=torch.int32, device=dev)
+        exact_params = percentile_params(Decimal(args.percentile), params_mode(args))
+        ctx.segmented_percentile(fser, exact_params, ev_, en_, ef_)
+        lt = torch.empty(m, dtype=torch.int64, device=dev)
+        le = torch.empty(m, dtype=torch.int64, device=dev)
+        ctx.rank_of(fser, torch.from_numpy(sk_vals).to(dev), lt, le)
+        torch.cuda.synchronize()
+        n = en_.cpu().numpy().astype(np.float64)
+        target = (n - 1) * float(args.percentile) / 100.0
+        ltn, len_ = lt.cpu().numpy(), le.cpu().numpy()
+        err = np.maximum(0.0, np.maximum(ltn - target, target - (len_ - 1))) / n
+        exact = ev_.cpu().numpy()
+        rel = np.abs(sk_vals - exact) / np.abs(exact)
+        result["sketch_error"] = {
+            "sample_series": m, "rank_error_max": float(err.max()), "rank_error_mean": float(err.mean()),
+            "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
+            "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
+                          "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import oracle
+
+            cs = max(1, min(args.cpu_sample * 5, S))
+            host = cpu.view(S, Lr)[:cs].cpu().numpy().ravel()
+            ho = (np.arange(cs + 1) * Lr).astype(np.int64)
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            ta = time.perf_counter()
+            oracle.percentile(host, ho, exact_params.mode, exact_params.p_num, exact_params.p_den, exact_params.q,
+                              False, threads)
+            tb = time.perf_counter()
+            result["cpu_baseline"] = {
+                "value": cs / (tb - ta), "unit": "cpu-series/s (exact)", "cores": threads, "kind": "port",
+                "sample": f"first {cs} series ({cs * Lr} samples) copied D2H; oracle/krr_oracle.c exact "
+                          f"{args.mode}, OpenMP {threads} threads on {_cpu_model()}"}
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def params_mode(args) -> str:
+    return args.mode if args.mode != "ref_index" else "linear"
 
 
 if __name__ == "__main__":

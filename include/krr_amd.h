@@ -76,6 +76,9 @@ typedef enum {
 /* bits 8..15 of a KRR_FLAG_CAPACITY result carry an internal reason code (diagnostic) */
 #define KRR_FLAG_EMPTY 4u     /* n == 0: value is NaN (reference: Decimal('NaN'),
                                  simple.py:26-27 and 33-34) */
+#define KRR_FLAG_SKETCH_RANGE 8u /* sketch mode: a needed rank fell in a lumped bin
+                                    (negative, below 2^min_exponent, or above the
+                                    binned octaves): the value is a coarse estimate */
 
 typedef struct {
     const double* values;    /* device pointer, n_values float64 */
@@ -140,6 +143,46 @@ int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value,
                      const int64_t* mem_count, const uint32_t* mem_flags, int64_t* records,
                      void* stream);
 
+/* ---- Sketch mode (config 5: time-sharded series too long for one window) ----
+ * A build-only extension: the reference cannot query 30d@15s.
+ * Per segment a log-linear histogram with data-independent bins: 2^mantissa_bits
+ * bins per octave over [2^min_exponent, 2^(min_exponent+octaves)), plus four
+ * lumped bins (negative, +-0, below range, above range).  Sketches of the same
+ * series' time slices on different ranks merge exactly by adding counts (and
+ * min/max by min/max); the query interpolates inside the bin holding the rank.
+ * Its rank error is reported by the caller (bench.py config 5), not assumed. */
+typedef struct {
+    int32_t mantissa_bits;   /* m in [0, 10]: relative bin width <= 2^-m */
+    int32_t min_exponent;    /* lowest binned octave [2^e, 2^(e+1)); e >= -1022 */
+    int32_t octaves;         /* binned octaves; min_exponent + octaves <= 1024 */
+    int32_t reserved;
+} krr_sketch_params;
+
+/* uint32 words per segment sketch: (octaves << mantissa_bits) + 4, or < 0 if invalid. */
+int64_t krr_sketch_width(const krr_sketch_params* sp);
+
+/* counts[S * width] (uint32), vmin/vmax[S] (NaN when empty), flags[S] (KRR_FLAG_NAN
+ * when a NaN sample is present and gaps_are_nan == 0).  Device pointers. */
+int krr_sketch_build(krr_ctx* ctx, const krr_series* series, const krr_sketch_params* sp,
+                     uint32_t* counts, double* vmin, double* vmax, uint32_t* flags, void* stream);
+
+/* Percentile from (merged) sketches: SORTED_LOWER or LINEAR over n = sum(counts).
+ * out_flags: KRR_FLAG_EMPTY, KRR_FLAG_SKETCH_RANGE.  REF_INDEX -> KRR_E_UNSUPPORTED
+ * (use krr_select_present on the time-sharded slices instead: it is exact). */
+int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const double* vmin,
+                     const double* vmax, const krr_sketch_params* sp, const krr_percentile_params* params,
+                     double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);
+
+/* Per segment: out_lt[s] = #present samples < values[s], out_le[s] = #<= values[s]. */
+int krr_rank_of(krr_ctx* ctx, const krr_series* series, const double* values, int64_t* out_lt,
+                int64_t* out_le, void* stream);
+
+/* Per segment: out[s] = the k[s]-th present sample (0-based, position order; NaN
+ * slots absent when gaps_are_nan), skipped when k[s] < 0.  The local step of the
+ * exact time-sharded REF_INDEX (simple.py:36 over the concatenated slices). */
+int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k, double* out,
+                       void* stream);
+
 /* Synthetic week-long series (bench/test data), generated on the device from a
  * counter-based hash so that no host packing or PCIe is involved.
  * kind 0 = CPU cores ~ Gamma(k=2, theta=0.05); kind 1 = memory bytes
@@ -149,6 +192,13 @@ int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value,
  * gap fraction ~ U(0, 0.2); gap slots are NaN. */
 int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
                    uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, void* stream);
+
+/* Same, for the time window [t0, t0 + len) of series of total_len slots: slot i
+ * of segment s holds global time index t0 + i, so slices generated on different
+ * ranks concatenate to the series krr_synth_fill would generate whole. */
+int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
+                          uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, int64_t t0,
+                          int64_t total_len, void* stream);
 
 #ifdef __cplusplus
 }

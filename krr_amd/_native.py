@@ -31,6 +31,7 @@ KRR_PCT_LINEAR = 2
 KRR_FLAG_NAN = 1
 KRR_FLAG_CAPACITY = 2
 KRR_FLAG_EMPTY = 4
+KRR_FLAG_SKETCH_RANGE = 8
 
 # Every symbol include/krr_amd.h declares (tests/test_abi.py checks the export table).
 EXPORTED_SYMBOLS = (
@@ -44,6 +45,12 @@ EXPORTED_SYMBOLS = (
     "krr_simple_run_host",
     "krr_pack_records",
     "krr_synth_fill",
+    "krr_synth_fill_window",
+    "krr_sketch_width",
+    "krr_sketch_build",
+    "krr_sketch_query",
+    "krr_rank_of",
+    "krr_select_present",
 )
 
 
@@ -76,6 +83,15 @@ class KrrPercentileParams(ctypes.Structure):
         ("p_num", ctypes.c_int64),
         ("p_den", ctypes.c_int64),
         ("q", ctypes.c_double),
+    ]
+
+
+class KrrSketchParams(ctypes.Structure):
+    _fields_ = [
+        ("mantissa_bits", ctypes.c_int32),
+        ("min_exponent", ctypes.c_int32),
+        ("octaves", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -120,6 +136,19 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_pack_records.restype = ctypes.c_int
         lib.krr_synth_fill.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, vp]
         lib.krr_synth_fill.restype = ctypes.c_int
+        lib.krr_synth_fill_window.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, i64, i64, vp]
+        lib.krr_synth_fill_window.restype = ctypes.c_int
+        skp = ctypes.POINTER(KrrSketchParams)
+        lib.krr_sketch_width.argtypes = [skp]
+        lib.krr_sketch_width.restype = i64
+        lib.krr_sketch_build.argtypes = [vp, sp, skp, vp, vp, vp, vp, vp]
+        lib.krr_sketch_build.restype = ctypes.c_int
+        lib.krr_sketch_query.argtypes = [vp, i64, vp, vp, vp, skp, pp, vp, vp, vp, vp]
+        lib.krr_sketch_query.restype = ctypes.c_int
+        lib.krr_rank_of.argtypes = [vp, sp, vp, vp, vp, vp]
+        lib.krr_rank_of.restype = ctypes.c_int
+        lib.krr_select_present.argtypes = [vp, sp, vp, vp, vp]
+        lib.krr_select_present.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
@@ -222,6 +251,58 @@ class Context:
         self._check(self._lib.krr_synth_fill(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
             int(kind), int(pod_len), int(bool(gaps)), self._stream(stream)))
+
+
+    # --- sketch mode / time-sharded helpers (config 5) ---------------------
+    def sketch_width(self, sp: KrrSketchParams) -> int:
+        w = int(self._lib.krr_sketch_width(ctypes.byref(sp)))
+        if w < 0:
+            raise ValueError("invalid sketch parameters")
+        return w
+
+    def sketch_build(self, series: KrrSeries, sp: KrrSketchParams, counts, vmin, vmax, flags, stream=None) -> None:
+        """counts: int32 [S, width] (uint32 bit patterns); vmin/vmax float64 [S]; flags int32 [S]."""
+        S = series.n_segments
+        _check_tensor(counts, "int32", S * self.sketch_width(sp))
+        _check_tensor(vmin, "float64", S)
+        _check_tensor(vmax, "float64", S)
+        _check_tensor(flags, "int32", S)
+        self._check(self._lib.krr_sketch_build(
+            self._h, ctypes.byref(series), ctypes.byref(sp), counts.data_ptr(), vmin.data_ptr(), vmax.data_ptr(),
+            flags.data_ptr(), self._stream(stream)))
+
+    def sketch_query(self, counts, vmin, vmax, sp: KrrSketchParams, params: KrrPercentileParams, out_value,
+                     out_count, out_flags, stream=None) -> None:
+        S = vmin.numel()
+        _check_tensor(counts, "int32", S * self.sketch_width(sp))
+        for t, dt in ((vmax, "float64"), (out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, S)
+        self._check(self._lib.krr_sketch_query(
+            self._h, S, counts.data_ptr(), vmin.data_ptr(), vmax.data_ptr(), ctypes.byref(sp), ctypes.byref(params),
+            out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(), self._stream(stream)))
+
+    def rank_of(self, series: KrrSeries, values, out_lt, out_le, stream=None) -> None:
+        S = series.n_segments
+        _check_tensor(values, "float64", S)
+        _check_tensor(out_lt, "int64", S)
+        _check_tensor(out_le, "int64", S)
+        self._check(self._lib.krr_rank_of(self._h, ctypes.byref(series), values.data_ptr(), out_lt.data_ptr(),
+                                          out_le.data_ptr(), self._stream(stream)))
+
+    def select_present(self, series: KrrSeries, k, out, stream=None) -> None:
+        S = series.n_segments
+        _check_tensor(k, "int64", S)
+        _check_tensor(out, "float64", S)
+        self._check(self._lib.krr_select_present(self._h, ctypes.byref(series), k.data_ptr(), out.data_ptr(),
+                                                 self._stream(stream)))
+
+    def synth_fill_window(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, t0: int,
+                          total_len: int, stream=None) -> None:
+        _check_tensor(values, "float64")
+        _check_tensor(offsets, "int64")
+        self._check(self._lib.krr_synth_fill_window(
+            self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
+            int(kind), int(pod_len), int(bool(gaps)), int(t0), int(total_len), self._stream(stream)))
 
 
 def _check_tensor(t, dtype: str, numel: Optional[int] = None) -> None:

@@ -1,0 +1,249 @@
+"""Sketch mode and time-sharded series (BASELINE config 5: 30d@15s, 172,800 samples).
+
+A build-only extension: the reference cannot query 30d@15s (SURVEY.md §0.5 —
+``timeframe_duration`` is whole minutes, ``core/abstract/strategies.py:23``) and
+keeps each object's samples in one Python list (``prometheus.py:150-155``).
+Here a series too long for one GPU's window is TIME-sharded: rank r holds the
+r-th contiguous time slice of every series.
+
+* Percentile (SORTED_LOWER / LINEAR): each rank builds a log-linear histogram
+  sketch per series slice (``krr_sketch_build``, one HBM pass).  Bins are
+  data-independent, so the W slices of a series merge exactly by adding counts:
+  ONE reduce-scatter (RCCL over xGMI) leaves each rank the merged sketches of a
+  contiguous block of series, which it queries (``krr_sketch_query``).  The value
+  is interpolated inside the bin holding the rank (relative bin width 2^-m); the
+  rank error is measured against the exact path, never assumed (bench.py).
+* REF_INDEX (the reference's rule, ``simple.py:36``) stays exact: all-gather the
+  per-slice present counts, the rank whose slice holds global index k selects it
+  (``krr_select_present``), one all-gather collects the answers.
+* Memory max stays exact: all-gather (max, count) per slice and merge in time
+  order with Python ``max()``'s first-maximum rule (``simple.py:29``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from krr_amd import _native
+
+
+@dataclass(frozen=True)
+class SketchConfig:
+    """Log-linear bins: 2^mantissa_bits per octave over [2^min_exponent, 2^(min_exponent+octaves))."""
+    mantissa_bits: int = 5     # relative bin width <= 1/32
+    min_exponent: int = -24    # 6e-8 cores
+    octaves: int = 36          # ... up to 4096 cores
+
+    def params(self) -> _native.KrrSketchParams:
+        return _native.KrrSketchParams(self.mantissa_bits, self.min_exponent, self.octaves, 0)
+
+    @property
+    def width(self) -> int:
+        return (self.octaves << self.mantissa_bits) + 4
+
+
+def build(ctx: _native.Context, series: _native.KrrSeries, cfg: SketchConfig, stream=None) -> dict:
+    """One HBM pass: per-series sketch of this rank's slices.  Device tensors."""
+    import torch
+
+    S = series.n_segments
+    dev = series._keep[0].device
+    out = {
+        "counts": torch.empty((S, cfg.width), dtype=torch.int32, device=dev),
+        "vmin": torch.empty(S, dtype=torch.float64, device=dev),
+        "vmax": torch.empty(S, dtype=torch.float64, device=dev),
+        "flags": torch.empty(S, dtype=torch.int32, device=dev),
+    }
+    ctx.sketch_build(series, cfg.params(), out["counts"], out["vmin"], out["vmax"], out["flags"], stream)
+    return out
+
+
+def owner_blocks(n_series: int, world: int) -> list[tuple[int, int]]:
+    """Series [0, S) in world contiguous blocks of ceil(S / world) (the last may be short)."""
+    per = -(-n_series // world) if world else 0
+    return [(min(r * per, n_series), min((r + 1) * per, n_series)) for r in range(world)]
+
+
+def _reduce_scatter(t, op, group, world: int):
+    """Rank r gets block r of the elementwise reduction of t ([world * per, ...])."""
+    import torch
+    import torch.distributed as dist
+
+    per = t.shape[0] // world
+    out = torch.empty((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "nccl":
+        dist.reduce_scatter_tensor(out, t, op=op, group=group)
+    else:  # gloo (CPU tests): same result through all_reduce
+        full = t.clone()
+        dist.all_reduce(full, op=op, group=group)
+        r = dist.get_rank(group)
+        out.copy_(full[r * per:(r + 1) * per])
+    return out
+
+
+def merge_time_sharded(sk: dict, group=None) -> dict:
+    """Merge the per-slice sketches of all ranks: rank r receives the merged
+    sketches of its owner block (owner_blocks) as counts/vmin/vmax/flags, plus
+    'block' = (lo, hi).  World size 1: the input, unchanged."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return dict(sk, block=(0, sk["vmin"].numel()))
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S = sk["vmin"].numel()
+    per = -(-S // world)
+    pad = per * world - S
+
+    def padded(t, fill):
+        if not pad:
+            return t
+        ext = torch.full((pad,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=t.device)
+        return torch.cat([t, ext], dim=0)
+
+    counts = _reduce_scatter(padded(sk["counts"], 0), dist.ReduceOp.SUM, group, world)
+    # NaN (an empty slice) must not win min/max: +-inf stand-ins, mapped back after
+    vmin = _reduce_scatter(padded(torch.nan_to_num(sk["vmin"], nan=float("inf")), float("inf")),
+                           dist.ReduceOp.MIN, group, world)
+    vmax = _reduce_scatter(padded(torch.nan_to_num(sk["vmax"], nan=float("-inf")), float("-inf")),
+                           dist.ReduceOp.MAX, group, world)
+    flags = _reduce_scatter(padded(sk["flags"], 0), dist.ReduceOp.MAX, group, world)
+    lo, hi = owner_blocks(S, world)[rank]
+    n = hi - lo
+    empty = counts[:n].sum(dim=1) == 0
+    vmin = torch.where(empty, torch.full_like(vmin[:n], float("nan")), vmin[:n])
+    vmax = torch.where(empty, torch.full_like(vmax[:n], float("nan")), vmax[:n])
+    return {"counts": counts[:n].contiguous(), "vmin": vmin.contiguous(), "vmax": vmax.contiguous(),
+            "flags": flags[:n].contiguous(), "block": (lo, hi)}
+
+
+def query(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native.KrrPercentileParams,
+          stream=None) -> dict:
+    """Percentile of every (merged) sketch.  KRR_FLAG_NAN from the build is carried over."""
+    import torch
+
+    S = merged["vmin"].numel()
+    dev = merged["vmin"].device
+    out = {"value": torch.empty(S, dtype=torch.float64, device=dev),
+           "count": torch.empty(S, dtype=torch.int64, device=dev),
+           "flags": torch.empty(S, dtype=torch.int32, device=dev)}
+    ctx.sketch_query(merged["counts"], merged["vmin"], merged["vmax"], cfg.params(), params, out["value"],
+                     out["count"], out["flags"], stream)
+    nan = (merged["flags"] & _native.KRR_FLAG_NAN) != 0
+    if bool(nan.any()):
+        out["flags"] |= merged["flags"] & _native.KRR_FLAG_NAN
+        out["value"] = torch.where(nan, torch.full_like(out["value"], float("nan")), out["value"])
+    return out
+
+
+# ----------------------------- exact time-sharded merges ------------------------------
+
+def exact_rank_np(n: np.ndarray, p_num: int, p_den: int) -> np.ndarray:
+    """floor((n-1) * p_num / (100 p_den)) exactly, elementwise (n >= 1)."""
+    n = np.asarray(n, dtype=np.int64)
+    a = n - 1
+    den = 100 * int(p_den)
+    if int(a.max(initial=0)) * int(p_num) < 2**63:
+        return (a * int(p_num)) // den
+    return np.array([(int(x) * int(p_num)) // den for x in a], dtype=np.int64)
+
+
+def refindex_locate(all_n: np.ndarray, p_num: int, p_den: int, rank: int):
+    """Global REF_INDEX position from per-slice present counts all_n[world, S]
+    (time order = rank order): n[S], k[S] (-1 if empty), owner[S] = the rank whose
+    slice holds k (-1 if empty), and this rank's local index (-1 if not its own)."""
+    all_n = np.asarray(all_n, dtype=np.int64)
+    n = all_n.sum(axis=0)
+    prefix = np.cumsum(all_n, axis=0) - all_n  # samples in earlier slices
+    k = np.where(n > 0, exact_rank_np(np.maximum(n, 1), p_num, p_den), -1)
+    inside = (k[None, :] >= prefix) & (k[None, :] < prefix + all_n)
+    owner = np.where(n > 0, np.argmax(inside, axis=0), -1)
+    k_local = np.where(owner == rank, k - prefix[rank], -1).astype(np.int64)
+    return n, k, owner, k_local
+
+
+def refindex_time_sharded(ctx: _native.Context, series: _native.KrrSeries, params: _native.KrrPercentileParams,
+                          group=None, stream=None) -> dict:
+    """Exact REF_INDEX (the reference's X[floor((n-1) p / 100)] over the time-ordered
+    concatenation of every rank's slices, simple.py:31-36).  Returns host arrays
+    value/count/flags for ALL series on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    S = series.n_segments
+    vals, offs = series._keep
+    dev = vals.device
+    inf = torch.full((S,), float("inf"), dtype=torch.float64, device=dev)
+    lt = torch.empty(S, dtype=torch.int64, device=dev)
+    le = torch.empty(S, dtype=torch.int64, device=dev)
+    if series.gaps_are_nan:
+        ctx.rank_of(series, inf, lt, le, stream)  # le(+inf) = present (non-NaN) samples of the slice
+        local_n = le
+    else:  # compact layout: every slot is a sample, NaN included (the reference indexes the list)
+        local_n = (offs[1:] - offs[:-1]).contiguous()
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if world > 1:
+        coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        g = [torch.empty(S, dtype=torch.int64, device=coll) for _ in range(world)]
+        dist.all_gather(g, local_n.to(coll), group=group)
+        all_n = torch.stack(g).cpu().numpy()  # [world, S], time order = rank order
+    else:
+        all_n = local_n.cpu().numpy()[None, :]
+    n, k, owner, k_local = refindex_locate(all_n, params.p_num, params.p_den, rank)
+    mine = owner == rank
+    kt = torch.from_numpy(k_local).to(dev)
+    found = torch.full((S,), float("nan"), dtype=torch.float64, device=dev)
+    ctx.select_present(series, kt, found, stream)
+    bits = torch.where(torch.from_numpy(mine).to(dev), found.view(torch.int64),
+                       torch.zeros(S, dtype=torch.int64, device=dev))
+    if world > 1:
+        coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        gb = [torch.empty(S, dtype=torch.int64, device=coll) for _ in range(world)]
+        dist.all_gather(gb, bits.to(coll), group=group)
+        allb = torch.stack(gb).cpu().numpy()
+        vbits = allb[np.maximum(owner, 0), np.arange(S)]
+    else:
+        vbits = bits.cpu().numpy()
+    value = vbits.view(np.float64).copy()
+    flags = np.zeros(S, dtype=np.uint32)
+    value[n == 0] = np.nan
+    flags[n == 0] |= _native.KRR_FLAG_EMPTY
+    return {"value": value, "count": n.astype(np.int64), "flags": flags}
+
+
+def max_time_sharded(local_value, local_count, local_flags, group=None) -> dict:
+    """Exact memory max over time slices: Python max() keeps the FIRST maximal
+    element in time order (only +-0 differ in bits), so merge in rank order taking
+    strictly greater values.  Inputs: per-slice device/host tensors [S]."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    v = local_value.view(torch.int64)
+    packed = torch.stack([v, local_count, local_flags.to(torch.int64)], dim=1)
+    if world > 1:
+        coll = packed.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        g = [torch.empty_like(packed, device=coll) for _ in range(world)]
+        dist.all_gather(g, packed.to(coll), group=group)
+        parts = [x.cpu().numpy() for x in g]
+    else:
+        parts = [packed.cpu().numpy()]
+    S = parts[0].shape[0]
+    best = np.full(S, np.nan)
+    count = np.zeros(S, dtype=np.int64)
+    flags = np.zeros(S, dtype=np.uint32)
+    for p in parts:  # time order
+        val = p[:, 0].copy().view(np.float64)
+        cnt = p[:, 1]
+        flg = p[:, 2].astype(np.uint32)
+        count += cnt
+        flags |= flg & _native.KRR_FLAG_NAN
+        take = (cnt > 0) & ((np.isnan(best)) | (val > best))
+        best = np.where(take, val, best)
+    flags[count == 0] |= _native.KRR_FLAG_EMPTY
+    best[(flags & _native.KRR_FLAG_NAN) != 0] = np.nan
+    return {"value": best, "count": count, "flags": flags}

@@ -1333,6 +1333,285 @@ __global__ void k_maxlen(const int64_t* __restrict__ offs, int64_t S, unsigned l
     if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)m);
 }
 
+// ------------------------------ SKETCH -------------------------------------
+// Mergeable log-linear histogram sketch (config 5: series too long for one
+// GPU's time window, time-sharded over ranks).  Bins are data-independent, so
+// the sketches of a series' time slices on different ranks merge EXACTLY by
+// adding counts (one RCCL reduce-scatter); min/max merge by min/max.
+// Bin layout per segment (ascending value order), width = nbins + 4 words:
+//   [0] negative  [1] +-0  [2] (0, 2^e_lo)  [3 .. 3+nbins) log-linear bins
+//   [3+nbins] >= 2^(e_lo + octaves) (incl. +inf)
+// bin i covers [2^E (1 + j 2^-m), 2^E (1 + (j+1) 2^-m)) with E = e_lo + (i >> m),
+// j = i & (2^m - 1): relative bin width <= 2^-m.  The query interpolates
+// linearly inside the bin holding the rank; its rank error is measured against
+// the exact path (bench.py config 5), not assumed.
+struct SketchGeom {
+    uint32_t m, nbins, width, base;  // base = (e_lo + 1023) << m
+    uint64_t low_bits;               // bits of 2^e_lo
+    int32_t e_lo;
+};
+
+__host__ __device__ inline SketchGeom sketch_geom(const krr_sketch_params& p) {
+    SketchGeom g;
+    g.m = (uint32_t)p.mantissa_bits;
+    g.nbins = (uint32_t)p.octaves << g.m;
+    g.width = g.nbins + 4;
+    g.e_lo = p.min_exponent;
+    g.base = (uint32_t)(p.min_exponent + 1023) << g.m;
+    g.low_bits = (uint64_t)(p.min_exponent + 1023) << 52;
+    return g;
+}
+
+struct SketchProc {
+    uint32_t* h;
+    SketchGeom g;
+    uint32_t nan_l;
+    double vmin, vmax;
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double d = slot_val(c, j);
+            const uint64_t x = dbits(d);
+            const bool nan = __builtin_isnan(d);
+            nan_l += nan ? 1u : 0u;
+            vmin = fmin(vmin, d);
+            vmax = fmax(vmax, d);
+            const uint64_t mag = x & ~kSignBit;
+            const uint32_t u = (uint32_t)(mag >> (52 - g.m)) - g.base;
+            uint32_t bin = u < g.nbins ? 3u + u : (mag < g.low_bits ? 2u : 3u + g.nbins);
+            bin = (x & kSignBit) ? 0u : bin;
+            bin = mag == 0 ? 1u : bin;
+            if (!nan) atomicAdd(&h[bin], 1u);
+            asm volatile("" ::: "memory");
+        }
+    }
+};
+
+struct OpMinF64Bits {  // fmin on f64 bit patterns: the non-NaN operand wins
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return dbits(fmin(bitsd(a), bitsd(b))); }
+};
+
+struct SketchBuildArgs {
+    const double* vals;
+    const int64_t* offs;
+    int64_t S;
+    int32_t gaps;
+    SketchGeom g;
+    uint32_t* counts;  // [S][width]
+    double* vmin;
+    double* vmax;
+    uint32_t* flags;
+};
+
+__global__ __launch_bounds__(64) void k_sketch_build(SketchBuildArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* h = reinterpret_cast<uint32_t*>(smem);
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        for (uint32_t i = lane; i < A.g.width; i += kWave) h[i] = 0;
+        __syncthreads();
+        SketchProc P;
+        P.h = h;
+        P.g = A.g;
+        P.nan_l = 0;
+        P.vmin = bitsd(kQuietNaN);
+        P.vmax = bitsd(kQuietNaN);
+        const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
+        __syncthreads();
+        const uint64_t nnan = wave_sum_u32(P.nan_l) - pad;
+        const double mn = bitsd(lane_bcast64(wave_scan64(dbits(P.vmin), kQuietNaN, OpMinF64Bits{}), kWave - 1));
+        const double mx = bitsd(lane_bcast64(wave_scan64(dbits(P.vmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1));
+        uint4* dst = reinterpret_cast<uint4*>(A.counts + (size_t)s * A.g.width);
+        const uint4* src = reinterpret_cast<const uint4*>(h);
+        for (uint32_t i = lane; i < A.g.width / 4; i += kWave) dst[i] = src[i];
+        if (lane == 0) {
+            A.vmin[s] = mn;
+            A.vmax[s] = mx;
+            A.flags[s] = (nnan && !A.gaps) ? KRR_FLAG_NAN : 0u;
+        }
+        __syncthreads();
+    }
+}
+
+struct SketchQueryArgs {
+    int64_t S;
+    SketchGeom g;
+    const uint32_t* counts;
+    const double* vmin;
+    const double* vmax;
+    int32_t mode;
+    int64_t p_num, p_den;
+    double q;
+    double* out_v;
+    int64_t* out_n;
+    uint32_t* out_f;
+};
+
+// Value estimate of ascending rank r inside bin b holding c keys, `before` below.
+__device__ __forceinline__ double sketch_value(const SketchGeom& g, uint32_t b, uint64_t r, uint64_t before, uint32_t c,
+                                               double mn, double mx, uint64_t n, uint32_t& flags) {
+    if (r == 0) return mn;
+    if (r == n - 1) return mx;
+    const double f = ((double)(r - before) + 0.5) / (double)c;
+    double lo, hi;
+    if (b == 1) return 0.0;
+    if (b == 0) {  // negatives: [min, 0)
+        lo = mn;
+        hi = 0.0;
+        flags |= KRR_FLAG_SKETCH_RANGE;
+    } else if (b == 2) {  // (0, 2^e_lo)
+        lo = 0.0;
+        hi = ldexp(1.0, g.e_lo);
+        flags |= KRR_FLAG_SKETCH_RANGE;
+    } else if (b == 3 + g.nbins) {  // [2^(e_lo + octaves), max]
+        lo = ldexp(1.0, g.e_lo + (int)(g.nbins >> g.m));
+        hi = mx;
+        flags |= KRR_FLAG_SKETCH_RANGE;
+    } else {
+        const uint32_t i = b - 3;
+        const int E = g.e_lo + (int)(i >> g.m);
+        const double j = (double)(i & ((1u << g.m) - 1u));
+        const double step = ldexp(1.0, E - (int)g.m);
+        lo = ldexp(1.0, E) + j * step;
+        hi = lo + step;
+    }
+    double v = lo + f * (hi - lo);
+    v = v < mn ? mn : v;
+    v = v > mx ? mx : v;
+    return v;
+}
+
+__global__ __launch_bounds__(64) void k_sketch_query(SketchQueryArgs A) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const uint32_t* h = A.counts + (size_t)s * A.g.width;
+        const uint32_t W = A.g.width;
+        const uint32_t per = (W + kWave - 1) / kWave;
+        const uint32_t b0 = (uint32_t)lane * per;
+        uint32_t t = 0;
+        for (uint32_t j = 0; j < per; ++j) t += b0 + j < W ? h[b0 + j] : 0u;
+        const uint32_t incl = wave_scan32(t, 0u, OpAdd32{});
+        const uint64_t n = lane_bcast32(incl, kWave - 1);
+        uint32_t flags = 0;
+        double result = bitsd(kQuietNaN);
+        if (n == 0) {
+            flags = KRR_FLAG_EMPTY;
+        } else {
+            Ranks R;
+            R.gamma = 0.0;
+            if (A.mode == KRR_PCT_SORTED_LOWER) {
+                R.r0 = R.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+            } else {
+                const double vidx = __dmul_rn((double)(n - 1), A.q);
+                if (vidx >= (double)(n - 1)) {
+                    R.r0 = R.r1 = (int64_t)n - 1;
+                    R.gamma = __dsub_rn(vidx, -1.0);
+                } else {
+                    const double fl = floor(vidx);
+                    R.r0 = (int64_t)fl;
+                    R.r1 = R.r0 + 1;
+                    R.gamma = __dsub_rn(vidx, fl);
+                }
+            }
+            double v[2];
+#pragma unroll 1
+            for (int qi = 0; qi < 2; ++qi) {
+                const uint64_t r = (uint64_t)(qi ? R.r1 : R.r0);
+                const uint64_t m = ballot(r < incl);
+                const int src = __ffsll((long long)m) - 1;
+                uint64_t run = lane_bcast32(incl - t, src);
+                // walk the source lane's bins (per <= a few dozen)
+                const uint32_t sb = (uint32_t)src * per;
+                uint32_t fb = sb, fc = 0;
+                uint64_t fbefore = run;
+                for (uint32_t j = 0; j < per && sb + j < W; ++j) {
+                    const uint32_t c = h[sb + j];
+                    if (r < run + c) {
+                        fb = sb + j;
+                        fc = c;
+                        fbefore = run;
+                        break;
+                    }
+                    run += c;
+                }
+                v[qi] = sketch_value(A.g, fb, r, fbefore, fc, A.vmin[s], A.vmax[s], n, flags);
+            }
+            result = A.mode == KRR_PCT_SORTED_LOWER ? v[0] : np_lerp(v[0], v[1], R.gamma);
+        }
+        if (lane == 0) {
+            A.out_v[s] = result;
+            A.out_n[s] = (int64_t)n;
+            A.out_f[s] = flags;
+        }
+    }
+}
+
+// Rank interval of a value per segment: #present samples < v and <= v (for
+// measuring a sketch answer's rank error against the data).
+struct RankOfProc {
+    double v;
+    uint32_t lt, le;
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double d = slot_val(c, j);
+            lt += d < v ? 1u : 0u;  // false for NaN
+            le += d <= v ? 1u : 0u;
+        }
+    }
+};
+
+__global__ __launch_bounds__(64) void k_rank_of(const double* __restrict__ vals, const int64_t* __restrict__ offs,
+                                                int64_t S, const double* __restrict__ v, int64_t* out_lt,
+                                                int64_t* out_le) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        RankOfProc P{v[s], 0u, 0u};
+        stream_segment<false>(vals, offs[s], offs[s + 1], P, lane);
+        const uint32_t lt = wave_sum_u32(P.lt), le = wave_sum_u32(P.le);
+        if (lane == 0) {
+            out_lt[s] = lt;
+            out_le[s] = le;
+        }
+    }
+}
+
+// The k[s]-th present sample (0-based, position order; NaN slots absent when
+// gaps) of each segment, k[s] < 0 -> skipped.  The time-sharded REF_INDEX: the
+// rank whose slice holds global index k selects it locally.
+__global__ __launch_bounds__(64) void k_select_present(const double* __restrict__ vals,
+                                                       const int64_t* __restrict__ offs, int64_t S, int32_t gaps,
+                                                       const int64_t* __restrict__ ks, double* out) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const int64_t k = ks[s];
+        if (k < 0) continue;
+        const int64_t beg = offs[s], end = offs[s + 1];
+        uint64_t found = kQuietNaN;
+        if (!gaps) {
+            if (beg + k < end) found = dbits(vals[beg + k]);
+        } else {
+            uint64_t run = 0;
+            for (int64_t base = beg; base < end; base += kWave) {
+                const int64_t i = base + lane;
+                const bool in = i < end;
+                const uint64_t u = in ? dbits(vals[i]) : kQuietNaN;
+                const bool p = in && !is_nan_bits(u);
+                const uint64_t m = ballot(p);
+                const uint32_t c = popc64(m);
+                if (run + c > (uint64_t)k) {
+                    const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)((uint64_t)k - run));
+                    found = lane_bcast64(u, __ffsll((long long)sel) - 1);
+                    break;
+                }
+                run += c;
+            }
+        }
+        if (lane == 0) out[s] = bitsd(found);
+    }
+}
+
 // ------------------------------ SYNTH --------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -1348,11 +1627,16 @@ __device__ __forceinline__ double unit01(uint64_t h) { return ((double)(h >> 11)
 
 __global__ __launch_bounds__(256) void k_synth(double* __restrict__ vals, const int64_t* __restrict__ offs,
                                               int64_t S, uint64_t seed, int kind, int64_t pod_len,
-                                              int gaps) {
+                                              int gaps, int64_t t0, int64_t total_len) {
+    // Slot i of segment s is global time index t = t0 + i of a series of
+    // total_len slots (0: the segment itself), so time slices generated on
+    // different ranks concatenate to exactly the series one rank would generate.
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
-        const int64_t beg = offs[s], L = offs[s + 1] - beg;
+        const int64_t beg = offs[s], Lloc = offs[s + 1] - beg;
+        const int64_t L = total_len > 0 ? total_len : Lloc;
         const int64_t plen = pod_len > 0 ? pod_len : (L > 0 ? L : 1);
-        for (int64_t t = threadIdx.x; t < L; t += blockDim.x) {
+        for (int64_t i = threadIdx.x; i < Lloc; i += blockDim.x) {
+            const int64_t t = t0 + i;
             const int64_t pod = t / plen;
             const int64_t tp = t - pod * plen;
             const int64_t pl = (L - pod * plen) < plen ? (L - pod * plen) : plen;
@@ -1380,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_synth(double* __restrict__ vals, const 
                     if (v < 0.0) v = 0.0;
                 }
             }
-            vals[beg + t] = v;
+            vals[beg + i] = v;
         }
     }
 }
@@ -1538,6 +1822,8 @@ int krr_create(int device, krr_ctx** out_ctx) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     (void)hipFuncSetAttribute((const void*)k_simple<CPU_HSELECT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
+    (void)hipFuncSetAttribute((const void*)k_sketch_build, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
 }
@@ -1740,17 +2026,103 @@ int krr_diag_attach(void* dev_buffer) {
 }
 #endif
 
-int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
-                   int32_t kind, int64_t pod_len, int32_t gaps, void* stream) {
+int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
+                          int32_t kind, int64_t pod_len, int32_t gaps, int64_t t0, int64_t total_len, void* stream) {
     if (!ctx) return KRR_E_INVALID;
-    if (n_segments < 0 || (n_segments > 0 && (!values || !offsets)) || kind < 0 || kind > 1)
+    if (n_segments < 0 || (n_segments > 0 && (!values || !offsets)) || kind < 0 || kind > 1 || t0 < 0 ||
+        total_len < 0)
         return set_err(ctx, KRR_E_INVALID, "bad synth arguments%s", "");
     if (n_segments == 0) return KRR_OK;
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     int64_t grid = n_segments < 65536 ? n_segments : 65536;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, values, offsets,
-                       n_segments, seed, kind, pod_len, gaps);
+                       n_segments, seed, kind, pod_len, gaps, t0, total_len);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
+                   int32_t kind, int64_t pod_len, int32_t gaps, void* stream) {
+    return krr_synth_fill_window(ctx, values, offsets, n_segments, seed, kind, pod_len, gaps, 0, 0, stream);
+}
+
+int64_t krr_sketch_width(const krr_sketch_params* sp) {
+    if (!sp || sp->mantissa_bits < 0 || sp->mantissa_bits > 10 || sp->octaves < 1 || sp->min_exponent < -1022 ||
+        (int64_t)sp->min_exponent + sp->octaves > 1024)
+        return -1;
+    return ((int64_t)sp->octaves << sp->mantissa_bits) + 4;
+}
+
+int krr_sketch_build(krr_ctx* ctx, const krr_series* series, const krr_sketch_params* sp, uint32_t* counts,
+                     double* vmin, double* vmax, uint32_t* flags, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    const int64_t W = krr_sketch_width(sp);
+    if (W < 0) return set_err(ctx, KRR_E_INVALID, "bad sketch params%s", "");
+    if ((size_t)W * 4 > ctx->max_lds || (W & 3)) return set_err(ctx, KRR_E_UNSUPPORTED, "sketch width %s%lld", "", W);
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!counts || !vmin || !vmax || !flags) return set_err(ctx, KRR_E_INVALID, "null outputs%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    SketchBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, sketch_geom(*sp), counts, vmin, vmax,
+                      flags};
+    hipLaunchKernelGGL(k_sketch_build, dim3(grid_for(S)), dim3(64), (size_t)W * 4, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const double* vmin,
+                     const double* vmax, const krr_sketch_params* sp, const krr_percentile_params* params,
+                     double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    if (params->mode == KRR_PCT_REF_INDEX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no sketch form: use krr_select_present%s", "");
+    if (krr_sketch_width(sp) < 0) return set_err(ctx, KRR_E_INVALID, "bad sketch params%s", "");
+    if (n_segments < 0) return set_err(ctx, KRR_E_INVALID, "negative n_segments%s", "");
+    if (n_segments == 0) return KRR_OK;
+    if (!counts || !vmin || !vmax || !out_value || !out_count || !out_flags)
+        return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    SketchQueryArgs A{n_segments, sketch_geom(*sp), counts, vmin, vmax, params->mode, params->p_num,
+                      params->p_den, params->q, out_value, out_count, out_flags};
+    hipLaunchKernelGGL(k_sketch_query, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_rank_of(krr_ctx* ctx, const krr_series* series, const double* values, int64_t* out_lt, int64_t* out_le,
+                void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!values || !out_lt || !out_le) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_rank_of, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
+                       series->offsets, S, values, out_lt, out_le);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k, double* out, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!k || !out) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_select_present, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
+                       series->offsets, S, series->gaps_are_nan, k, out);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "krr_amd.h")
 
 def _declared():
     text = open(HEADER).read()
-    return set(re.findall(r"^(?:int|const char\*)\s+(krr_\w+)\(", text, flags=re.M))
+    return set(re.findall(r"^(?:int|int64_t|const char\*)\s+(krr_\w+)\(", text, flags=re.M))
 
 
 @pytest.fixture(scope="module")
