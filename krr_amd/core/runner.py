@@ -54,8 +54,34 @@ class BatchedRunner:
 
     def recommend(self, objects: Sequence[K8sObjectData], histories: Sequence[HistoryData]) -> list[RunResult]:
         """Rounded RunResults, one per object (what _calculate_object_recommendations returns)."""
+        if len(objects) != len(histories):
+            raise ValueError("one HistoryData per object")
+        if hasattr(self.strategy, "format_packed"):  # SimpleStrategy: pack once, native rounding
+            return self.strategy.format_packed(self.strategy.pack(histories), self.cpu_min_value,
+                                               self.memory_min_value)
         return [format_result(r, self.cpu_min_value, self.memory_min_value)
                 for r in self.raw_results(objects, histories)]
+
+    def recommend_packed(self, fleet) -> list[RunResult]:
+        """Rounded RunResults for a PackedFleet (e.g. from recommend_from_bodies)."""
+        if hasattr(self.strategy, "format_packed"):
+            return self.strategy.format_packed(fleet, self.cpu_min_value, self.memory_min_value)
+        raise TypeError(f"{type(self.strategy).__name__} has no batched packed path; use recommend()")
+
+    def recommend_from_bodies(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
+                              threads: int = 0) -> list[RunResult]:
+        """The whole loader -> strategy -> rounding path from raw Prometheus query_range
+        response bodies: bodies[o][i] = pod i of object o (K8sObjectData.pods order),
+        as PrometheusLoader.gather_data would fetch them (prometheus.py:118-143).
+        Native JSON packing (no Decimal lists), one kernel pass, native rounding."""
+        from krr_amd.core.packing import PackedFleet
+        from krr_amd.core.prom_native import pack_query_range_bodies
+
+        if len(cpu_bodies) != len(mem_bodies):
+            raise ValueError("cpu and memory bodies need one entry per object each")
+        fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads),
+                            pack_query_range_bodies(mem_bodies, threads=threads))
+        return self.recommend_packed(fleet)
 
     def allocations(self, objects: Sequence[K8sObjectData],
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:

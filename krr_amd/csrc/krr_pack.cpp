@@ -1,0 +1,447 @@
+// krr_pack.cpp — native Prometheus query_range packer (host C++17, std::thread).
+//
+// The reference parses every pod's response in Python: response.json() in
+// prometheus_api_client, then Decimal(value) per sample (prometheus.py:147-155),
+// ~4.6 M samples/s on one core.  Here each body is scanned
+// once by a small recursive-descent JSON reader that walks only the path it
+// needs (status, data.result[0].values) and skips everything else (metric
+// labels, further series) while still validating it; numbers go through
+// std::from_chars.  Bodies are independent, so a pool of threads parses them in
+// parallel, then the kept samples are copied into one CSR buffer.
+#include "krr_pack.h"
+
+#include <algorithm>
+#include <atomic>
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+namespace {
+
+double strtod_exact(const char* b, const char* e);
+
+struct Reader {
+    const char* p;
+    const char* e;
+    int depth = 0;
+
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+    }
+    bool lit(char c) {
+        ws();
+        if (p < e && *p == c) {
+            ++p;
+            return true;
+        }
+        return false;
+    }
+    bool peek(char c) {
+        ws();
+        return p < e && *p == c;
+    }
+    // A JSON string; *raw = its bytes between the quotes (escapes not decoded).
+    bool str(std::string_view* raw, bool* esc) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        const char* b = ++p;
+        bool any = false;
+        while (p < e && *p != '"') {
+            const unsigned char c = (unsigned char)*p;
+            if (c < 0x20) return false;
+            if (c == '\\') {
+                any = true;
+                if (++p >= e) return false;
+                if (*p == 'u') {
+                    if (e - p < 5) return false;
+                    for (int k = 1; k <= 4; ++k)
+                        if (!isxdigit((unsigned char)p[k])) return false;
+                    p += 4;
+                } else if (!strchr("\"\\/bfnrt", *p)) {
+                    return false;
+                }
+            }
+            ++p;
+        }
+        if (p >= e) return false;
+        if (raw) *raw = std::string_view(b, (size_t)(p - b));
+        if (esc) *esc = any;
+        ++p;
+        return true;
+    }
+    // JSON number (grammar checked), value via from_chars.
+    bool num(double* out) {
+        ws();
+        const char* b = p;
+        if (p < e && *p == '-') ++p;
+        if (p >= e) return false;
+        if (*p == '0') {
+            ++p;
+        } else if (*p >= '1' && *p <= '9') {
+            while (p < e && isdigit((unsigned char)*p)) ++p;
+        } else {
+            return false;
+        }
+        if (p < e && *p == '.') {
+            ++p;
+            if (p >= e || !isdigit((unsigned char)*p)) return false;
+            while (p < e && isdigit((unsigned char)*p)) ++p;
+        }
+        if (p < e && (*p == 'e' || *p == 'E')) {
+            ++p;
+            if (p < e && (*p == '+' || *p == '-')) ++p;
+            if (p >= e || !isdigit((unsigned char)*p)) return false;
+            while (p < e && isdigit((unsigned char)*p)) ++p;
+        }
+        if (out) {
+            auto r = std::from_chars(b, p, *out);
+            if (r.ec == std::errc::result_out_of_range) *out = strtod_exact(b, p);
+            else if (r.ec != std::errc()) return false;
+        }
+        return true;
+    }
+    bool word(const char* w) {
+        ws();
+        const size_t n = strlen(w);
+        if ((size_t)(e - p) < n || memcmp(p, w, n) != 0) return false;
+        p += n;
+        return true;
+    }
+    bool skip() {
+        ws();
+        if (p >= e || depth > 256) return false;
+        switch (*p) {
+            case '{': {
+                ++p;
+                ++depth;
+                if (lit('}')) {
+                    --depth;
+                    return true;
+                }
+                do {
+                    if (!str(nullptr, nullptr) || !lit(':') || !skip()) return false;
+                } while (lit(','));
+                --depth;
+                return lit('}');
+            }
+            case '[': {
+                ++p;
+                ++depth;
+                if (lit(']')) {
+                    --depth;
+                    return true;
+                }
+                do {
+                    if (!skip()) return false;
+                } while (lit(','));
+                --depth;
+                return lit(']');
+            }
+            case '"':
+                return str(nullptr, nullptr);
+            case 't':
+                return word("true");
+            case 'f':
+                return word("false");
+            case 'n':
+                return word("null");
+            default:
+                return num(nullptr);
+        }
+    }
+};
+
+// Decode a JSON string body (escapes) for key comparison.
+std::string unescape(std::string_view s) {
+    std::string o;
+    o.reserve(s.size());
+    for (size_t i = 0; i < s.size(); ++i) {
+        char c = s[i];
+        if (c != '\\') {
+            o.push_back(c);
+            continue;
+        }
+        c = s[++i];
+        switch (c) {
+            case 'b': o.push_back('\b'); break;
+            case 'f': o.push_back('\f'); break;
+            case 'n': o.push_back('\n'); break;
+            case 'r': o.push_back('\r'); break;
+            case 't': o.push_back('\t'); break;
+            case 'u': {
+                unsigned v = 0;
+                std::from_chars(s.data() + i + 1, s.data() + i + 5, v, 16);
+                i += 4;
+                if (v < 0x80) o.push_back((char)v);
+                else o.push_back('?');  // non-ASCII never matches our keys
+                break;
+            }
+            default: o.push_back(c);
+        }
+    }
+    return o;
+}
+
+bool key_is(std::string_view raw, bool esc, const char* k) {
+    return esc ? unescape(raw) == k : raw == k;
+}
+
+// from_chars leaves the value unspecified on a range error; strtod (C locale)
+// returns the correctly rounded result there: +-HUGE_VAL, 0, or a subnormal.
+double strtod_exact(const char* b, const char* e) {
+    const std::string tmp(b, e);
+    return strtod(tmp.c_str(), nullptr);
+}
+
+// Prometheus sample value string -> float64 (what Decimal(string) denotes, rounded).
+bool parse_value(std::string_view s, double* out) {
+    const char* b = s.data();
+    const char* e = b + s.size();
+    bool neg = false;
+    if (b < e && (*b == '+' || *b == '-')) {
+        neg = *b == '-';
+        ++b;
+    }
+    if (b >= e || *b == '+' || *b == '-') return false;
+    double v;
+    auto r = std::from_chars(b, e, v);
+    if (r.ptr != e) return false;
+    if (r.ec == std::errc::result_out_of_range) {
+        v = strtod_exact(b, e);  // overflow -> inf, underflow -> 0 or the subnormal
+    } else if (r.ec != std::errc()) {
+        return false;
+    }
+    *out = neg ? -v : v;
+    return true;
+}
+
+struct Body {
+    std::vector<double> v, t;
+    int status = KRR_PACK_OK;
+    bool dropped = false;
+    std::string err;
+};
+
+// One query_range response: {"status": "success", "data": {"resultType": ..., "result": [...]}}
+void parse_body(const char* s, int64_t n, bool want_ts, Body& out) {
+    Reader r{s, s + n};
+    auto fail = [&](int code, const char* what) {
+        out.status = code;
+        char buf[160];
+        snprintf(buf, sizeof(buf), "%s at byte %lld", what, (long long)(r.p - s));
+        out.err = buf;
+    };
+    bool have_status = false, ok_status = false, have_result = false;
+    if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "expected a JSON object");
+    if (!r.peek('}')) {
+        do {
+            std::string_view k;
+            bool esc;
+            if (!r.str(&k, &esc) || !r.lit(':')) return fail(KRR_PACK_E_PARSE, "bad object key");
+            if (key_is(k, esc, "status")) {
+                std::string_view v;
+                bool vesc;
+                if (!r.str(&v, &vesc)) return fail(KRR_PACK_E_PARSE, "status is not a string");
+                have_status = true;
+                ok_status = key_is(v, vesc, "success");
+            } else if (key_is(k, esc, "data")) {
+                if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "data is not an object");
+                if (!r.peek('}')) {
+                    do {
+                        std::string_view dk;
+                        bool desc;
+                        if (!r.str(&dk, &desc) || !r.lit(':')) return fail(KRR_PACK_E_PARSE, "bad data key");
+                        if (!key_is(dk, desc, "result")) {
+                            if (!r.skip()) return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                            continue;
+                        }
+                        if (!r.lit('[')) return fail(KRR_PACK_E_PARSE, "result is not an array");
+                        have_result = true;
+                        if (r.lit(']')) {
+                            out.dropped = true;  // prometheus.py:154: a pod with no series is dropped
+                            continue;
+                        }
+                        // result[0]: the only series the reference reads (pod_result[0]["values"])
+                        if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "series is not an object");
+                        bool have_values = false;
+                        if (!r.peek('}')) {
+                            do {
+                                std::string_view sk;
+                                bool sesc;
+                                if (!r.str(&sk, &sesc) || !r.lit(':')) return fail(KRR_PACK_E_PARSE, "bad series key");
+                                if (!key_is(sk, sesc, "values")) {
+                                    if (!r.skip()) return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                                    continue;
+                                }
+                                have_values = true;
+                                if (!r.lit('[')) return fail(KRR_PACK_E_PARSE, "values is not an array");
+                                if (r.lit(']')) continue;
+                                do {
+                                    double ts, val;
+                                    std::string_view vs;
+                                    bool vesc;
+                                    if (!r.lit('[') || !r.num(want_ts ? &ts : nullptr) || !r.lit(',') ||
+                                        !r.str(&vs, &vesc) || !r.lit(']'))
+                                        return fail(KRR_PACK_E_PARSE, "sample is not [time, \"value\"]");
+                                    if (vesc || !parse_value(vs, &val))
+                                        return fail(KRR_PACK_E_VALUE, "sample value is not a number");
+                                    out.v.push_back(val);
+                                    if (want_ts) out.t.push_back(ts);
+                                } while (r.lit(','));
+                                if (!r.lit(']')) return fail(KRR_PACK_E_PARSE, "unterminated values");
+                            } while (r.lit(','));
+                        }
+                        if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated series");
+                        if (!have_values) return fail(KRR_PACK_E_PARSE, "series without values");
+                        while (r.lit(','))  // further series: never read by the reference; validated
+                            if (!r.skip()) return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                        if (!r.lit(']')) return fail(KRR_PACK_E_PARSE, "unterminated result");
+                    } while (r.lit(','));
+                }
+                if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated data");
+            } else if (!r.skip()) {
+                return fail(KRR_PACK_E_PARSE, "malformed JSON");
+            }
+        } while (r.lit(','));
+    }
+    if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated response");
+    r.ws();
+    if (r.p != r.e) return fail(KRR_PACK_E_PARSE, "trailing bytes");
+    if (!have_status || !ok_status) return fail(KRR_PACK_E_STATUS, "status is not \"success\"");
+    if (!have_result) return fail(KRR_PACK_E_PARSE, "no data.result");
+}
+
+int pool_size(int32_t threads, int64_t work) {
+    int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    if (t < 1) t = 1;
+    if ((int64_t)t > work) t = (int)std::max<int64_t>(work, 1);
+    return t;
+}
+
+template <class F>
+void parallel_for(int64_t n, int32_t threads, F f) {
+    const int t = pool_size(threads, n);
+    if (t <= 1) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+        for (;;) {
+            const int64_t b = next.fetch_add(8);
+            if (b >= n) return;
+            const int64_t e = std::min<int64_t>(b + 8, n);
+            for (int64_t i = b; i < e; ++i) f(i);
+        }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)t - 1);
+    for (int k = 1; k < t; ++k) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+struct krr_pack {
+    std::vector<Body> bodies;
+    std::vector<int64_t> obj;
+    int64_t n_objects = 0;
+    int64_t n_values = 0;
+    int64_t max_len = 0;
+    bool want_ts = false;
+    std::string err;
+};
+
+extern "C" {
+
+int krr_pack_abi_version(void) { return KRR_PACK_ABI_VERSION; }
+
+int krr_pack_parse(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies, const int64_t* obj_of_body,
+                   int64_t n_objects, int32_t want_timestamps, int32_t threads, krr_pack** out) {
+    if (!out) return KRR_PACK_E_INVALID;
+    *out = nullptr;
+    if (n_bodies < 0 || n_objects < 0 || (n_bodies > 0 && (!bodies || !body_lens || !obj_of_body)))
+        return KRR_PACK_E_INVALID;
+    for (int64_t b = 0; b < n_bodies; ++b) {
+        if (obj_of_body[b] < 0 || obj_of_body[b] >= n_objects || (b && obj_of_body[b] < obj_of_body[b - 1]) ||
+            body_lens[b] < 0 || (body_lens[b] > 0 && !bodies[b]))
+            return KRR_PACK_E_INVALID;
+    }
+    krr_pack* p = new (std::nothrow) krr_pack();
+    if (!p) return KRR_PACK_E_INVALID;
+    try {
+        p->bodies.resize((size_t)n_bodies);
+        p->obj.assign(obj_of_body, obj_of_body + n_bodies);
+    } catch (...) {
+        delete p;
+        return KRR_PACK_E_INVALID;
+    }
+    p->n_objects = n_objects;
+    p->want_ts = want_timestamps != 0;
+    parallel_for(n_bodies, threads, [&](int64_t b) {
+        try {
+            parse_body(bodies[b], body_lens[b], p->want_ts, p->bodies[(size_t)b]);
+        } catch (...) {
+            p->bodies[(size_t)b].status = KRR_PACK_E_INVALID;
+            p->bodies[(size_t)b].err = "out of memory";
+        }
+    });
+    int rc = KRR_PACK_OK;
+    std::vector<int64_t> seg((size_t)n_objects, 0);
+    for (int64_t b = 0; b < n_bodies; ++b) {
+        const Body& B = p->bodies[(size_t)b];
+        if (B.status != KRR_PACK_OK) {
+            if (rc == KRR_PACK_OK) {
+                rc = B.status;
+                p->err = "body " + std::to_string(b) + ": " + B.err;
+            }
+            continue;
+        }
+        seg[(size_t)p->obj[(size_t)b]] += (int64_t)B.v.size();
+        p->n_values += (int64_t)B.v.size();
+    }
+    for (int64_t s : seg) p->max_len = std::max(p->max_len, s);
+    *out = p;
+    return rc;
+}
+
+int64_t krr_pack_n_values(const krr_pack* p) { return p ? p->n_values : -1; }
+int64_t krr_pack_max_len(const krr_pack* p) { return p ? p->max_len : -1; }
+const char* krr_pack_error(const krr_pack* p) { return p ? p->err.c_str() : "null krr_pack"; }
+void krr_pack_free(krr_pack* p) { delete p; }
+
+int krr_pack_copy(const krr_pack* p, double* values, int64_t* offsets, double* timestamps, int64_t* pod_counts,
+                  int32_t threads) {
+    if (!p || !offsets || (p->n_values > 0 && !values)) return KRR_PACK_E_INVALID;
+    if (timestamps && !p->want_ts) return KRR_PACK_E_INVALID;
+    if (!p->err.empty()) return KRR_PACK_E_PARSE;
+    const int64_t nb = (int64_t)p->bodies.size();
+    std::vector<int64_t> start((size_t)nb, 0);
+    int64_t pos = 0;
+    for (int64_t s = 0; s <= p->n_objects; ++s) offsets[s] = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        start[(size_t)b] = pos;
+        const int64_t c = (int64_t)p->bodies[(size_t)b].v.size();
+        pos += c;
+        offsets[p->obj[(size_t)b] + 1] += c;
+        if (pod_counts) pod_counts[b] = p->bodies[(size_t)b].dropped ? -1 : c;
+    }
+    for (int64_t s = 0; s < p->n_objects; ++s) offsets[s + 1] += offsets[s];
+    parallel_for(nb, threads, [&](int64_t b) {
+        const Body& B = p->bodies[(size_t)b];
+        if (B.v.empty()) return;
+        memcpy(values + start[(size_t)b], B.v.data(), B.v.size() * sizeof(double));
+        if (timestamps) memcpy(timestamps + start[(size_t)b], B.t.data(), B.t.size() * sizeof(double));
+    });
+    return KRR_PACK_OK;
+}
+
+}  // extern "C"

@@ -121,8 +121,19 @@ class SimpleStrategy(BaseStrategy[SimpleStrategySettings]):
     def run_batch(self, histories: Sequence[HistoryData],
                   objects: Optional[Sequence[K8sObjectData]] = None) -> list[RunResult]:
         """One fleet-wide kernel pass for every object (the batched-runner hook)."""
-        fleet = PackedFleet(pack_resource(histories, ResourceType.CPU), pack_resource(histories, ResourceType.Memory))
-        return self.results_from_raw(self.settings.run_fleet(fleet))
+        return self.results_from_raw(self.settings.run_fleet(self.pack(histories)))
+
+    @staticmethod
+    def pack(histories: Sequence[HistoryData]) -> PackedFleet:
+        return PackedFleet(pack_resource(histories, ResourceType.CPU), pack_resource(histories, ResourceType.Memory))
+
+    def format_packed(self, fleet: PackedFleet, cpu_min_value: int, memory_min_value: int) -> list[RunResult]:
+        """Kernel pass + the reference's rounding (Runner._format_result) for a packed
+        fleet, the rounding done in native exact-decimal code (krr_amd.core.fast_round):
+        equal to format_result(r) for r in run_batch(...), ~20x cheaper per object."""
+        from krr_amd.core.fast_round import format_simple_batch
+
+        return format_simple_batch(self.settings.run_fleet(fleet), self.settings, cpu_min_value, memory_min_value)
 
     def results_from_raw(self, raw: RawResults) -> list[RunResult]:
         st = self.settings

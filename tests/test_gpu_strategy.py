@@ -120,6 +120,44 @@ def test_batched_runner_end_to_end():
         assert (cpu == "?" and want["cpu_request"] == "NaN") or str(cpu) == want["cpu_request"], c["name"]
 
 
+@pytest.mark.parametrize("path", list(PATHS))
+def test_batched_runner_recommend_and_bodies_match_reference(path):
+    """BatchedRunner.recommend (native rounding) and recommend_from_bodies (native JSON
+    packer + kernel + native rounding) against the reference's rounded outputs."""
+    from krr_amd.core.models.allocations import ResourceType
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+    from krr_amd.utils.prom_decimal import prom_format
+
+    kw = PATHS[path]
+    strat = SimpleStrategy(SimpleStrategySettings() if kw is None else SimpleStrategySettings(**kw))
+    cmin, mmin = MINS.get(path, (5, 10))
+    runner = BatchedRunner(strat, cmin, mmin)
+    cases = [c for c in DOC["cases"] if "rounded" in c["results"][path]]
+    got = runner.recommend([_obj(c["name"]) for c in cases], [_hist(c) for c in cases])
+
+    def body(vals):
+        res = [] if not vals else [{"metric": {"pod": "p"}, "values": [[1.7e9 + i, v] for i, v in enumerate(vals)]}]
+        return json.dumps({"status": "success", "data": {"resultType": "matrix", "result": res}}).encode()
+
+    # Prometheus can only send shortest-repr strings: cases whose samples are not are skipped
+    repr_ok = [all(prom_format(float(v)) == v for r in ("cpu", "mem") for vs in c[r].values() for v in vs)
+               for c in cases]
+    bc = [c for c, ok in zip(cases, repr_ok) if ok]
+    got_b = runner.recommend_from_bodies([[body(v) for v in c["cpu"].values()] for c in bc],
+                                         [[body(v) for v in c["mem"].values()] for c in bc])
+    for c, r in zip(cases, got):
+        want = c["results"][path]["rounded"]
+        assert {"cpu_request": _d(r[ResourceType.CPU].request), "cpu_limit": _d(r[ResourceType.CPU].limit),
+                "mem_request": _d(r[ResourceType.Memory].request),
+                "mem_limit": _d(r[ResourceType.Memory].limit)} == want, c["name"]
+    assert len(bc) > len(cases) // 2
+    for c, r in zip(bc, got_b):
+        want = c["results"][path]["rounded"]
+        assert _d(r[ResourceType.CPU].request) == want["cpu_request"], c["name"]
+        assert _d(r[ResourceType.Memory].request) == want["mem_request"], c["name"]
+
+
 def _fleet(seed, gaps):
     rng = np.random.default_rng(seed)
     S = 300

@@ -1,0 +1,150 @@
+"""Native query_range packer (libkrr_pack.so) vs the reference's semantics.
+
+The reference (core/integrations/prometheus.py:147-155) keeps, per pod, only
+result[0]["values"], drops a pod whose result list is empty, discards the
+timestamps and parses each value with Decimal().  The oracle below restates that
+with json + Decimal; the packer must give the same float64 bits, offsets and pod
+drops.  (No reference test pins this boundary: SURVEY.md §8c, "parity unpinned"
+by reference fixtures — these tests are the pin.)"""
+import json
+import math
+from decimal import Decimal
+
+import numpy as np
+import pytest
+
+from krr_amd.core.prom_native import PrometheusResponseError, pack_query_range_bodies
+
+
+def go_format(x: float) -> str:
+    """Prometheus' value formatting: strconv.FormatFloat(x, 'f', -1, 64), NaN/+Inf/-Inf."""
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "+Inf" if x > 0 else "-Inf"
+    r = repr(x)  # shortest round-trip digits
+    if "e" not in r and "E" not in r:
+        return r[:-2] if r.endswith(".0") else r
+    d = Decimal(r)
+    s = format(d, "f")
+    return s
+
+
+def body(series, status="success", extra_series=0, rng=None):
+    res = []
+    for k in range(1 + extra_series if series is not None else 0):
+        vals = series if k == 0 else [(1.0, "7")]
+        res.append({"metric": {"pod": "p\"o\\d", "container": "c", "ünï": "x"},
+                    "values": [[t, v] for t, v in vals]})
+    doc = {"status": status, "data": {"resultType": "matrix", "result": res}}
+    return json.dumps(doc).encode()
+
+
+def ref_pack(per_object_bodies):
+    """The reference's semantics (prometheus.py:147-155) + float()."""
+    vals, offs, counts = [], [0], []
+    for bodies in per_object_bodies:
+        n = 0
+        for b in bodies:
+            result = json.loads(b)["data"]["result"]
+            if result == []:
+                counts.append(-1)
+                continue
+            v = [float(Decimal(x)) for _, x in result[0]["values"]]
+            vals.extend(v)
+            n += len(v)
+            counts.append(len(v))
+        offs.append(offs[-1] + n)
+    return np.array(vals, dtype=np.float64), np.array(offs, dtype=np.int64), np.array(counts, dtype=np.int64)
+
+
+def _fleet(seed, n_obj=60):
+    rng = np.random.default_rng(seed)
+    per_obj = []
+    for o in range(n_obj):
+        pods = []
+        for p in range(int(rng.integers(0, 5))):
+            kind = rng.random()
+            if kind < 0.15:
+                pods.append(body(None))  # empty result: dropped
+                continue
+            n = int(rng.integers(0, 400))
+            xs = rng.gamma(2.0, 0.05, size=n)
+            special = rng.random(n)
+            xs[special < 0.01] = np.nan
+            xs[(special >= 0.01) & (special < 0.015)] = np.inf
+            xs[(special >= 0.015) & (special < 0.02)] = -np.inf
+            xs[(special >= 0.02) & (special < 0.05)] = np.floor(rng.normal(2e8, 2e7, size=int(((special >= 0.02) & (special < 0.05)).sum())))
+            xs[(special >= 0.05) & (special < 0.06)] = 1e-300 * rng.random(int(((special >= 0.05) & (special < 0.06)).sum()))
+            ts = 1.7e9 + 60.0 * np.arange(n) + 0.781
+            pods.append(body([(float(t), go_format(float(x))) for t, x in zip(ts, xs)],
+                             extra_series=int(rng.integers(0, 2))))
+        per_obj.append(pods)
+    return per_obj
+
+
+@pytest.mark.parametrize("threads", [1, 4, 0])
+def test_matches_reference_semantics(threads):
+    per_obj = _fleet(1)
+    ps, ts, counts = pack_query_range_bodies(per_obj, want_timestamps=True, threads=threads, return_pod_counts=True)
+    v, o, c = ref_pack(per_obj)
+    assert np.array_equal(ps.offsets, o)
+    assert np.array_equal(ps.values.view(np.uint64), v.view(np.uint64))
+    assert np.array_equal(counts, c)
+    assert ps.max_len == int(np.diff(o).max())
+    want_ts = []
+    for bodies in per_obj:
+        for b in bodies:
+            r = json.loads(b)["data"]["result"]
+            if r:
+                want_ts.extend(t for t, _ in r[0]["values"])
+    assert np.array_equal(ts, np.array(want_ts, dtype=np.float64))
+
+
+def test_shortest_repr_round_trip():
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.gamma(2.0, 0.05, 3000), np.exp(rng.uniform(-700, 700, 3000)),
+                         rng.integers(0, 2**53, 1000).astype(np.float64), [5e-324, 2.2250738585072014e-308,
+                                                                            1.7976931348623157e308, 0.0, -0.0]])
+    strs = [repr(float(x)) for x in xs] + [go_format(float(x)) for x in xs]
+    b = body([(0.0, s) for s in strs])
+    ps = pack_query_range_bodies([[b]])
+    want = np.array([float(s) for s in strs])
+    assert np.array_equal(ps.values.view(np.uint64), want.view(np.uint64))
+
+
+def test_layout_variants():
+    vals = [(1.0, "1.5"), (2.0, "2.5")]
+    a = body(vals)
+    # reordered keys, whitespace, escaped key names, leading data before status
+    b = (b'  {"data" : {"result":[ {"\\u0076alues": [[1, "1.5"] ,[2,"2.5"]], "metric":{"a":[1,{"b":null}]}} ],'
+         b' "resultType":"matrix"}, "status":"success", "warnings": ["x"]} \n')
+    ps = pack_query_range_bodies([[a], [b], []])
+    assert list(ps.offsets) == [0, 2, 4, 4]
+    assert list(ps.values) == [1.5, 2.5, 1.5, 2.5]
+
+
+@pytest.mark.parametrize("bad,code", [
+    (b'{"status":"error","errorType":"bad_data","error":"x"}', -3),
+    (b'{"status":"success","data":{"result":[{"values":[[1,"abc"]]}]}}', -4),
+    (b'{"status":"success","data":{"result":[{"values":[[1,1.5]]}]}}', -2),
+    (b'{"status":"success","data":{"result":[{"values":[[1,"1.5"]]}]}', -2),
+    (b'{"status":"success","data":{"resultType":"matrix"}}', -2),
+    (b'{"status":"success","data":{"result":[{"metric":{}}]}}', -2),
+    (b'not json', -2),
+    (b'{"status":"success","data":{"result":[{"values":[[1,"1.5"]]}]}} trailing', -2),
+    (b'{"status":"success","data":{"result":[{"values":[[1,"1_5"]]}]}}', -4),
+])
+def test_errors_name_the_body(bad, code):
+    good = body([(1.0, "1")])
+    with pytest.raises(PrometheusResponseError) as e:
+        pack_query_range_bodies([[good], [good, bad]])
+    assert e.value.code == code
+    assert "body 2" in str(e.value)
+
+
+def test_empty_fleet():
+    ps = pack_query_range_bodies([])
+    assert ps.values.size == 0 and list(ps.offsets) == [0]
+    ps = pack_query_range_bodies([[], []])
+    assert list(ps.offsets) == [0, 0, 0]
