@@ -52,7 +52,10 @@ def parse():
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
     ap.add_argument("--containers", type=int, default=0, help="override containers per rank (testing)")
-    ap.add_argument("--cpu-sample", type=int, default=400, help="containers in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="containers in the CPU-baseline / parity sample (0: the whole rank, capped at 1.1e9 slots)")
+    ap.add_argument("--numpy-seconds", type=float, default=5.0,
+                    help="time budget of the single-thread numpy reference-path baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="two launches (percentile, max) instead of the fused one")
@@ -243,7 +246,8 @@ def main():
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         from oracle import oracle
 
-        m = max(1, min(args.cpu_sample, S))
+        m = S if args.cpu_sample <= 0 else max(1, min(args.cpu_sample, S))
+        m = max(1, min(m, int(np.searchsorted(offs_np, 1_100_000_000, side="right")) - 1))
         end = int(offs_np[m])
         c_host = cpu[:end].cpu().numpy()
         m_host = mem[:end].cpu().numpy()
@@ -276,6 +280,29 @@ def main():
                       f"{args.mode} + max, OpenMP {threads} threads on {cpu_model or platform.processor()}",
         }
         result["parity_vs_oracle_on_sample"] = parity
+        result["parity_sample_containers"] = m
+        # the reference's path restated in numpy (single thread): per container, the
+        # pods' present samples -> np.percentile / np.max, as long as the time budget lasts
+        t_c = time.perf_counter()
+        done = 0
+        qv = float(args.percentile)
+        while done < m and time.perf_counter() - t_c < args.numpy_seconds:
+            a, b = int(o_host[done]), int(o_host[done + 1])
+            xc = c_host[a:b]
+            xm = m_host[a:b]
+            if gaps:
+                xc = xc[~np.isnan(xc)]
+                xm = xm[~np.isnan(xm)]
+            if xc.size:
+                np.percentile(xc, qv)
+            if xm.size:
+                xm.max()
+            done += 1
+        t_d = time.perf_counter()
+        result["cpu_baseline_numpy"] = {
+            "value": done / (t_d - t_c), "unit": "container-series/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} containers of this run, np.percentile(method='linear') + max per container, "
+                      f"one thread, {args.numpy_seconds:.0f} s budget"}
         # the reference's own CPU path, measured in the build container only (cannot travel):
         result["reference_cpu_measured_in_build_container"] = {
             "value": 492.0, "unit": "container-series/s", "cores": 1,
