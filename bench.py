@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
     ap.add_argument("--containers", type=int, default=0, help="override containers per rank (testing)")
+    ap.add_argument("--pods", type=int, default=5, help="config 2: pods per container (segment = pods x 10,080)")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="containers in the CPU-baseline / parity sample (0: the whole rank, capped at 1.1e9 slots)")
     ap.add_argument("--numpy-seconds", type=float, default=5.0,
@@ -63,13 +64,14 @@ def parse():
     return ap.parse_args()
 
 
-def workload(cfg: int, rank: int, world: int, override: int):
+def workload(cfg: int, rank: int, world: int, override: int, pods: int = 5):
     """Per-rank (offsets numpy array, pod_len, gaps, description, containers_total)."""
     if cfg == 2:
         n = override or 10_000
-        L = 5 * SLOTS_7D
+        L = pods * SLOTS_7D
         offs = np.arange(n + 1, dtype=np.int64) * L
-        return offs, SLOTS_7D, True, f"config2: {n} containers/rank x 5 pods x 10080 slots (7d@1m), NaN-gapped dense", n * world
+        return offs, SLOTS_7D, True, (f"config2: {n} containers/rank x {pods} pods x 10080 slots (7d@1m), "
+                                      f"NaN-gapped dense"), n * world
     if cfg == 3:
         n = override or 100_000
         rng = np.random.default_rng(3 + rank)
@@ -111,7 +113,7 @@ def main():
     if args.config == 5:
         return run_config5(args, world, rank, local, dev, coll_dev)
 
-    offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers)
+    offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers, args.pods)
     S = offs_np.size - 1
     N = int(offs_np[-1])
     maxlen = int(np.max(np.diff(offs_np))) if S else 0
@@ -235,7 +237,7 @@ def main():
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
-        key = f"config{args.config}:{args.mode}:{result['roofline']['kernel']}"
+        key = f"config{args.config}:{args.mode}:p{args.percentile}:{result['roofline']['kernel']}"
         if key in tr and int(tr[key].get("containers_per_rank", -1)) == S:
             result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
             result["roofline"]["traffic_source"] = tr[key].get("source")

@@ -31,6 +31,9 @@
 #ifndef KRR_SELECT_WAVES_PER_SIMD
 #define KRR_SELECT_WAVES_PER_SIMD 3  // __launch_bounds__ occupancy hint for the single-pass select
 #endif
+#ifndef KRR_MAX_DEPTH
+#define KRR_MAX_DEPTH 2  // chunks in flight in the multi-site streaming loop (k_max): 1 or 2
+#endif
 #ifndef KRR_HSEL_WAVES_PER_SIMD
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
@@ -170,6 +173,20 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
             proc.chunk(cur);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+        }
+    } else if constexpr (KRR_MAX_DEPTH >= 2) {
+        // three buffers with fixed roles: two chunks stay in flight while one is processed
+        double2 b0[kUnroll], b1[kUnroll], b2[kUnroll];
+        fill(b0, 0);
+        if (nch > 1) fill(b1, 1);
+        if (nch > 2) fill(b2, 2);
+        for (int64_t ci = 0; ci < nch; ci += 3) {
+            proc.chunk(b0);
+            if (ci + 3 < nch) fill(b0, ci + 3);
+            if (ci + 1 < nch) proc.chunk(b1);
+            if (ci + 4 < nch) fill(b1, ci + 4);
+            if (ci + 2 < nch) proc.chunk(b2);
+            if (ci + 5 < nch) fill(b2, ci + 5);
         }
     } else {
         double2 b0[kUnroll], b1[kUnroll];
@@ -716,7 +733,10 @@ __device__ __forceinline__ void write_result(const SelectArgs& A, int64_t s, dou
 // (kHistBins x 4 B) + collect buffer (kCollectCap x 8 B).
 
 // One CPU segment (SORTED_LOWER / LINEAR) by one wave, single HBM pass.
-__device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
+// `stream(P)` runs the segment's samples through P and returns the NaN padding.
+template <class Streamer>
+__device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t s, unsigned char* smem, int lane,
+                                                    Streamer stream) {
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t L = end - beg;
@@ -739,7 +759,7 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
         for (int d = 0; d < D_WORDS; ++d) P.diag[d] = 0;
         KRR_DIAG_T0(t_begin);
 #endif
-        const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);  // NaN padding slots
+        const uint32_t pad = stream(P);  // NaN padding slots
         __syncthreads();
 #ifdef KRR_DIAG
         KRR_DIAG_T0(t_final);
@@ -781,6 +801,12 @@ __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, u
         write_result(A, s, result, n, flags, lane);
         __syncthreads();
     }
+}
+
+__device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
+    const int64_t beg = A.offs[s], end = A.offs[s + 1];
+    select_segment_with(A, s, smem, lane,
+                        [&](SelectProc& P) { return stream_segment<true>(A.vals, beg, end, P, lane); });
 }
 
 // ---------------------------------------------------------------------------
@@ -956,7 +982,9 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
         Ranks R;
         R.r0 = R.r1 = 0;
         R.gamma = 0.0;
-        RankLoc loc[2];
+        RankLoc loc0, loc1;
+        loc0.lo = loc0.hi = loc1.lo = loc1.hi = 0;
+        loc0.exact = loc1.exact = 0;
         uint32_t done = 0;
 #pragma unroll 1
         for (int pass = 0; pass < 10 && !done; ++pass) {
@@ -997,11 +1025,11 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
             const HistScan hs = hist_scan(hist, lane);
             const uint64_t inr = hs.total;
             // locate both ranks
-#pragma unroll 1
-            for (int qi = 0; qi < 2; ++qi) {
-                const uint64_t r = (uint64_t)(qi ? R.r1 : R.r0);
-                RankLoc& l = loc[qi];
+            // two named locations (not an indexed array: that would live in scratch)
+            auto locate_rank = [&](uint64_t r) {
+                RankLoc l;
                 l.exact = 0;
+                l.below = l.count = 0;
                 if (r < below) {
                     if (zsplit && r >= zb - z0 && r < zb) {
                         l.exact = 1;
@@ -1038,19 +1066,22 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
                     l.count = n - below - inr;
                 }
                 if (!l.exact && l.lo == l.hi) l.exact = 1;
-            }
+                return l;
+            };
+            loc0 = locate_rank((uint64_t)R.r0);
+            loc1 = R.r1 != R.r0 ? locate_rank((uint64_t)R.r1) : loc0;
             __syncthreads();
-            if (loc[0].exact && loc[1].exact) {
+            if (loc0.exact && loc1.exact) {
                 done = 1;
                 break;
             }
             // the key range still to resolve (one range, or the union of two)
-            RankLoc u = loc[0].exact ? loc[1] : loc[0];
-            if (!loc[0].exact && !loc[1].exact && (loc[1].lo != loc[0].lo || loc[1].hi != loc[0].hi)) {
-                u.lo = loc[0].lo;
-                u.hi = loc[1].hi;
-                u.below = loc[0].below;
-                u.count = loc[1].below + loc[1].count - loc[0].below;
+            RankLoc u = loc0.exact ? loc1 : loc0;
+            if (!loc0.exact && !loc1.exact && (loc1.lo != loc0.lo || loc1.hi != loc0.hi)) {
+                u.lo = loc0.lo;
+                u.hi = loc1.hi;
+                u.below = loc0.below;
+                u.count = loc1.below + loc1.count - loc0.below;
             }
             if (u.count <= kCollectCap) {
                 // ---- collect pass: the range's keys into LDS, select there
@@ -1074,14 +1105,12 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
                 P.bad = 0;
                 uint64_t mn, mx;
                 P.buf_minmax(mn, mx);
-#pragma unroll 1
-                for (int qi = 0; qi < 2; ++qi) {
-                    if (loc[qi].exact) continue;
-                    const uint64_t r = (uint64_t)(qi ? R.r1 : R.r0);
-                    const uint64_t idx = r - u.below;  // ascending index in the range
-                    loc[qi].lo = P.kth_largest((uint32_t)(u.count - idx), mn, mx);
-                    loc[qi].exact = 1;
-                }
+                // ascending index in the range -> R-th largest (1-based)
+                if (!loc0.exact) loc0.lo = P.kth_largest((uint32_t)(u.count - ((uint64_t)R.r0 - u.below)), mn, mx);
+                if (!loc1.exact)
+                    loc1.lo = R.r1 == R.r0 ? loc0.lo
+                                           : P.kth_largest((uint32_t)(u.count - ((uint64_t)R.r1 - u.below)), mn, mx);
+                loc0.exact = loc1.exact = 1;
                 bad |= P.bad;
                 done = 1;
                 break;
@@ -1091,7 +1120,7 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
             hi = u.hi;
         }
         if (n && !(flags & (KRR_FLAG_EMPTY | KRR_FLAG_NAN))) {
-            if (done) result = finish_value(A, R, loc[0].lo, loc[1].lo, beg, end, lane);
+            if (done) result = finish_value(A, R, loc0.lo, loc1.lo, beg, end, lane);
             else bad |= 64u;
         }
         if (bad) flags |= KRR_FLAG_CAPACITY | (bad << 8);
@@ -1243,12 +1272,12 @@ struct MaxArgs {
     uint32_t* out_f;
 };
 
-template <bool ONE_SITE>
-__device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lane) {
+template <class Streamer>
+__device__ __forceinline__ void max_segment_with(const MaxArgs& A, int64_t s, int lane, Streamer stream) {
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         MaxProc M{__builtin_nan(""), 0u};
-        M.nn -= stream_segment<ONE_SITE>(A.vals, beg, end, M, lane);
+        M.nn -= stream(M);
         const uint64_t L = (uint64_t)(end - beg);
         const uint64_t n = A.gaps ? L - M.nn : L;
         const double mx = wave_max_f64(M.mx);
@@ -1271,6 +1300,12 @@ __device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lan
             A.out_f[s] = flags;
         }
     }
+}
+
+template <bool ONE_SITE>
+__device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lane) {
+    const int64_t beg = A.offs[s], end = A.offs[s + 1];
+    max_segment_with(A, s, lane, [&](MaxProc& M) { return stream_segment<ONE_SITE>(A.vals, beg, end, M, lane); });
 }
 
 __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
@@ -1814,6 +1849,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
         delete c;
         return KRR_E_HIP;
     }
+
     (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
     (void)hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1,4 +1,4 @@
 set -o pipefail
-timeout -k 10 500 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 200 --timeout-method thread > gpurun_out/gpu_tests_full.log 2>&1; rc=$?; tail -12 gpurun_out/gpu_tests_full.log; [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/gpu_tests_full.log | head; exit 1; }
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { tail -20 gpurun_out/bench_full.err; exit 1; }
-cat gpurun_out/bench_full.json
+V=krr_amd/lib/variants
+timeout -k 10 200 python -u scripts/ab_variants.py $V/lib_d1.so $V/lib_d2.so --rounds 7 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 200 python -u scripts/ab_variants.py $V/lib_d1.so $V/lib_d2.so --rounds 5 --config 3 --containers 100000 2>&1 | grep -v amdgpu.ids || exit 1

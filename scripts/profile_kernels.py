@@ -27,6 +27,20 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = _native.Context(0)
     n = a.containers
+    if a.config == 5:  # sketch build over 30d@15s series (bench.py config 5 at N=1)
+        from krr_amd.core import sketch
+
+        T = 172_800
+        offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * T
+        x = torch.empty(n * T, dtype=torch.float64, device=dev)
+        ctx.synth_fill_window(x, offs, 1000003 * 6, 0, 0, False, 0, T)
+        ser = ctx.series(x, offs, T, False)
+        cfg = sketch.SketchConfig()
+        for _ in range(a.reps):
+            sketch.build(ctx, ser, cfg)
+        torch.cuda.synchronize()
+        print("done", n, n * T)
+        return
     if a.config == 2:
         L, pod_len, gaps = 5 * 10080, 10080, True
         offs_np = np.arange(n + 1, dtype=np.int64) * L
