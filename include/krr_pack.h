@@ -69,6 +69,38 @@ const char* krr_pack_error(const krr_pack* p);
 
 void krr_pack_free(krr_pack* p);
 
+/* ---- Grouped responses (fleet-level query batching) ----
+ * One `sum by (pod) (...)` range query per (namespace, container) replaces one
+ * `sum(...{pod="..."})` query per pod (prometheus.py:118-143); its response holds
+ * one series per pod.  krr_pack_parse_series splits such a body into its series,
+ * each tagged with its metric's `label` value, for the caller to route to
+ * (object, pod) slots in K8sObjectData.pods order. */
+typedef struct krr_series_set krr_series_set;
+
+int krr_pack_parse_series(const char* body, int64_t len, const char* label, int32_t want_timestamps,
+                          krr_series_set** out);
+int64_t krr_series_count(const krr_series_set* h);
+/* NUL-terminated label value of series i; *len = its byte length, or -1 if the
+ * series has no such label. */
+const char* krr_series_label(const krr_series_set* h, int64_t i, int64_t* len);
+int64_t krr_series_len(const krr_series_set* h, int64_t i);
+int krr_series_copy(const krr_series_set* h, int64_t i, double* values, double* timestamps);
+const char* krr_series_error(const krr_series_set* h);
+void krr_series_free(krr_series_set* h);
+
+/* The whole fleet at once: n_bodies grouped response bodies in, one krr_pack out
+ * (read it with krr_pack_n_values / krr_pack_max_len / krr_pack_copy, exactly as
+ * krr_pack_parse's).  Slot s is one (object, pod) pair in fleet order: its pod name
+ * is slot_names[slot_name_offsets[s] .. slot_name_offsets[s+1]), its series is the
+ * first one in body slot_body[s] whose metric[label] equals that name (none: the
+ * pod is dropped, pod_counts[s] = -1, as the reference drops an empty result), and
+ * obj_of_slot is non-decreasing in [0, n_objects).  krr_pack_copy's pod_counts is
+ * then indexed by slot. */
+int krr_pack_parse_grouped(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies, const char* label,
+                           const int64_t* slot_body, const char* slot_names, const int64_t* slot_name_offsets,
+                           const int64_t* obj_of_slot, int64_t n_slots, int64_t n_objects, int32_t want_timestamps,
+                           int32_t threads, krr_pack** out);
+
 #ifdef __cplusplus
 }
 #endif

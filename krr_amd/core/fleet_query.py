@@ -1,0 +1,224 @@
+"""Fleet-level PromQL batching: one range query per
+(namespace, container) group instead of one per pod, demultiplexed natively.
+
+The reference issues ``sum(<metric>{namespace="ns", pod="p", container="c"})``
+once per pod, per object, per resource (``PrometheusLoader.gather_data``,
+``robusta_krr/core/integrations/prometheus.py:118-143``) — for a 10k-pod fleet
+that is 20k HTTP round trips, each returning one series.  Here the pods of every
+object that share a (namespace, container) pair go into one
+
+    sum by (pod) (<metric>{<same matchers>, namespace="ns", pod=~"p1|p2|...", container="c"})
+
+query (split when the pod regex grows past ``max_query_chars``).  ``sum by (pod)``
+evaluated over the same start/end/step yields, for every pod, exactly the series
+the per-pod ``sum(...{pod="p"})`` yields (same matchers, same aggregation inputs,
+same evaluation timestamps); a pod with no samples is absent from the grouped
+result just as its per-pod result list is empty, and is dropped the same way
+(prometheus.py:154).  ``krr_pack_parse_grouped`` (include/krr_pack.h) parses all
+grouped bodies in parallel and routes each series by its ``pod`` label into the
+fleet's (object, pod) order, producing the same CSR layout
+``pack_query_range_bodies`` produces from per-pod bodies — bit-identical values
+and offsets (tests/test_fleet_query.py).
+
+Host-only: no HIP, no torch.  ``FleetQueryPlan.fetch`` takes any callable that
+performs one query_range HTTP request and returns its raw body, so the plan works
+with the reference's ``PrometheusConnect`` session or a test double.
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Callable, Sequence
+
+import numpy as np
+
+from krr_amd.core.models.allocations import ResourceType
+from krr_amd.core.packing import PackedFleet, PackedSeries
+from krr_amd.core.prom_native import KRR_PACK_OK, PrometheusResponseError, _ptr, load_library
+
+# The reference's selectors (prometheus.py:123 and :137), without the pod/ns/container matchers.
+CPU_METRIC = "node_namespace_pod_container:container_cpu_usage_seconds_total:sum_irate"
+CPU_MATCHERS = ""
+MEMORY_METRIC = "container_memory_working_set_bytes"
+MEMORY_MATCHERS = 'job="kubelet", metrics_path="/metrics/cadvisor", image!="", '
+
+_METRIC = {ResourceType.CPU: (CPU_METRIC, CPU_MATCHERS), ResourceType.Memory: (MEMORY_METRIC, MEMORY_MATCHERS)}
+
+# RE2 metacharacters (Prometheus' =~ is a fully anchored RE2 match).
+_RE2_META = set("\\.+*?()|[]{}^$")
+
+
+def step_string(timeframe: datetime.timedelta) -> str:
+    """The reference's step argument (prometheus.py:126)."""
+    return f"{int(timeframe.total_seconds()) // 60}m"
+
+
+def pod_query(resource: ResourceType, namespace: str, pod: str, container: str) -> str:
+    """The reference's per-pod query, character for character (prometheus.py:123, :137)."""
+    metric, matchers = _resolve(resource)
+    return f'sum({metric}{{{matchers}namespace="{namespace}", pod="{pod}", container="{container}"}})'
+
+
+def pod_regex(pods: Sequence[str]) -> str:
+    """RE2 alternation matching exactly ``pods``, as it appears inside a PromQL
+    double-quoted string (every regex backslash doubled)."""
+    parts = []
+    for p in pods:
+        esc = "".join("\\\\" + c if c in _RE2_META else c for c in p)
+        parts.append(esc.replace('"', '\\"'))
+    return "|".join(parts)
+
+
+def group_query(resource: ResourceType, namespace: str, container: str, pods: Sequence[str]) -> str:
+    metric, matchers = _resolve(resource)
+    return (f'sum by (pod) ({metric}{{{matchers}namespace="{namespace}", pod=~"{pod_regex(pods)}", '
+            f'container="{container}"}})')
+
+
+def _resolve(resource) -> tuple[str, str]:
+    try:
+        return _METRIC[ResourceType(resource)]
+    except (KeyError, ValueError):
+        raise ValueError(f"Unknown resource type: {resource}") from None
+
+
+@dataclass
+class GroupQuery:
+    """One grouped range query: the pods of one (namespace, container) it covers."""
+    namespace: str
+    container: str
+    pods: list[str]
+
+    def query(self, resource: ResourceType) -> str:
+        return group_query(resource, self.namespace, self.container, self.pods)
+
+
+@dataclass
+class FleetQueryPlan:
+    """Grouping of a fleet's (object, pod) pairs into grouped range queries.
+
+    ``objects`` are K8sObjectData (anything with ``namespace``, ``container`` and
+    ``pods``); their order is the fleet order of the packed segments.  Each
+    object's pods are de-duplicated keeping first occurrence, as the reference's
+    ``{pod: result[i] for i, pod in enumerate(object.pods)}`` does
+    (prometheus.py:152).  A pod shared by several objects of the same group is
+    queried once and routed to each of them.
+    """
+    objects: Sequence
+    max_query_chars: int = 6000
+    groups: list[GroupQuery] = field(init=False)
+    slot_obj: np.ndarray = field(init=False)      # int64 [n_slots], non-decreasing
+    slot_group: np.ndarray = field(init=False)    # int64 [n_slots]
+    slot_pods: list[str] = field(init=False)
+
+    def __post_init__(self):
+        if self.max_query_chars < 1:
+            raise ValueError("max_query_chars must be positive")
+        self.groups = []
+        open_group: dict[tuple[str, str], int] = {}   # (ns, container) -> index of the group being filled
+        group_chars: list[int] = []
+        pod_group: dict[tuple[str, str, str], int] = {}
+        slot_obj, slot_group, slot_pods = [], [], []
+        for o, obj in enumerate(self.objects):
+            key = (obj.namespace, obj.container)
+            for pod in dict.fromkeys(obj.pods):
+                pk = (obj.namespace, obj.container, pod)
+                g = pod_group.get(pk)
+                if g is None:
+                    cost = len(pod_regex([pod])) + 1
+                    g = open_group.get(key)
+                    if g is None or (self.groups[g].pods and group_chars[g] + cost > self.max_query_chars):
+                        g = len(self.groups)
+                        self.groups.append(GroupQuery(obj.namespace, obj.container, []))
+                        group_chars.append(0)
+                        open_group[key] = g
+                    self.groups[g].pods.append(pod)
+                    group_chars[g] += cost
+                    pod_group[pk] = g
+                slot_obj.append(o)
+                slot_group.append(g)
+                slot_pods.append(pod)
+        self.slot_obj = np.asarray(slot_obj, dtype=np.int64)
+        self.slot_group = np.asarray(slot_group, dtype=np.int64)
+        self.slot_pods = slot_pods
+        names = [p.encode() for p in slot_pods]
+        self._names = b"".join(names)
+        self._name_offsets = np.zeros(len(names) + 1, dtype=np.int64)
+        if names:
+            np.cumsum([len(n) for n in names], out=self._name_offsets[1:])
+
+    @property
+    def n_objects(self) -> int:
+        return len(self.objects)
+
+    @property
+    def n_slots(self) -> int:
+        return len(self.slot_pods)
+
+    def queries(self, resource: ResourceType) -> list[str]:
+        return [g.query(resource) for g in self.groups]
+
+    def pack(self, bodies: Sequence[bytes], *, want_timestamps: bool = False, threads: int = 0,
+             return_pod_counts: bool = False):
+        """bodies[g] = the raw query_range response body of ``queries(resource)[g]``.
+
+        Returns a PackedSeries (segment o = object o's pods with data, concatenated
+        in K8sObjectData.pods order), plus the timestamps if ``want_timestamps`` and
+        the per-(object, pod) sample counts (-1: dropped) if ``return_pod_counts``.
+        """
+        if len(bodies) != len(self.groups):
+            raise ValueError(f"expected {len(self.groups)} bodies (one per group query), got {len(bodies)}")
+        lib = load_library()
+        flat = [b if isinstance(b, (bytes, bytearray)) else bytes(b) for b in bodies]
+        nb, ns, no = len(flat), self.n_slots, self.n_objects
+        ptrs = (ctypes.c_char_p * max(nb, 1))(*flat)
+        lens = np.array([len(b) for b in flat] or [0], dtype=np.int64)
+        slot_group = self.slot_group if ns else np.zeros(1, np.int64)
+        slot_obj = self.slot_obj if ns else np.zeros(1, np.int64)
+        h = ctypes.c_void_p()
+        rc = lib.krr_pack_parse_grouped(ctypes.cast(ptrs, ctypes.c_void_p), _ptr(lens), nb, b"pod",
+                                        _ptr(slot_group), self._names or b"\0", _ptr(self._name_offsets),
+                                        _ptr(slot_obj), ns, no, int(bool(want_timestamps)), int(threads),
+                                        ctypes.byref(h))
+        try:
+            if rc != KRR_PACK_OK:
+                msg = lib.krr_pack_error(h) if h else b""
+                raise PrometheusResponseError(rc, (msg or b"invalid arguments").decode())
+            n = int(lib.krr_pack_n_values(h))
+            values = np.empty(n, dtype=np.float64)
+            offsets = np.empty(no + 1, dtype=np.int64)
+            ts = np.empty(n, dtype=np.float64) if want_timestamps else None
+            counts = np.empty(max(ns, 1), dtype=np.int64) if return_pod_counts else None
+            rc = lib.krr_pack_copy(h, _ptr(values), _ptr(offsets), _ptr(ts) if ts is not None else None,
+                                   _ptr(counts) if counts is not None else None, int(threads))
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_copy failed")
+            max_len = int(lib.krr_pack_max_len(h))
+        finally:
+            if h:
+                lib.krr_pack_free(h)
+        out: list = [PackedSeries(values, offsets, max_len)]
+        if want_timestamps:
+            out.append(ts)
+        if return_pod_counts:
+            out.append(counts[:ns])
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def fetch(self, query_range: Callable[[str], bytes], *, max_workers: int = 16) -> dict:
+        """Run every grouped query for both resources; ``query_range(query)``
+        performs one /api/v1/query_range request (start, end and step — the
+        reference's ``step_string(timeframe)`` — bound by the caller)
+        and returns the raw body.  Returns {ResourceType: [body per group]}."""
+        jobs = [(rt, g.query(rt)) for rt in ResourceType for g in self.groups]
+        with ThreadPoolExecutor(max_workers=max(1, max_workers)) as ex:
+            bodies = list(ex.map(lambda j: query_range(j[1]), jobs))
+        n = len(self.groups)
+        return {rt: bodies[i * n:(i + 1) * n] for i, rt in enumerate(ResourceType)}
+
+    def pack_fleet(self, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes], threads: int = 0) -> PackedFleet:
+        return PackedFleet(self.pack(cpu_bodies, threads=threads), self.pack(mem_bodies, threads=threads))
+
+
+__all__ = ["FleetQueryPlan", "GroupQuery", "group_query", "pod_query", "pod_regex", "step_string"]

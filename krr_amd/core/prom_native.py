@@ -30,7 +30,9 @@ KRR_PACK_E_STATUS = -3
 KRR_PACK_E_VALUE = -4
 
 EXPORTED_SYMBOLS = ("krr_pack_abi_version", "krr_pack_parse", "krr_pack_n_values", "krr_pack_max_len",
-                    "krr_pack_copy", "krr_pack_error", "krr_pack_free", "krr_round_simple")
+                    "krr_pack_copy", "krr_pack_error", "krr_pack_free", "krr_pack_parse_series", "krr_series_count",
+                    "krr_series_label", "krr_series_len", "krr_series_copy", "krr_series_error", "krr_series_free",
+                    "krr_pack_parse_grouped", "krr_round_simple")
 
 
 class PackerUnavailable(RuntimeError):
@@ -77,6 +79,23 @@ def load_library() -> ctypes.CDLL:
         lib.krr_pack_error.restype = ctypes.c_char_p
         lib.krr_pack_free.argtypes = [vp]
         lib.krr_pack_free.restype = None
+        lib.krr_pack_parse_series.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i32, ctypes.POINTER(vp)]
+        lib.krr_pack_parse_series.restype = ctypes.c_int
+        lib.krr_series_count.argtypes = [vp]
+        lib.krr_series_count.restype = i64
+        lib.krr_series_label.argtypes = [vp, i64, ctypes.POINTER(i64)]
+        lib.krr_series_label.restype = ctypes.c_void_p
+        lib.krr_series_len.argtypes = [vp, i64]
+        lib.krr_series_len.restype = i64
+        lib.krr_series_copy.argtypes = [vp, i64, vp, vp]
+        lib.krr_series_copy.restype = ctypes.c_int
+        lib.krr_series_error.argtypes = [vp]
+        lib.krr_series_error.restype = ctypes.c_char_p
+        lib.krr_series_free.argtypes = [vp]
+        lib.krr_series_free.restype = None
+        lib.krr_pack_parse_grouped.argtypes = [vp, vp, i64, ctypes.c_char_p, vp, ctypes.c_char_p, vp, vp, i64, i64,
+                                               i32, i32, ctypes.POINTER(vp)]
+        lib.krr_pack_parse_grouped.restype = ctypes.c_int
         lib.krr_round_simple.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, i32]
         lib.krr_round_simple.restype = ctypes.c_int
         if lib.krr_pack_abi_version() != 1:
@@ -87,6 +106,34 @@ def load_library() -> ctypes.CDLL:
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def parse_series(body: bytes, label: str = "pod", *, want_timestamps: bool = False) -> list:
+    """Every series of one query_range response body: [(label value or None,
+    values float64[, timestamps float64])] in response order."""
+    lib = load_library()
+    body = body if isinstance(body, (bytes, bytearray)) else bytes(body)
+    h = ctypes.c_void_p()
+    rc = lib.krr_pack_parse_series(bytes(body), len(body), label.encode(), int(bool(want_timestamps)),
+                                   ctypes.byref(h))
+    try:
+        if rc != KRR_PACK_OK:
+            msg = lib.krr_series_error(h) if h else b""
+            raise PrometheusResponseError(rc, (msg or b"invalid arguments").decode())
+        out = []
+        for i in range(int(lib.krr_series_count(h))):
+            ln = ctypes.c_int64()
+            ptr = lib.krr_series_label(h, i, ctypes.byref(ln))
+            name = ctypes.string_at(ptr, ln.value).decode() if ln.value >= 0 else None
+            v = np.empty(int(lib.krr_series_len(h, i)), dtype=np.float64)
+            t = np.empty_like(v) if want_timestamps else None
+            if lib.krr_series_copy(h, i, _ptr(v), _ptr(t) if t is not None else None) != KRR_PACK_OK:
+                raise PrometheusResponseError(KRR_PACK_E_INVALID, "krr_series_copy failed")
+            out.append((name, v, t) if want_timestamps else (name, v))
+        return out
+    finally:
+        if h:
+            lib.krr_series_free(h)
 
 
 def pack_query_range_bodies(per_object_bodies: Sequence[Sequence[bytes]], *, want_timestamps: bool = False,

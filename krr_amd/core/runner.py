@@ -83,6 +83,13 @@ class BatchedRunner:
                             pack_query_range_bodies(mem_bodies, threads=threads))
         return self.recommend_packed(fleet)
 
+    def recommend_from_grouped(self, plan, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes],
+                               threads: int = 0) -> list[RunResult]:
+        """As recommend_from_bodies, from fleet-batched responses: ``plan`` is a
+        krr_amd.core.fleet_query.FleetQueryPlan and bodies[g] answers its g-th grouped
+        ``sum by (pod)`` query (one per (namespace, container), not one per pod)."""
+        return self.recommend_packed(plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads))
+
     def allocations(self, objects: Sequence[K8sObjectData],
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:
         return [to_allocations(r) for r in self.recommend(objects, histories)]

@@ -21,6 +21,7 @@
 #include <string>
 #include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -224,6 +225,11 @@ bool parse_value(std::string_view s, double* out) {
 
 struct Body {
     std::vector<double> v, t;
+    // grouped packing: the samples live in the parsed series set (no copy)
+    const std::vector<double>* pv = nullptr;
+    const std::vector<double>* pt = nullptr;
+    const std::vector<double>& V() const { return pv ? *pv : v; }
+    const std::vector<double>& T() const { return pt ? *pt : t; }
     int status = KRR_PACK_OK;
     bool dropped = false;
     std::string err;
@@ -318,6 +324,133 @@ void parse_body(const char* s, int64_t n, bool want_ts, Body& out) {
     if (!have_result) return fail(KRR_PACK_E_PARSE, "no data.result");
 }
 
+// ---- grouped responses: "sum by (pod) (...)" returns one series per pod ----
+struct Series {
+    std::string label;  // the metric's `label` entry ("" when absent)
+    bool has_label = false;
+    std::vector<double> v, t;
+};
+
+struct SeriesSet {
+    std::vector<Series> series;
+    int status = KRR_PACK_OK;
+    std::string err;
+};
+
+// Read a string value (escapes decoded) into *out.
+bool read_string(Reader& r, std::string* out) {
+    std::string_view raw;
+    bool esc;
+    if (!r.str(&raw, &esc)) return false;
+    *out = esc ? unescape(raw) : std::string(raw);
+    return true;
+}
+
+// {"status": "success", "data": {"result": [{"metric": {...}, "values": [...]}, ...]}}: every series.
+void parse_series_set(const char* s, int64_t n, const char* label, bool want_ts, SeriesSet& out) {
+    Reader r{s, s + n};
+    auto fail = [&](int code, const char* what) {
+        out.status = code;
+        char buf[160];
+        snprintf(buf, sizeof(buf), "%s at byte %lld", what, (long long)(r.p - s));
+        out.err = buf;
+    };
+    bool have_status = false, ok_status = false, have_result = false;
+    if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "expected a JSON object");
+    if (!r.peek('}')) {
+        do {
+            std::string_view k;
+            bool esc;
+            if (!r.str(&k, &esc) || !r.lit(':')) return fail(KRR_PACK_E_PARSE, "bad object key");
+            if (key_is(k, esc, "status")) {
+                std::string v;
+                if (!read_string(r, &v)) return fail(KRR_PACK_E_PARSE, "status is not a string");
+                have_status = true;
+                ok_status = v == "success";
+            } else if (key_is(k, esc, "data")) {
+                if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "data is not an object");
+                if (!r.peek('}')) {
+                    do {
+                        std::string_view dk;
+                        bool desc;
+                        if (!r.str(&dk, &desc) || !r.lit(':')) return fail(KRR_PACK_E_PARSE, "bad data key");
+                        if (!key_is(dk, desc, "result")) {
+                            if (!r.skip()) return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                            continue;
+                        }
+                        if (!r.lit('[')) return fail(KRR_PACK_E_PARSE, "result is not an array");
+                        have_result = true;
+                        if (r.lit(']')) continue;
+                        do {
+                            Series S;
+                            bool have_values = false;
+                            if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "series is not an object");
+                            if (!r.peek('}')) {
+                                do {
+                                    std::string_view sk;
+                                    bool sesc;
+                                    if (!r.str(&sk, &sesc) || !r.lit(':'))
+                                        return fail(KRR_PACK_E_PARSE, "bad series key");
+                                    if (key_is(sk, sesc, "metric")) {
+                                        if (!r.lit('{')) return fail(KRR_PACK_E_PARSE, "metric is not an object");
+                                        if (!r.peek('}')) {
+                                            do {
+                                                std::string_view lk;
+                                                bool lesc;
+                                                if (!r.str(&lk, &lesc) || !r.lit(':'))
+                                                    return fail(KRR_PACK_E_PARSE, "bad label");
+                                                if (key_is(lk, lesc, label)) {
+                                                    if (!read_string(r, &S.label))
+                                                        return fail(KRR_PACK_E_PARSE, "label value is not a string");
+                                                    S.has_label = true;
+                                                } else if (!r.skip()) {
+                                                    return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                                                }
+                                            } while (r.lit(','));
+                                        }
+                                        if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated metric");
+                                    } else if (key_is(sk, sesc, "values")) {
+                                        have_values = true;
+                                        if (!r.lit('[')) return fail(KRR_PACK_E_PARSE, "values is not an array");
+                                        if (r.lit(']')) continue;
+                                        do {
+                                            double ts, val;
+                                            std::string_view vs;
+                                            bool vesc;
+                                            if (!r.lit('[') || !r.num(want_ts ? &ts : nullptr) || !r.lit(',') ||
+                                                !r.str(&vs, &vesc) || !r.lit(']'))
+                                                return fail(KRR_PACK_E_PARSE, "sample is not [time, \"value\"]");
+                                            if (vesc || !parse_value(vs, &val))
+                                                return fail(KRR_PACK_E_VALUE, "sample value is not a number");
+                                            S.v.push_back(val);
+                                            if (want_ts) S.t.push_back(ts);
+                                        } while (r.lit(','));
+                                        if (!r.lit(']')) return fail(KRR_PACK_E_PARSE, "unterminated values");
+                                    } else if (!r.skip()) {
+                                        return fail(KRR_PACK_E_PARSE, "malformed JSON");
+                                    }
+                                } while (r.lit(','));
+                            }
+                            if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated series");
+                            if (!have_values) return fail(KRR_PACK_E_PARSE, "series without values");
+                            out.series.push_back(std::move(S));
+                        } while (r.lit(','));
+                        if (!r.lit(']')) return fail(KRR_PACK_E_PARSE, "unterminated result");
+                    } while (r.lit(','));
+                }
+                if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated data");
+            } else if (!r.skip()) {
+                return fail(KRR_PACK_E_PARSE, "malformed JSON");
+            }
+        } while (r.lit(','));
+    }
+    if (!r.lit('}')) return fail(KRR_PACK_E_PARSE, "unterminated response");
+    r.ws();
+    if (r.p != r.e) return fail(KRR_PACK_E_PARSE, "trailing bytes");
+    if (!have_status || !ok_status) return fail(KRR_PACK_E_STATUS, "status is not \"success\"");
+    if (!have_result) return fail(KRR_PACK_E_PARSE, "no data.result");
+}
+
 int pool_size(int32_t threads, int64_t work) {
     int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
     if (t < 1) t = 1;
@@ -332,12 +465,15 @@ void parallel_for(int64_t n, int32_t threads, F f) {
         for (int64_t i = 0; i < n; ++i) f(i);
         return;
     }
+    // chunks of up to 8 items, but at least ~4 chunks per thread so few large
+    // items (grouped bodies) still spread over the pool
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(8, n / ((int64_t)t * 4)));
     std::atomic<int64_t> next{0};
     auto worker = [&]() {
         for (;;) {
-            const int64_t b = next.fetch_add(8);
+            const int64_t b = next.fetch_add(chunk);
             if (b >= n) return;
-            const int64_t e = std::min<int64_t>(b + 8, n);
+            const int64_t e = std::min<int64_t>(b + chunk, n);
             for (int64_t i = b; i < e; ++i) f(i);
         }
     };
@@ -352,6 +488,7 @@ void parallel_for(int64_t n, int32_t threads, F f) {
 
 struct krr_pack {
     std::vector<Body> bodies;
+    std::vector<SeriesSet> sets;  // grouped packing only: bodies[] point into these
     std::vector<int64_t> obj;
     int64_t n_objects = 0;
     int64_t n_values = 0;
@@ -405,8 +542,8 @@ int krr_pack_parse(const char* const* bodies, const int64_t* body_lens, int64_t 
             }
             continue;
         }
-        seg[(size_t)p->obj[(size_t)b]] += (int64_t)B.v.size();
-        p->n_values += (int64_t)B.v.size();
+        seg[(size_t)p->obj[(size_t)b]] += (int64_t)B.V().size();
+        p->n_values += (int64_t)B.V().size();
     }
     for (int64_t s : seg) p->max_len = std::max(p->max_len, s);
     *out = p;
@@ -429,7 +566,7 @@ int krr_pack_copy(const krr_pack* p, double* values, int64_t* offsets, double* t
     for (int64_t s = 0; s <= p->n_objects; ++s) offsets[s] = 0;
     for (int64_t b = 0; b < nb; ++b) {
         start[(size_t)b] = pos;
-        const int64_t c = (int64_t)p->bodies[(size_t)b].v.size();
+        const int64_t c = (int64_t)p->bodies[(size_t)b].V().size();
         pos += c;
         offsets[p->obj[(size_t)b] + 1] += c;
         if (pod_counts) pod_counts[b] = p->bodies[(size_t)b].dropped ? -1 : c;
@@ -437,11 +574,152 @@ int krr_pack_copy(const krr_pack* p, double* values, int64_t* offsets, double* t
     for (int64_t s = 0; s < p->n_objects; ++s) offsets[s + 1] += offsets[s];
     parallel_for(nb, threads, [&](int64_t b) {
         const Body& B = p->bodies[(size_t)b];
-        if (B.v.empty()) return;
-        memcpy(values + start[(size_t)b], B.v.data(), B.v.size() * sizeof(double));
-        if (timestamps) memcpy(timestamps + start[(size_t)b], B.t.data(), B.t.size() * sizeof(double));
+        const std::vector<double>& v = B.V();
+        if (v.empty()) return;
+        memcpy(values + start[(size_t)b], v.data(), v.size() * sizeof(double));
+        if (timestamps) memcpy(timestamps + start[(size_t)b], B.T().data(), B.T().size() * sizeof(double));
     });
     return KRR_PACK_OK;
 }
+
+struct krr_series_set {
+    SeriesSet set;
+};
+
+int krr_pack_parse_grouped(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies, const char* label,
+                           const int64_t* slot_body, const char* slot_names, const int64_t* slot_name_offsets,
+                           const int64_t* obj_of_slot, int64_t n_slots, int64_t n_objects, int32_t want_timestamps,
+                           int32_t threads, krr_pack** out) {
+    if (!out) return KRR_PACK_E_INVALID;
+    *out = nullptr;
+    if (n_bodies < 0 || n_slots < 0 || n_objects < 0 || !label || (n_bodies > 0 && (!bodies || !body_lens)) ||
+        (n_slots > 0 && (!slot_body || !slot_name_offsets || !obj_of_slot)))
+        return KRR_PACK_E_INVALID;
+    for (int64_t b = 0; b < n_bodies; ++b)
+        if (body_lens[b] < 0 || (body_lens[b] > 0 && !bodies[b])) return KRR_PACK_E_INVALID;
+    if (n_slots > 0 && (slot_name_offsets[0] < 0 || (slot_name_offsets[n_slots] > 0 && !slot_names)))
+        return KRR_PACK_E_INVALID;
+    for (int64_t s = 0; s < n_slots; ++s) {
+        if (slot_body[s] < 0 || slot_body[s] >= n_bodies || obj_of_slot[s] < 0 || obj_of_slot[s] >= n_objects ||
+            (s && obj_of_slot[s] < obj_of_slot[s - 1]) || slot_name_offsets[s + 1] < slot_name_offsets[s])
+            return KRR_PACK_E_INVALID;
+    }
+    krr_pack* p = new (std::nothrow) krr_pack();
+    if (!p) return KRR_PACK_E_INVALID;
+    std::vector<SeriesSet>& sets = p->sets;
+    // per body: label value -> first series carrying it (the reference reads result[0])
+    std::vector<std::unordered_map<std::string_view, int64_t>> index;
+    try {
+        sets.resize((size_t)n_bodies);
+        index.resize((size_t)n_bodies);
+        p->bodies.resize((size_t)n_slots);
+        p->obj.assign(obj_of_slot, obj_of_slot + n_slots);
+    } catch (...) {
+        delete p;
+        return KRR_PACK_E_INVALID;
+    }
+    p->n_objects = n_objects;
+    p->want_ts = want_timestamps != 0;
+    parallel_for(n_bodies, threads, [&](int64_t b) {
+        SeriesSet& S = sets[(size_t)b];
+        try {
+            parse_series_set(bodies[b], body_lens[b], label, p->want_ts, S);
+            if (S.status != KRR_PACK_OK) return;
+            auto& ix = index[(size_t)b];
+            ix.reserve(S.series.size() * 2);
+            for (size_t i = 0; i < S.series.size(); ++i)
+                if (S.series[i].has_label) ix.emplace(std::string_view(S.series[i].label), (int64_t)i);
+        } catch (...) {
+            S.status = KRR_PACK_E_INVALID;
+            S.err = "out of memory";
+        }
+    });
+    int rc = KRR_PACK_OK;
+    for (int64_t b = 0; b < n_bodies; ++b) {
+        if (sets[(size_t)b].status != KRR_PACK_OK) {
+            rc = sets[(size_t)b].status;
+            p->err = "body " + std::to_string(b) + ": " + sets[(size_t)b].err;
+            break;
+        }
+    }
+    if (rc == KRR_PACK_OK) {
+        parallel_for(n_slots, threads, [&](int64_t s) {
+            Body& B = p->bodies[(size_t)s];
+            const int64_t b = slot_body[s];
+            const std::string_view name(slot_names + slot_name_offsets[s],
+                                        (size_t)(slot_name_offsets[s + 1] - slot_name_offsets[s]));
+            const auto& ix = index[(size_t)b];
+            const auto it = ix.find(name);
+            if (it == ix.end()) {
+                B.dropped = true;  // no series for this pod: prometheus.py:154 drops it
+                return;
+            }
+            const Series& src = p->sets[(size_t)b].series[(size_t)it->second];
+            B.pv = &src.v;
+            B.pt = &src.t;
+        });
+        std::vector<int64_t> seg((size_t)n_objects, 0);
+        for (int64_t s = 0; s < n_slots; ++s) {
+            const Body& B = p->bodies[(size_t)s];
+            if (B.status != KRR_PACK_OK) {
+                if (rc == KRR_PACK_OK) {
+                    rc = B.status;
+                    p->err = "slot " + std::to_string(s) + ": " + B.err;
+                }
+                continue;
+            }
+            seg[(size_t)p->obj[(size_t)s]] += (int64_t)B.V().size();
+            p->n_values += (int64_t)B.V().size();
+        }
+        for (int64_t v : seg) p->max_len = std::max(p->max_len, v);
+    }
+    *out = p;
+    return rc;
+}
+
+int krr_pack_parse_series(const char* body, int64_t len, const char* label, int32_t want_timestamps,
+                          krr_series_set** out) {
+    if (!out) return KRR_PACK_E_INVALID;
+    *out = nullptr;
+    if (len < 0 || (len > 0 && !body) || !label) return KRR_PACK_E_INVALID;
+    krr_series_set* h = new (std::nothrow) krr_series_set();
+    if (!h) return KRR_PACK_E_INVALID;
+    try {
+        parse_series_set(body, len, label, want_timestamps != 0, h->set);
+    } catch (...) {
+        h->set.status = KRR_PACK_E_INVALID;
+        h->set.err = "out of memory";
+    }
+    *out = h;
+    return h->set.status;
+}
+
+int64_t krr_series_count(const krr_series_set* h) { return h ? (int64_t)h->set.series.size() : -1; }
+
+const char* krr_series_label(const krr_series_set* h, int64_t i, int64_t* len) {
+    if (!h || i < 0 || i >= (int64_t)h->set.series.size()) return nullptr;
+    const Series& S = h->set.series[(size_t)i];
+    if (len) *len = S.has_label ? (int64_t)S.label.size() : -1;
+    return S.label.c_str();
+}
+
+int64_t krr_series_len(const krr_series_set* h, int64_t i) {
+    if (!h || i < 0 || i >= (int64_t)h->set.series.size()) return -1;
+    return (int64_t)h->set.series[(size_t)i].v.size();
+}
+
+int krr_series_copy(const krr_series_set* h, int64_t i, double* values, double* timestamps) {
+    if (!h || i < 0 || i >= (int64_t)h->set.series.size()) return KRR_PACK_E_INVALID;
+    const Series& S = h->set.series[(size_t)i];
+    if (!S.v.empty() && !values) return KRR_PACK_E_INVALID;
+    if (timestamps && S.t.size() != S.v.size()) return KRR_PACK_E_INVALID;
+    if (!S.v.empty()) memcpy(values, S.v.data(), S.v.size() * sizeof(double));
+    if (timestamps && !S.t.empty()) memcpy(timestamps, S.t.data(), S.t.size() * sizeof(double));
+    return KRR_PACK_OK;
+}
+
+const char* krr_series_error(const krr_series_set* h) { return h ? h->set.err.c_str() : "null krr_series_set"; }
+
+void krr_series_free(krr_series_set* h) { delete h; }
 
 }  // extern "C"

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--pods", type=int, default=3)
     ap.add_argument("--samples", type=int, default=10080)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--objects-per-group", type=int, default=10,
+                    help="objects sharing one (namespace, container): one grouped query for all their pods")
     ap.add_argument("--ref-objects", type=int, default=20, help="objects timed through the reference path")
     a = ap.parse_args()
     from krr_amd.core.prom_native import pack_query_range_bodies
@@ -57,8 +59,29 @@ def main():
                 vals = [Decimal(v) for _, v in res[0]["values"]]
                 n_ref += len(vals)
     t4 = time.perf_counter()
+    # fleet-batched form: one `sum by (pod)` body per (namespace, container) group
+    from krr_amd.core.fleet_query import FleetQueryPlan
+
+    class Obj:
+        def __init__(self, o):
+            self.namespace, self.container = "default", f"app-{o // a.objects_per_group}"
+            self.pods = [f"pod-{o}-{p}" for p in range(a.pods)]
+
+    objs = [Obj(o) for o in range(a.objects)]
+    plan = FleetQueryPlan(objs)
+    where = {(objs[o].container, pod): json.loads(b)["data"]["result"][0]
+             for o, pods in enumerate(per_obj) for pod, b in zip(objs[o].pods, pods)}
+    gbodies = [json.dumps({"status": "success", "data": {"resultType": "matrix", "result": [
+        where[(g.container, pod)] for pod in reversed(g.pods)]}}).encode() for g in plan.groups]
+    del where
+    t5 = time.perf_counter()
+    pg = plan.pack(gbodies, threads=a.threads)
+    t6 = time.perf_counter()
+    assert pg.values.tobytes() == ps.values.tobytes() and np.array_equal(pg.offsets, ps.offsets)
     threads = a.threads or os.cpu_count()
     out = {
+        "grouped_queries": len(plan.groups), "per_pod_queries": a.objects * a.pods,
+        "grouped_native_samples_per_s": total / (t6 - t5),
         "samples": total, "json_bytes": nbytes,
         "native_samples_per_s": total / (t1 - t0), "native_threads": threads,
         "native_1thread_samples_per_s": total / (t2 - t1),

@@ -157,6 +157,28 @@ def test_batched_runner_recommend_and_bodies_match_reference(path):
         assert _d(r[ResourceType.CPU].request) == want["cpu_request"], c["name"]
         assert _d(r[ResourceType.Memory].request) == want["mem_request"], c["name"]
 
+    # fleet-batched queries: one grouped body per (namespace, container), routed by pod label
+    from krr_amd.core.fleet_query import FleetQueryPlan
+
+    def grouped(per_pod):
+        res = [{"metric": {"pod": pod}, "values": [[1.7e9 + i, v] for i, v in enumerate(vals)]}
+               for pod, vals in reversed(list(per_pod.items())) if vals]
+        return json.dumps({"status": "success", "data": {"resultType": "matrix", "result": res}}).encode()
+
+    class _O:
+        def __init__(self, c):
+            self.namespace, self.container = "default", c["name"]
+            self.pods = list(dict.fromkeys(list(c["cpu"]) + list(c["mem"])))
+
+    plan = FleetQueryPlan([_O(c) for c in bc])
+    by_name = {c["name"]: c for c in bc}
+    assert len(by_name) == len(bc)
+    got_g = runner.recommend_from_grouped(plan, [grouped(by_name[g.container]["cpu"]) for g in plan.groups],
+                                          [grouped(by_name[g.container]["mem"]) for g in plan.groups])
+    for rb, rg in zip(got_b, got_g):
+        for rt in ResourceType:
+            assert _d(rb[rt].request) == _d(rg[rt].request) and _d(rb[rt].limit) == _d(rg[rt].limit)
+
 
 def _fleet(seed, gaps):
     rng = np.random.default_rng(seed)
