@@ -1,11 +1,8 @@
-"""Public model surface (reference robusta_krr/api/models.py:1-17).
-
-Result / Severity / ResourceScan (the downstream O(objects) bookkeeping,
-SURVEY.md §8f "next" rank 3) are not part of this build yet.
-"""
+"""Public model surface (reference robusta_krr/api/models.py:1-17)."""
 from krr_amd.core.abstract.strategies import HistoryData, ResourceRecommendation, RunResult
 from krr_amd.core.models.allocations import RecommendationValue, ResourceAllocations, ResourceType
 from krr_amd.core.models.objects import K8sObjectData
+from krr_amd.core.models.result import ResourceScan, Result, Severity
 
 __all__ = [
     "ResourceType",
@@ -15,4 +12,7 @@ __all__ = [
     "ResourceRecommendation",
     "HistoryData",
     "RunResult",
+    "Result",
+    "Severity",
+    "ResourceScan",
 ]

@@ -94,6 +94,13 @@ class BatchedRunner:
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:
         return [to_allocations(r) for r in self.recommend(objects, histories)]
 
+    def collect_result(self, objects: Sequence[K8sObjectData], histories: Sequence[HistoryData]):
+        """Runner._collect_result's Result (runner.py:122-131) from already gathered
+        histories: recommendations, then the fleet-vectorised ResourceScan/score."""
+        from krr_amd.core.models.result import collect_result
+
+        return collect_result(objects, self.allocations(objects, histories))
+
     async def gather_histories(self, objects: Sequence[K8sObjectData], loader: HistoryLoader) -> list[HistoryData]:
         settings = self.strategy.settings
 

@@ -252,3 +252,25 @@ def test_simple_run_host_entry():
     assert np.array_equal(outs[0], ov, equal_nan=True) and np.array_equal(outs[1], on)
     assert np.array_equal(outs[3], mv, equal_nan=True) and np.array_equal(outs[4], mn)
     ctx.close()
+
+
+def test_batched_runner_collect_result_matches_per_object_scans():
+    """BatchedRunner.collect_result (kernel + native rounding + vectorised scans) equals
+    the reference's per-object ResourceScan.calculate over the same allocations."""
+    from krr_amd.core.models.result import Result, ResourceScan
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings()), 5, 10)
+    cases = [c for c in DOC["cases"] if "rounded" in c["results"]["default_int"]]
+    from krr_amd.api.models import K8sObjectData, ResourceAllocations
+    quantities = [("100m", "128Mi"), ("1", "1Gi"), (None, "64Mi"), ("5m", None), ("250m", "10M")]
+    objs = [K8sObjectData(cluster=None, name=c["name"], container="c", pods=["p"], namespace="ns", kind="Deployment",
+                          allocations=ResourceAllocations(requests=dict(zip(["cpu", "memory"], quantities[i % 5])),
+                                                          limits=dict(zip(["cpu", "memory"], quantities[(i + 2) % 5]))))
+            for i, c in enumerate(cases)]
+    hists = [_hist(c) for c in cases]
+    result = runner.collect_result(objs, hists)
+    allocs = runner.allocations(objs, hists)
+    want = Result(scans=[ResourceScan.calculate(o, a) for o, a in zip(objs, allocs)])
+    assert result.scans == want.scans and result.score == want.score
