@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--sketch-bits", type=int, default=5, help="config 5: log-linear bins per octave = 2^bits")
+    ap.add_argument("--sketch-only", action="store_true",
+                    help="config 5: stop at the sketch answer (approximate) instead of the exact refinement")
     ap.add_argument("--error-sample", type=int, default=256, help="config 5: series checked against the exact path")
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
@@ -330,10 +332,13 @@ def _cpu_model() -> str:
 
 
 def run_config5(args, world, rank, local, dev, coll_dev):
-    """Config 5: time-sharded 30d@15s series, sketch mode (see krr_amd/core/sketch.py).
+    """Config 5: time-sharded 30d@15s series (see krr_amd/core/sketch.py).
 
     step = per-slice sketch build (one HBM pass) -> reduce-scatter of the sketches
-    (RCCL, N > 1) -> query of this rank's owner block -> results gathered to rank 0.
+    (RCCL, N > 1) -> exact refinement: locate the needed ranks' bins in the merged
+    sketches, all-gather them, collect every rank's samples in those bins (second
+    HBM pass), all-to-all them to the owners, select exactly -> results gathered to
+    rank 0.  ``--sketch-only`` stops at the interpolated sketch answer.
     """
     import torch
     import torch.distributed as dist
@@ -356,6 +361,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     ser = ctx.series(cpu, offs, Lr, False)
     cfg = sketch.SketchConfig(mantissa_bits=args.sketch_bits)
     params = percentile_params(Decimal(args.percentile), params_mode(args))
+    exact = not args.sketch_only
     stream = torch.cuda.current_stream()
     host_rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
     state = {}
@@ -367,7 +373,12 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         if ev is not None:
             ev[1].record(stream)
         merged = sketch.merge_time_sharded(sk)
-        res = sketch.query(ctx, merged, cfg, params, stream)
+        if exact:
+            res = sketch.exact_time_sharded(ctx, ser, sk, merged, cfg, params, stream=stream,
+                                            events=None if ev is None else ev[2:4])
+            state["collected"] = res["collected"]
+        else:
+            res = sketch.query(ctx, merged, cfg, params, stream)
         rec = torch.stack([res["value"].view(torch.int64), res["count"] | (res["flags"].to(torch.int64) << 48),
                            torch.zeros_like(res["count"]), torch.zeros_like(res["count"])], dim=1)
         if world > 1:
@@ -381,7 +392,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     t_a = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
@@ -396,10 +407,16 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     N = S * Lr
     kbytes = 8 * N + 8 * (S + 1) + S * (4 * cfg.width + 8 + 8 + 4)
+    kernels_ms = {"k_sketch_build": kms}
+    if exact:
+        # collect: every slot read once + locations in, collected samples out
+        cms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+        kernels_ms["k_sketch_collect"] = cms
+        cbytes = 8 * N + 8 * (S + 1) + 56 * S + 8 * S + 8 * int(state.get("collected", 0))
     result = {
         "metric": METRIC,
         "value": S / step_s,
-        "unit": "cpu-series/s (30d@15s, sketch mode)",
+        "unit": "cpu-series/s (30d@15s, exact)" if exact else "cpu-series/s (30d@15s, sketch mode)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -411,17 +428,31 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         "data": "synthetic (device counter-hash: CPU ~ Gamma(2, 0.05) cores), generated per time slice",
         "config": {
             "workload": f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
-                        f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave",
+                        f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave"
+                        + (" + exact refinement (collect + select in the located bins)" if exact else ""),
             "percentile_mode": params_mode(args), "cpu_percentile": args.percentile,
             "series": S, "slots_per_rank": N,
             "parallelism": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
         },
         "samples_per_s": S * T / step_s,
-        "kernels_ms": {"k_sketch_build": kms},
+        "kernels_ms": kernels_ms,
         "roofline": {"kernel": "k_sketch_build", "bound": "hbm", "achieved": kbytes / (kms * 1e-3) / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kbytes / (kms * 1e-3) / HBM_PEAK,
                      "traffic": None, "algorithmic_bytes_per_launch": kbytes},
     }
+    if exact:
+        result["roofline_collect"] = {"kernel": "k_sketch_collect", "bound": "hbm",
+                                      "achieved": cbytes / (cms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                                      "frac": cbytes / (cms * 1e-3) / HBM_PEAK, "algorithmic_bytes_per_launch": cbytes}
+    try:
+        with open(args.traffic) as fh:
+            tr = json.load(fh)
+        key = f"config5:{params_mode(args)}:p{args.percentile}:k_sketch_build"
+        if key in tr and int(tr[key].get("containers_per_rank", -1)) == S:
+            result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
+            result["roofline"]["traffic_source"] = tr[key].get("source")
+    except (OSError, ValueError):
+        pass
     # rank error of the sketch answers against the exact path on a sample of series
     m = max(1, min(args.error_sample, S))
     piece = cpu.view(S, Lr)[:m].contiguous()
@@ -455,17 +486,27 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         target = (n - 1) * float(args.percentile) / 100.0
         ltn, len_ = lt.cpu().numpy(), le.cpu().numpy()
         err = np.maximum(0.0, np.maximum(ltn - target, target - (len_ - 1))) / n
-        exact = ev_.cpu().numpy()
-        rel = np.abs(sk_vals - exact) / np.abs(exact)
-        result["sketch_error"] = {
-            "sample_series": m, "rank_error_max": float(err.max()), "rank_error_mean": float(err.mean()),
-            "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
-            "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
-                          "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
+        exact_v = ev_.cpu().numpy()
+        if exact:
+            same = (sk_vals.view(np.uint64) == exact_v.view(np.uint64)) | (np.isnan(sk_vals) & np.isnan(exact_v))
+            if params_mode(args) == "linear":  # zero sign of a LINEAR result is unspecified
+                same |= (sk_vals == exact_v)
+            result["parity_vs_single_window_select"] = bool(same.all())
+            result["parity_sample_series"] = m
+            result["parity_definition"] = ("exact refinement result (bits) == k_select/hselect over the gathered "
+                                           "full 172,800-sample series, first sample series")
+            result["collected_samples_per_rank"] = int(state.get("collected", 0))
+        else:
+            rel = np.abs(sk_vals - exact_v) / np.abs(exact_v)
+            result["sketch_error"] = {
+                "sample_series": m, "rank_error_max": float(err.max()), "rank_error_mean": float(err.mean()),
+                "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
+                "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
+                              "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
         if not args.no_cpu_baseline and world == 1:
             from oracle import oracle
 
-            cs = max(1, min(args.cpu_sample * 5, S))
+            cs = max(1, min(args.cpu_sample * 5 if args.cpu_sample else 4096, S))  # ~10 s on 16 cores
             host = cpu.view(S, Lr)[:cs].cpu().numpy().ravel()
             ho = (np.arange(cs + 1) * Lr).astype(np.int64)
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -173,6 +173,39 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
                      const double* vmax, const krr_sketch_params* sp, const krr_percentile_params* params,
                      double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);
 
+/* ---- Exact refinement of merged sketches (config 5, exact percentiles) ----
+ * The merged counts are exact, so they locate each needed rank's bin exactly:
+ *   1. krr_sketch_locate on the owner's merged sketches -> krr_sketch_loc per series;
+ *   2. every rank: krr_sketch_range_count (its local sketch) sizes, and
+ *      krr_sketch_collect fills, the CSR of its samples inside [bin_lo, bin_hi];
+ *   3. the owner concatenates the ranks' lists in time order (RCCL all-to-all) and
+ *      krr_sketch_refine selects the ranks inside them: the exact SORTED_LOWER /
+ *      LINEAR result (bit-identical to krr_segmented_percentile on the whole series). */
+typedef struct {
+    int64_t n;               /* present samples of the series (sum of merged counts) */
+    int64_t r0, r1;          /* ascending ranks needed (0-based); r1 == r0 for SORTED_LOWER */
+    int64_t before;          /* samples in bins below bin_lo */
+    double gamma;            /* LINEAR weight (numpy method="linear") */
+    uint32_t bin_lo, bin_hi; /* bins holding r0 and r1; bin_lo > bin_hi (empty) when n == 0 */
+    uint32_t flags;          /* KRR_FLAG_EMPTY */
+    int32_t mode;            /* KRR_PCT_SORTED_LOWER or KRR_PCT_LINEAR */
+} krr_sketch_loc;
+
+int krr_sketch_locate(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const krr_sketch_params* sp,
+                      const krr_percentile_params* params, krr_sketch_loc* out, void* stream);
+/* out[s] = local samples in [loc[s].bin_lo, loc[s].bin_hi] (from this rank's own sketch). */
+int krr_sketch_range_count(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const krr_sketch_params* sp,
+                           const krr_sketch_loc* loc, int64_t* out, void* stream);
+/* Segment s's present samples with bin in [bin_lo, bin_hi], position order, to
+ * out_values[out_offsets[s] ...]; out_count[s] (optional) = how many were written. */
+int krr_sketch_collect(krr_ctx* ctx, const krr_series* series, const krr_sketch_params* sp,
+                       const krr_sketch_loc* loc, const int64_t* out_offsets, double* out_values,
+                       int64_t* out_count, void* stream);
+/* collected: one segment per series (all ranks' lists, time order); out_flags adds
+ * KRR_FLAG_CAPACITY if a list does not hold the located ranks. */
+int krr_sketch_refine(krr_ctx* ctx, const krr_series* collected, const krr_sketch_loc* loc, double* out_value,
+                      int64_t* out_count, uint32_t* out_flags, void* stream);
+
 /* Per segment: out_lt[s] = #present samples < values[s], out_le[s] = #<= values[s]. */
 int krr_rank_of(krr_ctx* ctx, const krr_series* series, const double* values, int64_t* out_lt,
                 int64_t* out_le, void* stream);

@@ -49,6 +49,10 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_width",
     "krr_sketch_build",
     "krr_sketch_query",
+    "krr_sketch_locate",
+    "krr_sketch_range_count",
+    "krr_sketch_collect",
+    "krr_sketch_refine",
     "krr_rank_of",
     "krr_select_present",
 )
@@ -94,6 +98,24 @@ class KrrSketchParams(ctypes.Structure):
         ("reserved", ctypes.c_int32),
     ]
 
+
+class KrrSketchLoc(ctypes.Structure):
+    """include/krr_amd.h krr_sketch_loc (56 bytes): device arrays of it are int64
+    tensors [S, LOC_WORDS] (little-endian word view; gamma as float64 bits)."""
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("r0", ctypes.c_int64),
+        ("r1", ctypes.c_int64),
+        ("before", ctypes.c_int64),
+        ("gamma", ctypes.c_double),
+        ("bin_lo", ctypes.c_uint32),
+        ("bin_hi", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("mode", ctypes.c_int32),
+    ]
+
+
+LOC_WORDS = ctypes.sizeof(KrrSketchLoc) // 8
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -147,6 +169,14 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_sketch_query.restype = ctypes.c_int
         lib.krr_rank_of.argtypes = [vp, sp, vp, vp, vp, vp]
         lib.krr_rank_of.restype = ctypes.c_int
+        lib.krr_sketch_locate.argtypes = [vp, i64, vp, skp, pp, vp, vp]
+        lib.krr_sketch_locate.restype = ctypes.c_int
+        lib.krr_sketch_range_count.argtypes = [vp, i64, vp, skp, vp, vp, vp]
+        lib.krr_sketch_range_count.restype = ctypes.c_int
+        lib.krr_sketch_collect.argtypes = [vp, sp, skp, vp, vp, vp, vp, vp]
+        lib.krr_sketch_collect.restype = ctypes.c_int
+        lib.krr_sketch_refine.argtypes = [vp, sp, vp, vp, vp, vp, vp]
+        lib.krr_sketch_refine.restype = ctypes.c_int
         lib.krr_select_present.argtypes = [vp, sp, vp, vp, vp]
         lib.krr_select_present.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
@@ -280,6 +310,44 @@ class Context:
         self._check(self._lib.krr_sketch_query(
             self._h, S, counts.data_ptr(), vmin.data_ptr(), vmax.data_ptr(), ctypes.byref(sp), ctypes.byref(params),
             out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(), self._stream(stream)))
+
+    def sketch_locate(self, counts, sp: KrrSketchParams, params: KrrPercentileParams, out_loc,
+                      stream=None) -> None:
+        """out_loc: int64 [S, LOC_WORDS] (krr_sketch_loc per series)."""
+        S = out_loc.shape[0]
+        _check_tensor(counts, "int32", S * self.sketch_width(sp))
+        _check_tensor(out_loc, "int64", S * LOC_WORDS)
+        self._check(self._lib.krr_sketch_locate(self._h, S, counts.data_ptr(), ctypes.byref(sp), ctypes.byref(params),
+                                                out_loc.data_ptr(), self._stream(stream)))
+
+    def sketch_range_count(self, counts, sp: KrrSketchParams, loc, out, stream=None) -> None:
+        S = loc.shape[0]
+        _check_tensor(counts, "int32", S * self.sketch_width(sp))
+        _check_tensor(loc, "int64", S * LOC_WORDS)
+        _check_tensor(out, "int64", S)
+        self._check(self._lib.krr_sketch_range_count(self._h, S, counts.data_ptr(), ctypes.byref(sp),
+                                                     loc.data_ptr(), out.data_ptr(), self._stream(stream)))
+
+    def sketch_collect(self, series: KrrSeries, sp: KrrSketchParams, loc, out_offsets, out_values, out_count=None,
+                       stream=None) -> None:
+        S = series.n_segments
+        _check_tensor(loc, "int64", S * LOC_WORDS)
+        _check_tensor(out_offsets, "int64", S + 1)
+        _check_tensor(out_values, "float64")
+        if out_count is not None:
+            _check_tensor(out_count, "int64", S)
+        self._check(self._lib.krr_sketch_collect(
+            self._h, ctypes.byref(series), ctypes.byref(sp), loc.data_ptr(), out_offsets.data_ptr(),
+            out_values.data_ptr(), out_count.data_ptr() if out_count is not None else None, self._stream(stream)))
+
+    def sketch_refine(self, collected: KrrSeries, loc, out_value, out_count, out_flags, stream=None) -> None:
+        S = collected.n_segments
+        _check_tensor(loc, "int64", S * LOC_WORDS)
+        for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, S)
+        self._check(self._lib.krr_sketch_refine(self._h, ctypes.byref(collected), loc.data_ptr(),
+                                                out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(),
+                                                self._stream(stream)))
 
     def rank_of(self, series: KrrSeries, values, out_lt, out_le, stream=None) -> None:
         S = series.n_segments

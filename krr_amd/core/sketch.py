@@ -13,6 +13,13 @@ r-th contiguous time slice of every series.
   contiguous block of series, which it queries (``krr_sketch_query``).  The value
   is interpolated inside the bin holding the rank (relative bin width 2^-m); the
   rank error is measured against the exact path, never assumed (bench.py).
+* Exact percentiles (``exact_time_sharded``): the merged counts are exact, so they
+  say exactly which bin holds each needed rank and how many samples lie below it
+  (``krr_sketch_locate``).  One all-gather gives every rank those bins, each rank
+  collects its samples inside them (``krr_sketch_collect``, a second HBM pass), an
+  all-to-all hands them to the owner in time order, and ``krr_sketch_refine``
+  selects the ranks inside the short lists: bit-identical to selecting over the
+  whole series on one GPU.
 * REF_INDEX (the reference's rule, ``simple.py:36``) stays exact: all-gather the
   per-slice present counts, the rank whose slice holds global index k selects it
   (``krr_select_present``), one all-gather collects the answers.
@@ -136,6 +143,131 @@ def query(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native
     if bool(nan.any()):
         out["flags"] |= merged["flags"] & _native.KRR_FLAG_NAN
         out["value"] = torch.where(nan, torch.full_like(out["value"], float("nan")), out["value"])
+    return out
+
+
+# ------------------------- exact refinement of merged sketches -------------------------
+
+def locate(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native.KrrPercentileParams,
+           stream=None):
+    """krr_sketch_loc of every merged sketch: int64 [S_block, LOC_WORDS]."""
+    import torch
+
+    S = merged["counts"].shape[0]
+    loc = torch.empty((S, _native.LOC_WORDS), dtype=torch.int64, device=merged["counts"].device)
+    if S:
+        ctx.sketch_locate(merged["counts"], cfg.params(), params, loc, stream)
+    return loc
+
+
+def _all_gather_blocks(block, S: int, group, world: int):
+    """Concatenate every rank's owner block ([<= per, ...], owner_blocks order) -> [S, ...]."""
+    import torch
+    import torch.distributed as dist
+
+    per = -(-S // world)
+    dev = block.device
+    coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    pad = torch.zeros((per,) + tuple(block.shape[1:]), dtype=block.dtype, device=coll)
+    pad[: block.shape[0]] = block.to(coll)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    out = [p[: hi - lo] for p, (lo, hi) in zip(parts, owner_blocks(S, world))]
+    return torch.cat(out, dim=0).to(dev)
+
+
+def exchange_to_owners(values, counts, S: int, group=None):
+    """values: this rank's collected samples, CSR by series (counts[S] per series, all
+    S series in order).  Returns the owner block's lists of ALL ranks, concatenated
+    per series in rank (= time) order: (values, offsets[n_block + 1]) — the CSR
+    krr_sketch_refine reads.  World size 1: the input as CSR."""
+    import torch
+    import torch.distributed as dist
+
+    dev = values.device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        offs = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+        offs[1:] = torch.cumsum(counts, 0)
+        return values, offs
+    rank = dist.get_rank(group)
+    coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    blocks = owner_blocks(S, world)
+    per = -(-S // world)
+    cnt_pad = torch.zeros(world * per, dtype=torch.int64, device=coll)
+    for r, (lo, hi) in enumerate(blocks):
+        cnt_pad[r * per: r * per + (hi - lo)] = counts[lo:hi].to(coll)
+    recv_cnt = torch.empty_like(cnt_pad)
+    dist.all_to_all_single(recv_cnt, cnt_pad, group=group)  # [src][per] counts of my block
+    send_sizes = cnt_pad.view(world, per).sum(1).tolist()
+    c = recv_cnt.view(world, per)
+    recv_sizes = c.sum(1).tolist()
+    recv = torch.empty(int(sum(recv_sizes)), dtype=values.dtype, device=coll)
+    dist.all_to_all_single(recv, values.to(coll), output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
+                           group=group)
+    lo, hi = blocks[rank]
+    nb = hi - lo
+    c = c[:, :nb]
+    tot = c.sum(0)
+    offs = torch.zeros(nb + 1, dtype=torch.int64, device=coll)
+    offs[1:] = torch.cumsum(tot, 0)
+    if recv.numel() == 0:
+        return recv.to(dev), offs.to(dev)
+    # source-major (rank, series) pieces -> series-major, rank order inside each series
+    flat = c.reshape(-1)
+    src_start = torch.cumsum(flat, 0) - flat
+    dst_start = (offs[:-1][None, :] + (torch.cumsum(c, 0) - c)).reshape(-1)
+    piece = torch.repeat_interleave(torch.arange(flat.numel(), device=coll), flat)
+    pos = torch.arange(recv.numel(), device=coll)
+    dest = dst_start[piece] + (pos - src_start[piece])
+    grouped = torch.empty_like(recv)
+    grouped[dest] = recv
+    return grouped.to(dev), offs.to(dev)
+
+
+def exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, local: dict, merged: dict,
+                       cfg: SketchConfig, params: _native.KrrPercentileParams, group=None, stream=None,
+                       events=None) -> dict:
+    """Exact SORTED_LOWER / LINEAR percentile of every time-sharded series from this
+    rank's local sketches (``build``) and its owner block's merged sketches
+    (``merge_time_sharded``).  Returns device tensors value/count/flags for the
+    owner block (same layout as ``query``), plus 'block' and 'collected' (samples
+    this rank collected).  ``events``: optional pair of HIP events recorded around
+    the collect pass (its HBM time)."""
+    import torch
+    import torch.distributed as dist
+
+    S = series.n_segments
+    dev = series._keep[0].device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    loc_blk = locate(ctx, merged, cfg, params, stream)
+    loc = _all_gather_blocks(loc_blk, S, group, world) if world > 1 else loc_blk
+    cnt = torch.empty(S, dtype=torch.int64, device=dev)
+    ctx.sketch_range_count(local["counts"], cfg.params(), loc, cnt, stream)
+    offs = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(cnt, 0)
+    total = int(offs[-1].item())
+    vals = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+    if events is not None:
+        events[0].record(stream)
+    ctx.sketch_collect(series, cfg.params(), loc, offs, vals, None, stream)
+    if events is not None:
+        events[1].record(stream)
+    gvals, goffs = exchange_to_owners(vals[:total], cnt, S, group)
+    nb = loc_blk.shape[0]
+    gv = gvals if gvals.numel() else torch.empty(1, dtype=torch.float64, device=dev)
+    coll_ser = ctx.series(gv, goffs.contiguous(), 0, False)
+    out = {"value": torch.empty(nb, dtype=torch.float64, device=dev),
+           "count": torch.empty(nb, dtype=torch.int64, device=dev),
+           "flags": torch.empty(nb, dtype=torch.int32, device=dev)}
+    if nb:
+        ctx.sketch_refine(coll_ser, loc_blk, out["value"], out["count"], out["flags"], stream)
+    nan = (merged["flags"] & _native.KRR_FLAG_NAN) != 0
+    if bool(nan.any()):
+        out["flags"] |= merged["flags"] & _native.KRR_FLAG_NAN
+        out["value"] = torch.where(nan, torch.full_like(out["value"], float("nan")), out["value"])
+    out["block"] = merged.get("block", (0, nb))
+    out["collected"] = total
     return out
 
 

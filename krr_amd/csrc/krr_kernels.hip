@@ -1397,6 +1397,16 @@ __host__ __device__ inline SketchGeom sketch_geom(const krr_sketch_params& p) {
     return g;
 }
 
+// Bin of a non-NaN sample (bit pattern x); ascending in value.
+__device__ __forceinline__ uint32_t sketch_bin(const SketchGeom& g, uint64_t x) {
+    const uint64_t mag = x & ~kSignBit;
+    const uint32_t u = (uint32_t)(mag >> (52 - g.m)) - g.base;
+    uint32_t bin = u < g.nbins ? 3u + u : (mag < g.low_bits ? 2u : 3u + g.nbins);
+    bin = (x & kSignBit) ? 0u : bin;
+    bin = mag == 0 ? 1u : bin;
+    return bin;
+}
+
 struct SketchProc {
     uint32_t* h;
     SketchGeom g;
@@ -1411,11 +1421,7 @@ struct SketchProc {
             nan_l += nan ? 1u : 0u;
             vmin = fmin(vmin, d);
             vmax = fmax(vmax, d);
-            const uint64_t mag = x & ~kSignBit;
-            const uint32_t u = (uint32_t)(mag >> (52 - g.m)) - g.base;
-            uint32_t bin = u < g.nbins ? 3u + u : (mag < g.low_bits ? 2u : 3u + g.nbins);
-            bin = (x & kSignBit) ? 0u : bin;
-            bin = mag == 0 ? 1u : bin;
+            const uint32_t bin = sketch_bin(g, x);
             if (!nan) atomicAdd(&h[bin], 1u);
             asm volatile("" ::: "memory");
         }
@@ -1644,6 +1650,243 @@ __global__ __launch_bounds__(64) void k_select_present(const double* __restrict_
             }
         }
         if (lane == 0) out[s] = bitsd(found);
+    }
+}
+
+// --------------------- exact refinement of merged sketches ---------------------
+// Sketch counts are exact, so the merged sketch of a time-sharded series tells
+// exactly which bin holds each needed rank and how many samples lie below it.
+// Every rank then collects its samples in that bin range (k_sketch_collect), the
+// owner gathers them (RCCL all-to-all) and selects the exact order statistics
+// inside the small collected list (k_sketch_refine): results identical to the
+// single-window select, with one extra HBM pass.
+
+// Locate rank r among a segment's W bins (lane holds bins [lane*per, lane*per+per)
+// with inclusive prefix `incl` and own total t): bin index and samples below it.
+__device__ __forceinline__ void sketch_find(const uint32_t* h, uint32_t W, uint32_t per, uint32_t t, uint32_t incl,
+                                            uint64_t r, uint32_t& bin, uint64_t& before) {
+    const uint64_t m = ballot(r < incl);
+    const int src = __ffsll((long long)m) - 1;
+    uint64_t run = lane_bcast32(incl - t, src);
+    const uint32_t sb = (uint32_t)src * per;
+    bin = sb;
+    before = run;
+    for (uint32_t j = 0; j < per && sb + j < W; ++j) {
+        const uint32_t c = h[sb + j];
+        if (r < run + c) {
+            bin = sb + j;
+            before = run;
+            return;
+        }
+        run += c;
+    }
+}
+
+struct SketchLocateArgs {
+    int64_t S;
+    SketchGeom g;
+    const uint32_t* counts;
+    int32_t mode;
+    int64_t p_num, p_den;
+    double q;
+    krr_sketch_loc* out;
+};
+
+__global__ __launch_bounds__(64) void k_sketch_locate(SketchLocateArgs A) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const uint32_t* h = A.counts + (size_t)s * A.g.width;
+        const uint32_t W = A.g.width;
+        const uint32_t per = (W + kWave - 1) / kWave;
+        const uint32_t b0 = (uint32_t)lane * per;
+        uint32_t t = 0;
+        for (uint32_t j = 0; j < per; ++j) t += b0 + j < W ? h[b0 + j] : 0u;
+        const uint32_t incl = wave_scan32(t, 0u, OpAdd32{});
+        const uint64_t n = lane_bcast32(incl, kWave - 1);
+        krr_sketch_loc L;
+        L.n = (int64_t)n;
+        L.r0 = L.r1 = -1;
+        L.before = 0;
+        L.gamma = 0.0;
+        L.bin_lo = 1;
+        L.bin_hi = 0;  // empty range: nothing to collect
+        L.flags = 0;
+        L.mode = A.mode;
+        if (n == 0) {
+            L.flags = KRR_FLAG_EMPTY;
+        } else {
+            if (A.mode == KRR_PCT_SORTED_LOWER) {
+                L.r0 = L.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+            } else {  // numpy method="linear" (ranks_for)
+                const double vidx = __dmul_rn((double)(n - 1), A.q);
+                if (vidx >= (double)(n - 1)) {
+                    L.r0 = L.r1 = (int64_t)n - 1;
+                    L.gamma = __dsub_rn(vidx, -1.0);
+                } else {
+                    const double fl = floor(vidx);
+                    L.r0 = (int64_t)fl;
+                    L.r1 = L.r0 + 1;
+                    L.gamma = __dsub_rn(vidx, fl);
+                }
+            }
+            uint32_t blo, bhi;
+            uint64_t before, before_hi;
+            sketch_find(h, W, per, t, incl, (uint64_t)L.r0, blo, before);
+            if (L.r1 != L.r0) sketch_find(h, W, per, t, incl, (uint64_t)L.r1, bhi, before_hi);
+            else bhi = blo;
+            L.bin_lo = blo;
+            L.bin_hi = bhi;
+            L.before = (int64_t)before;
+        }
+        if (lane == 0) A.out[s] = L;
+    }
+}
+
+// Per segment: samples of this rank's local sketch inside [bin_lo, bin_hi].
+__global__ __launch_bounds__(64) void k_sketch_range_count(int64_t S, uint32_t W, const uint32_t* __restrict__ counts,
+                                                           const krr_sketch_loc* __restrict__ loc,
+                                                           int64_t* __restrict__ out) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const uint32_t lo = loc[s].bin_lo, hi = loc[s].bin_hi;
+        uint32_t c = 0;
+        if (lo <= hi && hi < W)
+            for (uint32_t b = lo + lane; b <= hi; b += kWave) c += counts[(size_t)s * W + b];
+        const uint32_t tot = wave_sum_u32(c);
+        if (lane == 0) out[s] = (int64_t)tot;
+    }
+}
+
+// Per segment: append, in position order, every present sample whose bin lies in
+// [bin_lo, bin_hi] to out_vals[out_offs[s] ...]; out_n[s] = how many (optional).
+__global__ __launch_bounds__(64) void k_sketch_collect(const double* __restrict__ vals,
+                                                       const int64_t* __restrict__ offs, int64_t S, SketchGeom g,
+                                                       const krr_sketch_loc* __restrict__ loc,
+                                                       const int64_t* __restrict__ out_offs,
+                                                       double* __restrict__ out_vals, int64_t* __restrict__ out_n) {
+    constexpr int U = 8;
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const uint32_t lo = loc[s].bin_lo, hi = loc[s].bin_hi;
+        uint64_t run = 0;
+        if (lo <= hi) {
+            const int64_t beg = offs[s], end = offs[s + 1];
+            double* __restrict__ dst = out_vals + out_offs[s];
+            for (int64_t base = beg; base < end; base += (int64_t)U * kWave) {
+                uint64_t x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t i = base + u * kWave + lane;
+                    x[u] = i < end ? dbits(__builtin_nontemporal_load(vals + i)) : kQuietNaN;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t b = sketch_bin(g, x[u]);
+                    const bool hit = !is_nan_bits(x[u]) && b >= lo && b <= hi;
+                    const uint64_t m = ballot(hit);
+                    if (m) {
+                        if (hit) dst[run + lane_prefix(m)] = bitsd(x[u]);
+                        run += popc64(m);
+                    }
+                }
+            }
+        }
+        if (lane == 0 && out_n) out_n[s] = (int64_t)run;
+    }
+}
+
+// Key for the refinement's ordering: numeric order with -0 == +0 (Python's
+// sorted() and numpy compare the zeros equal; SORTED_LOWER resolves which zero by
+// position afterwards, exactly as finish_value does).
+__device__ __forceinline__ uint64_t refine_key(uint64_t u) { return okey(is_zero_bits(u) ? 0ull : u); }
+
+// Key of ascending rank j among vals[beg, end) (no NaN): 8-bit MSD radix select,
+// eight passes over the (small, L2-resident) list.
+__device__ uint64_t radix_select(const double* __restrict__ vals, int64_t beg, int64_t end, uint64_t j,
+                                 uint32_t* hist, int lane) {
+    uint64_t prefix = 0, mask = 0;
+#pragma unroll 1
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int b = lane; b < 256; b += kWave) hist[b] = 0;
+        __syncthreads();
+        for (int64_t i = beg + lane; i < end; i += kWave) {
+            const uint64_t k = refine_key(dbits(vals[i]));
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        uint32_t c4[4], t = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            c4[q] = hist[lane * 4 + q];
+            t += c4[q];
+        }
+        const uint32_t incl = wave_scan32(t, 0u, OpAdd32{});
+        const uint64_t m = ballot(j < incl);
+        const int src = __ffsll((long long)m) - 1;
+        uint64_t run = lane_bcast32(incl - t, src);
+        uint32_t digit = (uint32_t)src * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t c = lane_bcast32(c4[q], src);
+            if (j >= run + c && q < 3) {
+                run += c;
+                digit = (uint32_t)src * 4 + q + 1;
+            } else {
+                break;
+            }
+        }
+        j -= run;
+        prefix |= (uint64_t)digit << shift;
+        mask |= 255ull << shift;
+        __syncthreads();
+    }
+    return prefix;
+}
+
+struct SketchRefineArgs {
+    const double* vals;  // collected samples, CSR by series, position (time) order within a series
+    const int64_t* offs;
+    int64_t S;
+    const krr_sketch_loc* loc;
+    double* out_v;
+    int64_t* out_n;
+    uint32_t* out_f;
+};
+
+__global__ __launch_bounds__(64) void k_sketch_refine(SketchRefineArgs A) {
+    __shared__ uint32_t hist[256];
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const krr_sketch_loc L = A.loc[s];
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        uint32_t flags = L.flags;
+        double result = bitsd(kQuietNaN);
+        if (L.n > 0) {
+            const int64_t j0 = L.r0 - L.before, j1 = L.r1 - L.before;
+            if (j0 < 0 || j1 < j0 || j1 >= end - beg) {
+                flags |= KRR_FLAG_CAPACITY;  // collected list inconsistent with the sketch
+            } else {
+                const uint64_t k0 = radix_select(A.vals, beg, end, (uint64_t)j0, hist, lane);
+                const uint64_t k1 = j1 != j0 ? radix_select(A.vals, beg, end, (uint64_t)j1, hist, lane) : k0;
+                const double a = bitsd(okey_inv(k0));
+                if (L.mode == KRR_PCT_SORTED_LOWER) {
+                    uint64_t bits = dbits(a);
+                    if (is_zero_bits(bits)) {  // the (j0 - #negatives)-th zero in time order
+                        const uint64_t neg = count_negative(A.vals, beg, end, lane);
+                        bits = nth_zero_bits(A.vals, beg, end, (uint64_t)j0 - neg, lane);
+                    }
+                    result = bitsd(bits);
+                } else {
+                    result = np_lerp(a, bitsd(okey_inv(k1)), L.gamma);
+                }
+            }
+        }
+        if (lane == 0) {
+            A.out_v[s] = result;
+            A.out_n[s] = L.n;
+            A.out_f[s] = flags;
+        }
+        __syncthreads();
     }
 }
 
@@ -2128,6 +2371,76 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
     SketchQueryArgs A{n_segments, sketch_geom(*sp), counts, vmin, vmax, params->mode, params->p_num,
                       params->p_den, params->q, out_value, out_count, out_flags};
     hipLaunchKernelGGL(k_sketch_query, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_sketch_locate(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const krr_sketch_params* sp,
+                      const krr_percentile_params* params, krr_sketch_loc* out, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    if (params->mode == KRR_PCT_REF_INDEX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no sketch form: use krr_select_present%s", "");
+    if (krr_sketch_width(sp) < 0) return set_err(ctx, KRR_E_INVALID, "bad sketch params%s", "");
+    if (n_segments < 0) return set_err(ctx, KRR_E_INVALID, "negative n_segments%s", "");
+    if (n_segments == 0) return KRR_OK;
+    if (!counts || !out) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    SketchLocateArgs A{n_segments, sketch_geom(*sp), counts, params->mode, params->p_num, params->p_den, params->q,
+                       out};
+    hipLaunchKernelGGL(k_sketch_locate, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_sketch_range_count(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, const krr_sketch_params* sp,
+                           const krr_sketch_loc* loc, int64_t* out, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    const int64_t W = krr_sketch_width(sp);
+    if (W < 0) return set_err(ctx, KRR_E_INVALID, "bad sketch params%s", "");
+    if (n_segments < 0) return set_err(ctx, KRR_E_INVALID, "negative n_segments%s", "");
+    if (n_segments == 0) return KRR_OK;
+    if (!counts || !loc || !out) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_sketch_range_count, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream,
+                       n_segments, (uint32_t)W, counts, loc, out);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_sketch_collect(krr_ctx* ctx, const krr_series* series, const krr_sketch_params* sp,
+                       const krr_sketch_loc* loc, const int64_t* out_offsets, double* out_values,
+                       int64_t* out_count, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    if (krr_sketch_width(sp) < 0) return set_err(ctx, KRR_E_INVALID, "bad sketch params%s", "");
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!loc || !out_offsets) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_sketch_collect, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
+                       series->offsets, S, sketch_geom(*sp), loc, out_offsets, out_values, out_count);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_sketch_refine(krr_ctx* ctx, const krr_series* collected, const krr_sketch_loc* loc, double* out_value,
+                      int64_t* out_count, uint32_t* out_flags, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, collected);
+    if (rc) return rc;
+    const int64_t S = collected->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!loc || !out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    SketchRefineArgs A{collected->values, collected->offsets, S, loc, out_value, out_count, out_flags};
+    hipLaunchKernelGGL(k_sketch_refine, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -101,3 +101,54 @@ def query(counts, vmin, vmax, m, e_lo, octaves, mode: str, p_num: int, p_den: in
     if mode == "sorted_lower":
         return vals[0], n
     return np_lerp(vals[0], vals[1], gamma), n
+
+
+# ---- exact refinement (krr_sketch_locate / _collect / _refine) ----------------------------
+
+def ranks(n: int, mode: str, p_num: int, p_den: int, q: float):
+    """(r0, r1, gamma): the ascending ranks SORTED_LOWER / LINEAR need (kernels' ranks_for)."""
+    if mode == "sorted_lower":
+        r = ((n - 1) * p_num) // (100 * p_den)
+        return r, r, 0.0
+    vidx = float(n - 1) * q
+    if vidx >= n - 1:
+        return n - 1, n - 1, vidx - (-1.0)
+    fl = math.floor(vidx)
+    return int(fl), int(fl) + 1, vidx - fl
+
+
+def locate(counts, mode: str, p_num: int, p_den: int, q: float):
+    """(n, r0, r1, before, gamma, bin_lo, bin_hi) of one merged sketch; bin_lo > bin_hi if empty."""
+    counts = np.asarray(counts, dtype=np.int64)
+    n = int(counts.sum())
+    if n == 0:
+        return 0, -1, -1, 0, 0.0, 1, 0
+    r0, r1, gamma = ranks(n, mode, p_num, p_den, q)
+    cum = np.cumsum(counts)
+    b0 = int(np.searchsorted(cum, r0, side="right"))
+    b1 = int(np.searchsorted(cum, r1, side="right"))
+    before = int(cum[b0 - 1]) if b0 else 0
+    return n, r0, r1, before, gamma, b0, b1
+
+
+def collect(x: np.ndarray, bin_lo: int, bin_hi: int, m: int, e_lo: int, octaves: int) -> np.ndarray:
+    """Present samples of x with bin in [bin_lo, bin_hi], position order."""
+    x = np.asarray(x, dtype=np.float64)
+    x = x[~np.isnan(x)]
+    if bin_lo > bin_hi or x.size == 0:
+        return x[:0]
+    b = bins_of(x, m, e_lo, octaves)
+    return x[(b >= bin_lo) & (b <= bin_hi)]
+
+
+def refine(lst: np.ndarray, j0: int, j1: int, gamma: float, mode: str) -> float:
+    """Exact result from the collected list (time order) and local ranks j0 <= j1."""
+    srt = np.sort(lst, kind="stable")
+    a = float(srt[j0])
+    if mode == "sorted_lower":
+        if a == 0.0:  # Python sorted() is stable: the zero at rank j0 by position
+            neg = int(np.count_nonzero(lst < 0))
+            zeros = lst[lst == 0.0]
+            return float(zeros[j0 - neg])
+        return a
+    return np_lerp(a, float(srt[j1]), gamma)

@@ -70,3 +70,4 @@ def test_struct_layouts_match_header():
 
     assert ctypes.sizeof(_native.KrrSeries) == 8 * 5 + 4 * 2
     assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 3
+    assert ctypes.sizeof(_native.KrrSketchLoc) == 8 * 5 + 4 * 4 and _native.LOC_WORDS == 7

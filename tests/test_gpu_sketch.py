@@ -197,3 +197,110 @@ def test_synth_window_concatenates(ctx):
         parts.append(buf.view(S, n))
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(parts, dim=1).reshape(-1), whole)
+
+
+def _same(got, want):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    return np.array_equal(got.view(np.uint64), want.view(np.uint64)) or \
+        (np.array_equal(got, want, equal_nan=True))
+
+
+@pytest.mark.parametrize("gaps", [False, True])
+@pytest.mark.parametrize("mode,pct", [("sorted_lower", "99"), ("linear", "99"), ("sorted_lower", "50"),
+                                      ("linear", "5"), ("linear", "100"), ("sorted_lower", "0.1")])
+def test_exact_refinement_world1(ctx, gaps, mode, pct):
+    """locate -> collect -> refine on one rank equals the single-window select
+    (krr_segmented_percentile path, C oracle) bit for bit, incl. zeros, negatives,
+    +inf, tiny/huge values (lumped bins) and empty series."""
+    import torch
+    from decimal import Decimal
+
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    rng = np.random.default_rng(11)
+    offs, x = _fleet(rng, S=30)
+    if gaps:
+        x[rng.random(x.size) < 0.2] = np.nan
+    ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, gaps)
+    cfg = sketch.SketchConfig(M, ELO, OCT)
+    params = percentile_params(Decimal(pct), mode)
+    local = sketch.build(ctx, ser, cfg)
+    merged = sketch.merge_time_sharded(local)
+    res = sketch.exact_time_sharded(ctx, ser, local, merged, cfg, params)
+    torch.cuda.synchronize()
+    ov, on, of = oracle.percentile(x, offs, params.mode, params.p_num, params.p_den, params.q, gaps)
+    got = res["value"].cpu().numpy()
+    if mode == "linear":  # the zero sign of a LINEAR result is unspecified (numpy's partition)
+        assert np.array_equal(got, ov, equal_nan=True)
+    else:
+        assert _same(got, ov)
+    assert np.array_equal(res["count"].cpu().numpy(), on)
+    assert np.array_equal(res["flags"].cpu().numpy().astype(np.uint32), of)
+    assert res["collected"] < x.size // 4  # only the located bins travel
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_exact_refinement_emulated_ranks(ctx, mode):
+    """Three time slices per series handled as three 'ranks' in one process: local
+    sketches summed (the reduce-scatter), per-slice collect, lists concatenated in
+    slice order (the all-to-all), refine — equals the select over whole series."""
+    import torch
+    from decimal import Decimal
+
+    from krr_amd import _native
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    rng = np.random.default_rng(12)
+    S, L, W = 20, 6000, 3
+    x = rng.gamma(2.0, 0.05, size=(S, L))
+    x[rng.random(x.shape) < 0.15] = np.nan
+    x[2] = np.where(rng.random(L) < 0.5, 0.0, -0.0)  # all-zero series: the sign comes from position
+    x[3, :4000] = np.nan                              # empty in the first two slices
+    x[4] = np.nan                                     # empty
+    x[5, ::7] = -x[5, ::7]
+    cfg = sketch.SketchConfig(M, ELO, OCT)
+    params = percentile_params(Decimal("99"), mode)
+    cuts = np.array_split(np.arange(L), W)
+    sers, locals_ = [], []
+    for c in cuts:
+        xs = np.ascontiguousarray(x[:, c]).ravel()
+        o = (np.arange(S + 1) * c.size).astype(np.int64)
+        ser = ctx.series(_dev(xs), _dev(o, np.int64), 0, True)
+        sers.append(ser)
+        locals_.append(sketch.build(ctx, ser, cfg))
+    merged = {"counts": sum(l["counts"] for l in locals_), "flags": torch.zeros(S, dtype=torch.int32, device="cuda:0")}
+    loc = sketch.locate(ctx, merged, cfg, params)
+    lists = []
+    for ser, l in zip(sers, locals_):
+        cnt = torch.empty(S, dtype=torch.int64, device="cuda:0")
+        ctx.sketch_range_count(l["counts"], cfg.params(), loc, cnt)
+        off = torch.zeros(S + 1, dtype=torch.int64, device="cuda:0")
+        off[1:] = torch.cumsum(cnt, 0)
+        vals = torch.empty(max(int(off[-1]), 1), dtype=torch.float64, device="cuda:0")
+        got_n = torch.empty(S, dtype=torch.int64, device="cuda:0")
+        ctx.sketch_collect(ser, cfg.params(), loc, off, vals, got_n)
+        assert torch.equal(got_n, cnt)
+        lists.append((vals.cpu().numpy(), off.cpu().numpy()))
+    cat, offs = [], [0]
+    for s in range(S):
+        for v, o in lists:
+            cat.append(v[o[s]:o[s + 1]])
+        offs.append(offs[-1] + sum(o[s + 1] - o[s] for _, o in lists))
+    cser = ctx.series(_dev(np.concatenate(cat) if cat else np.zeros(1)), _dev(np.array(offs), np.int64), 0, False)
+    ov_ = torch.empty(S, dtype=torch.float64, device="cuda:0")
+    on_ = torch.empty(S, dtype=torch.int64, device="cuda:0")
+    of_ = torch.empty(S, dtype=torch.int32, device="cuda:0")
+    ctx.sketch_refine(cser, loc, ov_, on_, of_)
+    full = x.ravel()
+    fo = (np.arange(S + 1) * L).astype(np.int64)
+    wv, wn, wf = oracle.percentile(full, fo, params.mode, params.p_num, params.p_den, params.q, True)
+    got = ov_.cpu().numpy()
+    if mode == "linear":
+        assert np.array_equal(got, wv, equal_nan=True)
+    else:
+        assert _same(got, wv)
+    assert np.array_equal(on_.cpu().numpy(), wn)
+    assert np.array_equal(of_.cpu().numpy().astype(np.uint32), wf)
+    assert (of_.cpu().numpy() & _native.KRR_FLAG_CAPACITY).sum() == 0

@@ -151,3 +151,74 @@ def test_time_sharded_merges_world2():
                     best = y
             assert np.float64(mx["value"][s]).view(np.uint64) == np.float64(best).view(np.uint64), s
             assert mx["count"][s] == v.size
+
+
+def _exact_worker(rank, world, port, q):
+    """The exact refinement's host flow with the kernels replaced by oracle/sketch_ref:
+    merged sketches (reduce-scatter) -> locate on the owner -> all-gather of the
+    locations -> local collect -> exchange_to_owners (all-to-all) -> exact select."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = _series()
+        S, L = x.shape
+        local = x[:, np.array_split(np.arange(L), world)[rank]]
+        built = [sketch_ref.build(local[s], M, ELO, OCT) for s in range(S)]
+        sk = {"counts": torch.tensor(np.stack([b[0] for b in built]), dtype=torch.int32),
+              "vmin": torch.tensor([b[1] for b in built], dtype=torch.float64),
+              "vmax": torch.tensor([b[2] for b in built], dtype=torch.float64),
+              "flags": torch.zeros(S, dtype=torch.int32)}
+        merged = sketch.merge_time_sharded(sk)
+        lo, hi = merged["block"]
+        out = {}
+        for mode, pn, pd in (("sorted_lower", 99, 1), ("linear", 99, 1), ("sorted_lower", 50, 1),
+                             ("linear", 5, 1)):
+            qv = pn / pd / 100
+            locs = [sketch_ref.locate(c, mode, pn, pd, qv) for c in merged["counts"].numpy()]
+            blk = torch.tensor([[n, r0, r1, bef, b0, b1] for n, r0, r1, bef, g, b0, b1 in locs],
+                               dtype=torch.int64).reshape(-1, 6)
+            every = sketch._all_gather_blocks(blk, S, None, world)
+            assert every.shape == (S, 6)
+            lists = [sketch_ref.collect(local[s], int(every[s, 4]), int(every[s, 5]), M, ELO, OCT) for s in range(S)]
+            cnt = torch.tensor([len(v) for v in lists], dtype=torch.int64)
+            vals = torch.tensor(np.concatenate(lists) if lists else np.zeros(0), dtype=torch.float64)
+            gv, go = sketch.exchange_to_owners(vals, cnt, S, None)
+            got = []
+            for i, (n, r0, r1, bef, g, b0, b1) in enumerate(locs):
+                lst = gv[int(go[i]):int(go[i + 1])].numpy()
+                got.append(np.nan if n == 0 else sketch_ref.refine(lst, r0 - bef, r1 - bef, g, mode))
+            out[(mode, pn)] = (lo, hi, got)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exact_refinement_host_flow(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_exact_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x = _series()
+    for (mode, pn), _ in res[0].items():
+        for r in range(world):
+            lo, hi, got = res[r][(mode, pn)]
+            for s in range(lo, hi):
+                v = x[s][~np.isnan(x[s])]
+                if v.size == 0:
+                    assert np.isnan(got[s - lo])
+                    continue
+                if mode == "linear":
+                    want = np.percentile(v, pn)
+                else:
+                    want = sorted(v.tolist())[((v.size - 1) * pn) // 100]
+                assert got[s - lo] == want, (mode, pn, s)
+                if mode == "sorted_lower":
+                    assert np.signbit(got[s - lo]) == np.signbit(want), (mode, pn, s)
