@@ -93,7 +93,7 @@ def main():
     import torch.distributed as dist
 
     from krr_amd import _native
-    from krr_amd.core.distributed import gather_records
+    from krr_amd.core.distributed import gather_records, record_counts
     from krr_amd.core.engine import percentile_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,7 +141,10 @@ def main():
     }
     stream = torch.cuda.current_stream()
     host_rec = torch.empty((containers_total if rank == 0 else S, 4), dtype=torch.int64, pin_memory=True)
+    # records go to the host on the compute stream: a copy stream overlapping the
+    # next step's kernel was measured to gain nothing (the blit slows the kernel)
     dev_rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
+    counts = record_counts(S, coll_dev) if world > 1 else None  # shard sizes are fixed: exchange once
 
     def step(events=None):
         if events is not None:
@@ -151,16 +154,17 @@ def main():
             if events is not None:
                 events[1].record(stream)
             ctx.segmented_max(ms, out["mem_value"], out["mem_count"], out["mem_flags"], stream)
-        else:  # one fused launch: CPU percentile + memory max for every container
-            ctx.simple_run(cs, ms, params, out, stream)
+            if events is not None:
+                events[2].record(stream)
+        if args.separate:
+            ctx.pack_records(out, dev_rec, stream)  # one launch: 32-B records
+        else:  # ONE launch: CPU percentile + memory max for every container, records included
+            ctx.simple_run(cs, ms, params, out, stream, records=dev_rec)
             if events is not None:
                 events[1].record(stream)
-        if events is not None:
-            events[2].record(stream)
-        ctx.pack_records(out, dev_rec, stream)  # one launch: 32-B records
         rec = dev_rec
         if world > 1:
-            rec = gather_records(rec.to(coll_dev), dst=0)
+            rec = gather_records(rec.to(coll_dev), dst=0, counts=counts)
         if rank == 0 or world == 1:
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
 
@@ -183,7 +187,7 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())
     k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs])) if args.separate else 0.0
 
     # algorithmic bytes per launch: every stored slot once, offsets, outputs
     seg_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S  # one resource
@@ -345,7 +349,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
 
     from krr_amd import _native
     from krr_amd.core import sketch
-    from krr_amd.core.distributed import gather_records
+    from krr_amd.core.distributed import gather_records, record_counts
     from krr_amd.core.engine import percentile_params
 
     S = args.containers or 100_000
@@ -363,6 +367,11 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     params = percentile_params(Decimal(args.percentile), params_mode(args))
     exact = not args.sketch_only
     stream = torch.cuda.current_stream()
+    if world > 1:  # owner blocks are fixed: exchange the record counts once
+        blk = sketch.owner_blocks(S, world)[rank]
+        counts = record_counts(blk[1] - blk[0], coll_dev)
+    else:
+        counts = None
     host_rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
     state = {}
 
@@ -382,7 +391,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         rec = torch.stack([res["value"].view(torch.int64), res["count"] | (res["flags"].to(torch.int64) << 48),
                            torch.zeros_like(res["count"]), torch.zeros_like(res["count"])], dim=1)
         if world > 1:
-            rec = gather_records(rec.to(coll_dev), dst=0)
+            rec = gather_records(rec.to(coll_dev), dst=0, counts=counts)
         if rank == 0:
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
         state["merged"] = merged

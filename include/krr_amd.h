@@ -126,6 +126,15 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
                    uint32_t* cpu_flags, double* mem_value, int64_t* mem_count,
                    uint32_t* mem_flags, void* stream);
 
+/* krr_simple_run that also writes each object's 32-byte result record
+ * (krr_pack_records layout: cpu bits, mem bits, cpu count | cpu flags << 48,
+ * mem count | mem flags << 48) from the same launch — no separate pack pass.
+ * records: device int64[4 * n_objects], or NULL (= krr_simple_run). */
+int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
+                           const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
+                           uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
+                           int64_t* records, void* stream);
+
 /* Same as krr_simple_run, but every pointer (inputs and outputs) is a HOST
  * pointer; copies in, runs, copies out and synchronises.  Includes PCIe. */
 int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* cpu_offsets,

@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "krr_segmented_percentile",
     "krr_segmented_max",
     "krr_simple_run",
+    "krr_simple_run_records",
     "krr_simple_run_host",
     "krr_pack_records",
     "krr_synth_fill",
@@ -151,6 +152,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_segmented_max.argtypes = [vp, sp, vp, vp, vp, vp]
         lib.krr_segmented_max.restype = ctypes.c_int
         lib.krr_simple_run.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_simple_run_records.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_simple_run_records.restype = ctypes.c_int
         lib.krr_simple_run.restype = ctypes.c_int
         lib.krr_simple_run_host.argtypes = [vp, vp, vp, vp, vp, i64, i32, pp, vp, vp, vp, vp, vp, vp]
         lib.krr_simple_run_host.restype = ctypes.c_int
@@ -254,17 +257,21 @@ class Context:
             self._stream(stream)))
 
     def simple_run(self, cpu: KrrSeries, mem: KrrSeries, params: KrrPercentileParams, out: dict,
-                   stream=None) -> None:
-        """out: dict with cpu_value/cpu_count/cpu_flags/mem_value/mem_count/mem_flags tensors."""
+                   stream=None, records=None) -> None:
+        """out: dict with cpu_value/cpu_count/cpu_flags/mem_value/mem_count/mem_flags tensors;
+        records (optional): int64 [S, 4] device tensor the same launch fills with the
+        32-B result records (krr_simple_run_records)."""
         n = cpu.n_segments
         for k, dt in (("cpu_value", "float64"), ("cpu_count", "int64"), ("cpu_flags", "int32"),
                       ("mem_value", "float64"), ("mem_count", "int64"), ("mem_flags", "int32")):
             _check_tensor(out[k], dt, n)
-        self._check(self._lib.krr_simple_run(
+        if records is not None:
+            _check_tensor(records, "int64", 4 * n)
+        self._check(self._lib.krr_simple_run_records(
             self._h, ctypes.byref(cpu), ctypes.byref(mem), ctypes.byref(params),
             out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
             out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
-            self._stream(stream)))
+            records.data_ptr() if records is not None else None, self._stream(stream)))
 
     def pack_records(self, out: dict, records, stream=None) -> None:
         """out: the six result tensors; records: int64 [S, 4] device tensor."""

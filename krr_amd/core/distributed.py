@@ -70,12 +70,26 @@ def unpack_records(rec) -> dict:
     }
 
 
-def gather_records(local, dst: int = 0, group=None) -> Optional[object]:
+def record_counts(n_local: int, device, group=None) -> list[int]:
+    """Every rank's record count (one all_gather of an int64; host sync)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([n_local], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    return [int(c.item()) for c in counts]
+
+
+def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None) -> Optional[object]:
     """Gather every rank's [n_r, 4] records to rank `dst`, concatenated in rank order.
 
-    Ranks may hold different n_r: counts are exchanged first (one all_gather of a
-    single int64), shards are padded to the max, gathered in ONE collective, and
-    trimmed on dst.  Returns the [sum n_r, 4] tensor on dst, None elsewhere.
+    Ranks may hold different n_r: counts are exchanged first (``record_counts``,
+    one all_gather of a single int64 and a host sync — pass ``counts`` to reuse
+    them when the shard sizes do not change between calls), shards are padded to
+    the max, gathered in ONE collective, and trimmed on dst.  Returns the
+    [sum n_r, 4] tensor on dst, None elsewhere.
     """
     import torch
     import torch.distributed as dist
@@ -83,10 +97,8 @@ def gather_records(local, dst: int = 0, group=None) -> Optional[object]:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = local.device
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
+    if counts is None:
+        counts = record_counts(local.shape[0], dev, group)
     width = max(max(counts), 1)
     padded = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
     if local.shape[0]:

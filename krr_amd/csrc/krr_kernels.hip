@@ -672,7 +672,16 @@ struct SelectArgs {
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
+    int64_t* rec = nullptr;  // optional 32-B result records (k_pack_records layout), CPU half
 };
+
+// One half of an object's 32-B record (k_pack_records layout): half 0 = CPU, 1 = memory.
+__device__ __forceinline__ void put_record(int64_t* rec, int64_t s, int half, double v, uint64_t n, uint32_t f) {
+    if (rec) {
+        rec[4 * s + half] = (int64_t)dbits(v);
+        rec[4 * s + 2 + half] = (int64_t)(n | ((uint64_t)f << 48));
+    }
+}
 
 // Ranks a SORTED_LOWER / LINEAR result needs among n present samples (ascending,
 // 0-based): SORTED_LOWER r0 = r1 = k; LINEAR numpy's prev/next with its gamma.
@@ -725,6 +734,7 @@ __device__ __forceinline__ void write_result(const SelectArgs& A, int64_t s, dou
         A.out_v[s] = v;
         A.out_n[s] = (int64_t)n;
         A.out_f[s] = flags;
+        put_record(A.rec, s, 0, v, n, flags);
     }
 }
 
@@ -1158,6 +1168,7 @@ struct RefArgs {
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
+    int64_t* rec = nullptr;  // optional records, CPU half
 };
 
 // NaN-gapped layout: the k-th PRESENT sample in position order.
@@ -1213,6 +1224,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
             A.out_v[s] = result;
             A.out_n[s] = (int64_t)n;
             A.out_f[s] = flags;
+            put_record(A.rec, s, 0, result, n, flags);
         }
     }
 }
@@ -1270,6 +1282,7 @@ struct MaxArgs {
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
+    int64_t* rec = nullptr;  // optional records, memory half
 };
 
 template <class Streamer>
@@ -1298,6 +1311,7 @@ __device__ __forceinline__ void max_segment_with(const MaxArgs& A, int64_t s, in
             A.out_v[s] = result;
             A.out_n[s] = (int64_t)n;
             A.out_f[s] = flags;
+            put_record(A.rec, s, 1, result, n, flags);
         }
     }
 }
@@ -2172,6 +2186,14 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
                    const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
                    uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
                    void* stream) {
+    return krr_simple_run_records(ctx, cpu, mem, params, cpu_value, cpu_count, cpu_flags, mem_value, mem_count,
+                                  mem_flags, nullptr, stream);
+}
+
+int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
+                           const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
+                           uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
+                           int64_t* records, void* stream) {
     if (!ctx) return KRR_E_INVALID;
     if (!cpu || !mem) return set_err(ctx, KRR_E_INVALID, "null series%s", "");
     if (cpu->n_segments != mem->n_segments)
@@ -2187,14 +2209,17 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
     if (params->mode == KRR_PCT_REF_INDEX && !cpu->gaps_are_nan) {
         // compact REF_INDEX is one gather per segment: nothing to fuse with
         rc = krr_segmented_percentile(ctx, cpu, params, cpu_value, cpu_count, cpu_flags, stream);
-        if (rc) return rc;
-        return krr_segmented_max(ctx, mem, mem_value, mem_count, mem_flags, stream);
+        if (!rc) rc = krr_segmented_max(ctx, mem, mem_value, mem_count, mem_flags, stream);
+        if (!rc && records)
+            rc = krr_pack_records(ctx, S, cpu_value, cpu_count, cpu_flags, mem_value, mem_count, mem_flags,
+                                  records, stream);
+        return rc;
     }
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     hipStream_t st = (hipStream_t)stream;
-    MaxArgs M{mem->values, mem->offsets, S, mem->gaps_are_nan, mem_value, mem_count, mem_flags};
-    RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags};
+    MaxArgs M{mem->values, mem->offsets, S, mem->gaps_are_nan, mem_value, mem_count, mem_flags, records};
+    RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags, records};
     SelectArgs A{};
     if (params->mode == KRR_PCT_REF_INDEX) {
         hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(2 * S)), dim3(64), 0, st, A, R, M);
@@ -2202,6 +2227,7 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
         size_t lds = 0;
         rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds);
         if (rc) return rc;
+        A.rec = records;
         if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
         else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
     }

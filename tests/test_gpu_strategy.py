@@ -231,6 +231,11 @@ def test_fused_simple_run_and_records(mode, gaps):
     assert np.array_equal(u["cpu_count"], on) and np.array_equal(u["cpu_flags"], of)
     assert np.array_equal(u["mem_value"], mv, equal_nan=True) and np.array_equal(u["mem_count"], mn)
     assert np.array_equal(u["mem_flags"], mf)
+    # the same launch writing the records itself (krr_simple_run_records) == k_pack_records
+    rec2 = torch.full((S, 4), -7, dtype=torch.int64, device=dev)
+    ctx.simple_run(cs, ms, params, out, records=rec2)
+    torch.cuda.synchronize()
+    assert torch.equal(rec2, rec)
     ctx.close()
 
 
