@@ -34,6 +34,9 @@
 #ifndef KRR_MAX_DEPTH
 #define KRR_MAX_DEPTH 2  // chunks in flight in the multi-site streaming loop (k_max): 1 or 2
 #endif
+#ifndef KRR_LANE_INSERT
+#define KRR_LANE_INSERT 1  // select fast path: per-lane masks + one scan (0: per-slot ballot insert)
+#endif
 #ifndef KRR_HSEL_WAVES_PER_SIMD
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
@@ -388,6 +391,40 @@ struct SelectProc {
         count_nan(c);
         // Steady state: fast inclusive threshold, the whole chunk fits.
         if (uni32(fast)) {
+#if KRR_LANE_INSERT
+            // Per-lane candidate mask (slot j -> bit 15 - j) built in VGPRs, ONE wave
+            // scan for every lane's write position, then predicated LDS writes
+            // (non-candidates write a per-lane scratch slot): ~4 VALU + 1 LDS per
+            // slot and no per-slot ballot/SALU work — with a 1-3% candidate rate
+            // nearly every 64-wide slot holds a candidate, so per-slot scalar
+            // bookkeeping was paid on most slots.
+            uint32_t vm = 0;
+#pragma unroll
+            for (int j = 0; j < 2 * kUnroll; ++j) {
+                const uint64_t x = dbits(slot_val(c, j));
+                vm = (vm << 1) + ((x - tb) < tlim ? 1u : 0u);
+            }
+            const uint32_t vc = __popc(vm);
+            const uint32_t incl_c = wave_scan32(vc, 0u, OpAdd32{});
+            const uint32_t C = lane_bcast32(incl_c, kWave - 1);
+            if (cnt + C <= cap) {
+                KRR_DIAG_ADD(D_INSERTED, C);
+                if (C) {
+                    uint32_t pos = cnt + incl_c - vc;
+                    uint64_t* const scratch = small + lane;
+#pragma unroll
+                    for (int j = 0; j < 2 * kUnroll; ++j) {
+                        const uint64_t x = dbits(slot_val(c, j));
+                        const uint32_t bit = (vm >> (2 * kUnroll - 1 - j)) & 1u;
+                        uint64_t* const dst = bit ? buf + pos : scratch;
+                        *dst = x | kSignBit;
+                        pos += bit;
+                    }
+                    cnt = uni32(cnt + C);
+                }
+                return;
+            }
+#else
             uint32_t C, E, jm;
             classify<true, false>(c, 0xFFFFu, C, E, jm);
             if (cnt + C <= cap) {
@@ -396,6 +433,7 @@ struct SelectProc {
                 if (jm) insert<true>(c, jm);
                 return;
             }
+#endif
         }
         chunk_general(c);
     }
