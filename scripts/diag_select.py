@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--mode", default="linear")
     ap.add_argument("--percentile", default="99")
     ap.add_argument("--containers", type=int, default=10000)
+    ap.add_argument("--length", type=int, default=5 * 10080, help="slots per segment")
+    ap.add_argument("--compact", action="store_true", help="no NaN gaps (config 3/4 layout)")
     a = ap.parse_args()
     import torch
 
@@ -35,16 +37,17 @@ def main():
     h = ctypes.c_void_p()
     assert lib.krr_create(0, ctypes.byref(h)) == 0
     n = a.containers
-    L = 5 * 10080
+    L = a.length
     offs_np = np.arange(n + 1, dtype=np.int64) * L
     offs = torch.from_numpy(offs_np).to(dev)
     N = int(offs_np[-1])
     cpu = torch.empty(N, dtype=torch.float64, device=dev)
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    assert lib.krr_synth_fill(h, cpu.data_ptr(), offs.data_ptr(), n, 7, 0, 10080, 1, sp) == 0
+    gaps = 0 if a.compact else 1
+    assert lib.krr_synth_fill(h, cpu.data_ptr(), offs.data_ptr(), n, 7, 0, 10080, gaps, sp) == 0
     diag = torch.zeros(n * 8, dtype=torch.int64, device=dev)
     assert lib.krr_diag_attach(ctypes.c_void_p(diag.data_ptr())) == 0
-    ser = _native.KrrSeries(cpu.data_ptr(), offs.data_ptr(), n, N, L, 1, 0)
+    ser = _native.KrrSeries(cpu.data_ptr(), offs.data_ptr(), n, N, L, gaps, 0)
     params = percentile_params(Decimal(a.percentile), a.mode)
     ov = torch.empty(n, dtype=torch.float64, device=dev)
     on = torch.empty(n, dtype=torch.int64, device=dev)

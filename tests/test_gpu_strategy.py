@@ -279,3 +279,24 @@ def test_batched_runner_collect_result_matches_per_object_scans():
     allocs = runner.allocations(objs, hists)
     want = Result(scans=[ResourceScan.calculate(o, a) for o, a in zip(objs, allocs)])
     assert result.scans == want.scans and result.score == want.score
+
+
+def test_concurrent_run_from_threads_matches_sequential():
+    """The reference calls strategy.run from executor threads (runner.py:104-106): the
+    ABI is reentrant per thread-local krr_ctx, so concurrent runs give the sequential
+    results bit for bit."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from krr_amd.core.models.allocations import ResourceType
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    strat = SimpleStrategy(SimpleStrategySettings(cpu_percentile="99", memory_buffer_percentage="5"))
+    cases = [c for c in DOC["cases"] if "error" not in c["results"]["cli_99_5"]][:40]
+    args = [(_hist(c), _obj(c["name"])) for c in cases]
+    seq = [strat.run(h, o) for h, o in args]
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        par = list(ex.map(lambda a: strat.run(*a), args * 3))
+    for i, r in enumerate(par):
+        s = seq[i % len(seq)]
+        for rt in ResourceType:
+            assert _d(r[rt].request) == _d(s[rt].request) and _d(r[rt].limit) == _d(s[rt].limit)
