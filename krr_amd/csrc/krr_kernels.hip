@@ -37,6 +37,9 @@
 #ifndef KRR_LANE_INSERT
 #define KRR_LANE_INSERT 1  // select fast path: per-lane masks + one scan (0: per-slot ballot insert)
 #endif
+#ifndef KRR_PAIR_RANKS
+#define KRR_PAIR_RANKS 1  // LINEAR's two adjacent ranks from one locate (0: two locates)
+#endif
 #ifndef KRR_HSEL_WAVES_PER_SIMD
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
@@ -640,6 +643,94 @@ struct SelectProc {
         return lane_bcast64(v, __ffsll((long long)sel) - 1);
     }
 
+    // Smallest key of buf above hi / largest below lo (one pass; ~0 / 0 if none).
+    __device__ __forceinline__ uint64_t min_above(uint64_t hi) const {
+        uint64_t m = ~0ull;
+        for (uint32_t i = lane; i < cnt; i += kWave) {
+            const uint64_t x = buf[i];
+            m = (x > hi && x < m) ? x : m;
+        }
+        return wave_min_u64(m);
+    }
+    __device__ __forceinline__ uint64_t max_below(uint64_t lo) const {
+        uint64_t m = 0;
+        for (uint32_t i = lane; i < cnt; i += kWave) {
+            const uint64_t x = buf[i];
+            m = (x < lo && x > m) ? x : m;
+        }
+        return wave_max_u64(m);
+    }
+
+    // The R-th largest key (ka) and its neighbour the (R + dir)-th largest (kb;
+    // dir = -1: the next larger key, +1: the next smaller) from ONE locate: LINEAR
+    // needs two adjacent ranks, which a second locate would find in the same range.
+    __device__ __forceinline__ void kth_pair(uint32_t R, int dir, uint64_t mn, uint64_t mx, uint64_t& ka,
+                                             uint64_t& kb) {
+        const Cut ct = locate(R, mn, mx, [](uint32_t, uint32_t c) { return c <= (uint32_t)kWave; });
+        ka = kb = 0;
+        if (!ct.ok) {
+            bad |= 16u;
+            return;
+        }
+        const uint32_t R2 = R - ct.above;  // 1-based rank inside [lo, hi]
+        const int64_t Rb = (int64_t)R2 + dir;
+        if (ct.lo == ct.hi) {
+            ka = ct.lo;
+            kb = (Rb >= 1 && Rb <= (int64_t)ct.cnt) ? ct.lo : (dir < 0 ? min_above(ct.hi) : max_below(ct.lo));
+            return;
+        }
+        uint32_t w = 0;
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bool inb = base + t * kWave + lane < cnt && x[t] >= ct.lo && x[t] <= ct.hi;
+                const uint64_t m = ballot(inb);
+                if (inb) small[w + lane_prefix(m)] = x[t];
+                w += popc64(m);
+            }
+        }
+        __syncthreads();
+        const uint64_t v = (uint32_t)lane < w ? small[lane] : 0ull;
+        uint32_t gt = 0, ge = 0;
+        for (uint32_t j = 0; j < w; ++j) {
+            const uint64_t y = small[j];
+            gt += y > v ? 1u : 0u;
+            ge += y >= v ? 1u : 0u;
+        }
+        const uint64_t sa = ballot((uint32_t)lane < w && gt < R2 && R2 <= ge);
+        const bool inside = Rb >= 1 && Rb <= (int64_t)w;
+        const uint64_t sb = ballot(inside && (uint32_t)lane < w && (int64_t)gt < Rb && Rb <= (int64_t)ge);
+        __syncthreads();
+        if (!sa || (inside && !sb)) {
+            bad |= 8u;
+            return;
+        }
+        ka = lane_bcast64(v, __ffsll((long long)sa) - 1);
+        kb = inside ? lane_bcast64(v, __ffsll((long long)sb) - 1) : (dir < 0 ? min_above(ct.hi) : max_below(ct.lo));
+    }
+
+    // Keys of ascending ranks r and r + 1 (LINEAR's pair) among nsel present samples.
+    __device__ __forceinline__ void rank_key_pair(uint64_t r, uint64_t nsel, uint64_t mn, uint64_t mx, uint64_t& k0,
+                                                  uint64_t& k1) {
+        const uint64_t rr0 = flip ? (nsel - 1 - r) : r;
+        const uint64_t rr1 = flip ? rr0 - 1 : rr0 + 1;
+        const uint64_t ties = incl ? 0u : eqs;
+        const uint64_t below = nsel - cnt - ties;
+        if ((rr0 < rr1 ? rr0 : rr1) < below + ties) {  // a rank among the ties / below: one by one
+            k0 = rank_key(r, nsel, mn, mx);
+            k1 = rank_key(r + 1, nsel, mn, mx);
+            return;
+        }
+        const uint32_t idx0 = (uint32_t)(rr0 - below - ties);
+        kth_pair(cnt - idx0, flip ? 1 : -1, mn, mx, k0, k1);
+    }
+
     // Key of the element with ascending rank r (0-based) among nsel present samples.
     __device__ __forceinline__ uint64_t rank_key(uint64_t r, uint64_t nsel, uint64_t mn, uint64_t mx) {
         const uint64_t rr = flip ? (nsel - 1 - r) : r;
@@ -826,6 +917,15 @@ __device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t
         } else {
             const Ranks R = ranks_for(A, n);
             uint64_t k0 = 0, k1 = 0;
+#if KRR_PAIR_RANKS
+            if (R.r1 != R.r0) {  // LINEAR: both adjacent ranks from one locate
+                P.rank_key_pair((uint64_t)R.r0, n, bmn, bmx, k0, k1);
+                k0 ^= P.flip;
+                k1 ^= P.flip;
+            } else {
+                k0 = P.rank_key((uint64_t)R.r0, n, bmn, bmx) ^ P.flip;
+            }
+#else
             // one rank-query body serves both ranks (a 1-2 iteration loop keeps it inlined once)
             const int nq = R.r1 != R.r0 ? 2 : 1;
 #pragma unroll 1
@@ -834,6 +934,7 @@ __device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t
                 if (qi) k1 = kq;
                 else k0 = kq;
             }
+#endif
             result = finish_value(A, R, k0, k1, beg, end, lane);
         }
         if (P.bad) flags |= KRR_FLAG_CAPACITY | (P.bad << 8);  // reason bits (diagnostic)

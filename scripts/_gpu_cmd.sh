@@ -1,7 +1,10 @@
 #!/bin/bash
 set -o pipefail
-mkdir -p gpurun_out/diag
-timeout -k 10 200 python -u scripts/diag_select.py krr_amd/lib/variants/lib_diag.so > gpurun_out/diag/c2.log 2>&1 || { tail -20 gpurun_out/diag/c2.log; exit 1; }
-cat gpurun_out/diag/c2.log | grep -v amdgpu.ids
-timeout -k 10 200 python -u scripts/diag_select.py krr_amd/lib/variants/lib_diag.so --length 10080 --compact --containers 200000 > gpurun_out/diag/c4.log 2>&1 || { tail -20 gpurun_out/diag/c4.log; exit 1; }
-cat gpurun_out/diag/c4.log | grep -v amdgpu.ids
+mkdir -p gpurun_out/ab
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_strategy.py tests/test_gpu_fullsize.py tests/test_gpu_sketch.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/t.log 2>&1 || { tail -30 gpurun_out/ab/t.log; exit 1; }
+tail -1 gpurun_out/ab/t.log
+V=krr_amd/lib/variants
+for c in "--config 2" "--config 3" "--config 4 --containers 100000"; do
+timeout -k 10 400 python -u scripts/ab_variants.py $V/lib_pair0.so $V/lib_pair1.so $V/lib_pair0.so $V/lib_pair1.so --rounds 4 $c > gpurun_out/ab/ab.log 2>&1 || { tail -20 gpurun_out/ab/ab.log; exit 1; }
+echo "== $c"; tail -2 gpurun_out/ab/ab.log
+done

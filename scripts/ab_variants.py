@@ -48,6 +48,9 @@ def main():
     if a.config == 2:
         L, pod_len, gaps = 5 * 10080, 10080, True
         offs_np = np.arange(n + 1, dtype=np.int64) * L
+    elif a.config == 4:  # 10,080-sample compact segments (one shard of config 4)
+        offs_np = np.arange(n + 1, dtype=np.int64) * 10080
+        pod_len, gaps = 0, False
     else:
         rng = np.random.default_rng(3)
         offs_np = np.concatenate([[0], np.cumsum(rng.integers(1, 15, size=n) * 1440)]).astype(np.int64)
