@@ -162,14 +162,26 @@ def main():
             ctx.simple_run(cs, ms, params, out, stream, records=dev_rec)
             if events is not None:
                 events[1].record(stream)
-        rec = dev_rec
-        if world > 1:
-            rec = gather_records(rec.to(coll_dev), dst=0, counts=counts)
-        if rank == 0 or world == 1:
-            host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+        if world == 1:
+            host_rec.copy_(dev_rec, non_blocking=True)
+            return
+        # N > 1: this step's gather stays in flight (RCCL stream) while the next
+        # step's kernel runs; it is waited for one step later (and by finish())
+        pend = gather_records(dev_rec.to(coll_dev), dst=0, counts=counts, async_op=True)
+        finish()
+        inflight.append(pend)
+
+    inflight = []
+
+    def finish():
+        while inflight:
+            rec = inflight.pop().wait()
+            if rank == 0:
+                host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
 
     for _ in range(args.warmup):
         step()
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -178,6 +190,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
+    finish()  # the last step's gather + host copy are inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

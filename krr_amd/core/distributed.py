@@ -82,14 +82,32 @@ def record_counts(n_local: int, device, group=None) -> list[int]:
     return [int(c.item()) for c in counts]
 
 
-def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None) -> Optional[object]:
+class PendingGather:
+    """An in-flight ``gather_records(..., async_op=True)``: ``wait()`` makes the
+    current stream wait for the collective and returns what the blocking call would."""
+
+    def __init__(self, work, bufs, counts):
+        self._work, self._bufs, self._counts = work, bufs, counts
+
+    def wait(self):
+        import torch
+
+        self._work.wait()
+        if self._bufs is None:
+            return None
+        return torch.cat([b[:c] for b, c in zip(self._bufs, self._counts)], dim=0)
+
+
+def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None, async_op: bool = False):
     """Gather every rank's [n_r, 4] records to rank `dst`, concatenated in rank order.
 
     Ranks may hold different n_r: counts are exchanged first (``record_counts``,
     one all_gather of a single int64 and a host sync — pass ``counts`` to reuse
     them when the shard sizes do not change between calls), shards are padded to
     the max, gathered in ONE collective, and trimmed on dst.  Returns the
-    [sum n_r, 4] tensor on dst, None elsewhere.
+    [sum n_r, 4] tensor on dst, None elsewhere — or, with ``async_op``, a
+    PendingGather whose ``wait()`` returns it (``local`` is copied before the
+    collective starts, so the caller may overwrite it at once).
     """
     import torch
     import torch.distributed as dist
@@ -103,9 +121,11 @@ def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = Non
     padded = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
     if local.shape[0]:
         padded[: local.shape[0]] = local
-    if rank == dst:
-        bufs = [torch.empty_like(padded) for _ in range(world)]
-        dist.gather(padded, gather_list=bufs, dst=dst, group=group)
-        return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
-    dist.gather(padded, gather_list=None, dst=dst, group=group)
-    return None
+    bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+    work = dist.gather(padded, gather_list=bufs, dst=dst, group=group, async_op=async_op)
+    pending = PendingGather(work, bufs, counts) if async_op else None
+    if async_op:
+        return pending
+    if bufs is None:
+        return None
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)

@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from krr_amd.core.distributed import gather_records, pack_records, shard_bounds, unpack_records
+from krr_amd.core.distributed import gather_records, pack_records, record_counts, shard_bounds, unpack_records
 from oracle import oracle
 
 
@@ -60,10 +60,17 @@ def _worker(rank, world, port, q):
         lo, hi = shard_bounds(np.diff(offs), world)[rank]
         rec = pack_records(_compute(offs, cpu, mem, lo, hi))
         out = gather_records(rec, dst=0)
+        # the pipelined form bench.py uses: counts exchanged once, gather in flight
+        # while the caller already overwrites its record buffer
+        counts = record_counts(rec.shape[0], rec.device)
+        pend = gather_records(rec, dst=0, counts=counts, async_op=True)
+        rec.fill_(-1)
+        out2 = pend.wait()
         if rank == 0:
+            assert torch.equal(out2, out)
             q.put(unpack_records(out))
         else:
-            assert out is None
+            assert out is None and out2 is None
     finally:
         dist.destroy_process_group()
 
