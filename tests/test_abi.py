@@ -71,3 +71,30 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.KrrSeries) == 8 * 5 + 4 * 2
     assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 3
     assert ctypes.sizeof(_native.KrrSketchLoc) == 8 * 5 + 4 * 4 and _native.LOC_WORDS == 7
+
+
+def _declared_host():
+    out = set()
+    for h in ("krr_pack.h", "krr_round.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        out |= set(re.findall(r"^(?:int|int64_t|void|const char\*)\s+(krr_\w+)\(", text, flags=re.M))
+    return out
+
+
+def test_host_headers_match_binding_table_and_exports():
+    """libkrr_host.so (JSON packer + exact rounding) exports exactly what
+    include/krr_pack.h and include/krr_round.h declare."""
+    import __graft_entry__ as g
+
+    g.build()
+    from krr_amd.core import prom_native
+
+    declared = _declared_host()
+    assert declared == set(prom_native.EXPORTED_SYMBOLS)
+    lib = prom_native.load_library()
+    for name in declared:
+        assert hasattr(lib, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", prom_native.LIB_PATH], capture_output=True, text=True)
+    exported = {ln.split()[-1] for ln in nm.stdout.splitlines() if " T " in ln}
+    assert declared <= exported
+    assert {s for s in exported if s.startswith("krr_")} == declared
