@@ -1299,6 +1299,8 @@ struct NanCountProc {
     }
 };
 
+constexpr int kRefBlock = 16;  // 64-slot blocks per REF_INDEX locate step
+
 struct RefArgs {
     const double* vals;
     const int64_t* offs;
@@ -1311,11 +1313,14 @@ struct RefArgs {
 };
 
 // NaN-gapped layout: the k-th PRESENT sample in position order.
+// ONE_SITE: the fused kernel's register budget (KRR_SELECT_WAVES_PER_SIMD) only fits
+// the one-site streaming loop; the standalone kernel uses the depth-2 loop.
+template <bool ONE_SITE>
 __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t s, int lane) {
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         NanCountProc C{0};
-        C.nn -= stream_segment<false>(A.vals, beg, end, C, lane);
+        C.nn -= stream_segment<ONE_SITE>(A.vals, beg, end, C, lane);
         const uint64_t n = (uint64_t)(end - beg) - C.nn;
         double result = bitsd(kQuietNaN);
         uint32_t flags = 0;
@@ -1323,36 +1328,32 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
             flags = KRR_FLAG_EMPTY;
         } else {
             const uint64_t k = (uint64_t)exact_rank((int64_t)n, A.p_num, A.p_den);
+            // walk from the nearer end in blocks of 16 x 64 slots whose loads are all
+            // in flight at once (one HBM round trip per 1,024 slots, not per 64)
+            const bool back = k >= n / 2;
+            const uint64_t want = back ? n - 1 - k : k;  // present samples to skip
+            const int64_t step = back ? -1 : 1;
             uint64_t run = 0;
             uint64_t found = kQuietNaN;
-            if (k >= n / 2) {  // walk back from the end: j-th present from the end
-                const uint64_t j = n - 1 - k;
-                for (int64_t top = end; top > beg; top -= kWave) {
-                    const int64_t i = top - 1 - lane;
-                    const bool in = i >= beg;
-                    const uint64_t u = in ? dbits(A.vals[i]) : kQuietNaN;
-                    const bool p = in && !is_nan_bits(u);
-                    const uint64_t m = ballot(p);
-                    const uint32_t c = popc64(m);
-                    if (run + c > j) {
-                        const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(j - run));
-                        found = lane_bcast64(u, __ffsll((long long)sel) - 1);
-                        break;
-                    }
-                    run += c;
+            bool done = false;
+            for (int64_t pos = back ? end - 1 : beg; !done && (back ? pos >= beg : pos < end);
+                 pos += step * kRefBlock * kWave) {
+                uint64_t u[kRefBlock];
+#pragma unroll
+                for (int b = 0; b < kRefBlock; ++b) {
+                    const int64_t i = pos + step * (b * kWave + lane);
+                    u[b] = (i >= beg && i < end) ? dbits(A.vals[i]) : kQuietNaN;
                 }
-            } else {
-                for (int64_t base = beg; base < end; base += kWave) {
-                    const int64_t i = base + lane;
-                    const bool in = i < end;
-                    const uint64_t u = in ? dbits(A.vals[i]) : kQuietNaN;
-                    const bool p = in && !is_nan_bits(u);
+#pragma unroll
+                for (int b = 0; b < kRefBlock; ++b) {
+                    if (done) break;
+                    const bool p = !is_nan_bits(u[b]);
                     const uint64_t m = ballot(p);
                     const uint32_t c = popc64(m);
-                    if (run + c > k) {
-                        const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(k - run));
-                        found = lane_bcast64(u, __ffsll((long long)sel) - 1);
-                        break;
+                    if (run + c > want) {
+                        const uint64_t sel = ballot(p && lane_prefix(m) == (uint32_t)(want - run));
+                        found = lane_bcast64(u[b], __ffsll((long long)sel) - 1);
+                        done = true;
                     }
                     run += c;
                 }
@@ -1369,7 +1370,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
 }
 
 __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment(A, s, threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment<false>(A, s, threadIdx.x);
 }
 
 // Compact CSR (every slot is a sample, NaN included): X[k] is one gather.
@@ -1482,7 +1483,7 @@ __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? KRR_HSEL_WAVES_PER_SI
         if (b < S_cpu) {
             if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, b, smem, threadIdx.x);
             else if constexpr (CPU_KIND == CPU_HSELECT) hselect_segment(A, b, smem, threadIdx.x);
-            else refindex_gaps_segment(R, b, threadIdx.x);
+            else refindex_gaps_segment<true>(R, b, threadIdx.x);
         } else {
             max_segment<true>(M, b - S_cpu, threadIdx.x);
         }
