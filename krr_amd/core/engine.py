@@ -71,7 +71,10 @@ class SimpleEngine:
         import torch
 
         dev = torch.device("cuda", self.device)
-        vals = torch.from_numpy(np.ascontiguousarray(ps.values, dtype=np.float64)).to(dev, non_blocking=False)
+        host = torch.from_numpy(np.ascontiguousarray(ps.values, dtype=np.float64))
+        # page-locked values (pinned_alloc) go by DMA without blocking the host; the
+        # caller synchronises before the host buffer is released
+        vals = host.to(dev, non_blocking=host.is_pinned())
         offs = torch.from_numpy(np.ascontiguousarray(ps.offsets, dtype=np.int64)).to(dev, non_blocking=False)
         return vals, offs
 
@@ -116,6 +119,14 @@ class SimpleEngine:
             host = {k: v.cpu().numpy() for k, v in out.items()}  # synchronises the stream
         return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"].view(np.uint32),
                           host["mem_value"], host["mem_count"], host["mem_flags"].view(np.uint32))
+
+
+def pinned_alloc(n: int) -> np.ndarray:
+    """float64[n] in page-locked host memory (a numpy view that keeps its torch
+    tensor alive): pass as ``alloc`` to the packers so the H2D copy runs by DMA."""
+    import torch
+
+    return torch.empty(max(int(n), 1), dtype=torch.float64, pin_memory=True).numpy()[: int(n)]
 
 
 _default_engines: dict[int, SimpleEngine] = {}

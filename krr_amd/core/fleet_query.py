@@ -161,12 +161,13 @@ class FleetQueryPlan:
         return [g.query(resource) for g in self.groups]
 
     def pack(self, bodies: Sequence[bytes], *, want_timestamps: bool = False, threads: int = 0,
-             return_pod_counts: bool = False):
+             return_pod_counts: bool = False, alloc=None):
         """bodies[g] = the raw query_range response body of ``queries(resource)[g]``.
 
         Returns a PackedSeries (segment o = object o's pods with data, concatenated
         in K8sObjectData.pods order), plus the timestamps if ``want_timestamps`` and
         the per-(object, pod) sample counts (-1: dropped) if ``return_pod_counts``.
+        ``alloc(n)``: optional allocator of the float64 value array (pinned memory).
         """
         if len(bodies) != len(self.groups):
             raise ValueError(f"expected {len(self.groups)} bodies (one per group query), got {len(bodies)}")
@@ -187,7 +188,7 @@ class FleetQueryPlan:
                 msg = lib.krr_pack_error(h) if h else b""
                 raise PrometheusResponseError(rc, (msg or b"invalid arguments").decode())
             n = int(lib.krr_pack_n_values(h))
-            values = np.empty(n, dtype=np.float64)
+            values = alloc(n) if alloc is not None else np.empty(n, dtype=np.float64)
             offsets = np.empty(no + 1, dtype=np.int64)
             ts = np.empty(n, dtype=np.float64) if want_timestamps else None
             counts = np.empty(max(ns, 1), dtype=np.int64) if return_pod_counts else None
@@ -217,8 +218,10 @@ class FleetQueryPlan:
         n = len(self.groups)
         return {rt: bodies[i * n:(i + 1) * n] for i, rt in enumerate(ResourceType)}
 
-    def pack_fleet(self, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes], threads: int = 0) -> PackedFleet:
-        return PackedFleet(self.pack(cpu_bodies, threads=threads), self.pack(mem_bodies, threads=threads))
+    def pack_fleet(self, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes], threads: int = 0,
+                   alloc=None) -> PackedFleet:
+        return PackedFleet(self.pack(cpu_bodies, threads=threads, alloc=alloc),
+                           self.pack(mem_bodies, threads=threads, alloc=alloc))
 
 
 __all__ = ["FleetQueryPlan", "GroupQuery", "group_query", "pod_query", "pod_regex", "step_string"]

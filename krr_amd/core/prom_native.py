@@ -137,14 +137,17 @@ def parse_series(body: bytes, label: str = "pod", *, want_timestamps: bool = Fal
 
 
 def pack_query_range_bodies(per_object_bodies: Sequence[Sequence[bytes]], *, want_timestamps: bool = False,
-                            threads: int = 0, return_pod_counts: bool = False):
+                            threads: int = 0, return_pod_counts: bool = False, alloc=None):
     """per_object_bodies[o][i] = the raw /api/v1/query_range response body (bytes)
     for pod i of object o (K8sObjectData.pods order), for ONE resource.
 
     Returns a PackedSeries (segment o = object o's kept pods concatenated), plus
     the timestamps (float64 seconds, same layout) if ``want_timestamps`` and the
     per-pod sample counts (-1 = dropped: empty result) if ``return_pod_counts``.
-    Raises PrometheusResponseError naming the first bad body.
+    Raises PrometheusResponseError naming the first bad body.  ``alloc(n)`` (optional)
+    returns the float64 array the samples are written into — e.g.
+    ``krr_amd.core.engine.pinned_alloc`` for page-locked memory the H2D copy reads
+    by DMA at full PCIe rate.
     """
     lib = load_library()
     flat: list[bytes] = []
@@ -166,7 +169,7 @@ def pack_query_range_bodies(per_object_bodies: Sequence[Sequence[bytes]], *, wan
             msg = lib.krr_pack_error(h) if h else b""
             raise PrometheusResponseError(rc, (msg or b"invalid arguments").decode())
         n = int(lib.krr_pack_n_values(h))
-        values = np.empty(n, dtype=np.float64)
+        values = alloc(n) if alloc is not None else np.empty(n, dtype=np.float64)
         offsets = np.empty(n_obj + 1, dtype=np.int64)
         ts = np.empty(n, dtype=np.float64) if want_timestamps else None
         counts = np.empty(max(nb, 1), dtype=np.int64) if return_pod_counts else None

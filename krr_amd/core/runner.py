@@ -79,8 +79,9 @@ class BatchedRunner:
 
         if len(cpu_bodies) != len(mem_bodies):
             raise ValueError("cpu and memory bodies need one entry per object each")
-        fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads),
-                            pack_query_range_bodies(mem_bodies, threads=threads))
+        alloc = _pinned_alloc_or_none()
+        fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
+                            pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
         return self.recommend_packed(fleet)
 
     def recommend_from_grouped(self, plan, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes],
@@ -88,7 +89,8 @@ class BatchedRunner:
         """As recommend_from_bodies, from fleet-batched responses: ``plan`` is a
         krr_amd.core.fleet_query.FleetQueryPlan and bodies[g] answers its g-th grouped
         ``sum by (pod)`` query (one per (namespace, container), not one per pod)."""
-        return self.recommend_packed(plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads))
+        return self.recommend_packed(plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads,
+                                                     alloc=_pinned_alloc_or_none()))
 
     def allocations(self, objects: Sequence[K8sObjectData],
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:
@@ -118,6 +120,20 @@ class BatchedRunner:
         histories = await self.gather_histories(objects, loader)
         # the kernel pass runs off the event loop, like the reference's to_thread (runner.py:106)
         return await asyncio.to_thread(self.allocations, objects, histories)
+
+
+def _pinned_alloc_or_none():
+    """Page-locked packer output when a HIP device is present (the kernels need one anyway)."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            from krr_amd.core.engine import pinned_alloc
+
+            return pinned_alloc
+    except ImportError:  # pragma: no cover
+        pass
+    return None
 
 
 def to_allocations(result: RunResult) -> ResourceAllocations:
