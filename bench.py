@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--sketch-bits", type=int, default=5, help="config 5: log-linear bins per octave = 2^bits")
     ap.add_argument("--sketch-only", action="store_true",
                     help="config 5: stop at the sketch answer (approximate) instead of the exact refinement")
+    ap.add_argument("--c5-refine", action="store_true",
+                    help="config 5 at N=1: run the time-sharded sketch + exact-refinement path instead of the "
+                         "direct single-window select (N>1 always uses it)")
     ap.add_argument("--error-sample", type=int, default=256, help="config 5: series checked against the exact path")
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
@@ -379,7 +382,14 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     cfg = sketch.SketchConfig(mantissa_bits=args.sketch_bits)
     params = percentile_params(Decimal(args.percentile), params_mode(args))
     exact = not args.sketch_only
+    # N = 1 holds every series whole: the exact answer is ONE single-window select pass;
+    # time sharding (sketch merge + refinement) is what N > 1 needs (or --c5-refine)
+    direct = exact and world == 1 and not args.c5_refine
     stream = torch.cuda.current_stream()
+    dres = None
+    if direct:
+        dres = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+                (("value", torch.float64), ("count", torch.int64), ("flags", torch.int32))}
     if world > 1:  # owner blocks are fixed: exchange the record counts once
         blk = sketch.owner_blocks(S, world)[rank]
         counts = record_counts(blk[1] - blk[0], coll_dev)
@@ -391,6 +401,15 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
+        if direct:
+            ctx.segmented_percentile(ser, params, dres["value"], dres["count"], dres["flags"], stream)
+            if ev is not None:
+                ev[1].record(stream)
+            rec = torch.stack([dres["value"].view(torch.int64),
+                               dres["count"] | (dres["flags"].to(torch.int64) << 48),
+                               torch.zeros_like(dres["count"]), torch.zeros_like(dres["count"])], dim=1)
+            host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+            return
         sk = sketch.build(ctx, ser, cfg, stream)
         if ev is not None:
             ev[1].record(stream)
@@ -429,8 +448,12 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     N = S * Lr
     kbytes = 8 * N + 8 * (S + 1) + S * (4 * cfg.width + 8 + 8 + 4)
-    kernels_ms = {"k_sketch_build": kms}
-    if exact:
+    kname = "k_sketch_build"
+    if direct:
+        kname = "k_select"
+        kbytes = 8 * N + 8 * (S + 1) + 20 * S
+    kernels_ms = {kname: kms}
+    if exact and not direct:
         # collect: every slot read once + locations in, collected samples out
         cms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
         kernels_ms["k_sketch_collect"] = cms
@@ -449,27 +472,30 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         "dtype": "f64",
         "data": "synthetic (device counter-hash: CPU ~ Gamma(2, 0.05) cores), generated per time slice",
         "config": {
-            "workload": f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
-                        f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave"
-                        + (" + exact refinement (collect + select in the located bins)" if exact else ""),
+            "workload": (f"config5: {S} CPU series x {T} samples (30d@15s) on one GPU: exact single-window "
+                         f"select, one pass (no time sharding at N=1)") if direct else
+                        (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
+                         f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave"
+                         + (" + exact refinement (collect + select in the located bins)" if exact else "")),
             "percentile_mode": params_mode(args), "cpu_percentile": args.percentile,
             "series": S, "slots_per_rank": N,
-            "parallelism": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
+            "parallelism": "single GPU, whole series" if direct else
+                           f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
         },
         "samples_per_s": S * T / step_s,
         "kernels_ms": kernels_ms,
-        "roofline": {"kernel": "k_sketch_build", "bound": "hbm", "achieved": kbytes / (kms * 1e-3) / 1e9,
+        "roofline": {"kernel": kname, "bound": "hbm", "achieved": kbytes / (kms * 1e-3) / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kbytes / (kms * 1e-3) / HBM_PEAK,
                      "traffic": None, "algorithmic_bytes_per_launch": kbytes},
     }
-    if exact:
+    if exact and not direct:
         result["roofline_collect"] = {"kernel": "k_sketch_collect", "bound": "hbm",
                                       "achieved": cbytes / (cms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                                       "frac": cbytes / (cms * 1e-3) / HBM_PEAK, "algorithmic_bytes_per_launch": cbytes}
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
-        key = f"config5:{params_mode(args)}:p{args.percentile}:k_sketch_build"
+        key = f"config5:{params_mode(args)}:p{args.percentile}:{kname}"
         if key in tr and int(tr[key].get("containers_per_rank", -1)) == S:
             result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
             result["roofline"]["traffic_source"] = tr[key].get("source")

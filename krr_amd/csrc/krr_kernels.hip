@@ -2183,7 +2183,7 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     if (rc) return rc;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = need > kSingleCapMax;  // every segment of the launch through hselect
+    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax);  // every segment through hselect
     const uint32_t cap = hsel ? 0u : need;
     *A = SelectArgs{};
     A->vals = series->values;

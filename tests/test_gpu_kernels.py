@@ -260,3 +260,26 @@ def test_maxlen_autodetect(ctx):
     got = _run_gpu(ctx, vals, offs, "linear", 99, 1, maxlen=0)
     want = _oracle(vals, offs, "linear", 99, 1)
     _assert_same(got, want, "linear", "autodetect")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_long_series_single_pass_large_buffer(ctx, mode):
+    """30d@15s series (172,800 slots) at p99 keep 1,730 keys: the single pass with the
+    larger (2,560-key) buffer, not hselect.  Adversarial orders included: increasing
+    (every sample a candidate), decreasing, constant, two values, gapped, signed zeros."""
+    rng = np.random.default_rng(31)
+    L = 172_800
+    segs = [rng.gamma(2.0, 0.05, L), np.arange(L, dtype=np.float64), np.arange(L, dtype=np.float64)[::-1].copy(),
+            np.full(L, 0.5), np.where(rng.random(L) < 0.995, 1.0, 2.0)]
+    g = rng.gamma(2.0, 0.05, L)
+    g[rng.random(L) < 0.3] = np.nan
+    segs.append(g)
+    z = rng.normal(size=L)
+    z[rng.random(L) < 0.5] = -0.0
+    segs.append(z)
+    vals = np.concatenate(segs)
+    offs = (np.arange(len(segs) + 1) * L).astype(np.int64)
+    for p_num, p_den in ((99, 1), (995, 10), (97, 1)):
+        got = _run_gpu(ctx, vals, offs, mode, p_num, p_den, gaps=True)
+        want = _oracle(vals, offs, mode, p_num, p_den, gaps=True)
+        _assert_same(got, want, mode, f"long single pass {mode} p{p_num}/{p_den}")
