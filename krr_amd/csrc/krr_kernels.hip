@@ -61,6 +61,22 @@ enum { D_TOTAL, D_COMPACT, D_FINAL, D_NCOMPACT, D_NFALLBACK, D_ACTIVE_SLOTS, D_I
     } while (0)
 #endif
 
+#ifndef KRR_XCD_REMAP
+#define KRR_XCD_REMAP 1  // per-XCD contiguous segment ranges (0: block i -> segment i)
+#endif
+// Workgroups are dispatched round-robin over the 8 XCDs (block i on XCD i % 8),
+// so block i -> segment i leaves every XCD's L2 fetching a fresh offsets line
+// per segment start.  Remap so that the blocks of one XCD (i, i+8, i+16, …)
+// walk one contiguous eighth of the items: their offsets (and result records)
+// share L2 lines.  A bijection of [0, n): the n % 8 trailing items map to
+// themselves.
+__device__ __forceinline__ int64_t xcd_item(int64_t i, int64_t n) {
+    if constexpr (!KRR_XCD_REMAP) return i;
+    const int64_t q = n >> 3;
+    if (i >= (q << 3)) return i;
+    return (i & 7) * q + (i >> 3);
+}
+
 // ---------------------------------------------------------------------------
 // Streaming skeleton.  One wave walks values[beg, end): the 16-byte aligned
 // body in chunks of kUnroll x 16 B per lane (8 KiB per wave), the next chunk
@@ -1285,8 +1301,8 @@ template <bool HSEL>
 __global__ __launch_bounds__(64, HSEL ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        if constexpr (HSEL) hselect_segment(A, s, smem, threadIdx.x);
-        else select_segment(A, s, smem, threadIdx.x);
+        if constexpr (HSEL) hselect_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
+        else select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
     }
 }
 
@@ -1370,7 +1386,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
 }
 
 __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment<false>(A, s, threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment<false>(A, xcd_item(s, A.S), threadIdx.x);
 }
 
 // Compact CSR (every slot is a sample, NaN included): X[k] is one gather.
@@ -1463,7 +1479,7 @@ __device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lan
 }
 
 __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) max_segment<false>(A, s, threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) max_segment<false>(A, xcd_item(s, A.S), threadIdx.x);
 }
 
 // ------------------------------ FUSED --------------------------------------
@@ -1480,12 +1496,15 @@ __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? KRR_HSEL_WAVES_PER_SI
     const int64_t S_cpu = CPU_KIND == CPU_REF_GAPS ? R.S : A.S;
     const int64_t total = S_cpu + M.S;
     for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+        // remap within each resource's half, so the CPU items still all precede
+        // the memory items in dispatch order
         if (b < S_cpu) {
-            if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, b, smem, threadIdx.x);
-            else if constexpr (CPU_KIND == CPU_HSELECT) hselect_segment(A, b, smem, threadIdx.x);
-            else refindex_gaps_segment<true>(R, b, threadIdx.x);
+            const int64_t s = xcd_item(b, S_cpu);
+            if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, s, smem, threadIdx.x);
+            else if constexpr (CPU_KIND == CPU_HSELECT) hselect_segment(A, s, smem, threadIdx.x);
+            else refindex_gaps_segment<true>(R, s, threadIdx.x);
         } else {
-            max_segment<true>(M, b - S_cpu, threadIdx.x);
+            max_segment<true>(M, xcd_item(b - S_cpu, M.S), threadIdx.x);
         }
     }
 }
