@@ -1,6 +1,8 @@
 #!/bin/bash
+# final-evidence pass: PMC traffic of the default bench kernel, then the bench line under rocprofv3 stats
 set -o pipefail
-mkdir -p gpurun_out/t
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t/t.log 2>&1 || { tail -30 gpurun_out/t/t.log; exit 1; }
-tail -1 gpurun_out/t/t.log
-bash scripts/gpu_refresh.sh "$1"
+TAG=$1
+bash scripts/pmc_fetch.sh "fetch_config2_linear_$TAG" || exit 1
+python scripts/pmc_traffic.py "gpurun_out/pmc_fetch_config2_linear_$TAG" "config2:linear:p99:k_simple" 10000 || exit 1
+cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
+bash scripts/gpu_refresh.sh "$TAG"
