@@ -41,6 +41,9 @@ HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SLOTS_7D = 10080
 
 
+_JSON_OUT = sys.stdout
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,6 +68,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="two launches (percentile, max) instead of the fused one")
+    ap.add_argument("--gather", choices=("pipelined", "blocking"), default="pipelined",
+                    help="N > 1 records path: pipelined = step k's gather overlaps step k+1's kernel; "
+                         "blocking = gather + host copy right after each kernel")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 path (process group + pipelined RCCL gather) even with one rank (testing)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -92,6 +100,12 @@ def workload(cfg: int, rank: int, world: int, override: int, pods: int = 5):
 
 def main():
     args = parse()
+    # Native libraries (RCCL's version banner, gloo's peer messages) write to fd 1:
+    # point fd 1 at stderr and keep the real stdout for the ONE JSON line.
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -102,6 +116,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --force-dist: run the N > 1 code path (process group, pipelined gather) even at
+    # one rank, so the RCCL path is exercised on a one-GPU box
+    dist_on = world > 1 or args.force_dist
     if os.environ.get("KRR_BENCH_BACKEND", "nccl") != "nccl":
         local %= max(torch.cuda.device_count(), 1)  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
@@ -109,7 +126,7 @@ def main():
     # RCCL ("nccl") over xGMI in production; KRR_BENCH_BACKEND=gloo rehearses the
     # N>1 path with several ranks on ONE GPU (RCCL refuses duplicate devices).
     backend = os.environ.get("KRR_BENCH_BACKEND", "nccl")
-    if world > 1:
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -147,7 +164,7 @@ def main():
     # records go to the host on the compute stream: a copy stream overlapping the
     # next step's kernel was measured to gain nothing (the blit slows the kernel)
     dev_rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
-    counts = record_counts(S, coll_dev) if world > 1 else None  # shard sizes are fixed: exchange once
+    counts = record_counts(S, coll_dev) if dist_on else None  # shard sizes are fixed: exchange once
 
     def step(events=None):
         if events is not None:
@@ -165,12 +182,16 @@ def main():
             ctx.simple_run(cs, ms, params, out, stream, records=dev_rec)
             if events is not None:
                 events[1].record(stream)
-        if world == 1:
+        if not dist_on:
             host_rec.copy_(dev_rec, non_blocking=True)
             return
         # N > 1: this step's gather stays in flight (RCCL stream) while the next
         # step's kernel runs; it is waited for one step later (and by finish())
         pend = gather_records(dev_rec.to(coll_dev), dst=0, counts=counts, async_op=True)
+        if args.gather == "blocking":  # no overlap: the step ends with its own gather
+            inflight.append(pend)
+            finish()
+            return
         finish()
         inflight.append(pend)
 
@@ -186,7 +207,7 @@ def main():
         step()
     finish()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     torch.cuda.synchronize()
@@ -195,11 +216,11 @@ def main():
         step(evs[k])
     finish()  # the last step's gather + host copy are inside the timed region
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
     dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())
     k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
@@ -333,8 +354,8 @@ def main():
             "source": "BASELINE.md (SimpleStrategy.run + _format_result, config 1)"}
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
+        print(json.dumps(result), file=_JSON_OUT, flush=True)
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
@@ -566,7 +587,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                 "value": cs / (tb - ta), "unit": "cpu-series/s (exact)", "cores": threads, "kind": "port",
                 "sample": f"first {cs} series ({cs * Lr} samples) copied D2H; oracle/krr_oracle.c exact "
                           f"{args.mode}, OpenMP {threads} threads on {_cpu_model()}"}
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_JSON_OUT, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -86,28 +86,41 @@ class PendingGather:
     """An in-flight ``gather_records(..., async_op=True)``: ``wait()`` makes the
     current stream wait for the collective and returns what the blocking call would."""
 
-    def __init__(self, work, bufs, counts):
-        self._work, self._bufs, self._counts = work, bufs, counts
+    def __init__(self, work, flat, counts):
+        self._work, self._flat, self._counts = work, flat, counts
 
     def wait(self):
-        import torch
-
         self._work.wait()
-        if self._bufs is None:
-            return None
-        return torch.cat([b[:c] for b, c in zip(self._bufs, self._counts)], dim=0)
+        return _assemble(self._flat, self._counts)
 
 
-def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None, async_op: bool = False):
+def _assemble(flat, counts):
+    """[world * width, 4] receive buffer -> the [sum n_r, 4] fleet (a view when no rank is padded)."""
+    if flat is None:
+        return None
+    import torch
+
+    width = flat.shape[0] // max(len(counts), 1)
+    if all(c == width for c in counts):
+        return flat
+    return torch.cat([flat[r * width: r * width + c] for r, c in enumerate(counts)], dim=0)
+
+
+def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None, async_op: bool = False,
+                   copy_local: bool = True):
     """Gather every rank's [n_r, 4] records to rank `dst`, concatenated in rank order.
 
     Ranks may hold different n_r: counts are exchanged first (``record_counts``,
     one all_gather of a single int64 and a host sync — pass ``counts`` to reuse
     them when the shard sizes do not change between calls), shards are padded to
-    the max, gathered in ONE collective, and trimmed on dst.  Returns the
-    [sum n_r, 4] tensor on dst, None elsewhere — or, with ``async_op``, a
-    PendingGather whose ``wait()`` returns it (``local`` is copied before the
-    collective starts, so the caller may overwrite it at once).
+    the max, gathered in ONE collective into one contiguous [world * max, 4]
+    buffer on dst, and trimmed there (no copy when no rank is padded).  Returns
+    the [sum n_r, 4] tensor on dst, None elsewhere — or, with ``async_op``, a
+    PendingGather whose ``wait()`` returns it.  By default ``local`` is copied
+    before the collective starts, so the caller may overwrite it at once; with
+    ``copy_local=False`` an unpadded shard is sent straight from ``local``, which
+    the caller must then leave untouched until ``wait()`` (bench.py alternates
+    two record buffers).
     """
     import torch
     import torch.distributed as dist
@@ -118,14 +131,15 @@ def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = Non
     if counts is None:
         counts = record_counts(local.shape[0], dev, group)
     width = max(max(counts), 1)
-    padded = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
-    if local.shape[0]:
-        padded[: local.shape[0]] = local
-    bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
-    work = dist.gather(padded, gather_list=bufs, dst=dst, group=group, async_op=async_op)
-    pending = PendingGather(work, bufs, counts) if async_op else None
+    if not copy_local and local.shape[0] == width and local.is_contiguous():
+        send = local
+    else:
+        send = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
+        if local.shape[0]:
+            send[: local.shape[0]] = local
+    flat = torch.empty((world * width, RECORD_WORDS), dtype=torch.int64, device=dev) if rank == dst else None
+    bufs = [flat[r * width:(r + 1) * width] for r in range(world)] if flat is not None else None
+    work = dist.gather(send, gather_list=bufs, dst=dst, group=group, async_op=async_op)
     if async_op:
-        return pending
-    if bufs is None:
-        return None
-    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+        return PendingGather(work, flat, counts)
+    return _assemble(flat, counts)

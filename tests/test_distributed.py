@@ -66,11 +66,22 @@ def _worker(rank, world, port, q):
         pend = gather_records(rec, dst=0, counts=counts, async_op=True)
         rec.fill_(-1)
         out2 = pend.wait()
+        # copy_local=False (bench.py's RCCL form with alternating record buffers):
+        # an unpadded shard is sent from the caller's buffer, which stays untouched
+        rec = pack_records(_compute(offs, cpu, mem, lo, hi))
+        out3 = gather_records(rec, dst=0, counts=counts, async_op=True, copy_local=False).wait()
+        # equal shard sizes: the receive buffer itself is the fleet (no trim copy)
+        eq = torch.full((7, 4), rank, dtype=torch.int64)
+        out4 = gather_records(eq, dst=0, counts=[7] * world, async_op=True, copy_local=False).wait()
+        empty = gather_records(eq[:0], dst=0)
         if rank == 0:
-            assert torch.equal(out2, out)
+            assert torch.equal(out2, out) and torch.equal(out3, out)
+            assert out4.shape == (7 * world, 4)
+            assert torch.equal(out4[:, 0], torch.arange(world).repeat_interleave(7))
+            assert empty.shape == (0, 4)
             q.put(unpack_records(out))
         else:
-            assert out is None and out2 is None
+            assert out is None and out2 is None and out3 is None and out4 is None and empty is None
     finally:
         dist.destroy_process_group()
 
