@@ -148,3 +148,67 @@ def test_empty_fleet():
     assert ps.values.size == 0 and list(ps.offsets) == [0]
     ps = pack_query_range_bodies([[], []])
     assert list(ps.offsets) == [0, 0, 0]
+
+
+def _decimal_strings(seed, n):
+    """Value strings over many forms and their rounding edges: shortest reprs and
+    fixed/scientific forms over many magnitudes, random digit strings with up to 25
+    digits and exponents to +-40, leading/trailing zeros, and exact ties between
+    adjacent doubles (integers 2^53 + odd, halfway decimals with many digits)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    mags = np.exp(rng.uniform(np.log(1e-35), np.log(1e35), n))
+    for x in mags:
+        x = float(x)
+        out.append(repr(x))
+        out.append(go_format(x))
+        out.append("%.*f" % (int(rng.integers(0, 26)), x))
+        out.append("%.*e" % (int(rng.integers(0, 22)), x))
+    for _ in range(n):
+        nd = int(rng.integers(1, 26))
+        digits = "".join(str(d) for d in rng.integers(0, 10, nd))
+        dot = int(rng.integers(0, nd + 1))
+        s = digits[:dot] + "." + digits[dot:] if rng.random() < 0.7 else digits
+        if s.startswith("."):
+            s = "0" + s
+        if s.endswith("."):
+            s += "0"
+        if rng.random() < 0.4:
+            s += "e%d" % int(rng.integers(-40, 41))
+        out.append(s)
+    for k in range(1, 400, 2):  # ties: 2^53 + k sits halfway between two doubles
+        out.append(str(2**53 + k))
+        out.append(str((2**53 + k) * 2**6))
+        out.append("%de-3" % (2**53 + k))
+    for x in rng.uniform(0.1, 1e6, 200):  # exact decimal midpoints (many digits -> fallback)
+        x = float(x)
+        out.append(format((Decimal(x) + Decimal(np.nextafter(x, np.inf))) / 2, "f"))
+    out += ["0", "0.0", "000.000", "0e5000", "1e-27", "1e27", "1e-28", "1e28", "9999999999999999999",
+            "99999999999999999999", "0.1000000000000000000000", "123456789012345678.9", "4.9e-324",
+            "2.2250738585072011e-308", "1.7976931348623157e308", "1e309", "1e-400", "0.000012345678901234567"]
+    return out
+
+
+def test_values_are_correctly_rounded():
+    strs = _decimal_strings(11, 3000)
+    signed = strs + ["-" + s for s in strs[::7]] + ["+" + s for s in strs[::11]]
+    b = body([(0.0, s) for s in signed])
+    ps = pack_query_range_bodies([[b]])
+    want = np.array([float(s) for s in signed])
+    bad = np.nonzero(ps.values.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, [signed[i] for i in bad[:10]]
+
+
+def test_timestamps_are_correctly_rounded():
+    import re
+
+    json_num = re.compile(r"-?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?$")
+    strs = [s for s in _decimal_strings(12, 500) if json_num.match(s)]
+    strs += ["-" + s for s in strs[::5]]
+    assert len(strs) > 2000
+    samples = [(float(s), "1") for s in strs]  # JSON numbers: the timestamp path (Reader::num)
+    raw = ",".join("[%s,\"1\"]" % s for s in strs)
+    b = ('{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},"values":[%s]}]}}' % raw).encode()
+    ps, ts = pack_query_range_bodies([[b]], want_timestamps=True)
+    want = np.array([t for t, _ in samples])
+    assert np.array_equal(ts.view(np.uint64), want.view(np.uint64))
