@@ -43,6 +43,15 @@
 #ifndef KRR_HSEL_WAVES_PER_SIMD
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
+#ifndef KRR_HSEL_BAND
+#define KRR_HSEL_BAND 1  // hselect's first pass also collects a probe-estimated key band (0: off)
+#endif
+#ifndef KRR_PROBE_BATCH
+#define KRR_PROBE_BATCH 8  // probe blocks (per 8 lanes) loaded per round trip
+#endif
+#ifndef KRR_HSEL_BAND_MIN
+#define KRR_HSEL_BAND_MIN 16384  // ... for segments of at least this many slots (the probe's fixed cost)
+#endif
 
 namespace krr {
 
@@ -992,12 +1001,17 @@ constexpr uint64_t kKeyPosInf = 0xFFF0000000000000ull;  // okey(+inf)
 constexpr uint64_t kKeyNegZero = 0x7FFFFFFFFFFFFFFFull; // okey(-0)
 constexpr uint64_t kKeyPosZero = 0x8000000000000000ull; // okey(+0)
 
-template <bool FIRST, bool ZSPLIT>
+template <bool FIRST, bool ZSPLIT, bool BAND = false>
 struct HistProc {
     uint32_t* hist;
     uint64_t lo, span;
     uint32_t sh;
     uint32_t below_l, zb_l, z0_l, nan_l, nneg_l;  // per-lane counters
+    // BAND: keys in [blo, blo + bspan] are also appended to bbuf (the first bcap of
+    // them; bcnt counts all), keys below blo counted per lane (+ negative NaNs).
+    uint64_t* bbuf;
+    uint64_t blo, bspan;
+    uint32_t bcnt, bbelow_l;
 
     __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
 #pragma unroll
@@ -1006,6 +1020,17 @@ struct HistProc {
             const uint64_t x = dbits(d);
             const uint64_t key = okey(x);
             below_l += key < lo ? 1u : 0u;  // + negative NaNs (key < okey(-inf)); removed later
+            if (BAND) {
+                // the band lies inside [okey(-inf), okey(+inf)]: no NaN key enters it
+                bbelow_l += key < blo ? 1u : 0u;
+                const bool inb = key - blo <= bspan;
+                const uint64_t m = ballot(inb);
+                if (m) {
+                    const uint32_t at = bcnt + lane_prefix(m);
+                    if (inb && at < kCollectCap) bbuf[at] = key;
+                    bcnt = uni32(bcnt + popc64(m));
+                }
+            }
             if (ZSPLIT) {
                 zb_l += key <= kKeyPosZero ? 1u : 0u;  // negatives, -0, +0 (+ negative NaNs)
                 z0_l += x == 0 ? 1u : 0u;
@@ -1025,17 +1050,23 @@ struct HistProc {
 
 struct HistCounts {
     uint32_t pad, below_l, zb_l, z0_l, nan_l, nneg_l;
+    uint32_t bcnt, bbelow_l;  // band (first pass with a band only)
 };
 
-template <bool FIRST, bool ZSPLIT>
+template <bool FIRST, bool ZSPLIT, bool BAND = false>
 __device__ __forceinline__ HistCounts hist_pass(const double* vals, int64_t beg, int64_t end, uint32_t* hist,
-                                                uint64_t lo, uint64_t span, uint32_t sh, int lane) {
-    HistProc<FIRST, ZSPLIT> HP;
+                                                uint64_t lo, uint64_t span, uint32_t sh, int lane,
+                                                uint64_t* bbuf = nullptr, uint64_t blo = 0, uint64_t bspan = 0) {
+    HistProc<FIRST, ZSPLIT, BAND> HP;
     HP.hist = hist;
     HP.lo = lo;
     HP.span = span;
     HP.sh = sh;
     HP.below_l = HP.zb_l = HP.z0_l = HP.nan_l = HP.nneg_l = 0;
+    HP.bbuf = bbuf;
+    HP.blo = blo;
+    HP.bspan = bspan;
+    HP.bcnt = HP.bbelow_l = 0;
     HistCounts hc;
     hc.pad = stream_segment<true>(vals, beg, end, HP, lane);
     hc.below_l = HP.below_l;
@@ -1043,6 +1074,8 @@ __device__ __forceinline__ HistCounts hist_pass(const double* vals, int64_t beg,
     hc.z0_l = HP.z0_l;
     hc.nan_l = HP.nan_l;
     hc.nneg_l = HP.nneg_l;
+    hc.bcnt = HP.bcnt;
+    hc.bbelow_l = HP.bbelow_l;
     return hc;
 }
 
@@ -1114,6 +1147,70 @@ struct RankLoc {
     uint32_t exact;
 };
 
+// hselect's band (KRR_HSEL_BAND): 2,048 samples from 128 evenly spread 128-B blocks
+// (16 KiB: 4% of a 50,400-slot segment) are ranked in LDS, and the keys around the
+// needed ranks' estimated position among them, sized to ~3/4 of the collect buffer,
+// become [blo, bhi].  The first streaming pass then collects that band beside its
+// histogram; when the exact counts show both ranks inside it, the segment is done in
+// one HBM pass.  Otherwise nothing changes: the pass's histogram drives the usual
+// collect pass.  Returns false when the segment is too short or too long for a band.
+constexpr int kProbeBlocks = 128;
+constexpr int kProbeSamples = kProbeBlocks * 16;
+
+__device__ __forceinline__ bool hselect_band(const SelectArgs& A, int64_t beg, int64_t L, unsigned char* smem,
+                                             int lane, uint64_t& blo, uint64_t& bhi) {
+    static_assert(KRR_HSEL_BAND_MIN >= 2 * kProbeSamples, "probe blocks must not overlap");
+    if (L < KRR_HSEL_BAND_MIN || !(A.q >= 0.0 && A.q <= 1.0)) return false;
+    // sample ranks one band may span: ~0.75 * kCollectCap keys, L / kProbeSamples keys per sample
+    const int64_t width = ((int64_t)kCollectCap * 3 * kProbeSamples) / (4 * L);
+    const int64_t delta = width / 2 - 1;
+    if (delta < 2) return false;
+    uint64_t* pbuf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);  // hist + collect area
+    static_assert(kProbeSamples * 8 <= kHselectLds, "probe keys fit hselect's LDS");
+    // KRR_PROBE_BATCH blocks' loads in flight at a time (registers: 2 doubles per block)
+    const int64_t sub = (lane & 7) * 2;
+    uint32_t cnt = 0;
+#pragma unroll 1
+    for (int it0 = 0; it0 < kProbeBlocks / 8; it0 += KRR_PROBE_BATCH) {
+        double v[2 * KRR_PROBE_BATCH];
+#pragma unroll
+        for (int it = 0; it < KRR_PROBE_BATCH; ++it) {
+            const int64_t b = (it0 + it) * 8 + (lane >> 3);
+            const int64_t i = beg + (b * (L - 16)) / (kProbeBlocks - 1) + sub;
+            v[2 * it] = A.vals[i];
+            v[2 * it + 1] = A.vals[i + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * KRR_PROBE_BATCH; ++j) {
+            const bool ok = !__builtin_isnan(v[j]);
+            const uint64_t m = ballot(ok);
+            if (ok) pbuf[cnt + lane_prefix(m)] = okey(dbits(v[j]));
+            cnt = uni32(cnt + popc64(m));
+        }
+    }
+    __syncthreads();
+    if (cnt < kProbeSamples / 8) return false;  // mostly gaps: no estimate worth a band
+    SelectProc P;
+    P.buf = pbuf;
+    P.H = reinterpret_cast<uint32_t*>(smem);
+    P.small = reinterpret_cast<uint64_t*>(smem + 1024);
+    P.lane = lane;
+    P.cnt = cnt;
+    P.bad = 0;
+    uint64_t mn, mx;
+    P.buf_minmax(mn, mx);
+    const int64_t rho = (int64_t)floor(A.q * (double)(cnt - 1));
+    const int64_t alo = rho - delta, ahi = rho + 1 + delta;  // ascending sample ranks
+    // R-th largest (1-based) of cnt keys = ascending rank cnt - R
+    blo = alo <= 0 ? kKeyNegInf : P.kth_largest((uint32_t)((int64_t)cnt - alo), mn, mx);
+    bhi = ahi >= (int64_t)cnt - 1 ? kKeyPosInf : P.kth_largest((uint32_t)((int64_t)cnt - ahi), mn, mx);
+    __syncthreads();
+    if (P.bad) return false;
+    blo = blo < kKeyNegInf ? kKeyNegInf : blo;
+    bhi = bhi > kKeyPosInf ? kKeyPosInf : bhi;
+    return blo <= bhi;
+}
+
 __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
@@ -1151,6 +1248,8 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
         loc0.lo = loc0.hi = loc1.lo = loc1.hi = 0;
         loc0.exact = loc1.exact = 0;
         uint32_t done = 0;
+        uint64_t blo = 0, bhi = 0;
+        const bool band = KRR_HSEL_BAND && hselect_band(A, beg, L, smem, lane, blo, bhi);
 #pragma unroll 1
         for (int pass = 0; pass < 10 && !done; ++pass) {
             // ---- histogram pass over [lo, hi]
@@ -1161,7 +1260,12 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
             __syncthreads();
             const uint32_t zsplit = lo > kKeyPosZero ? 1u : 0u;
             HistCounts HP;
-            if (pass == 0) {
+            if (pass == 0 && band) {
+                if (zsplit)
+                    HP = hist_pass<true, true, true>(A.vals, beg, end, hist, lo, span, sh, lane, cbuf, blo, bhi - blo);
+                else
+                    HP = hist_pass<true, false, true>(A.vals, beg, end, hist, lo, span, sh, lane, cbuf, blo, bhi - blo);
+            } else if (pass == 0) {
                 if (zsplit) HP = hist_pass<true, true>(A.vals, beg, end, hist, lo, span, sh, lane);
                 else HP = hist_pass<true, false>(A.vals, beg, end, hist, lo, span, sh, lane);
             } else {
@@ -1183,6 +1287,27 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
                     break;
                 }
                 R = ranks_for(A, n);
+                if (band && HP.bcnt <= kCollectCap) {
+                    // both ranks inside the collected band: select there, one HBM pass in all
+                    const uint64_t bb = wave_sum_u32(HP.bbelow_l) - nneg;
+                    if (bb <= (uint64_t)R.r0 && (uint64_t)R.r1 < bb + HP.bcnt) {
+                        SelectProc P;
+                        P.buf = cbuf;
+                        P.H = reinterpret_cast<uint32_t*>(smem);
+                        P.small = reinterpret_cast<uint64_t*>(smem + 1024);
+                        P.lane = lane;
+                        P.cnt = HP.bcnt;
+                        P.bad = 0;
+                        uint64_t mn, mx;
+                        P.buf_minmax(mn, mx);
+                        loc0.lo = P.kth_largest((uint32_t)(HP.bcnt - ((uint64_t)R.r0 - bb)), mn, mx);
+                        loc1.lo = R.r1 == R.r0 ? loc0.lo
+                                               : P.kth_largest((uint32_t)(HP.bcnt - ((uint64_t)R.r1 - bb)), mn, mx);
+                        bad |= P.bad;
+                        done = 1;
+                        break;
+                    }
+                }
             }
             const uint64_t below = wave_sum_u32(HP.below_l) - nneg;
             const uint64_t zb = zsplit ? wave_sum_u32(HP.zb_l) - nneg : 0;

@@ -112,7 +112,8 @@ KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L) {
 // hselect LDS after kSelectLdsFixed: histogram + collect buffer.
 constexpr int kHistBits = 11;
 constexpr uint32_t kHistBins = 1u << kHistBits;
-constexpr uint32_t kCollectCap = 1024;
+// 1,280 keys: hselect's LDS (1.5 + 8 + 10 KiB) x 8 waves still fits a CU's 160 KiB.
+constexpr uint32_t kCollectCap = 1280;
 constexpr size_t kHselectLds = (size_t)kHistBins * 4 + (size_t)kCollectCap * 8;
 
 }  // namespace krr

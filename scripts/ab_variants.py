@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--containers", type=int, default=10000)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--pods", type=int, default=5, help="config 2: pods per container")
     a = ap.parse_args()
     import torch
 
@@ -46,7 +47,7 @@ def main():
         libs.append((os.path.basename(path), lib, h))
     n = a.containers
     if a.config == 2:
-        L, pod_len, gaps = 5 * 10080, 10080, True
+        L, pod_len, gaps = a.pods * 10080, 10080, True
         offs_np = np.arange(n + 1, dtype=np.int64) * L
     elif a.config == 4:  # 10,080-sample compact segments (one shard of config 4)
         offs_np = np.arange(n + 1, dtype=np.int64) * 10080

@@ -283,3 +283,60 @@ def test_long_series_single_pass_large_buffer(ctx, mode):
         got = _run_gpu(ctx, vals, offs, mode, p_num, p_den, gaps=True)
         want = _oracle(vals, offs, mode, p_num, p_den, gaps=True)
         _assert_same(got, want, mode, f"long single pass {mode} p{p_num}/{p_den}")
+
+
+def _probe_slots(L):
+    """Slots hselect's band probe reads (KRR_HSEL_BAND): 16 from each of 128 evenly
+    spread blocks."""
+    starts = (np.arange(128, dtype=np.int64) * (L - 16)) // 127
+    return (starts[:, None] + np.arange(16)[None, :]).ravel()
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_hselect_band(ctx, mode):
+    """The one-pass band of hselect: hits, misses in both directions (the probe's blocks
+    unrepresentative of the segment), overflow (a crowded value inside the band), probes
+    that are mostly gaps, and lengths at the band's minimum (16,384 slots)."""
+    rng = np.random.default_rng(91)
+    segs = []
+    for L in (16383, 16384, 20160, 50400, 172800):
+        segs.append(("gamma", L, rng.gamma(2.0, 0.05, size=L), False))
+    L = 50400
+    ps = _probe_slots(L)
+    lo = rng.random(L) + 10.0
+    lo[ps] = rng.random(ps.size)  # the probe sees only small values: the band lies too low
+    segs.append(("probe_low", L, lo, False))
+    hi = rng.random(L)
+    hi[ps] = 1e6 + rng.random(ps.size)  # ... and too high
+    segs.append(("probe_high", L, hi, False))
+    half = rng.random(L)
+    half[ps[: ps.size // 2]] = -1.0  # half the probe below everything: band shifted
+    segs.append(("probe_shifted", L, half, False))
+    crowd = rng.gamma(2.0, 0.05, size=L)
+    crowd[rng.random(L) < 0.3] = np.median(crowd)  # thousands of ties inside the band
+    segs.append(("crowded_band", L, crowd, False))
+    g = rng.gamma(2.0, 0.05, size=L)
+    g[ps] = np.nan  # probe entirely in gaps: no band
+    segs.append(("probe_in_gaps", L, g, True))
+    g2 = rng.gamma(2.0, 0.05, size=L)
+    g2[rng.random(L) < 0.5] = np.nan  # half gaps everywhere: the present count is estimated
+    segs.append(("half_gaps", L, g2, True))
+    sz = rng.normal(size=L)
+    u = rng.random(L)
+    sz[u < 0.3] = 0.0
+    sz[(u >= 0.3) & (u < 0.5)] = -0.0
+    sz[(u >= 0.5) & (u < 0.52)] = np.inf
+    sz[(u >= 0.52) & (u < 0.54)] = -np.inf
+    segs.append(("signed_zero_inf", L, sz, False))
+    for gaps in (False, True):
+        chosen = [(nm, v) for nm, _, v, g_ in segs if g_ == gaps]
+        if not chosen:
+            continue
+        vals = np.concatenate([v for _, v in chosen])
+        offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
+        for pct in [(50, 1), (95, 1), (90, 1), (10, 1), (75, 1), (4999, 100), (1, 1)]:
+            got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
+            want = _oracle(vals, offs, mode, *pct, gaps=gaps)
+            for i, (nm, _) in enumerate(chosen):
+                one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
+                _assert_same(one[0], one[1], mode, f"band {nm} gaps={gaps} {mode} p={pct}")
