@@ -1147,38 +1147,42 @@ struct RankLoc {
     uint32_t exact;
 };
 
-// hselect's band (KRR_HSEL_BAND): 2,048 samples from 128 evenly spread 128-B blocks
-// (16 KiB: 4% of a 50,400-slot segment) are ranked in LDS, and the keys around the
+// hselect's band (KRR_HSEL_BAND): 16 consecutive samples from each of ~L/400 evenly
+// spread blocks (16 to 128 blocks: ~4% of the segment's bytes) are ranked in LDS, and the keys around the
 // needed ranks' estimated position among them, sized to ~3/4 of the collect buffer,
 // become [blo, bhi].  The first streaming pass then collects that band beside its
 // histogram; when the exact counts show both ranks inside it, the segment is done in
 // one HBM pass.  Otherwise nothing changes: the pass's histogram drives the usual
 // collect pass.  Returns false when the segment is too short or too long for a band.
-constexpr int kProbeBlocks = 128;
+constexpr int kProbeBlocks = 128;  // at most; ~L/400 blocks (probe = ~4% of the segment)
 constexpr int kProbeSamples = kProbeBlocks * 16;
 
 __device__ __forceinline__ bool hselect_band(const SelectArgs& A, int64_t beg, int64_t L, unsigned char* smem,
                                              int lane, uint64_t& blo, uint64_t& bhi) {
-    static_assert(KRR_HSEL_BAND_MIN >= 2 * kProbeSamples, "probe blocks must not overlap");
+    static_assert(KRR_HSEL_BAND_MIN >= 16 * 16 * 2, "probe blocks must not overlap");
     if (L < KRR_HSEL_BAND_MIN || !(A.q >= 0.0 && A.q <= 1.0)) return false;
-    // sample ranks one band may span: ~0.75 * kCollectCap keys, L / kProbeSamples keys per sample
-    const int64_t width = ((int64_t)kCollectCap * 3 * kProbeSamples) / (4 * L);
+    int64_t nb = (L / 400) & ~(int64_t)7;
+    nb = nb < 16 ? 16 : (nb > kProbeBlocks ? kProbeBlocks : nb);
+    // sample ranks one band may span: ~0.75 * kCollectCap keys, L / (16 nb) keys per sample
+    const int64_t width = ((int64_t)kCollectCap * 3 * 16 * nb) / (4 * L);
     const int64_t delta = width / 2 - 1;
     if (delta < 2) return false;
     uint64_t* pbuf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);  // hist + collect area
     static_assert(kProbeSamples * 8 <= kHselectLds, "probe keys fit hselect's LDS");
     // KRR_PROBE_BATCH blocks' loads in flight at a time (registers: 2 doubles per block)
     const int64_t sub = (lane & 7) * 2;
+    const int nrounds = (int)(nb / 8);
     uint32_t cnt = 0;
 #pragma unroll 1
-    for (int it0 = 0; it0 < kProbeBlocks / 8; it0 += KRR_PROBE_BATCH) {
+    for (int it0 = 0; it0 < nrounds; it0 += KRR_PROBE_BATCH) {
         double v[2 * KRR_PROBE_BATCH];
 #pragma unroll
         for (int it = 0; it < KRR_PROBE_BATCH; ++it) {
-            const int64_t b = (it0 + it) * 8 + (lane >> 3);
-            const int64_t i = beg + (b * (L - 16)) / (kProbeBlocks - 1) + sub;
-            v[2 * it] = A.vals[i];
-            v[2 * it + 1] = A.vals[i + 1];
+            const bool live = it0 + it < nrounds;  // wave-uniform
+            const int64_t b = live ? (int64_t)(it0 + it) * 8 + (lane >> 3) : 0;  // always a real slot
+            const int64_t i = beg + (b * (L - 16)) / (nb - 1) + sub;
+            v[2 * it] = live ? A.vals[i] : __builtin_nan("");
+            v[2 * it + 1] = live ? A.vals[i + 1] : __builtin_nan("");
         }
 #pragma unroll
         for (int j = 0; j < 2 * KRR_PROBE_BATCH; ++j) {
@@ -1189,7 +1193,7 @@ __device__ __forceinline__ bool hselect_band(const SelectArgs& A, int64_t beg, i
         }
     }
     __syncthreads();
-    if (cnt < kProbeSamples / 8) return false;  // mostly gaps: no estimate worth a band
+    if (cnt < (uint32_t)(2 * nb)) return false;  // mostly gaps: no estimate worth a band
     SelectProc P;
     P.buf = pbuf;
     P.H = reinterpret_cast<uint32_t*>(smem);

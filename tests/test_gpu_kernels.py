@@ -286,9 +286,10 @@ def test_long_series_single_pass_large_buffer(ctx, mode):
 
 
 def _probe_slots(L):
-    """Slots hselect's band probe reads (KRR_HSEL_BAND): 16 from each of 128 evenly
-    spread blocks."""
-    starts = (np.arange(128, dtype=np.int64) * (L - 16)) // 127
+    """Slots hselect's band probe reads (KRR_HSEL_BAND): 16 from each of nb evenly
+    spread blocks, nb = L/400 rounded down to a multiple of 8, within [16, 128]."""
+    nb = min(max((L // 400) & ~7, 16), 128)
+    starts = (np.arange(nb, dtype=np.int64) * (L - 16)) // (nb - 1)
     return (starts[:, None] + np.arange(16)[None, :]).ravel()
 
 
@@ -299,7 +300,7 @@ def test_hselect_band(ctx, mode):
     that are mostly gaps, and lengths at the band's minimum (16,384 slots)."""
     rng = np.random.default_rng(91)
     segs = []
-    for L in (16383, 16384, 20160, 50400, 172800):
+    for L in (4095, 4096, 8191, 16383, 16384, 20160, 50400, 172800):
         segs.append(("gamma", L, rng.gamma(2.0, 0.05, size=L), False))
     L = 50400
     ps = _probe_slots(L)
