@@ -49,6 +49,15 @@
 #ifndef KRR_PROBE_BATCH
 #define KRR_PROBE_BATCH 8  // probe blocks (per 8 lanes) loaded per round trip
 #endif
+#ifndef KRR_SELECT_PROBE
+#define KRR_SELECT_PROBE 1  // single-pass select: probe-estimated start threshold when compactions would pile up (0: off)
+#endif
+#ifndef KRR_PROBE_INLINE
+#define KRR_PROBE_INLINE __forceinline__
+#endif
+#ifndef KRR_PROBE_MIN_COMPACT
+#define KRR_PROBE_MIN_COMPACT 1.0f  // ... when tkeep * ln(L / cap) >= this many buffers' worth of free space
+#endif
 #ifndef KRR_HSEL_BAND_MIN
 #define KRR_HSEL_BAND_MIN 16384  // ... for segments of at least this many slots (the probe's fixed cost)
 #endif
@@ -769,7 +778,54 @@ struct SelectProc {
         const uint32_t idx = (uint32_t)(rr - below - ties);
         return kth_largest(cnt - idx, mn, mx);
     }
+
+    // Speculative start threshold for a long segment whose kept tail is large
+    // (e.g. p95 of 20,160 slots keeps ~1,000 keys: ~T ln(L/cap) inserts and ~5
+    // compactions from thr = lowest).  16 evenly spread blocks of 64 consecutive
+    // slots (1,024 samples, 8 KiB, all loads in flight) are ranked in buf; the
+    // key with ~1.5x the needed tail fraction above it becomes thr.  The buffer
+    // then only takes keys >= thr, which is exact whenever the needed ranks end
+    // up at or above thr; the caller checks that and re-streams from the lowest
+    // key otherwise.  Returns 0 (no speculation) when the probe cannot decide.
+    __device__ KRR_PROBE_INLINE uint64_t probe_threshold(const double* __restrict__ vals, int64_t beg, int64_t L) {
+        constexpr int kBlocks = 16;
+        double v[kBlocks];
+#pragma unroll
+        for (int b = 0; b < kBlocks; ++b) v[b] = vals[beg + ((int64_t)b * (L - kWave)) / (kBlocks - 1) + lane];
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < kBlocks; ++b) {
+            const bool ok = !__builtin_isnan(v[b]);
+            const uint64_t msk = ballot(ok);
+            if (ok) buf[m + lane_prefix(msk)] = okey(dbits(v[b]));
+            m += popc64(msk);
+        }
+        cnt = uni32(m);
+        __syncthreads();
+        // rank (from the top) of the probe key: 1.5x the kept fraction of slots, + 4
+        const uint64_t j = ((uint64_t)m * tkeep * 3 + 2 * (uint64_t)L - 1) / (2 * (uint64_t)L) + 4;
+        uint64_t t = 0;
+        if (m >= (uint32_t)kWave && j < m) {
+            uint64_t mn, mx;
+            buf_minmax(mn, mx);
+            t = kth_largest((uint32_t)j, mn, mx);
+            if (bad) t = 0;
+        }
+        __syncthreads();
+        cnt = 0;
+        bad = 0;
+        return uni64(t);
+    }
 };
+
+// The probe pays when the inserts past a full buffer (~tkeep ln(L/cap), a
+// record-breaking count) would need several compactions of (cap - tkeep - 128)
+// free keys each; for short tails (p99 of a week) it would only add a round trip.
+__device__ __forceinline__ bool select_probe_pays(int64_t L, uint32_t tkeep, uint32_t cap) {
+    if (L < 4 * (int64_t)cap || cap <= tkeep + 128) return false;
+    const float inserts = (float)tkeep * __logf((float)L / (float)cap);
+    return inserts >= KRR_PROBE_MIN_COMPACT * (float)(cap - tkeep - 128);
+}
 
 // Count present, numerically negative samples (x < -0.0) of [beg, end).
 __device__ uint64_t count_negative(const double* __restrict__ vals, int64_t beg, int64_t end, int lane) {
@@ -915,24 +971,42 @@ __device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t
         P.tstop = A.cap - kChunkElems / 2;
         P.flip = sp.bottom ? ~0ull : 0ull;
         P.cnt = 0;
-        P.eqs = 0;
-        P.nnan_lane = 0;
         P.bad = 0;
-        P.set_thr(0, 1u);  // inclusive at the lowest key: every sample is a candidate
 #ifdef KRR_DIAG
         for (int d = 0; d < D_WORDS; ++d) P.diag[d] = 0;
         KRR_DIAG_T0(t_begin);
 #endif
-        const uint32_t pad = stream(P);  // NaN padding slots
-        __syncthreads();
+        uint64_t thr0 = 0;  // inclusive at the lowest key: every sample is a candidate
+#if KRR_SELECT_PROBE
+        if (!sp.bottom && A.cap && select_probe_pays(L, sp.tkeep, A.cap)) thr0 = P.probe_threshold(A.vals, beg, L);
+#endif
+        uint32_t pad;
+        uint64_t nnan, n;
+#pragma unroll 1
+        for (;;) {
+            P.cnt = 0;
+            P.eqs = 0;
+            P.nnan_lane = 0;
+            P.bad = 0;
+            P.set_thr(thr0, 1u);
+            pad = stream(P);  // NaN padding slots
+            __syncthreads();
+            nnan = wave_sum_u32(P.nnan_lane) - pad;
+            n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
+            if (thr0 == 0 || n == 0 || (nnan && !A.gaps)) break;
+            // Speculative start: exact iff the lowest needed rank is held in buf
+            // (ranks below n - cnt - ties lie under thr0); else stream again from
+            // the lowest key.
+            const uint64_t ties = P.incl ? 0u : P.eqs;
+            if (!P.bad && (uint64_t)ranks_for(A, n).r0 >= n - P.cnt - ties) break;
+            thr0 = 0;
+        }
 #ifdef KRR_DIAG
         KRR_DIAG_T0(t_final);
 #endif
         uint64_t bmn = 0, bmx = 0;
         if (P.cnt) P.buf_minmax(bmn, bmx);
 
-        const uint64_t nnan = wave_sum_u32(P.nnan_lane) - pad;
-        const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;  // present samples
         uint32_t flags = 0;
         double result = bitsd(kQuietNaN);
         if (n == 0) {
@@ -980,7 +1054,13 @@ __device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t
 __device__ __forceinline__ void select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
     const int64_t beg = A.offs[s], end = A.offs[s + 1];
     select_segment_with(A, s, smem, lane,
-                        [&](SelectProc& P) { return stream_segment<true>(A.vals, beg, end, P, lane); });
+                        [&](SelectProc& P) {
+                            // opaque bounds: the speculative start's retry loop must not
+                            // hoist the stream's address set-up and keep it live throughout
+                            int64_t b = beg, e = end;
+                            asm volatile("" : "+s"(b), "+s"(e));
+                            return stream_segment<true>(A.vals, b, e, P, lane);
+                        });
 }
 
 // ---------------------------------------------------------------------------

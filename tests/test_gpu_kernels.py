@@ -341,3 +341,64 @@ def test_hselect_band(ctx, mode):
             for i, (nm, _) in enumerate(chosen):
                 one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
                 _assert_same(one[0], one[1], mode, f"band {nm} gaps={gaps} {mode} p={pct}")
+
+
+def _select_probe_slots(L):
+    """Slots the single-pass select's start-threshold probe reads (KRR_SELECT_PROBE):
+    64 consecutive slots from each of 16 evenly spread blocks."""
+    starts = (np.arange(16, dtype=np.int64) * (L - 64)) // 15
+    return (starts[:, None] + np.arange(64)[None, :]).ravel()
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_select_probe_start_threshold(ctx, mode):
+    """Tail percentiles of long segments start the single-pass select at a probe-estimated
+    threshold: hits, a probe that sees only huge values (threshold too high: the segment
+    is streamed again from the lowest key), only tiny values (too low: compactions as
+    before), a crowded value at the threshold, a probe in gaps, signed zeros and infinities,
+    monotone series, and lengths on both sides of the probe's gate."""
+    rng = np.random.default_rng(95)
+    segs = []
+    for L in (6000, 10080, 14000, 15000, 17280, 20160):
+        segs.append(("gamma", L, rng.gamma(2.0, 0.05, size=L), False))
+    L = 20160
+    ps = _select_probe_slots(L)
+    hi = rng.random(L)
+    hi[ps] = 1e6 + rng.random(ps.size)
+    segs.append(("probe_high", L, hi, False))
+    lo = rng.random(L) + 10.0
+    lo[ps] = rng.random(ps.size)
+    segs.append(("probe_low", L, lo, False))
+    crowd = rng.gamma(2.0, 0.05, size=L)
+    crowd[rng.random(L) < 0.2] = np.quantile(crowd, 0.96)
+    segs.append(("crowded_at_thr", L, crowd, False))
+    segs.append(("constant", L, np.full(L, 0.25), False))
+    segs.append(("increasing", L, np.arange(L, dtype=np.float64), False))
+    segs.append(("decreasing", L, np.arange(L, 0, -1, dtype=np.float64), False))
+    sz = rng.normal(size=L)
+    u = rng.random(L)
+    sz[u < 0.3] = 0.0
+    sz[(u >= 0.3) & (u < 0.5)] = -0.0
+    sz[(u >= 0.5) & (u < 0.56)] = np.inf
+    sz[(u >= 0.56) & (u < 0.58)] = -np.inf
+    segs.append(("signed_zero_inf", L, sz, False))
+    g = rng.gamma(2.0, 0.05, size=L)
+    g[ps] = np.nan
+    segs.append(("probe_in_gaps", L, g, True))
+    g2 = rng.gamma(2.0, 0.05, size=L)
+    g2[rng.random(L) < 0.3] = np.nan
+    g2[ps[::3]] = 50.0 + rng.random(ps[::3].size)
+    segs.append(("gaps_probe_high", L, g2, True))
+    g3 = rng.gamma(2.0, 0.05, size=L)
+    g3[rng.random(L) < 0.15] = np.nan
+    segs.append(("gaps", L, g3, True))
+    for gaps in (False, True):
+        chosen = [(nm, v) for nm, _, v, g_ in segs if g_ == gaps]
+        vals = np.concatenate([v for _, v in chosen])
+        offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
+        for pct in [(95, 1), (96, 1), (97, 1), (98, 1), (99, 1), (9499, 100), (5, 1)]:
+            got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
+            want = _oracle(vals, offs, mode, *pct, gaps=gaps)
+            for i, (nm, _) in enumerate(chosen):
+                one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
+                _assert_same(one[0], one[1], mode, f"probe {nm} gaps={gaps} {mode} p={pct}")
