@@ -55,8 +55,11 @@
 #ifndef KRR_PROBE_INLINE
 #define KRR_PROBE_INLINE __forceinline__
 #endif
+#ifndef KRR_PROBE_MARGIN_X4
+#define KRR_PROBE_MARGIN_X4 6  // ... aiming the start threshold at (this / 4) x the kept tail
+#endif
 #ifndef KRR_PROBE_MIN_COMPACT
-#define KRR_PROBE_MIN_COMPACT 1.0f  // ... when tkeep * ln(L / cap) >= this many buffers' worth of free space
+#define KRR_PROBE_MIN_COMPACT 0.25f  // ... when tkeep * ln(L / cap) >= this many buffers' worth of free space
 #endif
 #ifndef KRR_HSEL_BAND_MIN
 #define KRR_HSEL_BAND_MIN 16384  // ... for segments of at least this many slots (the probe's fixed cost)
@@ -802,8 +805,8 @@ struct SelectProc {
         }
         cnt = uni32(m);
         __syncthreads();
-        // rank (from the top) of the probe key: 1.5x the kept fraction of slots, + 4
-        const uint64_t j = ((uint64_t)m * tkeep * 3 + 2 * (uint64_t)L - 1) / (2 * (uint64_t)L) + 4;
+        // rank (from the top) of the probe key: 1.5x (KRR_PROBE_MARGIN_X4 / 4) the kept fraction of slots, + 4
+        const uint64_t j = ((uint64_t)m * tkeep * KRR_PROBE_MARGIN_X4 + 4 * (uint64_t)L - 1) / (4 * (uint64_t)L) + 4;
         uint64_t t = 0;
         if (m >= (uint32_t)kWave && j < m) {
             uint64_t mn, mx;
