@@ -134,9 +134,12 @@ def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = Non
     if not copy_local and local.shape[0] == width and local.is_contiguous():
         send = local
     else:
-        send = torch.zeros((width, RECORD_WORDS), dtype=torch.int64, device=dev)
+        # one copy kernel for an unpadded shard; only the padding rows are zeroed
+        send = torch.empty((width, RECORD_WORDS), dtype=torch.int64, device=dev)
         if local.shape[0]:
             send[: local.shape[0]] = local
+        if local.shape[0] < width:
+            send[local.shape[0]:].zero_()
     flat = torch.empty((world * width, RECORD_WORDS), dtype=torch.int64, device=dev) if rank == dst else None
     bufs = [flat[r * width:(r + 1) * width] for r in range(world)] if flat is not None else None
     work = dist.gather(send, gather_list=bufs, dst=dst, group=group, async_op=async_op)
