@@ -104,9 +104,22 @@ constexpr uint32_t kSingleCapMax = KRR_SINGLE_CAP_MAX;
 #endif
 constexpr uint32_t kSingleCapLong = KRR_SINGLE_CAP_LONG;
 
+// ... and up to this many keys when the longest segment is at least
+// KRR_PROBE_LEN_RATIO x the capacity: the start-threshold probe (krr_kernels.hip,
+// KRR_SELECT_PROBE) keeps such a buffer at ~1.5x the kept tail without
+// compactions.  A/B (profiles/r01/v16/ab_bigcap*.log): config 2 p95 +5%, p97 +12%;
+// launches of mixed lengths (config 3 p90, Lmax / need = 7.5) lose 4%, hence the ratio.
+#ifndef KRR_SINGLE_CAP_PROBE
+#define KRR_SINGLE_CAP_PROBE 3264
+#endif
+#ifndef KRR_PROBE_LEN_RATIO
+#define KRR_PROBE_LEN_RATIO 12
+#endif
+
 KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L) {
     if (need <= kSingleCapMax) return true;
-    return need <= kSingleCapLong && (int64_t)tkeep * 1000 <= (int64_t)KRR_LONG_KEEP_PERMILLE * L;
+    if (need <= kSingleCapLong && (int64_t)tkeep * 1000 <= (int64_t)KRR_LONG_KEEP_PERMILLE * L) return true;
+    return need <= KRR_SINGLE_CAP_PROBE && L >= (int64_t)KRR_PROBE_LEN_RATIO * need;
 }
 
 // hselect LDS after kSelectLdsFixed: histogram + collect buffer.

@@ -402,3 +402,40 @@ def test_select_probe_start_threshold(ctx, mode):
             for i, (nm, _) in enumerate(chosen):
                 one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
                 _assert_same(one[0], one[1], mode, f"probe {nm} gaps={gaps} {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_select_probe_large_buffer(ctx, mode):
+    """Launches whose longest segment is >= 12x the needed capacity run p95-p97 of 7d@1m x 5
+    pods (50,400 slots, ~2,500 kept keys) single-pass with a buffer of up to 3,264 keys behind
+    the start-threshold probe (krr_plan.h single_pass_ok): hits, a probe that sees only huge
+    values (re-stream), only tiny values, gaps, and a short segment sharing the launch."""
+    rng = np.random.default_rng(97)
+    L = 50400
+    ps = _select_probe_slots(L)
+    segs = [("gamma", rng.gamma(2.0, 0.05, size=L), False), ("short", rng.gamma(2.0, 0.05, size=3000), False)]
+    hi = rng.random(L)
+    hi[ps] = 1e6 + rng.random(ps.size)
+    segs.append(("probe_high", hi, False))
+    lo = rng.random(L) + 10.0
+    lo[ps] = rng.random(ps.size)
+    segs.append(("probe_low", lo, False))
+    crowd = rng.gamma(2.0, 0.05, size=L)
+    crowd[rng.random(L) < 0.2] = np.quantile(crowd, 0.955)
+    segs.append(("crowded_at_thr", crowd, False))
+    g = rng.gamma(2.0, 0.05, size=L)
+    g[rng.random(L) < 0.2] = np.nan
+    segs.append(("gaps", g, True))
+    g2 = rng.gamma(2.0, 0.05, size=L)
+    g2[ps] = np.nan
+    segs.append(("probe_in_gaps", g2, True))
+    for gaps in (False, True):
+        chosen = [(nm, v) for nm, v, g_ in segs if g_ == gaps]
+        vals = np.concatenate([v for _, v in chosen])
+        offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
+        for pct in [(95, 1), (96, 1), (97, 1), (9549, 100)]:
+            got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
+            want = _oracle(vals, offs, mode, *pct, gaps=gaps)
+            for i, (nm, _) in enumerate(chosen):
+                one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
+                _assert_same(one[0], one[1], mode, f"probe-large {nm} gaps={gaps} {mode} p={pct}")
