@@ -49,20 +49,17 @@
 #ifndef KRR_PROBE_BATCH
 #define KRR_PROBE_BATCH 8  // probe blocks (per 8 lanes) loaded per round trip
 #endif
+#ifndef KRR_HSEL_BAND_MIN
+#define KRR_HSEL_BAND_MIN 16384  // ... for segments of at least this many slots (the probe's fixed cost)
+#endif
 #ifndef KRR_SELECT_PROBE
 #define KRR_SELECT_PROBE 1  // single-pass select: probe-estimated start threshold when compactions would pile up (0: off)
-#endif
-#ifndef KRR_PROBE_INLINE
-#define KRR_PROBE_INLINE __forceinline__
 #endif
 #ifndef KRR_PROBE_MARGIN_X4
 #define KRR_PROBE_MARGIN_X4 6  // ... aiming the start threshold at (this / 4) x the kept tail
 #endif
 #ifndef KRR_PROBE_MIN_COMPACT
-#define KRR_PROBE_MIN_COMPACT 0.25f  // ... when tkeep * ln(L / cap) >= this many buffers' worth of free space
-#endif
-#ifndef KRR_HSEL_BAND_MIN
-#define KRR_HSEL_BAND_MIN 16384  // ... for segments of at least this many slots (the probe's fixed cost)
+#define KRR_PROBE_MIN_COMPACT 0.25f  // ... when tkeep * ln(L / cap) >= this x (cap - tkeep - 128) free keys
 #endif
 
 namespace krr {
@@ -790,7 +787,7 @@ struct SelectProc {
     // then only takes keys >= thr, which is exact whenever the needed ranks end
     // up at or above thr; the caller checks that and re-streams from the lowest
     // key otherwise.  Returns 0 (no speculation) when the probe cannot decide.
-    __device__ KRR_PROBE_INLINE uint64_t probe_threshold(const double* __restrict__ vals, int64_t beg, int64_t L) {
+    __device__ __forceinline__ uint64_t probe_threshold(const double* __restrict__ vals, int64_t beg, int64_t L) {
         constexpr int kBlocks = 16;
         double v[kBlocks];
 #pragma unroll

@@ -119,7 +119,11 @@ constexpr uint32_t kSingleCapLong = KRR_SINGLE_CAP_LONG;
 KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L) {
     if (need <= kSingleCapMax) return true;
     if (need <= kSingleCapLong && (int64_t)tkeep * 1000 <= (int64_t)KRR_LONG_KEEP_PERMILLE * L) return true;
+#if !defined(KRR_SELECT_PROBE) || KRR_SELECT_PROBE
     return need <= KRR_SINGLE_CAP_PROBE && L >= (int64_t)KRR_PROBE_LEN_RATIO * need;
+#else
+    return false;
+#endif
 }
 
 // hselect LDS after kSelectLdsFixed: histogram + collect buffer.
