@@ -107,10 +107,11 @@ constexpr uint32_t kSingleCapLong = KRR_SINGLE_CAP_LONG;
 // ... and up to this many keys when the longest segment is at least
 // KRR_PROBE_LEN_RATIO x the capacity: the start-threshold probe (krr_kernels.hip,
 // KRR_SELECT_PROBE) keeps such a buffer at ~1.5x the kept tail without
-// compactions.  A/B (profiles/r01/v16/ab_bigcap*.log): config 2 p95 +5%, p97 +12%;
+// compactions.  A/B (profiles/r01/v16/ab_bigcap*.log, v17/ab_cap2.log): config 2 p94 +6%,
+// p95 +5%, p97 +7%; 4,224 keys (p93) loses to hselect;
 // launches of mixed lengths (config 3 p90, Lmax / need = 7.5) lose 4%, hence the ratio.
 #ifndef KRR_SINGLE_CAP_PROBE
-#define KRR_SINGLE_CAP_PROBE 3264
+#define KRR_SINGLE_CAP_PROBE 3712
 #endif
 #ifndef KRR_PROBE_LEN_RATIO
 #define KRR_PROBE_LEN_RATIO 12

@@ -433,7 +433,7 @@ def test_select_probe_large_buffer(ctx, mode):
         chosen = [(nm, v) for nm, v, g_ in segs if g_ == gaps]
         vals = np.concatenate([v for _, v in chosen])
         offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
-        for pct in [(95, 1), (96, 1), (97, 1), (9549, 100)]:
+        for pct in [(94, 1), (95, 1), (96, 1), (97, 1), (9549, 100)]:
             got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
             want = _oracle(vals, offs, mode, *pct, gaps=gaps)
             for i, (nm, _) in enumerate(chosen):
