@@ -1,25 +1,36 @@
 """Throughput bench of the KRR SimpleStrategy hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--mode linear|sorted_lower|ref_index]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--mode linear|sorted_lower|ref_index]
 
 One "step" = one pass of the hot path over the rank's whole synthetic fleet
 shard, inputs resident in HBM: the CPU-percentile kernel over every CPU series,
 the max+count kernel over every memory series, and (N > 1) the RCCL gather of
 the 32-B per-container result records to rank 0, whose D2H copy ends the step.
 
-Workloads (BASELINE.json configs):
+Ranks: one process per GPU.  Under torchrun (WORLD_SIZE set) the world size must
+equal --gpus.  Without it, `--gpus N > 1` makes this process a launcher: it spawns
+N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT)
+before anything touches the GPU, never touches the GPU itself, and exits non-zero
+if any rank fails.  Backend "nccl" (RCCL over xGMI) needs N GPUs;
+KRR_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device).
+
+Workloads (BASELINE.json configs); every container is generated from its GLOBAL
+index, so an N-rank fleet is the N=1 fleet cut into shards (config 4) or extended
+by more containers (weak scaling, configs 2-3):
   2 (default) 10k containers x 5 pods x 10,080 slots (7d@1m) per rank, NaN-gapped dense layout
-  3           100k containers x 1 pod, windows of 1..14 days @1m (1,440-20,160 samples), compact CSR
+  3           100k containers per rank x 1 pod, windows of 1..14 days @1m (1,440-20,160 samples), compact CSR
   4           1M containers x 10,080 samples (7d@1m) split across the ranks, compact CSR
   5           sketch mode: 100k CPU series x 172,800 samples (30d@15s) TIME-sharded across the
               ranks (rank r holds the r-th time slice of every series); per-slice log-linear
               sketches merged by one reduce-scatter, rank error vs the exact path reported
-Data are generated on the device by krr_synth_fill (counter hash; no host packing, no PCIe).
+Data are generated on the device by krr_synth_fill_global (counter hash; no host packing, no PCIe).
 
 Prints ONE JSON line on rank 0 (contract in the task brief): value = containers of ALL
-ranks / max-over-ranks step time; roofline = the CPU-percentile kernel's algorithmic
+ranks / max-over-ranks step time; roofline = the fused kernel's algorithmic
 bytes / its average launch time (HIP events on the launch stream) against 8 TB/s;
-cpu_baseline = the C oracle (OpenMP) on a bounded sample copied from the device.
+cpu_baseline = the C oracle (OpenMP, the lease's cores) on a bounded sample copied from
+the device (N = 1); parity_vs_oracle_on_sample = this run's results (N > 1: the records
+gathered to rank 0) against the oracle on a sample regenerated from every shard.
 """
 from __future__ import annotations
 
@@ -65,8 +76,11 @@ def parse():
                     help="containers in the CPU-baseline / parity sample (0: the whole rank, capped at 1.1e9 slots)")
     ap.add_argument("--numpy-seconds", type=float, default=5.0,
                     help="time budget of the single-thread numpy reference-path baseline")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the lease's cores (affinity set, capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-blocks", type=int, default=4, help="N > 1 parity: sampled blocks per shard")
+    ap.add_argument("--parity-block", type=int, default=128, help="N > 1 parity: containers per sampled block")
     ap.add_argument("--separate", action="store_true", help="two launches (percentile, max) instead of the fused one")
     ap.add_argument("--gather", choices=("pipelined", "blocking"), default="pipelined",
                     help="N > 1 records path: pipelined = step k's gather overlaps step k+1's kernel; "
@@ -77,29 +91,113 @@ def parse():
     return ap.parse_args()
 
 
-def workload(cfg: int, rank: int, world: int, override: int, pods: int = 5):
-    """Per-rank (offsets numpy array, pod_len, gaps, description, containers_total)."""
+def _splitmix(x: np.ndarray) -> np.ndarray:
+    z = (x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15))
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def container_lengths(cfg: int, g0: int, g1: int, pods: int = 5) -> np.ndarray:
+    """Slots per container for GLOBAL container indices [g0, g1) (same on every rank)."""
+    n = max(g1 - g0, 0)
     if cfg == 2:
-        n = override or 10_000
-        L = pods * SLOTS_7D
-        offs = np.arange(n + 1, dtype=np.int64) * L
-        return offs, SLOTS_7D, True, (f"config2: {n} containers/rank x {pods} pods x 10080 slots (7d@1m), "
-                                      f"NaN-gapped dense"), n * world
-    if cfg == 3:
-        n = override or 100_000
-        rng = np.random.default_rng(3 + rank)
-        L = rng.integers(1, 15, size=n) * 1440
-        offs = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
-        return offs, 0, False, f"config3: {n} containers/rank x 1 pod, 1..14 days @1m, compact CSR", n * world
+        return np.full(n, pods * SLOTS_7D, dtype=np.int64)
+    if cfg == 3:  # window uniform over {1..14} days @1m
+        with np.errstate(over="ignore"):
+            h = _splitmix(np.arange(g0, g1, dtype=np.uint64) ^ np.uint64(0xC0F1_6303))
+        return ((h % np.uint64(14)).astype(np.int64) + 1) * 1440
+    return np.full(n, SLOTS_7D, dtype=np.int64)
+
+
+def fleet_shard(cfg: int, rank: int, world: int, override: int) -> tuple[int, int, int]:
+    """(g0, g1, containers_total): the global container range rank `rank` owns."""
+    if cfg in (2, 3):  # weak scaling: a fixed number of containers per rank
+        n = override or (10_000 if cfg == 2 else 100_000)
+        return rank * n, (rank + 1) * n, n * world
     total = override * world if override else 1_000_000
-    lo, hi = (total * rank) // world, (total * (rank + 1)) // world
-    n = hi - lo
-    offs = np.arange(n + 1, dtype=np.int64) * SLOTS_7D
-    return offs, 0, False, f"config4: {total} containers x 10080 samples (7d@1m) over {world} ranks, compact CSR", total
+    from krr_amd.core.distributed import shard_bounds  # equal lengths: contiguous equal cuts
+
+    g0, g1 = shard_bounds(np.full(total, SLOTS_7D, dtype=np.int64), world)[rank]
+    return g0, g1, total
+
+
+def workload(cfg: int, rank: int, world: int, override: int, pods: int = 5):
+    """Per-rank (offsets, pod_len, gaps, description, containers_total, g0)."""
+    g0, g1, total = fleet_shard(cfg, rank, world, override)
+    L = container_lengths(cfg, g0, g1, pods)
+    offs = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+    n = g1 - g0
+    if cfg == 2:
+        return offs, SLOTS_7D, True, (f"config2: {n} containers/rank x {pods} pods x 10080 slots (7d@1m), "
+                                      f"NaN-gapped dense"), total, g0
+    if cfg == 3:
+        return offs, 0, False, f"config3: {n} containers/rank x 1 pod, 1..14 days @1m, compact CSR", total, g0
+    return offs, 0, False, (f"config4: {total} containers x 10080 samples (7d@1m) over {world} ranks, "
+                            f"compact CSR"), total, g0
+
+
+def cpu_lease() -> dict:
+    """Host cores this process may use: the affinity set, capped by OMP_NUM_THREADS when the
+    box sets it (the GPU box leases 16 CPUs per GPU but shows the whole machine's)."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = list(range(os.cpu_count() or 1))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    n = len(aff)
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return {"threads": max(n, 1), "nproc": os.cpu_count(), "affinity_cpus": len(aff),
+            "omp_num_threads": omp or None}
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without torchrun: spawn N ranks (fresh interpreters, nothing here
+    touches the GPU), stream their output through, return the first failing exit code."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    alive = set(range(args.gpus))
+    deadline = None
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py launcher: rank {r} exited with {c}; stopping the others", file=sys.stderr)
+                for q in alive:
+                    procs[q].send_signal(signal.SIGTERM)
+                deadline = time.time() + 20
+        if deadline is not None and time.time() > deadline:
+            for q in alive:
+                procs[q].kill()
+            deadline = None
+        time.sleep(0.1)
+    return rc
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                     f"(launch one rank per GPU: torchrun --nproc-per-node {args.gpus}, or no torchrun)")
+    elif args.gpus > 1:
+        sys.exit(launch_ranks(args))
     # Native libraries (RCCL's version banner, gloo's peer messages) write to fd 1:
     # point fd 1 at stderr and keep the real stdout for the ONE JSON line.
     global _JSON_OUT
@@ -119,8 +217,12 @@ def main():
     # --force-dist: run the N > 1 code path (process group, pipelined gather) even at
     # one rank, so the RCCL path is exercised on a one-GPU box
     dist_on = world > 1 or args.force_dist
+    ndev = torch.cuda.device_count()
     if os.environ.get("KRR_BENCH_BACKEND", "nccl") != "nccl":
-        local %= max(torch.cuda.device_count(), 1)  # rehearsal: several ranks may share a GPU
+        local %= max(ndev, 1)  # rehearsal: several ranks may share a GPU
+    elif local >= ndev:
+        sys.exit(f"bench.py rank {rank}: LOCAL_RANK {local} but only {ndev} GPU(s) visible; RCCL needs one GPU "
+                 f"per rank (KRR_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # RCCL ("nccl") over xGMI in production; KRR_BENCH_BACKEND=gloo rehearses the
@@ -135,7 +237,8 @@ def main():
     if args.config == 5:
         return run_config5(args, world, rank, local, dev, coll_dev)
 
-    offs_np, pod_len, gaps, desc, containers_total = workload(args.config, rank, world, args.containers, args.pods)
+    offs_np, pod_len, gaps, desc, containers_total, g0 = workload(args.config, rank, world, args.containers,
+                                                                   args.pods)
     S = offs_np.size - 1
     N = int(offs_np[-1])
     maxlen = int(np.max(np.diff(offs_np))) if S else 0
@@ -143,9 +246,9 @@ def main():
     offs = torch.from_numpy(offs_np).to(dev)
     cpu = torch.empty(N, dtype=torch.float64, device=dev)
     mem = torch.empty(N, dtype=torch.float64, device=dev)
-    seed = 1000003 * (args.config + 1) + rank
-    ctx.synth_fill(cpu, offs, seed, 0, pod_len, gaps)
-    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, pod_len, gaps)
+    seed = 1000003 * (args.config + 1)  # one fleet: containers are generated from their global index
+    ctx.synth_fill(cpu, offs, seed, 0, pod_len, gaps, seg_base=g0)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, pod_len, gaps, seg_base=g0)
     torch.cuda.synchronize()
 
     params = percentile_params(Decimal(args.percentile), args.mode)
@@ -297,7 +400,8 @@ def main():
         c_host = cpu[:end].cpu().numpy()
         m_host = mem[:end].cpu().numpy()
         o_host = offs_np[: m + 1].copy()
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        lease = cpu_lease()
+        threads = args.cpu_threads or lease["threads"]
         t_a = time.perf_counter()
         ov, on, of = oracle.percentile(c_host, o_host, params.mode, params.p_num, params.p_den, params.q, gaps,
                                        threads)
@@ -323,6 +427,7 @@ def main():
             "kind": "port",
             "sample": f"first {m} containers of this run ({2 * end} slots) copied D2H; oracle/krr_oracle.c "
                       f"{args.mode} + max, OpenMP {threads} threads on {cpu_model or platform.processor()}",
+            "host": {"cpu_model": cpu_model or platform.processor(), **lease},
         }
         result["parity_vs_oracle_on_sample"] = parity
         result["parity_sample_containers"] = m
@@ -353,12 +458,79 @@ def main():
             "value": 492.0, "unit": "container-series/s", "cores": 1,
             "source": "BASELINE.md (SimpleStrategy.run + _format_result, config 1)"}
 
+    if world > 1:
+        result["config"]["backend"] = backend
+        if backend != "nccl":
+            result["config"]["ranks_share_gpus"] = f"{world} ranks on {ndev} GPU(s) (gloo rehearsal)"
+        if rank == 0:
+            result.update(parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed))
     if rank == 0:
         print(json.dumps(result), file=_JSON_OUT, flush=True)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
+
+
+def parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed) -> dict:
+    """N > 1: check the records gathered to rank 0 against a sample regenerated from
+    EVERY shard (blocks of consecutive global containers at the start, inside and at
+    the end of each rank's range): the C oracle on the host, and this GPU's own
+    kernel on the same containers (a shard computed elsewhere must equal it bit for bit)."""
+    import torch
+
+    from krr_amd.core.distributed import unpack_records
+    from oracle import oracle
+
+    threads = args.cpu_threads or cpu_lease()["threads"]
+    gathered = unpack_records(host_rec.numpy())
+    ok_oracle = ok_local = True
+    checked = 0
+    for r in range(world):
+        g0, g1, _ = fleet_shard(args.config, r, world, args.containers)
+        n = g1 - g0
+        b = max(1, min(args.parity_block, n))
+        starts = sorted({g0 + ((n - b) * j) // max(args.parity_blocks - 1, 1) for j in range(args.parity_blocks)})
+        for a in starts:
+            L = container_lengths(args.config, a, a + b, args.pods)
+            offs_np = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+            offs = torch.from_numpy(offs_np).to(dev)
+            N = int(offs_np[-1])
+            cpu = torch.empty(N, dtype=torch.float64, device=dev)
+            mem = torch.empty(N, dtype=torch.float64, device=dev)
+            ctx.synth_fill(cpu, offs, seed, 0, pod_len, gaps, seg_base=a)
+            ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, pod_len, gaps, seg_base=a)
+            out = {k: torch.empty(b, dtype=dt, device=dev) for k, dt in
+                   (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+                    ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+            maxlen = int(L.max())
+            ctx.simple_run(ctx.series(cpu, offs, maxlen, gaps), ctx.series(mem, offs, maxlen, gaps), params, out)
+            c_host, m_host = cpu.cpu().numpy(), mem.cpu().numpy()
+            ov, on, _ = oracle.percentile(c_host, offs_np, params.mode, params.p_num, params.p_den, params.q, gaps,
+                                          threads)
+            mv, mn, _ = oracle.seg_max(m_host, offs_np, gaps, threads)
+            gv = gathered["cpu_value"][a:a + b]
+            same = (gv.view(np.uint64) == ov.view(np.uint64)) | (np.isnan(gv) & np.isnan(ov))
+            if args.mode == "linear":  # the sign of a zero LINEAR result is unspecified
+                same |= (gv == 0) & (ov == 0)
+            ok_oracle &= bool(same.all() and np.array_equal(gathered["cpu_count"][a:a + b], on)
+                              and np.array_equal(gathered["mem_value"][a:a + b], mv, equal_nan=True)
+                              and np.array_equal(gathered["mem_count"][a:a + b], mn))
+            lv = out["cpu_value"].cpu().numpy()
+            ok_local &= bool(np.array_equal(gv.view(np.uint64), lv.view(np.uint64))
+                             and np.array_equal(gathered["mem_value"][a:a + b].view(np.uint64),
+                                                out["mem_value"].cpu().numpy().view(np.uint64))
+                             and np.array_equal(gathered["cpu_count"][a:a + b], out["cpu_count"].cpu().numpy())
+                             and np.array_equal(gathered["mem_count"][a:a + b], out["mem_count"].cpu().numpy())
+                             and np.array_equal(gathered["cpu_flags"][a:a + b],
+                                                out["cpu_flags"].cpu().numpy().view(np.uint32)))
+            checked += b
+            del cpu, mem, offs, out
+    return {"parity_vs_oracle_on_sample": ok_oracle, "parity_gathered_vs_rank0_kernel": ok_local,
+            "parity_sample_containers": checked,
+            "parity_definition": (f"records gathered to rank 0 vs oracle/krr_oracle.c and vs rank 0's own kernel on "
+                                  f"{args.parity_blocks} blocks of {args.parity_block} consecutive containers per "
+                                  f"shard, regenerated on rank 0 from their global indices")}
 
 
 SLOTS_30D_15S = 30 * 24 * 60 * 4  # 172,800
@@ -578,7 +750,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             cs = max(1, min(args.cpu_sample * 5 if args.cpu_sample else 4096, S))  # ~10 s on 16 cores
             host = cpu.view(S, Lr)[:cs].cpu().numpy().ravel()
             ho = (np.arange(cs + 1) * Lr).astype(np.int64)
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads = args.cpu_threads or cpu_lease()["threads"]
             ta = time.perf_counter()
             oracle.percentile(host, ho, exact_params.mode, exact_params.p_num, exact_params.p_den, exact_params.q,
                               False, threads)

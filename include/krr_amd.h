@@ -152,6 +152,44 @@ int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value,
                      const int64_t* mem_count, const uint32_t* mem_flags, int64_t* records,
                      void* stream);
 
+/* ---- Multi-GPU result collection: RCCL over xGMI, one process per GPU ----
+ * Replaces the reference's fleet fan-out (asyncio.gather over objects,
+ * robusta_krr/core/runner.py:109-120) once the fleet is sharded over ranks: every
+ * rank runs krr_simple_run_records on its contiguous object range, then the
+ * records meet on the root.  RCCL is resolved at run time: the librccl.so.1
+ * already loaded in the process (e.g. PyTorch's, so a communicator taken from a
+ * torch.distributed "nccl" process group works) or else ROCm's.  `comm` is an
+ * ncclComm_t.  Returns KRR_E_UNSUPPORTED when no RCCL can be loaded. */
+
+/* unique_id: 128 bytes (ncclUniqueId), created on one rank and shared out of band. */
+int krr_comm_unique_id(krr_ctx* ctx, void* unique_id);
+/* ncclCommInitRank on the ctx's device. */
+int krr_comm_init(krr_ctx* ctx, int nranks, const void* unique_id, int rank, void** out_comm);
+int krr_comm_destroy(krr_ctx* ctx, void* comm);
+
+/* Gather every rank's n_local records (device int64[4 * n_local]) to `root`,
+ * concatenated in rank order into `out` (device, root only; ignored elsewhere).
+ * counts: HOST int64[nranks] with every rank's n_local, read on the root only; NULL
+ * means every rank sends the root's n_local.  One grouped send/recv round (ragged
+ * shards need no padding); asynchronous on `stream`. */
+int krr_gather_results(krr_ctx* ctx, void* comm, int root, const int64_t* records, int64_t n_local,
+                       const int64_t* counts, int64_t* out, void* stream);
+
+/* ---- Launch plan (host only: no device, no ctx) ----
+ * What krr_segmented_percentile / krr_simple_run choose for SORTED_LOWER / LINEAR
+ * when the longest segment has max_segment_len slots. */
+typedef struct {
+    int32_t hselect;      /* 1: histogram select (1-2 HBM passes); 0: single-pass LDS candidate buffer */
+    int32_t bottom;       /* 1: the smallest keys are kept (low percentiles) */
+    int64_t tkeep;        /* keys a segment of max length must keep */
+    int64_t cap_keys;     /* single-pass candidate capacity (0 with hselect) */
+    int64_t lds_bytes;    /* dynamic LDS per workgroup */
+    int32_t probe;        /* 1: a max-length segment starts at a probe-estimated threshold */
+    int32_t reserved;
+} krr_select_plan_info;
+
+int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params, krr_select_plan_info* out);
+
 /* ---- Sketch mode (config 5: time-sharded series too long for one window) ----
  * A build-only extension: the reference cannot query 30d@15s.
  * Per segment a log-linear histogram with data-independent bins: 2^mantissa_bits
@@ -241,6 +279,13 @@ int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t
 int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
                           uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, int64_t t0,
                           int64_t total_len, void* stream);
+
+/* Same, with segment s of this call being GLOBAL segment seg_base + s of the fleet:
+ * a rank that owns objects [seg_base, seg_base + n_segments) generates exactly the
+ * series a single GPU generates for them (krr_synth_fill == seg_base 0). */
+int krr_synth_fill_global(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
+                          uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, int64_t seg_base,
+                          int64_t t0, int64_t total_len, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "krr_pack_records",
     "krr_synth_fill",
     "krr_synth_fill_window",
+    "krr_synth_fill_global",
     "krr_sketch_width",
     "krr_sketch_build",
     "krr_sketch_query",
@@ -56,6 +57,11 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_refine",
     "krr_rank_of",
     "krr_select_present",
+    "krr_select_plan",
+    "krr_comm_unique_id",
+    "krr_comm_init",
+    "krr_comm_destroy",
+    "krr_gather_results",
 )
 
 
@@ -118,6 +124,22 @@ class KrrSketchLoc(ctypes.Structure):
 
 LOC_WORDS = ctypes.sizeof(KrrSketchLoc) // 8
 
+
+class KrrSelectPlanInfo(ctypes.Structure):
+    """include/krr_amd.h krr_select_plan_info (40 bytes)."""
+    _fields_ = [
+        ("hselect", ctypes.c_int32),
+        ("bottom", ctypes.c_int32),
+        ("tkeep", ctypes.c_int64),
+        ("cap_keys", ctypes.c_int64),
+        ("lds_bytes", ctypes.c_int64),
+        ("probe", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+NCCL_UNIQUE_ID_BYTES = 128
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -163,6 +185,18 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_synth_fill.restype = ctypes.c_int
         lib.krr_synth_fill_window.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, i64, i64, vp]
         lib.krr_synth_fill_window.restype = ctypes.c_int
+        lib.krr_synth_fill_global.argtypes = [vp, vp, vp, i64, u64, i32, i64, i32, i64, i64, i64, vp]
+        lib.krr_synth_fill_global.restype = ctypes.c_int
+        lib.krr_select_plan.argtypes = [i64, pp, ctypes.POINTER(KrrSelectPlanInfo)]
+        lib.krr_select_plan.restype = ctypes.c_int
+        lib.krr_comm_unique_id.argtypes = [vp, vp]
+        lib.krr_comm_unique_id.restype = ctypes.c_int
+        lib.krr_comm_init.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.krr_comm_init.restype = ctypes.c_int
+        lib.krr_comm_destroy.argtypes = [vp, vp]
+        lib.krr_comm_destroy.restype = ctypes.c_int
+        lib.krr_gather_results.argtypes = [vp, vp, ctypes.c_int, vp, i64, vp, vp, vp]
+        lib.krr_gather_results.restype = ctypes.c_int
         skp = ctypes.POINTER(KrrSketchParams)
         lib.krr_sketch_width.argtypes = [skp]
         lib.krr_sketch_width.restype = i64
@@ -282,12 +316,47 @@ class Context:
             out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
             records.data_ptr(), self._stream(stream)))
 
-    def synth_fill(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, stream=None) -> None:
+    def synth_fill(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, stream=None,
+                   seg_base: int = 0) -> None:
+        """Synthetic series; segment s is global segment seg_base + s of the fleet."""
         _check_tensor(values, "float64")
         _check_tensor(offsets, "int64")
-        self._check(self._lib.krr_synth_fill(
+        self._check(self._lib.krr_synth_fill_global(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
-            int(kind), int(pod_len), int(bool(gaps)), self._stream(stream)))
+            int(kind), int(pod_len), int(bool(gaps)), int(seg_base), 0, 0, self._stream(stream)))
+
+    # --- multi-GPU result collection (RCCL, include/krr_amd.h krr_gather_results) ---
+    def comm_unique_id(self) -> bytes:
+        buf = ctypes.create_string_buffer(NCCL_UNIQUE_ID_BYTES)
+        self._check(self._lib.krr_comm_unique_id(self._h, buf))
+        return buf.raw
+
+    def comm_init(self, nranks: int, unique_id: bytes, rank: int) -> int:
+        """ncclCommInitRank on this ctx's device; returns the ncclComm_t as an int."""
+        if len(unique_id) != NCCL_UNIQUE_ID_BYTES:
+            raise ValueError("unique_id must be 128 bytes")
+        comm = ctypes.c_void_p()
+        self._check(self._lib.krr_comm_init(self._h, int(nranks), ctypes.c_char_p(unique_id), int(rank),
+                                            ctypes.byref(comm)))
+        return int(comm.value or 0)
+
+    def comm_destroy(self, comm: int) -> None:
+        self._check(self._lib.krr_comm_destroy(self._h, ctypes.c_void_p(comm)))
+
+    def gather_results(self, comm: int, root: int, records, counts=None, out=None, stream=None) -> None:
+        """records: int64 [n_local, 4] device tensor; on the root, out: int64 [sum(counts), 4]
+        device tensor and counts: every rank's n_local (None: all equal n_local)."""
+        _check_tensor(records, "int64")
+        n_local = records.numel() // 4
+        carr = None
+        if counts is not None:
+            carr = (ctypes.c_int64 * len(counts))(*[int(c) for c in counts])
+        if out is not None:
+            _check_tensor(out, "int64", 4 * (sum(counts) if counts is not None else n_local))
+        self._check(self._lib.krr_gather_results(
+            self._h, ctypes.c_void_p(comm), int(root), records.data_ptr(), n_local,
+            ctypes.cast(carr, ctypes.c_void_p) if carr is not None else None,
+            out.data_ptr() if out is not None else None, self._stream(stream)))
 
 
     # --- sketch mode / time-sharded helpers (config 5) ---------------------
@@ -378,6 +447,17 @@ class Context:
         self._check(self._lib.krr_synth_fill_window(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
             int(kind), int(pod_len), int(bool(gaps)), int(t0), int(total_len), self._stream(stream)))
+
+
+def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectPlanInfo:
+    """The launch plan krr_segmented_percentile / krr_simple_run choose for SORTED_LOWER /
+    LINEAR (host only: no device needed).  Raises NativeError for REF_INDEX."""
+    lib = load_library()
+    info = KrrSelectPlanInfo()
+    rc = lib.krr_select_plan(int(max_segment_len), ctypes.byref(params), ctypes.byref(info))
+    if rc != KRR_OK:
+        raise NativeError(rc, "krr_select_plan")
+    return info
 
 
 def _check_tensor(t, dtype: str, numel: Optional[int] = None) -> None:

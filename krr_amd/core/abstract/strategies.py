@@ -91,9 +91,34 @@ class BaseStrategy(abc.ABC, Generic[_StrategySettings]):
         return get_args(cls.__orig_bases__[0])[0]  # type: ignore[attr-defined]
 
 
+def _defined_in(cls: type, name: str) -> Optional[type]:
+    for k in cls.__mro__:
+        if name in k.__dict__:
+            return k
+    return None
+
+
 def supports_batch(strategy: BaseStrategy) -> bool:
-    """True if the strategy implements the optional fleet-wide ``run_batch`` hook."""
-    return callable(getattr(strategy, "run_batch", None))
+    """True if the strategy's fleet-wide ``run_batch`` hook computes what its ``run()`` does.
+
+    The hook must come from the class that defines ``run()`` or from a subclass of it:
+    a user subclass of SimpleStrategy that overrides only ``run()`` inherits
+    ``run_batch`` but must still get its own ``run()`` per object, as the reference's
+    Runner always calls ``strategy.run()`` (runner.py:106)."""
+    if not callable(getattr(strategy, "run_batch", None)):
+        return False
+    cls = type(strategy)
+    rb, r = _defined_in(cls, "run_batch"), _defined_in(cls, "run")
+    return rb is not None and (r is None or issubclass(rb, r))
+
+
+def supports_packed(strategy: BaseStrategy) -> bool:
+    """True if the strategy takes the packed-fleet path (kernel + native rounding)."""
+    if not supports_batch(strategy) or not callable(getattr(strategy, "format_packed", None)):
+        return False
+    cls = type(strategy)
+    fp, r = _defined_in(cls, "format_packed"), _defined_in(cls, "run")
+    return fp is not None and (r is None or issubclass(fp, r))
 
 
 def run_each(strategy: BaseStrategy, histories: Sequence[HistoryData],

@@ -12,6 +12,7 @@ Record layout (int64[4] per object, 32 B):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -108,7 +109,8 @@ def _assemble(flat, counts):
 
 def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = None, async_op: bool = False,
                    copy_local: bool = True):
-    """Gather every rank's [n_r, 4] records to rank `dst`, concatenated in rank order.
+    """Gather every rank's [n_r, 4] records to rank `dst` (a rank of `group`),
+    concatenated in rank order.
 
     Ranks may hold different n_r: counts are exchanged first (``record_counts``,
     one all_gather of a single int64 and a host sync — pass ``counts`` to reuse
@@ -126,7 +128,8 @@ def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = Non
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    rank = dist.get_rank(group)  # group-local, like dst
+    gdst = dist.get_global_rank(group, dst) if group is not None else dst  # torch's gather takes a global rank
     dev = local.device
     if counts is None:
         counts = record_counts(local.shape[0], dev, group)
@@ -142,7 +145,59 @@ def gather_records(local, dst: int = 0, group=None, counts: Optional[list] = Non
             send[local.shape[0]:].zero_()
     flat = torch.empty((world * width, RECORD_WORDS), dtype=torch.int64, device=dev) if rank == dst else None
     bufs = [flat[r * width:(r + 1) * width] for r in range(world)] if flat is not None else None
-    work = dist.gather(send, gather_list=bufs, dst=dst, group=group, async_op=async_op)
+    work = dist.gather(send, gather_list=bufs, dst=gdst, group=group, async_op=async_op)
     if async_op:
         return PendingGather(work, flat, counts)
     return _assemble(flat, counts)
+
+
+# ---------------------------------------------------------------------------
+# Sharded fleets (krr_amd.core.runner.BatchedRunner's multi-GPU mode)
+# ---------------------------------------------------------------------------
+
+def slice_series(ps, lo: int, hi: int):
+    """Objects [lo, hi) of a PackedSeries (values are a view, offsets rebased)."""
+    from krr_amd.core.packing import PackedSeries
+
+    a, b = int(ps.offsets[lo]), int(ps.offsets[hi])
+    offs = (ps.offsets[lo:hi + 1] - a).astype(np.int64)
+    lens = np.diff(offs)
+    return PackedSeries(ps.values[a:b], offs, int(lens.max()) if lens.size else 0, ps.gaps_are_nan)
+
+
+def slice_fleet(fleet, lo: int, hi: int):
+    from krr_amd.core.packing import PackedFleet
+
+    return PackedFleet(slice_series(fleet.cpu, lo, hi), slice_series(fleet.mem, lo, hi))
+
+
+def fleet_shard_bounds(fleet, world_size: int) -> list[tuple[int, int]]:
+    """Contiguous object ranges with ~equal slots (CPU + memory) per rank."""
+    w = np.diff(fleet.cpu.offsets) + np.diff(fleet.mem.offsets)
+    return shard_bounds(w, world_size)
+
+
+def raw_from_records(rec):
+    """int64 [S, 4] records (tensor or array) -> krr_amd.core.engine.RawResults."""
+    from krr_amd.core.engine import RawResults
+
+    u = unpack_records(rec)
+    return RawResults(u["cpu_value"], u["cpu_count"], u["cpu_flags"], u["mem_value"], u["mem_count"], u["mem_flags"])
+
+
+def collective_device(group=None):
+    """Where a collective's tensors live: the rank's GPU for "nccl" (RCCL), host for gloo."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def local_device() -> int:
+    """This rank's HIP device: LOCAL_RANK (modulo the visible devices, so a gloo rehearsal
+    may put several ranks on one GPU)."""
+    import torch
+
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)

@@ -121,6 +121,35 @@ class SimpleEngine:
                           host["mem_value"], host["mem_count"], host["mem_flags"].view(np.uint32))
 
 
+    def run_packed_records(self, fleet: PackedFleet, params: _native.KrrPercentileParams):
+        """The fused kernel pass over a (shard of a) fleet, returning its 32-B result
+        records as an int64 [S, 4] device tensor (krr_simple_run_records: written by the
+        same launch) on the current stream — what a rank sends to rank 0."""
+        import torch
+
+        if fleet.cpu.n_segments != fleet.mem.n_segments:
+            raise ValueError("cpu and memory need one segment per object each")
+        self.context()
+        S = fleet.n_objects
+        dev = torch.device("cuda", self.device)
+        rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
+        if S == 0:
+            return rec
+        with torch.cuda.device(self.device):
+            cv, co = self._to_device(fleet.cpu)
+            mv, mo = self._to_device(fleet.mem)
+            out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+                   (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+                    ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+            ctx = self.context()
+            ctx.simple_run(ctx.series(cv, co, max(fleet.cpu.max_len, 1), fleet.cpu.gaps_are_nan),
+                           ctx.series(mv, mo, max(fleet.mem.max_len, 1), fleet.mem.gaps_are_nan),
+                           params, out, records=rec)
+            # the host buffers may be pinned and released by the caller: finish the copies
+            torch.cuda.current_stream(self.device).synchronize()
+        return rec
+
+
 def pinned_alloc(n: int) -> np.ndarray:
     """float64[n] in page-locked host memory (a numpy view that keeps its torch
     tensor alive): pass as ``alloc`` to the packers so the H2D copy runs by DMA."""

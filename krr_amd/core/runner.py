@@ -7,6 +7,13 @@ robusta_krr/core/runner.py:88-120).
      any other BaseStrategy subclass: the reference's per-object ``run()`` loop;
   3. exact-decimal rounding + minimum clamp (runner.py:49-86, krr_amd.core.rounding);
   4. ResourceAllocations (NaN -> "?", allocations.py:40-41).
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): the fleet fan-out
+(runner.py:109-120) becomes a contiguous, sample-balanced object shard per rank,
+ONE fused kernel pass per rank writing 32-B result records, one gather of the
+records to the destination rank, and the exact-decimal rounding there
+(``recommend_shard`` / ``recommend_packed_sharded`` /
+``gather_objects_recommendations_sharded``).
 """
 from __future__ import annotations
 
@@ -21,6 +28,7 @@ from krr_amd.core.abstract.strategies import (
     RunResult,
     run_each,
     supports_batch,
+    supports_packed,
 )
 from krr_amd.core.models.allocations import ResourceAllocations, ResourceType
 from krr_amd.core.models.objects import K8sObjectData
@@ -56,7 +64,7 @@ class BatchedRunner:
         """Rounded RunResults, one per object (what _calculate_object_recommendations returns)."""
         if len(objects) != len(histories):
             raise ValueError("one HistoryData per object")
-        if hasattr(self.strategy, "format_packed"):  # SimpleStrategy: pack once, native rounding
+        if supports_packed(self.strategy):  # SimpleStrategy: pack once, native rounding
             return self.strategy.format_packed(self.strategy.pack(histories), self.cpu_min_value,
                                                self.memory_min_value)
         return [format_result(r, self.cpu_min_value, self.memory_min_value)
@@ -64,9 +72,56 @@ class BatchedRunner:
 
     def recommend_packed(self, fleet) -> list[RunResult]:
         """Rounded RunResults for a PackedFleet (e.g. from recommend_from_bodies)."""
-        if hasattr(self.strategy, "format_packed"):
-            return self.strategy.format_packed(fleet, self.cpu_min_value, self.memory_min_value)
-        raise TypeError(f"{type(self.strategy).__name__} has no batched packed path; use recommend()")
+        self._require_packed()
+        return self.strategy.format_packed(fleet, self.cpu_min_value, self.memory_min_value)
+
+    def _require_packed(self) -> None:
+        if not supports_packed(self.strategy):
+            raise TypeError(f"{type(self.strategy).__name__} has no batched packed path; use recommend()")
+
+    # --- multi-GPU: one process per GPU ------------------------------------------
+    def recommend_shard(self, local_fleet, group=None, dst: int = 0, device: Optional[int] = None):
+        """This rank's contiguous object shard -> ONE kernel pass (records written by the
+        same launch) -> records gathered to rank ``dst`` of ``group`` (RCCL for "nccl",
+        host tensors for gloo) -> the rounded RunResults of every rank's objects, in rank
+        order, on ``dst``; None on the other ranks.  Collective: every rank calls it."""
+        from krr_amd.core.distributed import collective_device, gather_records, local_device, raw_from_records
+
+        self._require_packed()
+        rec = self.strategy.settings.run_fleet_records(local_fleet, local_device() if device is None else device)
+        full = gather_records(rec.to(collective_device(group)), dst=dst, group=group)
+        if full is None:
+            return None
+        return self.strategy.format_raw(raw_from_records(full), self.cpu_min_value, self.memory_min_value)
+
+    def recommend_packed_sharded(self, fleet, group=None, dst: int = 0, device: Optional[int] = None):
+        """Every rank holds the same packed fleet: each runs its sample-balanced contiguous
+        shard (``fleet_shard_bounds``) and ``dst`` receives the whole fleet's results."""
+        import torch.distributed as dist
+
+        from krr_amd.core.distributed import fleet_shard_bounds, slice_fleet
+
+        lo, hi = fleet_shard_bounds(fleet, dist.get_world_size(group))[dist.get_rank(group)]
+        return self.recommend_shard(slice_fleet(fleet, lo, hi), group=group, dst=dst, device=device)
+
+    async def gather_objects_recommendations_sharded(self, objects: Sequence[K8sObjectData], loader: HistoryLoader,
+                                                     group=None, dst: int = 0,
+                                                     device: Optional[int] = None) -> Optional[list]:
+        """The reference's fleet fan-out (runner.py:109-120) over ranks: every rank knows the
+        object list, fetches ONLY its shard's histories (objects cut by expected samples =
+        pod count), packs them, runs one kernel pass; ``dst`` gets every object's
+        ResourceAllocations in object order, the other ranks None."""
+        import torch.distributed as dist
+
+        from krr_amd.core.distributed import shard_bounds
+
+        self._require_packed()
+        lo, hi = shard_bounds([max(len(o.pods), 1) for o in objects],
+                              dist.get_world_size(group))[dist.get_rank(group)]
+        histories = await self.gather_histories(objects[lo:hi], loader)
+        fleet = self.strategy.pack(histories)
+        res = await asyncio.to_thread(self.recommend_shard, fleet, group, dst, device)
+        return None if res is None else [to_allocations(r) for r in res]
 
     def recommend_from_bodies(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
                               threads: int = 0) -> list[RunResult]:

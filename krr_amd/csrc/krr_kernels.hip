@@ -19,7 +19,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: RCCL is resolved with dlopen/dlsym (krr_comm_*)
+
 #include <new>
+#include <type_traits>
 
 #include "krr_amd.h"
 #include "krr_device.h"
@@ -58,9 +62,7 @@
 #ifndef KRR_PROBE_MARGIN_X4
 #define KRR_PROBE_MARGIN_X4 6  // ... aiming the start threshold at (this / 4) x the kept tail
 #endif
-#ifndef KRR_PROBE_MIN_COMPACT
-#define KRR_PROBE_MIN_COMPACT 0.25f  // ... when tkeep * ln(L / cap) >= this x (cap - tkeep - 128) free keys
-#endif
+// (KRR_PROBE_MIN_COMPACT, the rule for when the start-threshold probe pays: krr_plan.h)
 
 namespace krr {
 
@@ -818,14 +820,6 @@ struct SelectProc {
     }
 };
 
-// The probe pays when the inserts past a full buffer (~tkeep ln(L/cap), a
-// record-breaking count) would need several compactions of (cap - tkeep - 128)
-// free keys each; for short tails (p99 of a week) it would only add a round trip.
-__device__ __forceinline__ bool select_probe_pays(int64_t L, uint32_t tkeep, uint32_t cap) {
-    if (L < 4 * (int64_t)cap || cap <= tkeep + 128) return false;
-    const float inserts = (float)tkeep * __logf((float)L / (float)cap);
-    return inserts >= KRR_PROBE_MIN_COMPACT * (float)(cap - tkeep - 128);
-}
 
 // Count present, numerically negative samples (x < -0.0) of [beg, end).
 __device__ uint64_t count_negative(const double* __restrict__ vals, int64_t beg, int64_t end, int lane) {
@@ -2287,12 +2281,15 @@ __device__ __forceinline__ double unit01(uint64_t h) { return ((double)(h >> 11)
 
 __global__ __launch_bounds__(256) void k_synth(double* __restrict__ vals, const int64_t* __restrict__ offs,
                                               int64_t S, uint64_t seed, int kind, int64_t pod_len,
-                                              int gaps, int64_t t0, int64_t total_len) {
+                                              int gaps, int64_t seg_base, int64_t t0, int64_t total_len) {
     // Slot i of segment s is global time index t = t0 + i of a series of
     // total_len slots (0: the segment itself), so time slices generated on
     // different ranks concatenate to exactly the series one rank would generate.
+    // Segment s is global segment g = seg_base + s, so object shards generated on
+    // different ranks are exactly the fleet one rank would generate.
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t beg = offs[s], Lloc = offs[s + 1] - beg;
+        const uint64_t g = (uint64_t)(seg_base + s);
         const int64_t L = total_len > 0 ? total_len : Lloc;
         const int64_t plen = pod_len > 0 ? pod_len : (L > 0 ? L : 1);
         for (int64_t i = threadIdx.x; i < Lloc; i += blockDim.x) {
@@ -2302,19 +2299,19 @@ __global__ __launch_bounds__(256) void k_synth(double* __restrict__ vals, const 
             const int64_t pl = (L - pod * plen) < plen ? (L - pod * plen) : plen;
             bool gap = false;
             if (gaps) {
-                const uint64_t hp = hash4(seed, (uint64_t)s, (uint64_t)pod, 0xA11CEull);
+                const uint64_t hp = hash4(seed, g, (uint64_t)pod, 0xA11CEull);
                 int64_t start = 0;
                 if ((hp & 0xFFFF) < 19661 && pl > 1440)  // p = 0.3: the pod started late
                     start = (int64_t)((hp >> 16) % (uint64_t)(pl - 1440 + 1));
-                const double f = 0.2 * unit01(hash4(seed, (uint64_t)s, (uint64_t)pod, 0xF00Dull));
-                const double ub = unit01(hash4(seed ^ 0x5EEDull, (uint64_t)s, (uint64_t)pod, (uint64_t)(tp / 30)));
+                const double f = 0.2 * unit01(hash4(seed, g, (uint64_t)pod, 0xF00Dull));
+                const double ub = unit01(hash4(seed ^ 0x5EEDull, g, (uint64_t)pod, (uint64_t)(tp / 30)));
                 gap = tp < start || (tp >= start + 1440 && ub <= f);
             }
             double v;
             if (gap) {
                 v = bitsd(kQuietNaN);
             } else {
-                const uint64_t h1 = hash4(seed, (uint64_t)s, (uint64_t)t, (uint64_t)kind);
+                const uint64_t h1 = hash4(seed, g, (uint64_t)t, (uint64_t)kind);
                 const uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
                 if (kind == 0) {  // Gamma(k=2, theta=0.05) cores = sum of two exponentials
                     v = -0.05 * (log(unit01(h1)) + log(unit01(h2)));
@@ -2411,7 +2408,7 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     if (rc) return rc;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax);  // every segment through hselect
+    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax, sp.bottom);  // every segment through hselect
     const uint32_t cap = hsel ? 0u : need;
     *A = SelectArgs{};
     A->vals = series->values;
@@ -2699,20 +2696,27 @@ int krr_diag_attach(void* dev_buffer) {
 }
 #endif
 
-int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
-                          int32_t kind, int64_t pod_len, int32_t gaps, int64_t t0, int64_t total_len, void* stream) {
+int krr_synth_fill_global(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
+                          int32_t kind, int64_t pod_len, int32_t gaps, int64_t seg_base, int64_t t0, int64_t total_len,
+                          void* stream) {
     if (!ctx) return KRR_E_INVALID;
     if (n_segments < 0 || (n_segments > 0 && (!values || !offsets)) || kind < 0 || kind > 1 || t0 < 0 ||
-        total_len < 0)
+        total_len < 0 || seg_base < 0)
         return set_err(ctx, KRR_E_INVALID, "bad synth arguments%s", "");
     if (n_segments == 0) return KRR_OK;
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     int64_t grid = n_segments < 65536 ? n_segments : 65536;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, values, offsets,
-                       n_segments, seed, kind, pod_len, gaps, t0, total_len);
+                       n_segments, seed, kind, pod_len, gaps, seg_base, t0, total_len);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
+}
+
+int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
+                          int32_t kind, int64_t pod_len, int32_t gaps, int64_t t0, int64_t total_len, void* stream) {
+    return krr_synth_fill_global(ctx, values, offsets, n_segments, seed, kind, pod_len, gaps, 0, t0, total_len,
+                                 stream);
 }
 
 int krr_synth_fill(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments, uint64_t seed,
@@ -2867,6 +2871,175 @@ int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k,
     hipLaunchKernelGGL(k_select_present, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
                        series->offsets, S, series->gaps_are_nan, k, out);
     KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params, krr_select_plan_info* out) {
+    if (!out || max_segment_len < 0) return KRR_E_INVALID;
+    int rc = check_params(nullptr, params);
+    if (rc) return rc;
+    *out = krr_select_plan_info{};
+    if (params->mode == KRR_PCT_REF_INDEX) return KRR_E_UNSUPPORTED;  // no selection: an index walk
+    const int64_t Lmax = max_segment_len > 0 ? max_segment_len : 1;
+    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
+    const uint32_t need = capacity_for(sp.tkeep);
+    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax, sp.bottom);
+    out->hselect = hsel ? 1 : 0;
+    out->bottom = (int32_t)sp.bottom;
+    out->tkeep = sp.tkeep;
+    out->cap_keys = hsel ? 0 : need;
+    out->lds_bytes = (int64_t)kSelectLdsFixed + (int64_t)(hsel ? kHselectLds : (size_t)need * 8);
+#if KRR_SELECT_PROBE
+    out->probe = (!hsel && !sp.bottom && select_probe_pays(Lmax, sp.tkeep, need)) ? 1 : 0;
+#endif
+    return KRR_OK;
+}
+
+}  // extern "C"
+
+// ---- RCCL, resolved at run time --------------------------------------------
+// The process may already hold a librccl.so.1 (PyTorch's); binding to that copy
+// keeps communicators created by torch.distributed valid here.  Otherwise ROCm's
+// is loaded (this library's RUNPATH holds /opt/rocm/lib).
+namespace {
+struct RcclApi {
+    bool ok = false;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return a;
+        bool all = true;
+        auto sym = [&](auto& fp, const char* name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            all = all && fp != nullptr;
+        };
+        sym(a.get_unique_id, "ncclGetUniqueId");
+        sym(a.comm_init_rank, "ncclCommInitRank");
+        sym(a.comm_destroy, "ncclCommDestroy");
+        sym(a.comm_count, "ncclCommCount");
+        sym(a.comm_user_rank, "ncclCommUserRank");
+        sym(a.send, "ncclSend");
+        sym(a.recv, "ncclRecv");
+        sym(a.group_start, "ncclGroupStart");
+        sym(a.group_end, "ncclGroupEnd");
+        sym(a.error_string, "ncclGetErrorString");
+        a.ok = all;
+        return a;
+    }();
+    return api;
+}
+
+int nccl_err(krr_ctx* ctx, const char* what, ncclResult_t r) {
+    return set_err(ctx, KRR_E_HIP, "RCCL %s failed (%lld)", what, (long long)r);
+}
+}  // namespace
+
+extern "C" {
+
+int krr_comm_unique_id(krr_ctx* ctx, void* unique_id) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!unique_id) return set_err(ctx, KRR_E_INVALID, "null unique_id%s", "");
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    ncclUniqueId id;
+    const ncclResult_t r = R.get_unique_id(&id);
+    if (r != ncclSuccess) return nccl_err(ctx, "ncclGetUniqueId", r);
+    memcpy(unique_id, &id, sizeof(id));
+    return KRR_OK;
+}
+
+int krr_comm_init(krr_ctx* ctx, int nranks, const void* unique_id, int rank, void** out_comm) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!unique_id || !out_comm || nranks < 1 || rank < 0 || rank >= nranks)
+        return set_err(ctx, KRR_E_INVALID, "bad comm arguments%s", "");
+    *out_comm = nullptr;
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = R.comm_init_rank(&comm, nranks, id, rank);
+    if (r != ncclSuccess) return nccl_err(ctx, "ncclCommInitRank", r);
+    *out_comm = comm;
+    return KRR_OK;
+}
+
+int krr_comm_destroy(krr_ctx* ctx, void* comm) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!comm) return KRR_OK;
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    DeviceGuard g(ctx->device);
+    const ncclResult_t r = R.comm_destroy((ncclComm_t)comm);
+    return r == ncclSuccess ? KRR_OK : nccl_err(ctx, "ncclCommDestroy", r);
+}
+
+int krr_gather_results(krr_ctx* ctx, void* comm, int root, const int64_t* records, int64_t n_local,
+                       const int64_t* counts, int64_t* out, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!comm || n_local < 0 || (n_local > 0 && !records))
+        return set_err(ctx, KRR_E_INVALID, "bad gather arguments%s", "");
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    ncclComm_t c = (ncclComm_t)comm;
+    int nranks = 0, me = 0;
+    ncclResult_t r = R.comm_count(c, &nranks);
+    if (r == ncclSuccess) r = R.comm_user_rank(c, &me);
+    if (r != ncclSuccess) return nccl_err(ctx, "ncclCommCount/UserRank", r);
+    if (root < 0 || root >= nranks) return set_err(ctx, KRR_E_INVALID, "root %s%lld out of range", "", root);
+    if (me == root) {
+        if (!out) return set_err(ctx, KRR_E_INVALID, "null out on the root%s", "");
+        if (counts && counts[root] != n_local)
+            return set_err(ctx, KRR_E_INVALID, "counts[root] != n_local%s", "");
+        for (int q = 0; q < nranks && counts; ++q)
+            if (counts[q] < 0) return set_err(ctx, KRR_E_INVALID, "negative count for rank %s%lld", "", q);
+    }
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipStream_t st = (hipStream_t)stream;
+    constexpr size_t kWords = 4;  // int64 words per 32-B record
+    r = R.group_start();
+    if (r != ncclSuccess) return nccl_err(ctx, "ncclGroupStart", r);
+    hipError_t he = hipSuccess;
+    if (me == root) {
+        int64_t off = 0;
+        for (int q = 0; q < nranks; ++q) {
+            const int64_t nq = counts ? counts[q] : n_local;
+            if (nq > 0) {
+                int64_t* dst = out + off * (int64_t)kWords;
+                if (q == root) {
+                    if (dst != records) he = hipMemcpyAsync(dst, records, (size_t)nq * kWords * 8,
+                                                            hipMemcpyDeviceToDevice, st);
+                } else if (r == ncclSuccess) {
+                    r = R.recv(dst, (size_t)nq * kWords, ncclInt64, q, c, st);
+                }
+            }
+            off += nq;
+        }
+    } else if (n_local > 0) {
+        r = R.send(records, (size_t)n_local * kWords, ncclInt64, root, c, st);
+    }
+    const ncclResult_t re = R.group_end();
+    if (he != hipSuccess) return set_err(ctx, KRR_E_HIP, "D2D copy failed: %s%lld", hipGetErrorString(he), 0);
+    if (r != ncclSuccess) return nccl_err(ctx, "ncclSend/ncclRecv", r);
+    if (re != ncclSuccess) return nccl_err(ctx, "ncclGroupEnd", re);
     return KRR_OK;
 }
 

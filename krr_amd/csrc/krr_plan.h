@@ -117,12 +117,35 @@ constexpr uint32_t kSingleCapLong = KRR_SINGLE_CAP_LONG;
 #define KRR_PROBE_LEN_RATIO 12
 #endif
 
-KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L) {
+// The start-threshold probe pays when the inserts past a full buffer (~tkeep
+// ln(L/cap), a record-breaking count) would need several compactions of
+// (cap - tkeep - 128) free keys each; for short tails (p99 of a week) it would
+// only add a round trip.  Top side only.
+#ifndef KRR_PROBE_MIN_COMPACT
+#define KRR_PROBE_MIN_COMPACT 0.25f  // ... when tkeep * ln(L / cap) >= this x (cap - tkeep - 128) free keys
+#endif
+KRR_HD inline bool select_probe_pays(int64_t L, uint32_t tkeep, uint32_t cap) {
+    if (L < 4 * (int64_t)cap || cap <= tkeep + 128) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float inserts = (float)tkeep * __logf((float)L / (float)cap);
+#else
+    const float inserts = (float)tkeep * logf((float)L / (float)cap);
+#endif
+    return inserts >= KRR_PROBE_MIN_COMPACT * (float)(cap - tkeep - 128);
+}
+
+// `bottom`: the plan keeps the smallest keys.  The start-threshold probe only
+// runs for the top side (krr_kernels.hip select_segment_with), so the probe-backed
+// capacity is top-side only; a low percentile of a long series (p5 of 50,400
+// slots keeps ~2,500 keys) would otherwise stream from the lowest key into a big
+// buffer and compact a dozen times per segment.
+KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L, uint32_t bottom) {
     if (need <= kSingleCapMax) return true;
     if (need <= kSingleCapLong && (int64_t)tkeep * 1000 <= (int64_t)KRR_LONG_KEEP_PERMILLE * L) return true;
 #if !defined(KRR_SELECT_PROBE) || KRR_SELECT_PROBE
-    return need <= KRR_SINGLE_CAP_PROBE && L >= (int64_t)KRR_PROBE_LEN_RATIO * need;
+    return !bottom && need <= KRR_SINGLE_CAP_PROBE && L >= (int64_t)KRR_PROBE_LEN_RATIO * need;
 #else
+    (void)bottom;
     return false;
 #endif
 }

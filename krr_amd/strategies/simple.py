@@ -79,6 +79,10 @@ class SimpleStrategySettings(StrategySettings):
     def run_fleet(self, fleet: PackedFleet) -> RawResults:
         return default_engine(self.device).run_packed(fleet, self.params())
 
+    def run_fleet_records(self, fleet: PackedFleet, device: Optional[int] = None):
+        """One kernel pass over a fleet shard -> int64 [S, 4] device records (multi-GPU path)."""
+        return default_engine(self.device if device is None else device).run_packed_records(fleet, self.params())
+
     def _run_single(self, history: HistoryData) -> RawResults:
         return self.run_fleet(pack_histories([history]))
 
@@ -131,9 +135,13 @@ class SimpleStrategy(BaseStrategy[SimpleStrategySettings]):
         """Kernel pass + the reference's rounding (Runner._format_result) for a packed
         fleet, the rounding done in native exact-decimal code (krr_amd.core.fast_round):
         equal to format_result(r) for r in run_batch(...), ~20x cheaper per object."""
+        return self.format_raw(self.settings.run_fleet(fleet), cpu_min_value, memory_min_value)
+
+    def format_raw(self, raw: RawResults, cpu_min_value: int, memory_min_value: int) -> list[RunResult]:
+        """Rounded RunResults from raw kernel results (e.g. records gathered from every rank)."""
         from krr_amd.core.fast_round import format_simple_batch
 
-        return format_simple_batch(self.settings.run_fleet(fleet), self.settings, cpu_min_value, memory_min_value)
+        return format_simple_batch(raw, self.settings, cpu_min_value, memory_min_value)
 
     def results_from_raw(self, raw: RawResults) -> list[RunResult]:
         st = self.settings

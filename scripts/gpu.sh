@@ -1,0 +1,73 @@
+#!/bin/bash
+# One GPU-box pass, parameterised (replaces the per-version launchers of round 1).
+#   bash scripts/gpu.sh TAG STEP...
+# steps:
+#   tests        pytest -m gpu (one process, per-test timeout) + smoke()
+#   tests:EXPR   only the GPU tests matching -k EXPR
+#   bench        bench.py default (config 2, linear p99) -> bench.json
+#   bench:ARGS   bench.py with ARGS (commas for spaces), e.g. bench:--config,3
+#   prof         rocprofv3 --kernel-trace --stats of the default bench -> kernel_stats.csv
+#   prof:ARGS    the same for bench.py ARGS
+#   pmc          FETCH_SIZE / WRITE_SIZE passes of the default bench (separate runs)
+#   pmc:ARGS     the same for bench.py ARGS
+# Every GPU step runs under its own timeout; the first failure ends the script.
+set -u
+TAG=${1:?tag}
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R"
+export TMPDIR=/tmp
+
+name_of() { echo "$1" | tr -d ' -' | tr ',' '_' | tr '=' '_'; }
+
+for step in "$@"; do
+  kind=${step%%:*}
+  arg=""
+  [[ "$step" == *:* ]] && arg=${step#*:}
+  args=${arg//,/ }
+  n=$(name_of "$arg")
+  case "$kind" in
+    tests)
+      sel=()
+      [[ -n "$arg" ]] && sel=(-k "$arg")
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${sel[@]}" \
+        > "$OUT/pytest${n:+_$n}.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$OUT/pytest${n:+_$n}.log"; exit 1; }
+      tail -3 "$OUT/pytest${n:+_$n}.log"
+      if [[ -z "$arg" ]]; then
+        timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+          || { echo "smoke failed"; tail -20 "$OUT/smoke.log"; exit 1; }
+        tail -1 "$OUT/smoke.log"
+      fi
+      ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $args > "$OUT/bench${n:+_$n}.json" 2> "$OUT/bench${n:+_$n}.err" \
+        || { echo "bench $args failed"; tail -20 "$OUT/bench${n:+_$n}.err"; exit 1; }
+      python - "$OUT/bench${n:+_$n}.json" "$args" <<'EOF'
+import json, sys
+d = json.load(open(sys.argv[1]))
+print(sys.argv[2] or "default", "value", round(d["value"]), "ms", round(d["ms_per_step"], 4), "kernels", d.get("kernels_ms"),
+      "frac", round(d["roofline"]["frac"], 4), "parity", d.get("parity_vs_oracle_on_sample"))
+EOF
+      ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof${n:+_$n}" -o run -- \
+        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline $args > "$OUT/prof${n:+_$n}.log" 2>&1 \
+        || { echo "prof $args failed"; tail -20 "$OUT/prof${n:+_$n}.log"; exit 1; }
+      f=$(find "$OUT/prof${n:+_$n}" -name '*kernel_stats.csv' | head -1)
+      cp "$f" "$OUT/kernel_stats${n:+_$n}.csv"
+      head -4 "$OUT/kernel_stats${n:+_$n}.csv" | cut -c1-200
+      ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc "$c" -d "$OUT/pmc${n:+_$n}_$c" -o run -- \
+          python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $args > "$OUT/pmc${n:+_$n}_$c.log" 2>&1 \
+          || { echo "pmc $c $args failed"; tail -20 "$OUT/pmc${n:+_$n}_$c.log"; exit 1; }
+      done
+      ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "gpu.sh $TAG done"

@@ -1,0 +1,121 @@
+"""One rank of the multi-GPU BatchedRunner tests (started as a fresh interpreter per rank
+by tests/test_distributed.py and tests/test_gpu_multirank.py; RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT come from the environment, backend gloo).
+
+    python tests/_sharded_worker.py --compute oracle|gpu --entry packed|loader --path cli_99_5 --out rows.json
+
+--compute oracle: the per-rank kernel pass is stood in for by the CPU oracle (test
+infrastructure, so the sharding / gather / rounding logic runs on a GPU-less host);
+--compute gpu: the real HIP path (ranks may share one GPU: LOCAL_RANK modulo devices).
+Rank 0 writes the rounded rows of the whole config-1 fleet to --out.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import numpy as np  # noqa: E402
+
+
+def _oracle_records(settings, fleet):
+    import torch
+
+    from oracle import oracle
+
+    p = settings.params()
+    cv, cn, cf = oracle.percentile(fleet.cpu.values, fleet.cpu.offsets, p.mode, p.p_num, p.p_den, p.q,
+                                   fleet.cpu.gaps_are_nan)
+    mv, mn, mf = oracle.seg_max(fleet.mem.values, fleet.mem.offsets, fleet.mem.gaps_are_nan)
+    rec = np.stack([cv.view(np.int64), mv.view(np.int64),
+                    cn.astype(np.int64) | (cf.astype(np.int64) << 48),
+                    mn.astype(np.int64) | (mf.astype(np.int64) << 48)], axis=1)
+    return torch.from_numpy(np.ascontiguousarray(rec))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--compute", choices=("oracle", "gpu"), required=True)
+    ap.add_argument("--entry", choices=("packed", "loader"), default="packed")
+    ap.add_argument("--path", default="cli_99_5")
+    ap.add_argument("--out", required=True)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import config1
+    from krr_amd.core.models.allocations import ResourceType
+    from krr_amd.core.models.objects import K8sObjectData
+    from krr_amd.core.packing import PackedFleet, PackedSeries
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+    from krr_amd.utils.prom_decimal import prom_format
+
+    if args.compute == "oracle":
+        SimpleStrategySettings.run_fleet_records = lambda self, fleet, device=None: _oracle_records(self, fleet)
+    else:
+        from krr_amd.core.distributed import local_device
+
+        torch.cuda.set_device(local_device())
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    kw = dict(cpu_percentile="99", memory_buffer_percentage="5") if args.path == "cli_99_5" else {}
+    runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(**kw)))
+    cpu, mem = config1.inputs()
+    O, P, T = cpu.shape
+    if args.entry == "packed":
+        offs = np.arange(0, O * P * T + 1, P * T, dtype=np.int64)
+        fleet = PackedFleet(PackedSeries(cpu.reshape(-1).copy(), offs, P * T),
+                            PackedSeries(mem.reshape(-1).copy(), offs.copy(), P * T))
+        res = runner.recommend_packed_sharded(fleet)
+        rows = None if res is None else [
+            [str(r[ResourceType.CPU].request), str(r[ResourceType.Memory].request), str(r[ResourceType.Memory].limit)]
+            for r in res]
+    else:
+        from decimal import Decimal
+
+        from krr_amd.core.models.allocations import ResourceAllocations
+
+        none = {ResourceType.CPU: None, ResourceType.Memory: None}
+        objects = [K8sObjectData(cluster=None, name=f"app-{o:03d}", container="main", pods=config1.pod_names(o),
+                                 namespace="default", kind="Deployment",
+                                 allocations=ResourceAllocations(requests=none, limits=none)) for o in range(O)]
+        index = {o.name: i for i, o in enumerate(objects)}
+        fetched = []
+
+        class Loader:  # what PrometheusLoader.gather_data returns, from the config-1 arrays
+            async def gather_data(self, obj, resource, period, *, timeframe):
+                i = index[obj.name]
+                fetched.append(i)
+                x = cpu if resource == ResourceType.CPU else mem
+                return {pod: [Decimal(prom_format(float(v))) for v in x[i, p]] for p, pod in enumerate(obj.pods)}
+
+        allocs = asyncio.run(runner.gather_objects_recommendations_sharded(objects, Loader()))
+        # every rank fetched only its own shard
+        counts = [None] * dist.get_world_size()
+        dist.all_gather_object(counts, sorted(set(fetched)))
+        if rank == 0:
+            flat = sorted(i for c in counts for i in c)
+            assert flat == list(range(O)), "shards must cover every object exactly once"
+        rows = None if allocs is None else [
+            [str(a.requests[ResourceType.CPU]), str(a.requests[ResourceType.Memory]),
+             str(a.limits[ResourceType.Memory])] for a in allocs]
+    if rank == 0:
+        with open(args.out, "w") as fh:
+            json.dump({"rows": rows, "world": dist.get_world_size()}, fh)
+    else:
+        assert rows is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

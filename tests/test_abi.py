@@ -98,3 +98,58 @@ def test_host_headers_match_binding_table_and_exports():
     exported = {ln.split()[-1] for ln in nm.stdout.splitlines() if " T " in ln}
     assert declared <= exported
     assert {s for s in exported if s.startswith("krr_")} == declared
+
+
+def test_select_plan_layout_and_null_handling(lib):
+    from krr_amd import _native
+
+    assert ctypes.sizeof(_native.KrrSelectPlanInfo) == 4 * 2 + 8 * 3 + 4 * 2
+    assert lib.krr_gather_results(None, None, 0, None, 0, None, None, None) == -1
+    assert lib.krr_comm_unique_id(None, None) == -1
+    assert lib.krr_comm_init(None, 1, None, 0, None) == -1
+    assert lib.krr_comm_destroy(None, None) == -1
+    assert lib.krr_synth_fill_global(None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, None) == -1
+    info = _native.KrrSelectPlanInfo()
+    assert lib.krr_select_plan(-1, None, ctypes.byref(info)) == -1
+
+
+def _plan(L, p, mode="linear"):
+    from decimal import Decimal
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+
+    return _native.select_plan(L, percentile_params(Decimal(p), mode))
+
+
+@pytest.mark.parametrize("p,hselect,probe,bottom", [
+    ("99", 0, 1, 0),    # headline: ~507 kept keys; the start-threshold probe saves compactions
+    ("94", 0, 1, 0),    # probe-backed big buffer (up to 3,712 keys) on 50,400 slots
+    ("97", 0, 1, 0),
+    ("50", 1, 0, 0),    # mid percentile: hselect
+    ("93", 1, 0, 0),    # 4,224 keys would be needed: hselect
+    ("5", 1, 0, 1),     # low percentiles keep the bottom side, which has no probe
+    ("6", 1, 0, 1),
+    ("3", 1, 0, 1),     # 1,515 bottom keys: just past the 3% kept-fraction rule of the 2,560-key cap
+    ("2", 0, 0, 1),     # 1,012 bottom keys: single pass, no probe on the bottom side
+    ("1", 0, 0, 1),
+])
+def test_select_plan_decisions_config2(lib, p, hselect, probe, bottom):
+    """krr_select_plan reports the path the launch takes (krr_plan.h single_pass_ok), so the
+    big-buffer boundary and the top-side-only probe are pinned without a GPU."""
+    info = _plan(5 * 10080, p)
+    assert (info.hselect, info.probe, info.bottom) == (hselect, probe, bottom), (p, info.tkeep, info.cap_keys)
+    if hselect:
+        assert info.cap_keys == 0
+    else:
+        assert info.tkeep < info.cap_keys <= 3712 and info.lds_bytes == 1536 + 8 * info.cap_keys
+
+
+def test_select_plan_ref_index_is_not_a_selection(lib):
+    from decimal import Decimal
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+
+    with pytest.raises(_native.NativeError):
+        _native.select_plan(50400, percentile_params(Decimal("99"), "ref_index"))

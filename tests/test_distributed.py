@@ -126,3 +126,94 @@ def test_record_roundtrip_keeps_bits_and_flags():
     assert np.signbit(u["cpu_value"][1]) and np.isnan(u["cpu_value"][0])
     assert u["cpu_count"].tolist() == [0, 3, 2**40] and u["cpu_flags"].tolist() == [4, 0, 1]
     assert u["mem_flags"].tolist() == [0, 2, 4] and np.isinf(u["mem_value"][1])
+
+
+# ---------------------------------------------------------------------------
+# BatchedRunner's multi-GPU mode (shard -> one pass per rank -> gather -> round on rank 0),
+# two gloo ranks as fresh interpreters; the per-rank kernel pass is the oracle stand-in.
+# ---------------------------------------------------------------------------
+import json  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "config1_reference.json")) as _fh:
+    CONFIG1 = json.load(_fh)
+
+
+def run_sharded_workers(world, compute, entry, path, tmp_path, timeout=300):
+    """Start `world` ranks of tests/_sharded_worker.py (gloo); rank 0's rows."""
+    port = _free_port()
+    out = tmp_path / f"rows_{compute}_{entry}_{path}_{world}.json"
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_sharded_worker.py"), "--compute", compute,
+                                       "--entry", entry, "--path", path, "--out", str(out)], env=env))
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=timeout))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert codes == [0] * world, codes
+    with open(out) as fh:
+        doc = json.load(fh)
+    assert doc["world"] == world
+    return doc["rows"]
+
+
+def expected_rows(path):
+    return [[w["rounded"]["cpu_request"], w["rounded"]["mem_request"], w["rounded"]["mem_limit"]]
+            for w in CONFIG1["results"][path]]
+
+
+@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "cli_99_5"), ("packed", "default_int")])
+def test_sharded_runner_matches_reference_fixture(entry, path, tmp_path):
+    """recommend_packed_sharded / gather_objects_recommendations_sharded on 2 ranks give the
+    reference's own config-1 strings (tests/golden/config1_reference.json) for every object."""
+    assert run_sharded_workers(2, "oracle", entry, path, tmp_path) == expected_rows(path)
+
+
+def test_sharded_runner_three_ranks_equals_one(tmp_path):
+    assert run_sharded_workers(3, "oracle", "packed", "cli_99_5", tmp_path) == \
+        run_sharded_workers(1, "oracle", "packed", "cli_99_5", tmp_path)
+
+
+def test_slice_fleet_and_balanced_bounds():
+    from krr_amd.core.distributed import fleet_shard_bounds, slice_fleet
+    from krr_amd.core.packing import PackedFleet, PackedSeries
+
+    offs, cpu, mem = _fleet()
+    fleet = PackedFleet(PackedSeries(cpu, offs, int(np.diff(offs).max())),
+                        PackedSeries(mem, offs.copy(), int(np.diff(offs).max())))
+    for world in (1, 2, 5):
+        b = fleet_shard_bounds(fleet, world)
+        parts = [slice_fleet(fleet, lo, hi) for lo, hi in b]
+        assert sum(p.n_objects for p in parts) == fleet.n_objects
+        assert np.array_equal(np.concatenate([p.cpu.values for p in parts]), cpu)
+        for (lo, hi), p in zip(b, parts):
+            assert p.cpu.offsets[0] == 0 and np.array_equal(np.diff(p.cpu.offsets), np.diff(offs[lo:hi + 1]))
+            assert p.cpu.max_len == (int(np.diff(offs[lo:hi + 1]).max()) if hi > lo else 0)
+
+
+def test_subclass_overriding_run_is_not_batched():
+    """a SimpleStrategy subclass that overrides only run() keeps its run()."""
+    from krr_amd.core.abstract.strategies import supports_batch, supports_packed
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    class Mine(SimpleStrategy):
+        def run(self, history_data, object_data):
+            return {}
+
+    class Batched(SimpleStrategy):
+        def run_batch(self, histories, objects=None):
+            return []
+
+    st = SimpleStrategySettings()
+    assert supports_batch(SimpleStrategy(st)) and supports_packed(SimpleStrategy(st))
+    assert not supports_batch(Mine(st)) and not supports_packed(Mine(st))
+    assert supports_batch(Batched(st))

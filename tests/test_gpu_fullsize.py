@@ -141,3 +141,110 @@ def test_config5_sketch_rank_error_bound(ctx):
     maxbin = sk["counts"].max(1).values.to(torch.int64)
     assert bool((err <= maxbin).all())
     assert float(err.max()) / T < 1e-3
+
+
+def _oracle_subset(ctx, cpu2d, mem2d, out, rows, mode, pct, gaps=False):
+    """Bit-exact oracle check of the given rows of a [S, L] fleet."""
+    from decimal import Decimal
+
+    from krr_amd.core.engine import percentile_params
+    from oracle import oracle
+
+    c = cpu2d[rows].cpu().numpy()
+    m = mem2d[rows].cpu().numpy()
+    L = c.shape[1]
+    o = np.arange(len(rows) + 1, dtype=np.int64) * L
+    p = percentile_params(Decimal(str(pct)), mode)
+    ov, on, _ = oracle.percentile(c.ravel(), o, p.mode, p.p_num, p.p_den, p.q, gaps)
+    mv, mn, _ = oracle.seg_max(m.ravel(), o, gaps)
+    idx = np.asarray(rows)
+    gv = out["cpu_value"].cpu().numpy()[idx]
+    same = (gv.view(np.uint64) == ov.view(np.uint64)) | (np.isnan(gv) & np.isnan(ov))
+    if mode == "linear":
+        same |= (gv == 0) & (ov == 0)
+    assert same.all(), np.nonzero(~same)[0][:8]
+    assert np.array_equal(out["cpu_count"].cpu().numpy()[idx], on)
+    assert np.array_equal(out["mem_value"].cpu().numpy()[idx].view(np.uint64), mv.view(np.uint64))
+    assert np.array_equal(out["mem_count"].cpu().numpy()[idx], mn)
+
+
+@pytest.mark.parametrize("mode,pct", [("linear", 99.0), ("sorted_lower", 95.0)])
+def test_config4_shard_full_size(ctx, mode, pct):
+    """One rank's shard of config 4 at N = 8 (125,000 containers x 10,080 samples, compact,
+    20 GB resident), generated from its global indices as bench.py does: size-independent
+    properties on every container + the oracle, bit for bit, on 2,000 of them."""
+    import torch
+
+    S, L = 125_000, 10080
+    g0 = 3 * S  # rank 3 of 8
+    seed = 1000003 * 5  # bench.py's config-4 seed
+    dev = torch.device("cuda:0")
+    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    cpu = torch.empty(S * L, dtype=torch.float64, device=dev)
+    mem = torch.empty(S * L, dtype=torch.float64, device=dev)
+    ctx.synth_fill(cpu, offs, seed, 0, 0, False, seg_base=g0)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, 0, False, seg_base=g0)
+    out = _run(ctx, cpu, mem, offs, L, False, mode, pct)
+    c2, m2 = cpu.view(S, L), mem.view(S, L)
+    for a in range(0, S, 5000):
+        sub = {k: v[a:a + 5000] for k, v in out.items()}
+        _check_dense(c2[a:a + 5000], m2[a:a + 5000], sub, mode, pct)
+    rows = list(range(1000)) + list(range(S - 1000, S))
+    _oracle_subset(ctx, c2, m2, out, rows, mode, pct)
+    del cpu, mem
+    torch.cuda.empty_cache()
+
+
+def test_config3_full_size(ctx):
+    """Config 3 at full size (100,000 containers, 1..14-day windows from bench.py's
+    global-index lengths, ~1.08e9 samples per resource): properties on every container,
+    the oracle bit for bit on 2,000 of them."""
+    import torch
+
+    import bench
+
+    S = 100_000
+    lens = bench.container_lengths(3, 0, S)
+    offs_np = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    dev = torch.device("cuda:0")
+    offs = torch.from_numpy(offs_np).to(dev)
+    N = int(offs_np[-1])
+    cpu = torch.empty(N, dtype=torch.float64, device=dev)
+    mem = torch.empty(N, dtype=torch.float64, device=dev)
+    seed = 1000003 * 4
+    ctx.synth_fill(cpu, offs, seed, 0, 0, False)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, 0, False)
+    out = _run(ctx, cpu, mem, offs, int(lens.max()), False, "linear", 99.0)
+    n = torch.from_numpy(lens).to(dev)
+    assert torch.equal(out["cpu_count"], n)
+    r0, r1 = _ranks(n, "linear", 99.0)
+    for a in range(0, S, 20_000):  # bounded temporaries
+        b = min(S, a + 20_000)
+        lo, hi = int(offs_np[a]), int(offs_np[b])
+        seg = torch.repeat_interleave(torch.arange(b - a, device=dev), n[a:b])
+        x = cpu[lo:hi]
+        v = out["cpu_value"][a:b][seg]
+        lt = torch.zeros(b - a, dtype=torch.int64, device=dev).index_add_(0, seg, (x < v).to(torch.int64))
+        le = torch.zeros(b - a, dtype=torch.int64, device=dev).index_add_(0, seg, (x <= v).to(torch.int64))
+        assert bool((lt <= r1[a:b]).all()) and bool((le >= r0[a:b] + 1).all())
+        mmax = torch.full((b - a,), -float("inf"), dtype=torch.float64, device=dev).scatter_reduce(
+            0, seg, mem[lo:hi], "amax")
+        assert torch.equal(out["mem_value"][a:b], mmax)
+    from decimal import Decimal
+
+    from krr_amd.core.engine import percentile_params
+    from oracle import oracle
+
+    sel = np.r_[0:1000, S - 1000:S]
+    for a, b in ((0, 1000), (S - 1000, S)):
+        lo, hi = int(offs_np[a]), int(offs_np[b])
+        o = offs_np[a:b + 1] - lo
+        p = percentile_params(Decimal("99"), "linear")
+        ov, on, _ = oracle.percentile(cpu[lo:hi].cpu().numpy(), o, p.mode, p.p_num, p.p_den, p.q, False)
+        mv, mn, _ = oracle.seg_max(mem[lo:hi].cpu().numpy(), o, False)
+        gv = out["cpu_value"][a:b].cpu().numpy()
+        assert (((gv.view(np.uint64) == ov.view(np.uint64)) | ((gv == 0) & (ov == 0))).all())
+        assert np.array_equal(out["mem_value"][a:b].cpu().numpy().view(np.uint64), mv.view(np.uint64))
+    assert sel.size == 2000
+    del cpu, mem
+    torch.cuda.empty_cache()

@@ -1,0 +1,147 @@
+"""Multi-rank paths on the GPU box (one MI355X: ranks share it over gloo; RCCL gets a
+one-rank communicator), each rank a fresh interpreter started by a parent process:
+
+* BatchedRunner's sharded mode (shard -> one fused kernel pass per rank -> records gathered
+  -> exact rounding on rank 0) against the reference's own config-1 strings;
+* `bench.py --gpus 2` (self-launching two ranks, gloo rehearsal): n_gpus 2 and the gathered
+  records equal the oracle and rank 0's kernel on samples regenerated from every shard;
+* the C-ABI gather (krr_gather_results over RCCL, include/krr_amd.h), with a communicator of
+  its own and with PyTorch's;
+* global-index synthesis: shards generated apart equal the fleet generated whole.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+
+from test_distributed import expected_rows, run_sharded_workers  # noqa: E402
+
+
+@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "default_int")])
+def test_sharded_runner_two_ranks_on_gpu(entry, path, tmp_path):
+    assert run_sharded_workers(2, "gpu", entry, path, tmp_path, timeout=240) == expected_rows(path)
+
+
+def _bench(args, timeout=240):
+    env = dict(os.environ, KRR_BENCH_BACKEND="gloo")
+    p = subprocess.run(["timeout", "-k", "10", str(timeout), sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                       capture_output=True, text=True, env=env, timeout=timeout + 30)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("cfg,extra", [("2", ["--containers", "400"]), ("3", ["--containers", "2000"]),
+                                       ("4", ["--containers", "3000", "--mode", "sorted_lower"])])
+def test_bench_self_launches_ranks(cfg, extra):
+    r = _bench(["--gpus", "2", "--config", cfg, "--steps", "2", "--warmup", "1", "--parity-block", "64", *extra])
+    assert r["n_gpus"] == 2 and r["config"]["backend"] == "gloo"
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_gathered_vs_rank0_kernel"] is True, r
+    assert r["parity_sample_containers"] >= 2 * 64
+    assert "cpu_baseline" not in r  # rank 0 at N = 1 only
+
+
+def test_synth_global_index_shards_equal_whole_fleet():
+    import torch
+
+    from krr_amd import _native
+
+    ctx = _native.Context(0)
+    dev = torch.device("cuda:0")
+    S, L = 600, 5 * 10080
+    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    whole = torch.empty(S * L, dtype=torch.float64, device=dev)
+    ctx.synth_fill(whole, offs, 1234, 0, 10080, True)
+    parts = []
+    for a, b in ((0, 250), (250, 600)):
+        o = torch.arange(b - a + 1, dtype=torch.int64, device=dev) * L
+        x = torch.empty((b - a) * L, dtype=torch.float64, device=dev)
+        ctx.synth_fill(x, o, 1234, 0, 10080, True, seg_base=a)
+        parts.append(x)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(parts).view(torch.int64), whole.view(torch.int64))
+    ctx.close()
+
+
+def _records(n, seed, dev):
+    import torch
+
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randint(-2**62, 2**62, (n, 4), generator=g, dtype=torch.int64).to(dev)
+
+
+def test_c_abi_gather_one_rank_rccl():
+    """krr_comm_unique_id -> krr_comm_init(1 rank) -> krr_gather_results: the root's own
+    records land in `out` (counts given and not given), and bad arguments are refused."""
+    import torch
+
+    from krr_amd import _native
+
+    ctx = _native.Context(0)
+    dev = torch.device("cuda:0")
+    uid = ctx.comm_unique_id()
+    comm = ctx.comm_init(1, uid, 0)
+    try:
+        rec = _records(1000, 1, dev)
+        out = torch.full((1000, 4), -1, dtype=torch.int64, device=dev)
+        ctx.gather_results(comm, 0, rec, counts=[1000], out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, rec)
+        out2 = torch.zeros((1000, 4), dtype=torch.int64, device=dev)
+        ctx.gather_results(comm, 0, rec, out=out2)
+        torch.cuda.synchronize()
+        assert torch.equal(out2, rec)
+        with pytest.raises(_native.NativeError):
+            ctx.gather_results(comm, 1, rec, out=out2)  # root out of range
+        with pytest.raises(_native.NativeError):
+            ctx.gather_results(comm, 0, rec, counts=[999], out=out2)  # counts[root] != n_local
+    finally:
+        ctx.comm_destroy(comm)
+        ctx.close()
+
+
+def test_c_abi_gather_with_torch_process_group_comm():
+    """The communicator of a torch.distributed "nccl" group (PyTorch's own librccl.so.1) goes
+    straight into krr_gather_results: the ABI binds the RCCL already in the process."""
+    import torch
+    import torch.distributed as dist
+
+    from krr_amd import _native
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    ctx = _native.Context(0)
+    try:
+        t = torch.ones(4, device=dev)
+        dist.all_reduce(t)  # creates the communicator
+        backend = dist.group.WORLD._get_backend(dev)
+        comm_ptr = getattr(backend, "_comm_ptr", None)
+        if comm_ptr is None:
+            pytest.skip("this torch build does not expose the RCCL communicator")
+        rec = _records(777, 2, dev)
+        out = torch.zeros((777, 4), dtype=torch.int64, device=dev)
+        ctx.gather_results(int(comm_ptr()), 0, rec, counts=[777], out=out,
+                           stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert torch.equal(out, rec)
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
