@@ -190,6 +190,11 @@ typedef struct {
 
 int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params, krr_select_plan_info* out);
 
+/* Counters of the ctx since krr_create (synchronises the device): segments whose
+ * one-pass window select (wselect) missed and were finished by the two-pass
+ * histogram select.  Diagnostic: results are exact either way. */
+int krr_get_stats(krr_ctx* ctx, int64_t* wselect_fallbacks);
+
 /* ---- Sketch mode (config 5: time-sharded series too long for one window) ----
  * A build-only extension: the reference cannot query 30d@15s.
  * Per segment a log-linear histogram with data-independent bins: 2^mantissa_bits

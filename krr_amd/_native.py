@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "krr_rank_of",
     "krr_select_present",
     "krr_select_plan",
+    "krr_get_stats",
     "krr_comm_unique_id",
     "krr_comm_init",
     "krr_comm_destroy",
@@ -189,6 +190,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_synth_fill_global.restype = ctypes.c_int
         lib.krr_select_plan.argtypes = [i64, pp, ctypes.POINTER(KrrSelectPlanInfo)]
         lib.krr_select_plan.restype = ctypes.c_int
+        lib.krr_get_stats.argtypes = [vp, ctypes.POINTER(i64)]
+        lib.krr_get_stats.restype = ctypes.c_int
         lib.krr_comm_unique_id.argtypes = [vp, vp]
         lib.krr_comm_unique_id.restype = ctypes.c_int
         lib.krr_comm_init.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
@@ -324,6 +327,12 @@ class Context:
         self._check(self._lib.krr_synth_fill_global(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
             int(kind), int(pod_len), int(bool(gaps)), int(seg_base), 0, 0, self._stream(stream)))
+
+    def wselect_fallbacks(self) -> int:
+        """Segments whose one-pass window select missed (cumulative; synchronises)."""
+        v = ctypes.c_int64()
+        self._check(self._lib.krr_get_stats(self._h, ctypes.byref(v)))
+        return int(v.value)
 
     # --- multi-GPU result collection (RCCL, include/krr_amd.h krr_gather_results) ---
     def comm_unique_id(self) -> bytes:

@@ -32,6 +32,12 @@
 #ifndef KRR_STREAM_DEPTH
 #define KRR_STREAM_DEPTH 2  // chunks in flight per wave
 #endif
+#ifndef KRR_ONE_SITE_DEPTH
+#define KRR_ONE_SITE_DEPTH 1  // chunks in flight beyond the one processed, single-call-site streaming loop
+#endif
+#ifndef KRR_LDS_MIN
+#define KRR_LDS_MIN 0  // experiments: minimum dynamic LDS per select workgroup (caps waves per CU)
+#endif
 #ifndef KRR_SELECT_WAVES_PER_SIMD
 #define KRR_SELECT_WAVES_PER_SIMD 3  // __launch_bounds__ occupancy hint for the single-pass select
 #endif
@@ -179,17 +185,22 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
             if (ci < nfull) {
                 load_chunk(c, p + ci * CH);
             } else {
+                // opaque base: the 8 per-u zero-chunk addresses are rebuilt here, not
+                // hoisted to kernel entry and held in 16 VGPRs for the whole kernel
+                const double2* zpl = zp;
+                int ln = lane;
+                asm volatile("" : "+v"(zpl), "+v"(ln));
                 const double2* q[kUnroll];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
-                    const int64_t j = ci * CH + u * kWave + lane;
-                    q[u] = (ci < nch && j < nunits) ? v2 + i0 + j : zp + u * kWave;
+                    const int64_t j = ci * CH + u * kWave + ln;
+                    q[u] = (ci < nch && j < nunits) ? v2 + i0 + j : zpl + u * kWave;
                 }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) c[u] = load16(q[u]);
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
-                    const int64_t j = ci * CH + u * kWave + lane;
+                    const int64_t j = ci * CH + u * kWave + ln;
                     if (j >= nunits) c[u] = make_double2(qnan, qnan);
                 }
                 if (lane == kWave - 1) {
@@ -201,20 +212,57 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
         // cur only ever receives register copies of nxt (here and at the bottom of
         // the loop), so on every path into proc.chunk(cur) the only loads in
         // flight are nxt's and the wait the compiler places is for nothing.
-        double2 cur[kUnroll], nxt[kUnroll];
-        fill_u(nxt, 0);
+        // KRR_ONE_SITE_DEPTH > 1: a ring of that many chunks in flight (for launches
+        // whose LDS budget leaves few waves per CU to cover HBM latency).
+        double2 cur[kUnroll];
+        if constexpr (KRR_ONE_SITE_DEPTH <= 1) {
+            double2 nxt[kUnroll];
+            fill_u(nxt, 0);
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            double x = nxt[u].x, y = nxt[u].y;
-            asm volatile("" : "+v"(x), "+v"(y));
-            cur[u] = make_double2(x, y);
-        }
+            for (int u = 0; u < kUnroll; ++u) {
+                double x = nxt[u].x, y = nxt[u].y;
+                asm volatile("" : "+v"(x), "+v"(y));
+                cur[u] = make_double2(x, y);
+            }
 #pragma unroll 1
-        for (int64_t ci = 0; ci < nch; ++ci) {
-            fill_u(nxt, ci + 1);
-            proc.chunk(cur);
+            for (int64_t ci = 0; ci < nch; ++ci) {
+                fill_u(nxt, ci + 1);
+                proc.chunk(cur);
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+                for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+            }
+        } else {
+            // Ring of D buffers with compile-time roles: the loop body is unrolled D
+            // times, so at sub-step k buffer (k + D - 1) % D takes chunk ci + k + D
+            // and cur receives buffer k — the OLDEST group in flight, so the wait
+            // before that copy leaves the D - 1 newer chunks' loads outstanding.
+            // (Register shifting would wait for every load.)  D call sites of
+            // proc.chunk.
+            constexpr int D = KRR_ONE_SITE_DEPTH;
+            double2 ring[D][kUnroll];
+            {
+                double2 first[kUnroll];
+                fill_u(first, 0);
+#pragma unroll
+                for (int d = 0; d + 1 < D; ++d) fill_u(ring[d], d + 1);
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    double x = first[u].x, y = first[u].y;
+                    asm volatile("" : "+v"(x), "+v"(y));
+                    cur[u] = make_double2(x, y);
+                }
+            }
+#pragma unroll 1
+            for (int64_t ci = 0; ci < nch; ci += D) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (ci + k >= nch) break;  // wave-uniform
+                    fill_u(ring[(k + D - 1) % D], ci + k + D);
+                    proc.chunk(cur);
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u) cur[u] = ring[k][u];
+                }
+            }
         }
     } else if constexpr (KRR_MAX_DEPTH >= 2) {
         // three buffers with fixed roles: two chunks stay in flight while one is processed
@@ -877,6 +925,7 @@ struct SelectArgs {
     int64_t* out_n;
     uint32_t* out_f;
     int64_t* rec = nullptr;  // optional 32-B result records (k_pack_records layout), CPU half
+    unsigned long long* stats = nullptr;  // optional: [0] += segments wselect handed to hselect
 };
 
 // One half of an object's 32-B record (k_pack_records layout): half 0 = CPU, 1 = memory.
@@ -1228,7 +1277,8 @@ struct RankLoc {
 // histogram; when the exact counts show both ranks inside it, the segment is done in
 // one HBM pass.  Otherwise nothing changes: the pass's histogram drives the usual
 // collect pass.  Returns false when the segment is too short or too long for a band.
-constexpr int kProbeBlocks = 128;  // at most; ~L/400 blocks (probe = ~4% of the segment)
+// at most 128 (and what hselect's LDS holds); ~L/400 blocks (probe = ~4% of the segment)
+constexpr int kProbeBlocks = (int)((kHselectLds / (16 * 8) < 128 ? kHselectLds / (16 * 8) : 128) & ~(size_t)7);
 constexpr int kProbeSamples = kProbeBlocks * 16;
 
 __device__ __forceinline__ bool hselect_band(const SelectArgs& A, int64_t beg, int64_t L, unsigned char* smem,
@@ -1497,6 +1547,341 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// wselect: the first choice for order statistics whose candidate set does not
+// fit LDS (mid percentiles of long series), in ONE HBM pass.  The wave keeps an
+// inclusive key window [lo, hi]: LDS holds every present sample seen so far
+// whose key lies in it, and per-lane counters hold how many fell below it.  The
+// window starts as every key; whenever the buffer fills it shrinks around the
+// target's estimated rank among the samples seen so far (seen-rank):
+//   S seen present samples, at most U unseen ones (unread slots), q = p / 100;
+//   the target's seen-rank has mean ~ q (S - 1) and, for exchangeable samples,
+//   standard deviation sqrt(q (1 - q) S U / (S + U)) (0 once nothing is unseen);
+//   the new window spans KRR_WSEL_Z of those plus a few ranks each way.
+// For config 2's p50 (50,400 slots) that is ~2 shrinks per segment and a final
+// window of ~1,300 keys.  The window only ever narrows, so what it holds stays
+// exact; nothing here is trusted: at the end the exact counts decide.  When both
+// needed ranks lie inside the window they are selected there; otherwise (a
+// trending series the estimate misjudged, a crowded key, a NaN in the compact
+// layout) the segment runs hselect below (two passes), so the answer is exact
+// whatever the data.  A window of one key (e.g. p50 of a mostly-zero series)
+// only counts.  No histogram atomics and no probe: the per-slot work is the
+// single-pass select's (a range test, a below count, a NaN count).
+// ---------------------------------------------------------------------------
+#ifndef KRR_WSEL
+#define KRR_WSEL 1
+#endif
+#ifndef KRR_WSEL_Z
+#define KRR_WSEL_Z 4.0
+#endif
+#ifndef KRR_WSEL_FIRST
+#define KRR_WSEL_FIRST 1024  // the first shrink comes once this many keys are held (later ones: a full buffer)
+#endif
+#ifndef KRR_WSEL_BINS
+#define KRR_WSEL_BINS 1  // shrink to histogram-bin edges (one pass) instead of exact keys (0)
+#endif
+// hselect's LDS (histogram + collect buffer) holds this many window keys.
+constexpr uint32_t kWselCap = (uint32_t)(kHselectLds / 8) & ~63u;
+
+struct WindowProc {
+    SelectProc sp;            // buffer algebra (locate / kth / pair) over buf
+    uint64_t* buf;
+    int lane;
+    uint32_t cap;
+    uint32_t limit;           // keys held before the next shrink: KRR_WSEL_FIRST, then cap
+    uint32_t shrinks;
+    uint64_t lo, hi, span;    // inclusive key window
+    uint64_t lob;             // raw bits of lo (fast windows: inside [+0, +inf])
+    uint32_t fast, point;
+    uint32_t cnt;             // window keys seen (stored unless point)
+    uint32_t below_l, nan_l, negnan_l;  // per lane, committed chunks only
+    uint64_t below_extra;     // keys dropped below lo by shrinks (uniform)
+    uint64_t seen;            // slots of committed chunks (uniform; padding included)
+    int64_t L;
+    int64_t p_num, p_den;     // percentile p = p_num / p_den
+    uint32_t fail;
+#ifdef KRR_DIAG
+    unsigned long long diag[D_WORDS];
+#endif
+
+    __device__ __forceinline__ void set_window(uint64_t l, uint64_t h) {
+        lo = uni64(l);
+        hi = uni64(h);
+        span = hi - lo;
+        fast = (lo >= kKeyPosZero && hi <= kKeyPosInf) ? 1u : 0u;
+        lob = lo ^ kSignBit;
+        point = lo == hi ? 1u : 0u;
+    }
+
+    // Classify the slots of smask: per-lane window mask (slot j -> bit 15 - j),
+    // and this lane's below / NaN / negative-NaN counts (not yet committed).
+    template <bool FAST>
+    __device__ __forceinline__ uint32_t classify(const double2 (&c)[kUnroll], uint32_t smask, uint32_t& b,
+                                                 uint32_t& nn, uint32_t& ng) const {
+        uint32_t vm = 0;
+        b = nn = ng = 0;
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const uint64_t x = dbits(slot_val(c, j));
+            const bool on = (smask >> j) & 1u;  // wave-uniform
+            const bool nan = is_nan_bits(x);
+            bool in, below;
+            if (FAST) {
+                in = (x - lob) <= span;                      // rejects negatives and NaNs
+                below = (int64_t)x < (int64_t)lob;           // negatives (incl. -0, negative NaNs) are below
+            } else {
+                const uint64_t key = okey(x);
+                in = (key - lo) <= span;                     // NaN keys lie outside [okey(-inf), okey(+inf)]
+                below = key < lo;                            // + negative NaNs, removed via ng
+            }
+            in = in && on;
+            vm = (vm << 1) | (in ? 1u : 0u);
+            b += (on && below) ? 1u : 0u;
+            nn += (on && nan) ? 1u : 0u;
+            ng += (on && nan && (x >> 63)) ? 1u : 0u;
+        }
+        return vm;
+    }
+
+    // Every chunk fits: the buffer is shrunk right after a chunk that leaves less than
+    // a chunk of room (so the chunk's registers are dead during the shrink).  Only a
+    // window crowded by a few repeated keys can overflow: then the segment falls back.
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+        if (uni32(fail)) return;
+        uint32_t b, nn, ng, vm;
+        if (uni32(fast)) vm = classify<true>(c, 0xFFFFu, b, nn, ng);
+        else vm = classify<false>(c, 0xFFFFu, b, nn, ng);
+        const uint32_t vc = __popc(vm);
+        const uint32_t incl = wave_scan32(vc, 0u, OpAdd32{});
+        const uint32_t C = lane_bcast32(incl, kWave - 1);
+        if (!point && cnt + C > cap) {
+            fail = 1;
+            return;
+        }
+        if (C && !point) {
+            uint32_t pos = cnt + incl - vc;
+            uint64_t* const scratch = sp.small + lane;
+#pragma unroll
+            for (int j = 0; j < 2 * kUnroll; ++j) {
+                const uint64_t x = dbits(slot_val(c, j));
+                const uint32_t bit = (vm >> (2 * kUnroll - 1 - j)) & 1u;
+                uint64_t* const dst = bit ? buf + pos : scratch;
+                *dst = okey(x);
+                pos += bit;
+            }
+        }
+        cnt = uni32(cnt + C);
+        below_l += b;
+        nan_l += nn;
+        negnan_l += ng;
+        seen += kChunkElems;
+        if (!point && cnt + kChunkElems > limit) shrink();
+    }
+
+    // Keep the buffer keys in [nl, nh] (in place); the dropped keys below nl join
+    // below_extra.  A block of 4 x 64 keys is read before any survivor is written.
+    __device__ __forceinline__ void filter_window(uint64_t nl, uint64_t nh) {
+        uint32_t w = 0, dropped_below = 0;
+        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
+            uint64_t x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t i = base + t * kWave + lane;
+                x[t] = i < cnt ? buf[i] : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bool inr = base + t * kWave + lane < cnt;
+                const bool keep = inr && x[t] >= nl && x[t] <= nh;
+                dropped_below += popc64(ballot(inr && x[t] < nl));
+                const uint64_t m = ballot(keep);
+                if (keep) buf[w + lane_prefix(m)] = x[t];
+                w += popc64(m);
+            }
+        }
+        __syncthreads();
+        cnt = uni32(w);
+        below_extra += uni32(dropped_below);
+    }
+
+    // Narrow the window around the target's estimated seen-rank (header comment).
+    __device__ __forceinline__ void shrink() {
+        limit = cap;
+        if (point || cnt == 0) return;
+        const uint64_t nanc = wave_sum_u32(nan_l);
+        const uint64_t below = (uint64_t)wave_sum_u32(below_l) - wave_sum_u32(negnan_l) + below_extra;
+        const uint64_t S = seen - nanc;  // present samples seen
+        const double U = L > (int64_t)seen ? (double)(L - (int64_t)seen) : 0.0;
+        // q from the kernel's scalars here, not a per-segment value the compiler would
+        // hoist to kernel entry and keep in registers for the whole launch
+        int64_t pn = p_num, pd = p_den;
+        asm volatile("" : "+s"(pn), "+s"(pd));
+        const double qq = (double)pn / (100.0 * (double)pd);
+        const double Sd = (double)S;
+        const double c = qq * (Sd - 1.0);
+        const double sig = (S > 0 && U > 0.0) ? sqrt(qq * (1.0 - qq) * Sd * U / (Sd + U)) : 0.0;
+        const double w = KRR_WSEL_Z * sig + 4.0;
+        const int64_t jlo = (int64_t)floor(c - w);
+        const int64_t jhi = (int64_t)ceil(c + w) + 1;
+        int64_t ilo = jlo - (int64_t)below;  // ascending buffer indices
+        int64_t ihi = jhi - (int64_t)below;
+        const int64_t last = (int64_t)cnt - 1;
+        ilo = ilo < 0 ? 0 : (ilo > last ? last : ilo);
+        ihi = ihi < 0 ? 0 : (ihi > last ? last : ihi);
+        __syncthreads();
+        KRR_DIAG_T0(t0);
+        sp.cnt = cnt;
+        sp.bad = 0;
+        uint64_t mn = lo, mx = hi;  // after a shrink the window is tight around the keys
+        if (shrinks == 0) sp.buf_minmax(mn, mx);
+        ++shrinks;
+        uint64_t nl = lo, nh = hi;
+#if KRR_WSEL_BINS
+        // The bounds need not be the keys at ranks ilo / ihi: any window holding them
+        // works.  One 256-bin histogram of the buffer gives the edges of the bins that
+        // hold them (a bin is ~cnt / 256 keys wider than needed on each side).
+        {
+            const uint32_t sh = sp.hist_range(mn, mx);
+            uint32_t keep_hi_side = cnt, keep_lo_side = 0;  // keys >= nl, keys > nh
+            if (ilo > 0) {
+                const BinHit bl = find_bin_desc(sp.H, (uint32_t)(cnt - ilo), 0u, lane);
+                nl = uni64(mn + ((uint64_t)bl.b << sh));
+                keep_hi_side = bl.above + bl.cnt;
+            }
+            if (ihi < last) {
+                const BinHit bh = find_bin_desc(sp.H, (uint32_t)(cnt - ihi), 0u, lane);
+                const uint64_t w1 = (1ull << sh) - 1, blo = mn + ((uint64_t)bh.b << sh);
+                nh = uni64(mx - blo <= w1 ? mx : blo + w1);
+                keep_lo_side = bh.above;
+            }
+            __syncthreads();
+            // crowded bins leave too much: exact bounds instead
+            if (keep_hi_side - keep_lo_side > cap - kChunkElems / 2) {
+                nl = ilo > 0 ? sp.kth_largest((uint32_t)(cnt - ilo), mn, mx) : lo;
+                nh = ihi < last ? sp.kth_largest((uint32_t)(cnt - ihi), mn, mx) : hi;
+            }
+        }
+#else
+        // the R-th largest (1-based) is ascending index cnt - R
+        nl = ilo > 0 ? sp.kth_largest((uint32_t)(cnt - ilo), mn, mx) : lo;
+        nh = ihi < last ? sp.kth_largest((uint32_t)(cnt - ihi), mn, mx) : hi;
+#endif
+        __syncthreads();
+        if (sp.bad || nl > nh) {
+            fail = 1;
+            return;
+        }
+        filter_window(nl, nh);
+        set_window(nl, nh);
+#ifdef KRR_DIAG
+        diag[D_COMPACT] += __builtin_amdgcn_s_memtime() - t0;
+        diag[D_NCOMPACT] += 1;
+#endif
+    }
+};
+
+// One CPU segment by wselect; hselect_segment when the window misses.
+__device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
+    const int64_t beg = A.offs[s], end = A.offs[s + 1];
+    const int64_t L = end - beg;
+    WindowProc W;
+    W.buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+    W.sp.buf = W.buf;
+    W.sp.H = reinterpret_cast<uint32_t*>(smem);
+    W.sp.small = reinterpret_cast<uint64_t*>(smem + 1024);
+    W.sp.lane = lane;
+    W.sp.flip = 0;
+    W.sp.cnt = 0;
+    W.sp.bad = 0;
+    W.lane = lane;
+    W.cap = kWselCap;
+    W.limit = KRR_WSEL_FIRST < kWselCap ? KRR_WSEL_FIRST : kWselCap;
+    W.shrinks = 0;
+    W.cnt = 0;
+    W.below_l = W.nan_l = W.negnan_l = 0;
+    W.below_extra = 0;
+    W.seen = 0;
+    W.L = L;
+    W.p_num = A.p_num;
+    W.p_den = A.p_den;
+    W.fail = 0;
+    W.set_window(kKeyNegInf, kKeyPosInf);
+#ifdef KRR_DIAG
+    for (int d = 0; d < D_WORDS; ++d) W.diag[d] = 0;
+    KRR_DIAG_T0(t_begin);
+#endif
+    // opaque bounds (see select_segment): no address set-up hoisted across the pass
+    int64_t b = beg, e = end;
+    asm volatile("" : "+s"(b), "+s"(e));
+    const uint32_t pad = stream_segment<true>(A.vals, b, e, W, lane);
+    __syncthreads();
+    const uint64_t nnan = (uint64_t)wave_sum_u32(W.nan_l) - pad;
+    const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;
+    uint32_t flags = 0;
+    double result = bitsd(kQuietNaN);
+    bool done = false;
+#ifdef KRR_DIAG
+    KRR_DIAG_T0(t_final);
+#endif
+    if (W.fail) {
+        // a failed window stopped counting part-way: nothing above is meaningful
+    } else if (n == 0) {
+        flags = KRR_FLAG_EMPTY;
+        done = true;
+    } else if (nnan && !A.gaps) {
+        flags = KRR_FLAG_NAN;
+        done = true;
+    } else {
+        const Ranks R = ranks_for(A, n);
+        const uint64_t below = (uint64_t)wave_sum_u32(W.below_l) - wave_sum_u32(W.negnan_l) + W.below_extra;
+        if (below <= (uint64_t)R.r0 && (uint64_t)R.r1 < below + W.cnt) {
+            uint64_t k0, k1;
+            if (W.point) {
+                k0 = k1 = W.lo;
+            } else {
+                W.sp.cnt = W.cnt;
+                W.sp.bad = 0;
+                uint64_t mn = W.lo, mx = W.hi;  // tight after a shrink
+                if (W.shrinks == 0) W.sp.buf_minmax(mn, mx);
+                const uint32_t Rt = (uint32_t)(W.cnt - ((uint64_t)R.r0 - below));  // R-th largest = rank r0
+                if (R.r1 != R.r0) {
+                    W.sp.kth_pair(Rt, -1, mn, mx, k0, k1);
+                } else {
+                    k0 = k1 = W.sp.kth_largest(Rt, mn, mx);
+                }
+            }
+            if (!W.sp.bad) {
+                result = finish_value(A, R, k0, k1, beg, end, lane);
+                done = true;
+            }
+        }
+    }
+#ifdef KRR_DIAG
+    {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        W.diag[D_TOTAL] = t_end - t_begin;
+        W.diag[D_FINAL] = t_end - t_final;
+        W.diag[D_NFALLBACK] = done ? 0ull : 1ull;
+        W.diag[D_INSERTED] = W.cnt;
+        if (lane == 0 && g_diag)
+            for (int d = 0; d < D_WORDS; ++d) g_diag[(size_t)s * D_WORDS + d] = W.diag[d];
+    }
+#endif
+    __syncthreads();
+    if (!done) {
+        if (lane == 0 && A.stats) atomicAdd(A.stats, 1ull);
+        hselect_segment(A, s, smem, lane);
+        return;
+    }
+    write_result(A, s, result, n, flags, lane);
+    __syncthreads();
+}
+
+__device__ __forceinline__ void mid_select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
+    if constexpr (KRR_WSEL) wselect_segment(A, s, smem, lane);
+    else hselect_segment(A, s, smem, lane);
+}
+
 // k_select<false>: every segment in one pass (the launch's longest segment fits
 // A.cap keys); k_select<true>: every segment through hselect.  Separate kernels
 // keep each one's register allocation to its own path.
@@ -1504,7 +1889,7 @@ template <bool HSEL>
 __global__ __launch_bounds__(64, HSEL ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        if constexpr (HSEL) hselect_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
+        if constexpr (HSEL) mid_select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
         else select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
     }
 }
@@ -1704,7 +2089,7 @@ __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? KRR_HSEL_WAVES_PER_SI
         if (b < S_cpu) {
             const int64_t s = xcd_item(b, S_cpu);
             if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, s, smem, threadIdx.x);
-            else if constexpr (CPU_KIND == CPU_HSELECT) hselect_segment(A, s, smem, threadIdx.x);
+            else if constexpr (CPU_KIND == CPU_HSELECT) mid_select_segment(A, s, smem, threadIdx.x);
             else refindex_gaps_segment<true>(R, s, threadIdx.x);
         } else {
             max_segment<true>(M, xcd_item(b - S_cpu, M.S), threadIdx.x);
@@ -2335,7 +2720,7 @@ struct krr_ctx {
     int device;
     int num_cus;
     size_t max_lds;
-    unsigned long long* d_tmp;
+    unsigned long long* d_tmp;    // [0] scratch (max segment length), [1] stats: wselect fallbacks
     char err[512];
 };
 
@@ -2423,7 +2808,9 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->out_v = ov;
     A->out_n = on;
     A->out_f = of;
+    A->stats = ctx->d_tmp + 1;
     *lds = kSelectLdsFixed + (hsel ? kHselectLds : (size_t)cap * 8);
+    if (*lds < (size_t)KRR_LDS_MIN) *lds = (size_t)KRR_LDS_MIN;
     if (*lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "select needs %s%lld B of LDS", "", (long long)*lds);
     return KRR_OK;
 }
@@ -2467,7 +2854,8 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->num_cus = prop.multiProcessorCount;
     c->max_lds = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 65536;
     if (c->max_lds > 163840) c->max_lds = 163840;
-    if (hipMalloc(&c->d_tmp, sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&c->d_tmp, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_tmp, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return KRR_E_HIP;
     }
@@ -2871,6 +3259,17 @@ int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k,
     hipLaunchKernelGGL(k_select_present, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
                        series->offsets, S, series->gaps_are_nan, k, out);
     KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_get_stats(krr_ctx* ctx, int64_t* wselect_fallbacks) {
+    if (!ctx || !wselect_fallbacks) return KRR_E_INVALID;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    unsigned long long h = 0;
+    KRR_HIP(ctx, hipDeviceSynchronize());
+    KRR_HIP(ctx, hipMemcpy(&h, ctx->d_tmp + 1, sizeof(h), hipMemcpyDeviceToHost));
+    *wselect_fallbacks = (int64_t)h;
     return KRR_OK;
 }
 
