@@ -9,7 +9,11 @@ object that share a (namespace, container) pair go into one
 
     sum by (pod) (<metric>{<same matchers>, namespace="ns", pod=~"p1|p2|...", container="c"})
 
-query (split when the pod regex grows past ``max_query_chars``).  ``sum by (pod)``
+query, split when the pod regex grows past ``max_query_chars`` or the group's
+expected samples (pods x ``series_per_pod`` x points per series) would pass
+``max_query_samples`` — Prometheus refuses a query that loads more than its
+``--query.max-samples`` (default 50,000,000) [external], where the per-pod queries
+it replaces would each pass.  ``sum by (pod)``
 evaluated over the same start/end/step yields, for every pod, exactly the series
 the per-pod ``sum(...{pod="p"})`` yields (same matchers, same aggregation inputs,
 same evaluation timestamps); a pod with no samples is absent from the grouped
@@ -108,6 +112,9 @@ class FleetQueryPlan:
     """
     objects: Sequence
     max_query_chars: int = 6000
+    points_per_series: int = 0           # evaluation timestamps per series (0: no sample bound)
+    max_query_samples: int = 50_000_000  # Prometheus' default --query.max-samples [external]
+    series_per_pod: int = 4              # raw series the selector may match per pod (restarts, ids)
     groups: list[GroupQuery] = field(init=False)
     slot_obj: np.ndarray = field(init=False)      # int64 [n_slots], non-decreasing
     slot_group: np.ndarray = field(init=False)    # int64 [n_slots]
@@ -116,6 +123,11 @@ class FleetQueryPlan:
     def __post_init__(self):
         if self.max_query_chars < 1:
             raise ValueError("max_query_chars must be positive")
+        if self.points_per_series < 0 or self.max_query_samples < 1 or self.series_per_pod < 1:
+            raise ValueError("points_per_series must be >= 0, max_query_samples and series_per_pod positive")
+        # pods one grouped query may hold under the sample bound (at least one)
+        per_pod = self.points_per_series * self.series_per_pod
+        max_pods = max(1, self.max_query_samples // per_pod) if per_pod else None
         self.groups = []
         open_group: dict[tuple[str, str], int] = {}   # (ns, container) -> index of the group being filled
         group_chars: list[int] = []
@@ -129,7 +141,9 @@ class FleetQueryPlan:
                 if g is None:
                     cost = len(pod_regex([pod])) + 1
                     g = open_group.get(key)
-                    if g is None or (self.groups[g].pods and group_chars[g] + cost > self.max_query_chars):
+                    if g is None or (self.groups[g].pods and (group_chars[g] + cost > self.max_query_chars or
+                                                              (max_pods is not None and
+                                                               len(self.groups[g].pods) >= max_pods))):
                         g = len(self.groups)
                         self.groups.append(GroupQuery(obj.namespace, obj.container, []))
                         group_chars.append(0)
@@ -148,6 +162,14 @@ class FleetQueryPlan:
         self._name_offsets = np.zeros(len(names) + 1, dtype=np.int64)
         if names:
             np.cumsum([len(n) for n in names], out=self._name_offsets[1:])
+
+    @classmethod
+    def for_settings(cls, objects: Sequence, settings, **kw) -> "FleetQueryPlan":
+        """Sample-bounded plan for a strategy's settings: points per series = the range
+        query's evaluation timestamps, history / step + 1 (prometheus.py:124-126)."""
+        step_s = int(settings.timeframe_timedelta.total_seconds()) // 60 * 60
+        points = int(settings.history_timedelta.total_seconds()) // max(step_s, 1) + 1
+        return cls(objects, points_per_series=points, **kw)
 
     @property
     def n_objects(self) -> int:

@@ -63,6 +63,14 @@ def _from_chunks(chunks: list[np.ndarray], lens: list[int], gaps: bool = False) 
 def _decimals_to_f64(xs: Sequence[Decimal]) -> np.ndarray:
     # float(Decimal) is correctly rounded; for Prometheus' shortest-repr strings it
     # recovers the exact float64 the server formatted.
+    #
+    # Contract of the HistoryData path: every Decimal is what the reference's loader
+    # builds, Decimal(<Prometheus sample string>) (prometheus.py:152), and Prometheus
+    # formats samples with Go's strconv.FormatFloat(v, 'f', -1, 64) — the shortest
+    # string that round-trips — so prom_decimal(float(d)) == d.  A hand-made Decimal
+    # with more significant digits than a float64 holds (e.g. 100000000.0000000000000001)
+    # or a non-canonical form ('0.10') is NOT reproduced: the kernel selects float64
+    # values and the host rebuilds the Decimal from the float's shortest repr.
     return np.fromiter((float(x) for x in xs), dtype=np.float64, count=len(xs))
 
 

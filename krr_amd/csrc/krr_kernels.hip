@@ -35,6 +35,9 @@
 #ifndef KRR_ONE_SITE_DEPTH
 #define KRR_ONE_SITE_DEPTH 1  // chunks in flight beyond the one processed, single-call-site streaming loop
 #endif
+#ifndef KRR_LDS_BATCH
+#define KRR_LDS_BATCH 4  // keys per lane read before use in the buffer passes (minmax, histogram, filter, gather)
+#endif
 #ifndef KRR_LDS_MIN
 #define KRR_LDS_MIN 0  // experiments: minimum dynamic LDS per select workgroup (caps waves per CU)
 #endif
@@ -52,6 +55,21 @@
 #endif
 #ifndef KRR_HSEL_WAVES_PER_SIMD
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
+#endif
+#ifndef KRR_WSEL_WAVES_PER_SIMD
+#define KRR_WSEL_WAVES_PER_SIMD 3  // ... and for the window select (wselect)
+#endif
+#ifndef KRR_WSEL_CAP
+#define KRR_WSEL_CAP 1472  // wselect's LDS keys: 1.5 + 11.5 KiB per wave -> 12 waves per CU
+#endif
+#ifndef KRR_WSEL_CAP_LONG
+#define KRR_WSEL_CAP_LONG 2304  // ... for launches of long segments (1.5 + 18 KiB -> 8 waves per CU)
+#endif
+#ifndef KRR_WSEL_LONG
+#define KRR_WSEL_LONG 32768  // longest segment from which a launch takes KRR_WSEL_CAP_LONG
+#endif
+#ifndef KRR_FALLBACK_GRID
+#define KRR_FALLBACK_GRID 1024  // workgroups of the hselect pass over the segments wselect missed
 #endif
 #ifndef KRR_HSEL_BAND
 #define KRR_HSEL_BAND 1  // hselect's first pass also collects a probe-estimated key band (0: off)
@@ -71,6 +89,8 @@
 // (KRR_PROBE_MIN_COMPACT, the rule for when the start-threshold probe pays: krr_plan.h)
 
 namespace krr {
+
+constexpr int kLdsBatch = KRR_LDS_BATCH;
 
 // Diagnostic build (-DKRR_DIAG): per-segment cycle and event counters written
 // to a buffer attached with krr_diag_attach(); never compiled into the product.
@@ -550,15 +570,15 @@ struct SelectProc {
     // min and max key of buf; four LDS reads in flight per lane.
     __device__ __forceinline__ void buf_minmax(uint64_t& mn_out, uint64_t& mx_out) const {
         uint64_t mn = ~0ull, mx = 0;
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : buf[0];
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 mn = x[t] < mn ? x[t] : mn;
                 mx = x[t] > mx ? x[t] : mx;
             }
@@ -575,15 +595,15 @@ struct SelectProc {
         const uint32_t sh = uni32(bits > 8 ? (uint32_t)(bits - 8) : 0u);
         for (uint32_t i = lane; i < 256; i += kWave) H[i] = 0;
         __syncthreads();
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : 0ull;
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < kLdsBatch; ++t)
                 if (base + t * kWave + lane < cnt && x[t] >= lo && x[t] <= hi)
                     atomicAdd(&H[(uint32_t)((x[t] - lo) >> sh)], 1u);
         }
@@ -635,15 +655,15 @@ struct SelectProc {
     // block start, so nothing unread is overwritten.
     __device__ __forceinline__ void filter(uint64_t nt, uint32_t inclusive) {
         uint32_t w = 0, e = 0;
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : 0ull;
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const bool in = base + t * kWave + lane < cnt;
                 const bool keep = in && (inclusive ? x[t] >= nt : x[t] > nt);
                 e += popc64(ballot(in && x[t] == nt));
@@ -694,15 +714,15 @@ struct SelectProc {
         }
         if (ct.lo == ct.hi) return ct.lo;
         uint32_t w = 0;
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : 0ull;
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const bool inb = base + t * kWave + lane < cnt && x[t] >= ct.lo && x[t] <= ct.hi;
                 const uint64_t m = ballot(inb);
                 if (inb) small[w + lane_prefix(m)] = x[t];
@@ -764,15 +784,15 @@ struct SelectProc {
             return;
         }
         uint32_t w = 0;
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : 0ull;
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const bool inb = base + t * kWave + lane < cnt && x[t] >= ct.lo && x[t] <= ct.hi;
                 const uint64_t m = ballot(inb);
                 if (inb) small[w + lane_prefix(m)] = x[t];
@@ -921,11 +941,16 @@ struct SelectArgs {
     int64_t p_num, p_den;
     double q;
     uint32_t cap;        // single-pass candidate capacity (keys); longer segments use hselect
+    uint32_t wcap;       // window select (wselect) capacity (keys)
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
     int64_t* rec = nullptr;  // optional 32-B result records (k_pack_records layout), CPU half
     unsigned long long* stats = nullptr;  // optional: [0] += segments wselect handed to hselect
+    // wselect misses: segment ids for the hselect pass that follows (k_hselect_list)
+    int64_t* fail_list = nullptr;
+    unsigned int* fail_count = nullptr;   // this launch's list length
+    unsigned int* fail_reset = nullptr;   // the previous launch's counter: zeroed for the next one
 };
 
 // One half of an object's 32-B record (k_pack_records layout): half 0 = CPU, 1 = memory.
@@ -1572,23 +1597,26 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
 #define KRR_WSEL 1
 #endif
 #ifndef KRR_WSEL_Z
-#define KRR_WSEL_Z 4.0
-#endif
-#ifndef KRR_WSEL_FIRST
-#define KRR_WSEL_FIRST 1024  // the first shrink comes once this many keys are held (later ones: a full buffer)
+#define KRR_WSEL_Z 4.5
 #endif
 #ifndef KRR_WSEL_BINS
 #define KRR_WSEL_BINS 1  // shrink to histogram-bin edges (one pass) instead of exact keys (0)
 #endif
-// hselect's LDS (histogram + collect buffer) holds this many window keys.
-constexpr uint32_t kWselCap = (uint32_t)(kHselectLds / 8) & ~63u;
+// Window keys in LDS.  Misses are finished by a separate hselect launch
+// (k_hselect_list), so the window kernel's LDS and registers are its own.
+constexpr uint32_t kWselCap = (uint32_t)KRR_WSEL_CAP & ~63u;
+constexpr uint32_t kWselCapLong = (uint32_t)KRR_WSEL_CAP_LONG & ~63u;
+static_assert(kWselCap >= kChunkElems + 256 && kWselCapLong >= kWselCap,
+              "the window buffer takes a chunk before its first shrink");
+// Per launch: more waves per CU for shorter segments (their fixed per-segment work
+// needs the overlap), a larger window for long ones (fewer shrinks).
+KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax) { return Lmax >= KRR_WSEL_LONG ? kWselCapLong : kWselCap; }
 
 struct WindowProc {
     SelectProc sp;            // buffer algebra (locate / kth / pair) over buf
     uint64_t* buf;
     int lane;
     uint32_t cap;
-    uint32_t limit;           // keys held before the next shrink: KRR_WSEL_FIRST, then cap
     uint32_t shrinks;
     uint64_t lo, hi, span;    // inclusive key window
     uint64_t lob;             // raw bits of lo (fast windows: inside [+0, +inf])
@@ -1675,22 +1703,25 @@ struct WindowProc {
         nan_l += nn;
         negnan_l += ng;
         seen += kChunkElems;
-        if (!point && cnt + kChunkElems > limit) shrink();
+        // room for the next chunk: a whole chunk while every key is a candidate, then
+        // twice this chunk's candidates (>= 256): the window's share of slots only falls
+        const uint32_t room = shrinks == 0 ? kChunkElems : (2 * C > 256 ? 2 * C : 256u);
+        if (!point && seen < (uint64_t)L && cnt + room > cap) shrink();
     }
 
     // Keep the buffer keys in [nl, nh] (in place); the dropped keys below nl join
     // below_extra.  A block of 4 x 64 keys is read before any survivor is written.
     __device__ __forceinline__ void filter_window(uint64_t nl, uint64_t nh) {
         uint32_t w = 0, dropped_below = 0;
-        for (uint32_t base = 0; base < cnt; base += 4 * kWave) {
-            uint64_t x[4];
+        for (uint32_t base = 0; base < cnt; base += kLdsBatch * kWave) {
+            uint64_t x[kLdsBatch];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const uint32_t i = base + t * kWave + lane;
                 x[t] = i < cnt ? buf[i] : 0ull;
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kLdsBatch; ++t) {
                 const bool inr = base + t * kWave + lane < cnt;
                 const bool keep = inr && x[t] >= nl && x[t] <= nh;
                 dropped_below += popc64(ballot(inr && x[t] < nl));
@@ -1706,7 +1737,6 @@ struct WindowProc {
 
     // Narrow the window around the target's estimated seen-rank (header comment).
     __device__ __forceinline__ void shrink() {
-        limit = cap;
         if (point || cnt == 0) return;
         const uint64_t nanc = wave_sum_u32(nan_l);
         const uint64_t below = (uint64_t)wave_sum_u32(below_l) - wave_sum_u32(negnan_l) + below_extra;
@@ -1780,7 +1810,11 @@ struct WindowProc {
     }
 };
 
-// One CPU segment by wselect; hselect_segment when the window misses.
+// One CPU segment by wselect.  A miss goes to hselect: inline (INLINE_FALLBACK,
+// the long-segment kernels, whose register budget holds both paths and whose
+// rare misses then overlap the other waves' work) or through the miss list that
+// k_hselect_list finishes after the launch (the 3-waves-per-SIMD kernels).
+template <bool INLINE_FALLBACK>
 __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
     const int64_t beg = A.offs[s], end = A.offs[s + 1];
     const int64_t L = end - beg;
@@ -1794,8 +1828,7 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
     W.sp.cnt = 0;
     W.sp.bad = 0;
     W.lane = lane;
-    W.cap = kWselCap;
-    W.limit = KRR_WSEL_FIRST < kWselCap ? KRR_WSEL_FIRST : kWselCap;
+    W.cap = A.wcap;
     W.shrinks = 0;
     W.cnt = 0;
     W.below_l = W.nan_l = W.negnan_l = 0;
@@ -1870,26 +1903,51 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
     __syncthreads();
     if (!done) {
         if (lane == 0 && A.stats) atomicAdd(A.stats, 1ull);
-        hselect_segment(A, s, smem, lane);
+        if constexpr (INLINE_FALLBACK) {
+            hselect_segment(A, s, smem, lane);
+        } else if (lane == 0) {
+            A.fail_list[atomicAdd(A.fail_count, 1u)] = s;  // finished by k_hselect_list
+        }
         return;
     }
     write_result(A, s, result, n, flags, lane);
     __syncthreads();
 }
 
+template <bool LONG>
 __device__ __forceinline__ void mid_select_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
-    if constexpr (KRR_WSEL) wselect_segment(A, s, smem, lane);
+    if constexpr (KRR_WSEL) wselect_segment<LONG>(A, s, smem, lane);
     else hselect_segment(A, s, smem, lane);
 }
 
-// k_select<false>: every segment in one pass (the launch's longest segment fits
-// A.cap keys); k_select<true>: every segment through hselect.  Separate kernels
-// keep each one's register allocation to its own path.
-template <bool HSEL>
-__global__ __launch_bounds__(64, HSEL ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_select(SelectArgs A) {
+// The segments wselect missed, by hselect (launched right after the window kernel
+// on the same stream).  With no misses every workgroup reads the count and exits.
+// The last workgroup to finish resets the list for the next launch.
+// Launches alternate between two counters: the window kernel of launch k + 1
+// zeroes launch k's (its fallback pass has finished by then, same stream), which
+// launch k + 2 counts into — no extra memset or completion counter per launch.
+__global__ __launch_bounds__(64, KRR_HSEL_WAVES_PER_SIMD) void k_hselect_list(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const unsigned int n = __builtin_nontemporal_load(A.fail_count);
+    for (unsigned int i = blockIdx.x; i < n; i += gridDim.x) hselect_segment(A, A.fail_list[i], smem, threadIdx.x);
+}
+
+// k_select<SEL_SINGLE>: every segment in one pass (the launch's longest segment fits
+// A.cap keys); k_select<SEL_WINDOW / SEL_WINDOW_LONG>: every segment through the
+// window select (hselect when KRR_WSEL is 0).  Separate kernels keep each one's
+// register allocation to its own path; the two window kernels differ only in their
+// occupancy bound (long segments: a larger window at 2 waves per SIMD).
+enum { SEL_SINGLE = 0, SEL_WINDOW = 1, SEL_WINDOW_LONG = 2 };
+constexpr int window_waves(bool longseg) {
+    return !KRR_WSEL ? KRR_HSEL_WAVES_PER_SIMD : (longseg ? KRR_HSEL_WAVES_PER_SIMD : KRR_WSEL_WAVES_PER_SIMD);
+}
+template <int KIND>
+__global__ __launch_bounds__(64, KIND == SEL_SINGLE ? KRR_SELECT_WAVES_PER_SIMD : window_waves(KIND == SEL_WINDOW_LONG))
+void k_select(SelectArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (KIND != SEL_SINGLE && A.fail_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.fail_reset = 0;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        if constexpr (HSEL) mid_select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
+        if constexpr (KIND != SEL_SINGLE) mid_select_segment<KIND == SEL_WINDOW_LONG>(A, xcd_item(s, A.S), smem, threadIdx.x);
         else select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
     }
 }
@@ -2076,20 +2134,24 @@ __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
 // The dispatcher hands out blocks in order, so the shorter memory-max blocks
 // fill CUs as the CPU blocks drain instead of leaving a partly idle last round
 // per kernel; one launch is also one roofline for the whole step.
-enum { CPU_SELECT = 0, CPU_REF_GAPS = 1, CPU_HSELECT = 2 };
+enum { CPU_SELECT = 0, CPU_REF_GAPS = 1, CPU_HSELECT = 2, CPU_HSELECT_LONG = 3 };  // HSELECT: window select
 
 template <int CPU_KIND>
-__global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? KRR_HSEL_WAVES_PER_SIMD : KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
+__global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? window_waves(false)
+                                : CPU_KIND == CPU_HSELECT_LONG ? window_waves(true)
+                                                               : KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t S_cpu = CPU_KIND == CPU_REF_GAPS ? R.S : A.S;
     const int64_t total = S_cpu + M.S;
+    constexpr bool kWindow = CPU_KIND == CPU_HSELECT || CPU_KIND == CPU_HSELECT_LONG;
+    if (kWindow && A.fail_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.fail_reset = 0;
     for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
         // remap within each resource's half, so the CPU items still all precede
         // the memory items in dispatch order
         if (b < S_cpu) {
             const int64_t s = xcd_item(b, S_cpu);
             if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, s, smem, threadIdx.x);
-            else if constexpr (CPU_KIND == CPU_HSELECT) mid_select_segment(A, s, smem, threadIdx.x);
+            else if constexpr (kWindow) mid_select_segment<CPU_KIND == CPU_HSELECT_LONG>(A, s, smem, threadIdx.x);
             else refindex_gaps_segment<true>(R, s, threadIdx.x);
         } else {
             max_segment<true>(M, xcd_item(b - S_cpu, M.S), threadIdx.x);
@@ -2721,6 +2783,10 @@ struct krr_ctx {
     int num_cus;
     size_t max_lds;
     unsigned long long* d_tmp;    // [0] scratch (max segment length), [1] stats: wselect fallbacks
+    unsigned int* d_fail_count;   // wselect miss list lengths: [epoch & 1]
+    unsigned int fail_epoch;
+    int64_t* d_fail_list;         // segment ids (capacity fail_cap)
+    int64_t fail_cap;
     char err[512];
 };
 
@@ -2809,9 +2875,35 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->out_n = on;
     A->out_f = of;
     A->stats = ctx->d_tmp + 1;
-    *lds = kSelectLdsFixed + (hsel ? kHselectLds : (size_t)cap * 8);
+    A->wcap = wsel_cap_for(Lmax);
+    if (hsel && KRR_WSEL && A->wcap != kWselCapLong) {  // misses: a list for the hselect launch that follows
+        if (ctx->fail_cap < series->n_segments) {
+            if (ctx->d_fail_list) KRR_HIP(ctx, hipFree(ctx->d_fail_list));
+            ctx->d_fail_list = nullptr;
+            ctx->fail_cap = 0;
+            KRR_HIP(ctx, hipMalloc(&ctx->d_fail_list, (size_t)series->n_segments * sizeof(int64_t)));
+            ctx->fail_cap = series->n_segments;
+        }
+        A->fail_list = ctx->d_fail_list;
+        const unsigned int e = ctx->fail_epoch++ & 1u;
+        A->fail_count = ctx->d_fail_count + e;
+        A->fail_reset = ctx->d_fail_count + (e ^ 1u);
+    }
+    // the long kernels finish misses inline: hselect's LDS too
+    const size_t wlds = A->wcap == kWselCapLong ? ((size_t)A->wcap * 8 > kHselectLds ? (size_t)A->wcap * 8 : kHselectLds)
+                                                : (size_t)A->wcap * 8;
+    *lds = kSelectLdsFixed + (hsel ? (KRR_WSEL ? wlds : kHselectLds) : (size_t)cap * 8);
     if (*lds < (size_t)KRR_LDS_MIN) *lds = (size_t)KRR_LDS_MIN;
     if (*lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "select needs %s%lld B of LDS", "", (long long)*lds);
+    return KRR_OK;
+}
+
+// After a window-select launch: hselect over the segments it missed (none, usually).
+int launch_fallback(krr_ctx* ctx, const SelectArgs& A, int64_t S, hipStream_t st) {
+    if (!A.fail_list) return KRR_OK;
+    const int64_t g = S < (int64_t)KRR_FALLBACK_GRID ? S : (int64_t)KRR_FALLBACK_GRID;
+    hipLaunchKernelGGL(k_hselect_list, dim3((unsigned)g), dim3(64), kSelectLdsFixed + kHselectLds, st, A);
+    KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
 
@@ -2854,21 +2946,27 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->num_cus = prop.multiProcessorCount;
     c->max_lds = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 65536;
     if (c->max_lds > 163840) c->max_lds = 163840;
+    c->d_fail_count = nullptr;
+    c->fail_epoch = 0;
+    c->d_fail_list = nullptr;
+    c->fail_cap = 0;
     if (hipMalloc(&c->d_tmp, 2 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_tmp, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMemset(c->d_tmp, 0, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_fail_count, 2 * sizeof(unsigned int)) != hipSuccess ||
+        hipMemset(c->d_fail_count, 0, 2 * sizeof(unsigned int)) != hipSuccess) {
+        if (c->d_tmp) (void)hipFree(c->d_tmp);
+        if (c->d_fail_count) (void)hipFree(c->d_fail_count);
         delete c;
         return KRR_E_HIP;
     }
 
-    (void)hipFuncSetAttribute((const void*)k_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)c->max_lds);
-    (void)hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)c->max_lds);
-    (void)hipFuncSetAttribute((const void*)k_simple<CPU_SELECT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
-    (void)hipFuncSetAttribute((const void*)k_simple<CPU_HSELECT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
+    for (const void* f : {(const void*)k_select<SEL_SINGLE>, (const void*)k_select<SEL_WINDOW>,
+                          (const void*)k_select<SEL_WINDOW_LONG>, (const void*)k_simple<CPU_SELECT>,
+                          (const void*)k_simple<CPU_HSELECT>, (const void*)k_simple<CPU_HSELECT_LONG>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     (void)hipFuncSetAttribute((const void*)k_sketch_build, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)c->max_lds);
+    (void)hipFuncSetAttribute((const void*)k_hselect_list, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -2878,6 +2976,8 @@ int krr_destroy(krr_ctx* ctx) {
     if (!ctx) return KRR_OK;
     DeviceGuard g(ctx->device);
     if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
+    if (ctx->d_fail_count) (void)hipFree(ctx->d_fail_count);
+    if (ctx->d_fail_list) (void)hipFree(ctx->d_fail_list);
     delete ctx;
     return KRR_OK;
 }
@@ -2913,10 +3013,11 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
     size_t lds = 0;
     rc = plan_select(ctx, series, params, st, out_value, out_count, out_flags, &A, &lds);
     if (rc) return rc;
-    if (A.cap) hipLaunchKernelGGL(k_select<false>, dim3(grid_for(S)), dim3(64), lds, st, A);
-    else hipLaunchKernelGGL(k_select<true>, dim3(grid_for(S)), dim3(64), lds, st, A);
+    if (A.cap) hipLaunchKernelGGL(k_select<SEL_SINGLE>, dim3(grid_for(S)), dim3(64), lds, st, A);
+    else if (A.wcap == kWselCapLong) hipLaunchKernelGGL(k_select<SEL_WINDOW_LONG>, dim3(grid_for(S)), dim3(64), lds, st, A);
+    else hipLaunchKernelGGL(k_select<SEL_WINDOW>, dim3(grid_for(S)), dim3(64), lds, st, A);
     KRR_HIP(ctx, hipGetLastError());
-    return KRR_OK;
+    return launch_fallback(ctx, A, S, st);
 }
 
 int krr_segmented_max(krr_ctx* ctx, const krr_series* series, double* out_value, int64_t* out_count,
@@ -2982,7 +3083,11 @@ int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series
         if (rc) return rc;
         A.rec = records;
         if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
+        else if (A.wcap == kWselCapLong)
+            hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
         else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
+        KRR_HIP(ctx, hipGetLastError());
+        return launch_fallback(ctx, A, S, st);
     }
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
@@ -3287,7 +3392,8 @@ int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params
     out->bottom = (int32_t)sp.bottom;
     out->tkeep = sp.tkeep;
     out->cap_keys = hsel ? 0 : need;
-    out->lds_bytes = (int64_t)kSelectLdsFixed + (int64_t)(hsel ? kHselectLds : (size_t)need * 8);
+    out->lds_bytes = (int64_t)kSelectLdsFixed +
+                     (int64_t)(hsel ? (KRR_WSEL ? (size_t)wsel_cap_for(Lmax) * 8 : kHselectLds) : (size_t)need * 8);
 #if KRR_SELECT_PROBE
     out->probe = (!hsel && !sp.bottom && select_probe_pays(Lmax, sp.tkeep, need)) ? 1 : 0;
 #endif

@@ -35,11 +35,13 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.init()
     base = _native.load_library()
-    names = ("krr_create", "krr_segmented_percentile", "krr_segmented_max", "krr_simple_run")
+    names = ("krr_create", "krr_segmented_percentile", "krr_segmented_max", "krr_simple_run", "krr_get_stats")
     libs = []
     for path in a.libs:
         lib = ctypes.CDLL(os.path.abspath(path))
         for name in names:
+            if not hasattr(lib, name):
+                continue
             getattr(lib, name).argtypes = getattr(base, name).argtypes
             getattr(lib, name).restype = ctypes.c_int
         h = ctypes.c_void_p()
@@ -109,9 +111,15 @@ def main():
         gm = o[name][3][:m].cpu().numpy()
         ok = bool(np.all((got.view(np.uint64) == ov.view(np.uint64)) | ((got == 0) & (ov == 0)))
                   and np.array_equal(gm, mvo, equal_nan=True))
+        fb = ""
+        lib_h = next((lb, hh) for nm, lb, hh in libs if nm == name)
+        if hasattr(lib_h[0], "krr_get_stats"):
+            v = ctypes.c_int64()
+            lib_h[0].krr_get_stats(lib_h[1], ctypes.byref(v))
+            fb = f" | fallbacks {v.value / (2 * a.rounds) / S:.4%}"
         print(f"{name:28s} pct {t['pct']:.4f} ms ({seg_bytes / t['pct'] / 1e6:.0f} GB/s) | "
               f"max {t['max']:.4f} ms ({seg_bytes / t['max'] / 1e6:.0f} GB/s) | "
-              f"fused {t['fused']:.4f} ms ({2 * seg_bytes / t['fused'] / 1e6:.0f} GB/s) | parity {ok}", flush=True)
+              f"fused {t['fused']:.4f} ms ({2 * seg_bytes / t['fused'] / 1e6:.0f} GB/s) | parity {ok}{fb}", flush=True)
 
 
 if __name__ == "__main__":

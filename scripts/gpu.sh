@@ -52,7 +52,7 @@ print(sys.argv[2] or "default", "value", round(d["value"]), "ms", round(d["ms_pe
 EOF
       ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof${n:+_$n}" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof${n:+_$n}" -o run -- \
         python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline $args > "$OUT/prof${n:+_$n}.log" 2>&1 \
         || { echo "prof $args failed"; tail -20 "$OUT/prof${n:+_$n}.log"; exit 1; }
       f=$(find "$OUT/prof${n:+_$n}" -name '*kernel_stats.csv' | head -1)
@@ -61,7 +61,7 @@ EOF
       ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 120 rocprofv3 --pmc "$c" -d "$OUT/pmc${n:+_$n}_$c" -o run -- \
+        timeout -s KILL 120 rocprofv3 --pmc "$c" --output-format csv -d "$OUT/pmc${n:+_$n}_$c" -o run -- \
           python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $args > "$OUT/pmc${n:+_$n}_$c.log" 2>&1 \
           || { echo "pmc $c $args failed"; tail -20 "$OUT/pmc${n:+_$n}_$c.log"; exit 1; }
       done

@@ -237,3 +237,36 @@ def test_parse_series_labels_and_first_match():
     plan = FleetQueryPlan([Obj("n", "c", ['a"b'])])
     s = plan.pack([json.dumps(doc).encode()])
     assert s.values.tolist() == [1.0, 0.002]
+
+
+@pytest.mark.parametrize("max_samples", [10_000, 25_000, 1])
+@pytest.mark.parametrize("resource", list(ResourceType))
+def test_sample_bounded_groups_keep_the_per_pod_csr(resource, max_samples):
+    """Groups split by expected samples (pods x series_per_pod x points <= max_query_samples)
+    still pack to the per-pod CSR byte for byte."""
+    objects, prom = make_fleet()
+    points = 1000
+    plan = FleetQueryPlan(objects, points_per_series=points, max_query_samples=max_samples, series_per_pod=2)
+    cap = max(1, max_samples // (points * 2))
+    assert all(1 <= len(g.pods) <= cap for g in plan.groups)
+    grouped = [prom.query_range(q) for q in plan.queries(resource)]
+    got = plan.pack(grouped)
+    exp = pack_query_range_bodies(per_pod_bodies(objects, prom, resource))
+    np.testing.assert_array_equal(got.offsets, exp.offsets)
+    assert got.values.tobytes() == exp.values.tobytes()
+    unbounded = FleetQueryPlan(objects)
+    assert len(plan.groups) >= len(unbounded.groups)
+
+
+def test_plan_for_settings_counts_points():
+    from krr_amd.strategies.simple import SimpleStrategySettings
+
+    objects, _ = make_fleet()
+    plan = FleetQueryPlan.for_settings(objects, SimpleStrategySettings())  # 336 h @ 15 min
+    assert plan.points_per_series == 336 * 4 + 1
+    big = [Obj("ns", "c", [f"p{i}" for i in range(20_000)])]
+    pods_per_group = [len(g.pods) for g in FleetQueryPlan.for_settings(big, SimpleStrategySettings(),
+                                                                       max_query_chars=10**9).groups]
+    assert max(pods_per_group) == 50_000_000 // (1345 * 4) and sum(pods_per_group) == 20_000
+    with pytest.raises(ValueError):
+        FleetQueryPlan(objects, points_per_series=-1)
