@@ -10,6 +10,9 @@
 #   prof:ARGS    the same for bench.py ARGS
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of the default bench (separate runs)
 #   pmc:ARGS     the same for bench.py ARGS
+#   ab:ARGS      same-process A/B of every krr_amd/lib/variants/lib_*.so (scripts/build_variants.sh)
+#                on the ab_variants.py workload ARGS, e.g. ab:--config,3,--percentile,50
+#   diag:ARGS    per-segment phase breakdown with krr_amd/lib/variants/lib_diag.so (-DKRR_DIAG)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -u
 TAG=${1:?tag}
@@ -65,6 +68,17 @@ EOF
           python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $args > "$OUT/pmc${n:+_$n}_$c.log" 2>&1 \
           || { echo "pmc $c $args failed"; tail -20 "$OUT/pmc${n:+_$n}_$c.log"; exit 1; }
       done
+      ;;
+    ab)
+      libs=$(ls krr_amd/lib/variants/lib_*.so | grep -v lib_diag)
+      timeout -k 10 300 python -u scripts/ab_variants.py $libs $args > "$OUT/ab${n:+_$n}.log" 2>&1 \
+        || { echo "ab $args failed"; tail -20 "$OUT/ab${n:+_$n}.log"; exit 1; }
+      echo "== ab $args"; grep fused "$OUT/ab${n:+_$n}.log"
+      ;;
+    diag)
+      timeout -k 10 120 python -u scripts/diag_select.py krr_amd/lib/variants/lib_diag.so $args \
+        > "$OUT/diag${n:+_$n}.log" 2>&1 || { echo "diag $args failed"; tail -20 "$OUT/diag${n:+_$n}.log"; exit 1; }
+      echo "== diag $args"; grep -E "kernel|total|compact |final|n_compact|n_fallback|inserted|shares" "$OUT/diag${n:+_$n}.log"
       ;;
     *)
       echo "unknown step $step"; exit 2 ;;
