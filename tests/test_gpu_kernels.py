@@ -406,10 +406,13 @@ def test_select_probe_start_threshold(ctx, mode):
 
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
 def test_select_probe_large_buffer(ctx, mode):
-    """Launches whose longest segment is >= 12x the needed capacity run p95-p97 of 7d@1m x 5
-    pods (50,400 slots, ~2,500 kept keys) single-pass with a buffer of up to 3,264 keys behind
-    the start-threshold probe (krr_plan.h single_pass_ok): hits, a probe that sees only huge
-    values (re-stream), only tiny values, gaps, and a short segment sharing the launch."""
+    """Launches whose longest segment is >= 12x the needed capacity run p94-p97 of 7d@1m x 5
+    pods (50,400 slots, ~2,500-3,030 kept keys) single-pass with a buffer of up to 3,712 keys
+    behind the start-threshold probe (krr_plan.h single_pass_ok; the plan itself is pinned by
+    tests/test_abi.py::test_select_plan_decisions_config2): hits, a probe that sees only huge
+    values (re-stream), only tiny values, gaps, and a short segment sharing the launch.  p5 / p6
+    keep the BOTTOM ~2,500-3,000 keys, for which there is no probe: those launches take the
+    window select instead."""
     rng = np.random.default_rng(97)
     L = 50400
     ps = _select_probe_slots(L)
@@ -433,7 +436,7 @@ def test_select_probe_large_buffer(ctx, mode):
         chosen = [(nm, v) for nm, v, g_ in segs if g_ == gaps]
         vals = np.concatenate([v for _, v in chosen])
         offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
-        for pct in [(94, 1), (95, 1), (96, 1), (97, 1), (9549, 100)]:
+        for pct in [(94, 1), (95, 1), (96, 1), (97, 1), (9549, 100), (5, 1), (6, 1)]:
             got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
             want = _oracle(vals, offs, mode, *pct, gaps=gaps)
             for i, (nm, _) in enumerate(chosen):
