@@ -1612,6 +1612,12 @@ static_assert(kWselCap >= kChunkElems + 256 && kWselCapLong >= kWselCap,
 // needs the overlap), a larger window for long ones (fewer shrinks).
 KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax) { return Lmax >= KRR_WSEL_LONG ? kWselCapLong : kWselCap; }
 
+enum { WIN_GENERAL = 0, WIN_FAST = 1, WIN_FULL = 2 };  // window classify modes (WindowProc::classify)
+
+// LANE_COUNTS: below / NaN counts per lane in VALU (the long-segment kernels: their
+// gapped layouts put NaNs in many chunks, and at 2 waves per SIMD the stream, not
+// the vector unit, bounds them); otherwise scalar ballot popcounts (see classify).
+template <bool LANE_COUNTS>
 struct WindowProc {
     SelectProc sp;            // buffer algebra (locate / kth / pair) over buf
     uint64_t* buf;
@@ -1620,9 +1626,10 @@ struct WindowProc {
     uint32_t shrinks;
     uint64_t lo, hi, span;    // inclusive key window
     uint64_t lob;             // raw bits of lo (fast windows: inside [+0, +inf])
-    uint32_t fast, point;
+    uint32_t fast, full, point;
     uint32_t cnt;             // window keys seen (stored unless point)
-    uint32_t below_l, nan_l, negnan_l;  // per lane, committed chunks only
+    uint64_t below_u, nan_u;  // present samples below the window, NaN slots (committed chunks)
+    uint32_t below_l, nan_l, negnan_l;  // LANE_COUNTS: per lane (below_l includes negative NaNs)
     uint64_t below_extra;     // keys dropped below lo by shrinks (uniform)
     uint64_t seen;            // slots of committed chunks (uniform; padding included)
     int64_t L;
@@ -1637,38 +1644,110 @@ struct WindowProc {
         hi = uni64(h);
         span = hi - lo;
         fast = (lo >= kKeyPosZero && hi <= kKeyPosInf) ? 1u : 0u;
+        full = (lo <= kKeyNegInf && hi >= kKeyPosInf) ? 1u : 0u;
         lob = lo ^ kSignBit;
         point = lo == hi ? 1u : 0u;
     }
 
-    // Classify the slots of smask: per-lane window mask (slot j -> bit 15 - j),
-    // and this lane's below / NaN / negative-NaN counts (not yet committed).
+    // Classify a chunk: per-lane window mask (slot j -> bit 15 - j) and the chunk's
+    // below / NaN counts (not yet committed).  The counts are ballot popcounts, so
+    // the scalar unit adds them up beside the vector work (the classify loop is
+    // what bounds mid percentiles of short series: VALU-issue, not HBM).
+    //   WIN_FULL     the window is every key (before the first shrink): in = not NaN;
+    //   WIN_FAST     the window lies inside [+0, +inf]: one unsigned range test on the
+    //                raw bits; "below" is a signed compare (every negative, negative
+    //                NaNs too); NaN slots are only ORed into a mask, and a chunk that
+    //                holds one is recounted (rare outside gapped layouts);
+    //   WIN_GENERAL  order-preserving keys.
+    template <int MODE>
+    __device__ __forceinline__ uint32_t classify(const double2 (&c)[kUnroll], uint32_t& b, uint32_t& nn) const {
+        uint32_t vm = 0;
+        b = nn = 0;
+        uint64_t anynan = 0;
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const double v = slot_val(c, j);
+            const uint64_t x = dbits(v);
+            bool in;
+            if constexpr (MODE == WIN_FULL) {
+                in = !__builtin_isnan(v);
+                nn += popc64(ballot(!in));
+            } else if constexpr (MODE == WIN_FAST) {
+                in = (x - lob) <= span;                          // rejects negatives and NaNs
+                b += popc64(ballot((int64_t)x < (int64_t)lob));  // negatives (incl. -0) are below
+                anynan |= ballot(__builtin_isnan(v));
+            } else {
+                const bool nan = __builtin_isnan(v);
+                const uint64_t key = okey(x);
+                in = (key - lo) <= span;                         // NaN keys lie outside [okey(-inf), okey(+inf)]
+                b += popc64(ballot(key < lo && !nan));
+                nn += popc64(ballot(nan));
+            }
+            vm = (vm << 1) | (in ? 1u : 0u);
+        }
+        if (MODE == WIN_FAST && anynan) {
+#pragma unroll
+            for (int j = 0; j < 2 * kUnroll; ++j) {
+                const double v = slot_val(c, j);
+                const bool nan = __builtin_isnan(v);
+                nn += popc64(ballot(nan));
+                b -= popc64(ballot(nan && (int64_t)dbits(v) < 0));  // negative NaNs were counted below
+            }
+        }
+        return vm;
+    }
+
+    // Append the chunk's window keys (vm) at pos: predicated LDS writes, a
+    // non-candidate writes this lane's scratch slot.  Keys of a fast window are
+    // non-negative numbers: okey is the sign bit.
+    template <int MODE>
+    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], uint32_t vm, uint32_t pos) {
+        uint64_t* const scratch = sp.small + lane;
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const uint64_t x = dbits(slot_val(c, j));
+            const uint32_t bit = (vm >> (2 * kUnroll - 1 - j)) & 1u;
+            uint64_t* const dst = bit ? buf + pos : scratch;
+            *dst = MODE == WIN_FAST ? (x | kSignBit) : okey(x);
+            pos += bit;
+        }
+    }
+
+    // LANE_COUNTS classify: per-lane below / NaN / negative-NaN counts.
     template <bool FAST>
-    __device__ __forceinline__ uint32_t classify(const double2 (&c)[kUnroll], uint32_t smask, uint32_t& b,
-                                                 uint32_t& nn, uint32_t& ng) const {
+    __device__ __forceinline__ uint32_t classify_lanes(const double2 (&c)[kUnroll], uint32_t& b, uint32_t& nn,
+                                                       uint32_t& ng) const {
         uint32_t vm = 0;
         b = nn = ng = 0;
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             const uint64_t x = dbits(slot_val(c, j));
-            const bool on = (smask >> j) & 1u;  // wave-uniform
             const bool nan = is_nan_bits(x);
             bool in, below;
             if (FAST) {
-                in = (x - lob) <= span;                      // rejects negatives and NaNs
-                below = (int64_t)x < (int64_t)lob;           // negatives (incl. -0, negative NaNs) are below
+                in = (x - lob) <= span;             // rejects negatives and NaNs
+                below = (int64_t)x < (int64_t)lob;  // negatives (incl. -0, negative NaNs) are below
             } else {
                 const uint64_t key = okey(x);
-                in = (key - lo) <= span;                     // NaN keys lie outside [okey(-inf), okey(+inf)]
-                below = key < lo;                            // + negative NaNs, removed via ng
+                in = (key - lo) <= span;            // NaN keys lie outside [okey(-inf), okey(+inf)]
+                below = key < lo;                   // + negative NaNs, removed via ng
             }
-            in = in && on;
             vm = (vm << 1) | (in ? 1u : 0u);
-            b += (on && below) ? 1u : 0u;
-            nn += (on && nan) ? 1u : 0u;
-            ng += (on && nan && (x >> 63)) ? 1u : 0u;
+            b += below ? 1u : 0u;
+            nn += nan ? 1u : 0u;
+            ng += (nan && (x >> 63)) ? 1u : 0u;
         }
         return vm;
+    }
+
+    // Present samples below the window and NaN slots of the committed chunks.
+    __device__ __forceinline__ uint64_t below_total() const {
+        if constexpr (LANE_COUNTS) return (uint64_t)wave_sum_u32(below_l) - wave_sum_u32(negnan_l) + below_extra;
+        return below_u + below_extra;
+    }
+    __device__ __forceinline__ uint64_t nan_total() const {
+        if constexpr (LANE_COUNTS) return wave_sum_u32(nan_l);
+        return nan_u;
     }
 
     // Every chunk fits: the buffer is shrunk right after a chunk that leaves less than
@@ -1676,9 +1755,17 @@ struct WindowProc {
     // window crowded by a few repeated keys can overflow: then the segment falls back.
     __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
         if (uni32(fail)) return;
-        uint32_t b, nn, ng, vm;
-        if (uni32(fast)) vm = classify<true>(c, 0xFFFFu, b, nn, ng);
-        else vm = classify<false>(c, 0xFFFFu, b, nn, ng);
+        uint32_t b, nn, ng = 0, vm, mode;
+        if constexpr (LANE_COUNTS) {
+            mode = uni32(fast) ? WIN_FAST : WIN_GENERAL;
+            if (mode == WIN_FAST) vm = classify_lanes<true>(c, b, nn, ng);
+            else vm = classify_lanes<false>(c, b, nn, ng);
+        } else {
+            mode = uni32(full) ? WIN_FULL : (uni32(fast) ? WIN_FAST : WIN_GENERAL);
+            if (mode == WIN_FAST) vm = classify<WIN_FAST>(c, b, nn);
+            else if (mode == WIN_FULL) vm = classify<WIN_FULL>(c, b, nn);
+            else vm = classify<WIN_GENERAL>(c, b, nn);
+        }
         const uint32_t vc = __popc(vm);
         const uint32_t incl = wave_scan32(vc, 0u, OpAdd32{});
         const uint32_t C = lane_bcast32(incl, kWave - 1);
@@ -1687,21 +1774,18 @@ struct WindowProc {
             return;
         }
         if (C && !point) {
-            uint32_t pos = cnt + incl - vc;
-            uint64_t* const scratch = sp.small + lane;
-#pragma unroll
-            for (int j = 0; j < 2 * kUnroll; ++j) {
-                const uint64_t x = dbits(slot_val(c, j));
-                const uint32_t bit = (vm >> (2 * kUnroll - 1 - j)) & 1u;
-                uint64_t* const dst = bit ? buf + pos : scratch;
-                *dst = okey(x);
-                pos += bit;
-            }
+            if (mode == WIN_FAST) insert<WIN_FAST>(c, vm, cnt + incl - vc);
+            else insert<WIN_GENERAL>(c, vm, cnt + incl - vc);
         }
         cnt = uni32(cnt + C);
-        below_l += b;
-        nan_l += nn;
-        negnan_l += ng;
+        if constexpr (LANE_COUNTS) {
+            below_l += b;
+            nan_l += nn;
+            negnan_l += ng;
+        } else {
+            below_u += b;
+            nan_u += nn;
+        }
         seen += kChunkElems;
         // room for the next chunk: a whole chunk while every key is a candidate, then
         // twice this chunk's candidates (>= 256): the window's share of slots only falls
@@ -1738,8 +1822,8 @@ struct WindowProc {
     // Narrow the window around the target's estimated seen-rank (header comment).
     __device__ __forceinline__ void shrink() {
         if (point || cnt == 0) return;
-        const uint64_t nanc = wave_sum_u32(nan_l);
-        const uint64_t below = (uint64_t)wave_sum_u32(below_l) - wave_sum_u32(negnan_l) + below_extra;
+        const uint64_t nanc = nan_total();
+        const uint64_t below = below_total();
         const uint64_t S = seen - nanc;  // present samples seen
         const double U = L > (int64_t)seen ? (double)(L - (int64_t)seen) : 0.0;
         // q from the kernel's scalars here, not a per-segment value the compiler would
@@ -1818,7 +1902,7 @@ template <bool INLINE_FALLBACK>
 __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, unsigned char* smem, int lane) {
     const int64_t beg = A.offs[s], end = A.offs[s + 1];
     const int64_t L = end - beg;
-    WindowProc W;
+    WindowProc<INLINE_FALLBACK> W;
     W.buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
     W.sp.buf = W.buf;
     W.sp.H = reinterpret_cast<uint32_t*>(smem);
@@ -1831,6 +1915,7 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
     W.cap = A.wcap;
     W.shrinks = 0;
     W.cnt = 0;
+    W.below_u = W.nan_u = 0;
     W.below_l = W.nan_l = W.negnan_l = 0;
     W.below_extra = 0;
     W.seen = 0;
@@ -1848,7 +1933,7 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
     asm volatile("" : "+s"(b), "+s"(e));
     const uint32_t pad = stream_segment<true>(A.vals, b, e, W, lane);
     __syncthreads();
-    const uint64_t nnan = (uint64_t)wave_sum_u32(W.nan_l) - pad;
+    const uint64_t nnan = W.nan_total() - pad;
     const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;
     uint32_t flags = 0;
     double result = bitsd(kQuietNaN);
@@ -1866,7 +1951,7 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
         done = true;
     } else {
         const Ranks R = ranks_for(A, n);
-        const uint64_t below = (uint64_t)wave_sum_u32(W.below_l) - wave_sum_u32(W.negnan_l) + W.below_extra;
+        const uint64_t below = W.below_total();
         if (below <= (uint64_t)R.r0 && (uint64_t)R.r1 < below + W.cnt) {
             uint64_t k0, k1;
             if (W.point) {

@@ -12,6 +12,7 @@
 #   pmc:ARGS     the same for bench.py ARGS
 #   ab:ARGS      same-process A/B of every krr_amd/lib/variants/lib_*.so (scripts/build_variants.sh)
 #                on the ab_variants.py workload ARGS, e.g. ab:--config,3,--percentile,50
+#   sq:ARGS      SQ issue / wait counters (two rocprofv3 --pmc passes) of the ab_variants.py workload
 #   diag:ARGS    per-segment phase breakdown with krr_amd/lib/variants/lib_diag.so (-DKRR_DIAG)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -u
@@ -79,6 +80,20 @@ EOF
       timeout -k 10 120 python -u scripts/diag_select.py krr_amd/lib/variants/lib_diag.so $args \
         > "$OUT/diag${n:+_$n}.log" 2>&1 || { echo "diag $args failed"; tail -20 "$OUT/diag${n:+_$n}.log"; exit 1; }
       echo "== diag $args"; grep -E "kernel|total|compact |final|n_compact|n_fallback|inserted|shares" "$OUT/diag${n:+_$n}.log"
+      ;;
+    sq)
+      # SQ issue / wait counters of every kernel of the ab_variants.py workload ARGS, run on
+      # the in-tree library (SQLIB overrides); two separate passes (8 SQ counters each at most)
+      lib=${SQLIB:-krr_amd/lib/libkrr_amd.so}
+      i=0
+      for cs in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU" \
+                "SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC"; do
+        i=$((i + 1))
+        timeout -s KILL 120 rocprofv3 --pmc $cs --output-format csv -d "$OUT/sq${n:+_$n}_$i" -o run -- \
+          python3 scripts/ab_variants.py $lib $args --rounds 2 > "$OUT/sq${n:+_$n}_$i.log" 2>&1 \
+          || { echo "sq pass $i $args failed"; tail -20 "$OUT/sq${n:+_$n}_$i.log"; exit 1; }
+      done
+      python3 scripts/pmc_summary.py "$OUT" > "$OUT/sq${n:+_$n}.txt" 2>&1 && cat "$OUT/sq${n:+_$n}.txt"
       ;;
     *)
       echo "unknown step $step"; exit 2 ;;
