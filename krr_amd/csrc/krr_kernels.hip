@@ -1649,10 +1649,10 @@ struct WindowProc {
         point = lo == hi ? 1u : 0u;
     }
 
-    // Classify a chunk: per-lane window mask (slot j -> bit 15 - j) and the chunk's
-    // below / NaN counts (not yet committed).  The counts are ballot popcounts, so
-    // the scalar unit adds them up beside the vector work (the classify loop is
-    // what bounds mid percentiles of short series: VALU-issue, not HBM).
+    // Classify a chunk: per-slot window bits (in[j] = 1: slot j's key is in the window)
+    // and the chunk's below / NaN counts (not yet committed).  The counts are ballot
+    // popcounts, so the scalar unit adds them up beside the vector work: the chunk loop
+    // is what bounds mid percentiles of short series (VALU issue, not HBM).
     //   WIN_FULL     the window is every key (before the first shrink): in = not NaN;
     //   WIN_FAST     the window lies inside [+0, +inf]: one unsigned range test on the
     //                raw bits; "below" is a signed compare (every negative, negative
@@ -1660,30 +1660,34 @@ struct WindowProc {
     //                holds one is recounted (rare outside gapped layouts);
     //   WIN_GENERAL  order-preserving keys.
     template <int MODE>
-    __device__ __forceinline__ uint32_t classify(const double2 (&c)[kUnroll], uint32_t& b, uint32_t& nn) const {
-        uint32_t vm = 0;
+    __device__ __forceinline__ void classify(const double2 (&c)[kUnroll], uint32_t (&in)[2 * kUnroll], uint32_t& b,
+                                             uint32_t& nn) const {
         b = nn = 0;
         uint64_t anynan = 0;
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             const double v = slot_val(c, j);
             const uint64_t x = dbits(v);
-            bool in;
+            bool w;
             if constexpr (MODE == WIN_FULL) {
-                in = !__builtin_isnan(v);
-                nn += popc64(ballot(!in));
+                w = !__builtin_isnan(v);
+                nn += popc64(ballot(!w));
             } else if constexpr (MODE == WIN_FAST) {
-                in = (x - lob) <= span;                          // rejects negatives and NaNs
+                w = (x - lob) <= span;                           // rejects negatives and NaNs
                 b += popc64(ballot((int64_t)x < (int64_t)lob));  // negatives (incl. -0) are below
                 anynan |= ballot(__builtin_isnan(v));
             } else {
                 const bool nan = __builtin_isnan(v);
                 const uint64_t key = okey(x);
-                in = (key - lo) <= span;                         // NaN keys lie outside [okey(-inf), okey(+inf)]
+                w = (key - lo) <= span;                          // NaN keys lie outside [okey(-inf), okey(+inf)]
                 b += popc64(ballot(key < lo && !nan));
                 nn += popc64(ballot(nan));
             }
-            vm = (vm << 1) | (in ? 1u : 0u);
+            // materialised here: a mask held in scalar registers until after the
+            // mode branches would be sixteen 64-bit SGPR pairs
+            uint32_t t = w ? 1u : 0u;
+            asm volatile("" : "+v"(t));
+            in[j] = t;
         }
         if (MODE == WIN_FAST && anynan) {
 #pragma unroll
@@ -1694,50 +1698,49 @@ struct WindowProc {
                 b -= popc64(ballot(nan && (int64_t)dbits(v) < 0));  // negative NaNs were counted below
             }
         }
-        return vm;
     }
 
-    // Append the chunk's window keys (vm) at pos: predicated LDS writes, a
-    // non-candidate writes this lane's scratch slot.  Keys of a fast window are
-    // non-negative numbers: okey is the sign bit.
+    // Append the chunk's window keys (in[]) from buffer index pos on: predicated LDS
+    // writes, a slot outside the window writes this lane's scratch slot (the address
+    // is scratch + in * (next - scratch): one 24-bit multiply-add).  Keys of a fast
+    // window are non-negative numbers: okey is the sign bit.
     template <int MODE>
-    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], uint32_t vm, uint32_t pos) {
-        uint64_t* const scratch = sp.small + lane;
+    __device__ __forceinline__ void insert(const double2 (&c)[kUnroll], const uint32_t (&in)[2 * kUnroll],
+                                           uint32_t pos) {
+        unsigned char* const scratch = reinterpret_cast<unsigned char*>(sp.small + lane);
+        uint32_t d = (uint32_t)(reinterpret_cast<unsigned char*>(buf + pos) - scratch);  // > 0: buf lies above small
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             const uint64_t x = dbits(slot_val(c, j));
-            const uint32_t bit = (vm >> (2 * kUnroll - 1 - j)) & 1u;
-            uint64_t* const dst = bit ? buf + pos : scratch;
-            *dst = MODE == WIN_FAST ? (x | kSignBit) : okey(x);
-            pos += bit;
+            *reinterpret_cast<uint64_t*>(scratch + __umul24(in[j], d)) = MODE == WIN_FAST ? (x | kSignBit) : okey(x);
+            d += in[j] << 3;
+            asm volatile("" : "+v"(d));  // a running offset: not re-derived from prefix sums of in[]
         }
     }
 
     // LANE_COUNTS classify: per-lane below / NaN / negative-NaN counts.
     template <bool FAST>
-    __device__ __forceinline__ uint32_t classify_lanes(const double2 (&c)[kUnroll], uint32_t& b, uint32_t& nn,
-                                                       uint32_t& ng) const {
-        uint32_t vm = 0;
+    __device__ __forceinline__ void classify_lanes(const double2 (&c)[kUnroll], uint32_t (&in)[2 * kUnroll],
+                                                   uint32_t& b, uint32_t& nn, uint32_t& ng) const {
         b = nn = ng = 0;
 #pragma unroll
         for (int j = 0; j < 2 * kUnroll; ++j) {
             const uint64_t x = dbits(slot_val(c, j));
             const bool nan = is_nan_bits(x);
-            bool in, below;
+            bool w, below;
             if (FAST) {
-                in = (x - lob) <= span;             // rejects negatives and NaNs
+                w = (x - lob) <= span;              // rejects negatives and NaNs
                 below = (int64_t)x < (int64_t)lob;  // negatives (incl. -0, negative NaNs) are below
             } else {
                 const uint64_t key = okey(x);
-                in = (key - lo) <= span;            // NaN keys lie outside [okey(-inf), okey(+inf)]
+                w = (key - lo) <= span;             // NaN keys lie outside [okey(-inf), okey(+inf)]
                 below = key < lo;                   // + negative NaNs, removed via ng
             }
-            vm = (vm << 1) | (in ? 1u : 0u);
+            in[j] = w ? 1u : 0u;
             b += below ? 1u : 0u;
             nn += nan ? 1u : 0u;
             ng += (nan && (x >> 63)) ? 1u : 0u;
         }
-        return vm;
     }
 
     // Present samples below the window and NaN slots of the committed chunks.
@@ -1755,18 +1758,20 @@ struct WindowProc {
     // window crowded by a few repeated keys can overflow: then the segment falls back.
     __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
         if (uni32(fail)) return;
-        uint32_t b, nn, ng = 0, vm, mode;
+        uint32_t b, nn, ng = 0, vc = 0, mode;
+        uint32_t in[2 * kUnroll];
         if constexpr (LANE_COUNTS) {
             mode = uni32(fast) ? WIN_FAST : WIN_GENERAL;
-            if (mode == WIN_FAST) vm = classify_lanes<true>(c, b, nn, ng);
-            else vm = classify_lanes<false>(c, b, nn, ng);
+            if (mode == WIN_FAST) classify_lanes<true>(c, in, b, nn, ng);
+            else classify_lanes<false>(c, in, b, nn, ng);
         } else {
             mode = uni32(full) ? WIN_FULL : (uni32(fast) ? WIN_FAST : WIN_GENERAL);
-            if (mode == WIN_FAST) vm = classify<WIN_FAST>(c, b, nn);
-            else if (mode == WIN_FULL) vm = classify<WIN_FULL>(c, b, nn);
-            else vm = classify<WIN_GENERAL>(c, b, nn);
+            if (mode == WIN_FAST) classify<WIN_FAST>(c, in, b, nn);
+            else if (mode == WIN_FULL) classify<WIN_FULL>(c, in, b, nn);
+            else classify<WIN_GENERAL>(c, in, b, nn);
         }
-        const uint32_t vc = __popc(vm);
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) vc += in[j];
         const uint32_t incl = wave_scan32(vc, 0u, OpAdd32{});
         const uint32_t C = lane_bcast32(incl, kWave - 1);
         if (!point && cnt + C > cap) {
@@ -1774,8 +1779,8 @@ struct WindowProc {
             return;
         }
         if (C && !point) {
-            if (mode == WIN_FAST) insert<WIN_FAST>(c, vm, cnt + incl - vc);
-            else insert<WIN_GENERAL>(c, vm, cnt + incl - vc);
+            if (mode == WIN_FAST) insert<WIN_FAST>(c, in, cnt + incl - vc);
+            else insert<WIN_GENERAL>(c, in, cnt + incl - vc);
         }
         cnt = uni32(cnt + C);
         if constexpr (LANE_COUNTS) {
