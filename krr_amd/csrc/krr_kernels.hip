@@ -2949,7 +2949,7 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     if (rc) return rc;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax, sp.bottom);  // every segment through hselect
+    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom);  // every segment through hselect
     const uint32_t cap = hsel ? 0u : need;
     *A = SelectArgs{};
     A->vals = series->values;
@@ -3477,7 +3477,7 @@ int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params
     const int64_t Lmax = max_segment_len > 0 ? max_segment_len : 1;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = !single_pass_ok(need, sp.tkeep, Lmax, sp.bottom);
+    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom);
     out->hselect = hsel ? 1 : 0;
     out->bottom = (int32_t)sp.bottom;
     out->tkeep = sp.tkeep;

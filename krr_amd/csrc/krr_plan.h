@@ -150,6 +150,26 @@ KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L, uint
 #endif
 }
 
+// The launch's selection path: single pass (its candidate set fits LDS) or the window
+// select (wselect, hselect for its misses).  The window select also takes launches the
+// single pass could hold when their kept tail is a large share of the segment (more than
+// KRR_WSEL_KEEP_PERMILLE) and the single-pass buffer would exceed KRR_WSEL_MIN_NEED keys:
+// there the single pass pays compactions (or the probe-backed big buffer's lower
+// occupancy) that the window's shrinking key range avoids.  Same-process A/B, fused
+// launch (profiles/r02/ab18, ab19): config 2 p94 1.288 -> 1.220 ms, p95 1.221 -> 1.180,
+// p96 1.189 -> 1.184; config 3 p95 2.56 -> 2.44, p96 2.46 -> 2.43; p97 and up (<= 3%
+// kept) and the 10,080-slot config-4 shape equal or better on the single pass.
+#ifndef KRR_WSEL_KEEP_PERMILLE
+#define KRR_WSEL_KEEP_PERMILLE 35
+#endif
+#ifndef KRR_WSEL_MIN_NEED
+#define KRR_WSEL_MIN_NEED 1200
+#endif
+KRR_HD inline bool window_select(uint32_t need, uint32_t tkeep, int64_t L, uint32_t bottom) {
+    if (!single_pass_ok(need, tkeep, L, bottom)) return true;
+    return need > (uint32_t)KRR_WSEL_MIN_NEED && (int64_t)tkeep * 1000 > (int64_t)KRR_WSEL_KEEP_PERMILLE * L;
+}
+
 // hselect LDS after kSelectLdsFixed: histogram + collect buffer.
 #ifndef KRR_HIST_BITS
 #define KRR_HIST_BITS 10

@@ -405,16 +405,16 @@ def test_select_probe_start_threshold(ctx, mode):
 
 
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
-def test_select_probe_large_buffer(ctx, mode):
-    """Launches whose longest segment is >= 12x the needed capacity run p94-p97 of 7d@1m x 5
-    pods (50,400 slots, ~2,500-3,030 kept keys) single-pass with a buffer of up to 3,712 keys
-    behind the start-threshold probe (krr_plan.h single_pass_ok; the plan itself is pinned by
-    tests/test_abi.py::test_select_plan_decisions_config2): hits, a probe that sees only huge
-    values (re-stream), only tiny values, gaps, and a short segment sharing the launch.  p5 / p6
-    keep the BOTTOM ~2,500-3,000 keys, for which there is no probe: those launches take the
-    window select instead."""
+@pytest.mark.parametrize("L", [50400, 100800])
+def test_select_probe_large_buffer(ctx, mode, L):
+    """Long launches run p97 single-pass behind the start-threshold probe with a buffer of
+    up to 3,712 keys (100,800 slots: 3,027 kept keys; 50,400: 1,515), and p94-p96 (4-6%
+    kept) through the window select (krr_plan.h single_pass_ok / window_select; the plan
+    itself is pinned by tests/test_abi.py::test_select_plan_decisions): hits, a probe that
+    sees only huge values (re-stream), only tiny values, gaps, and a short segment sharing
+    the launch.  p5 / p6 keep the BOTTOM keys, for which there is no probe: window select
+    (ADVICE r1)."""
     rng = np.random.default_rng(97)
-    L = 50400
     ps = _select_probe_slots(L)
     segs = [("gamma", rng.gamma(2.0, 0.05, size=L), False), ("short", rng.gamma(2.0, 0.05, size=3000), False)]
     hi = rng.random(L)
