@@ -5,6 +5,8 @@ one-rank communicator), each rank a fresh interpreter started by a parent proces
   -> exact rounding on rank 0) against the reference's own config-1 strings;
 * `bench.py --gpus 2` (self-launching two ranks, gloo rehearsal): n_gpus 2 and the gathered
   records equal the oracle and rank 0's kernel on samples regenerated from every shard;
+* config 5 at 2 and 3 time-sharded ranks: sketch reduce-scatter + exact refinement equal one
+  select over the regathered full series; sketch-only rank error within bound;
 * the C-ABI gather (krr_gather_results over RCCL, include/krr_amd.h), with a communicator of
   its own and with PyTorch's;
 * global-index synthesis: shards generated apart equal the fleet generated whole.
@@ -49,6 +51,30 @@ def test_bench_self_launches_ranks(cfg, extra):
     assert r["parity_vs_oracle_on_sample"] is True and r["parity_gathered_vs_rank0_kernel"] is True, r
     assert r["parity_sample_containers"] >= 2 * 64
     assert "cpu_baseline" not in r  # rank 0 at N = 1 only
+
+
+@pytest.mark.parametrize("world,mode,pct", [(2, "linear", "99"), (3, "sorted_lower", "50"), (2, "linear", "95")])
+def test_bench_config5_time_sharded_ranks(world, mode, pct):
+    """Config 5 through `bench.py --gpus N` (gloo ranks sharing the GPU): every series is
+    time-sharded over N ranks, the per-slice sketches are reduce-scattered, the needed
+    ranks' bins located, the samples in them all-to-all'd to the owners and selected
+    exactly; rank 0 checks the gathered answers bit for bit against one k_select/hselect
+    pass over the full 172,800-sample series (regathered from every rank)."""
+    r = _bench(["--gpus", str(world), "--config", "5", "--containers", "600", "--steps", "2", "--warmup", "1",
+                "--mode", mode, "--percentile", pct, "--error-sample", "600"], timeout=300)
+    assert r["n_gpus"] == world and r["config"]["parallelism"].startswith(f"time-shard{world}")
+    assert r["parity_vs_single_window_select"] is True and r["parity_sample_series"] == 600, r
+    assert "cpu_baseline" not in r
+
+
+def test_bench_config5_sketch_only_two_ranks():
+    """Sketch-only answers merged across two time-sharded ranks: the rank error stays within
+    the log-linear sketch's bin mass (2^5 bins per octave; the same bound the N = 1 sketch
+    test holds) and is reported beside the value."""
+    r = _bench(["--gpus", "2", "--config", "5", "--containers", "600", "--steps", "2", "--warmup", "1",
+                "--sketch-only", "--error-sample", "600"], timeout=300)
+    e = r["sketch_error"]
+    assert e["sample_series"] == 600 and 0.0 <= e["rank_error_max"] < 1e-3 and e["value_rel_error_max"] < 0.01, e
 
 
 def test_synth_global_index_shards_equal_whole_fleet():
