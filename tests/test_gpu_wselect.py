@@ -141,11 +141,15 @@ def test_adversarial_orders_exact_with_fallback(ctx, mode):
 
 
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
-def test_gaps_nan_and_empty(ctx, mode):
+@pytest.mark.parametrize("lens", [(50400, 0, 30000, 50400, 17000, 50400), (20160, 0, 12000, 20160, 7000, 20160)],
+                         ids=["long_kernel", "short_kernel"])
+def test_gaps_nan_and_empty(ctx, mode, lens):
     """Gapped segments (incl. negative NaN gaps, all-gap and empty segments) and a real
-    NaN sample in the compact layout (flagged) through the window select."""
+    NaN sample in the compact layout (flagged) through the window select: the long-segment
+    kernel (per-lane counts) and the 12-waves/CU kernel, whose scalar counts recount every
+    chunk holding a NaN and take negative NaNs back out of "below"."""
     rng = np.random.default_rng(77)
-    lens = np.array([50400, 0, 30000, 50400, 17000, 50400], dtype=np.int64)
+    lens = np.array(lens, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     v = rng.gamma(2.0, 0.05, size=int(offs[-1]))
     v[rng.random(v.size) < 0.3] = np.nan
