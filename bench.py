@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--gather", choices=("pipelined", "blocking"), default="pipelined",
                     help="N > 1 records path: pipelined = step k's gather overlaps step k+1's kernel; "
                          "blocking = gather + host copy right after each kernel")
+    ap.add_argument("--records", choices=("host", "device"), default="host",
+                    help="N = 1: the fused launch writes the 32-B records straight into page-locked host "
+                         "memory (host) or into HBM followed by a D2H copy (device)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N > 1 path (process group + pipelined RCCL gather) even with one rank (testing)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -269,9 +272,18 @@ def main():
     dev_rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
     counts = record_counts(S, coll_dev) if dist_on else None  # shard sizes are fixed: exchange once
 
+    # N = 1, fused: the launch can write its records straight into the page-locked host
+    # buffer (mapped into the device's address space) instead of HBM + a D2H copy
+    zero_copy = args.records == "host" and not dist_on and not args.separate
+
     def step(events=None):
         if events is not None:
             events[0].record(stream)
+        if zero_copy:
+            ctx.simple_run(cs, ms, params, out, stream, records=host_rec)
+            if events is not None:
+                events[1].record(stream)
+            return
         if args.separate:
             ctx.segmented_percentile(cs, params, out["cpu_value"], out["cpu_count"], out["cpu_flags"], stream)
             if events is not None:
@@ -379,6 +391,12 @@ def main():
     }
     if args.mode == "ref_index" and not gaps:
         result["roofline"]["note"] = "compact REF_INDEX is one gather per segment: bytes count every slot anyway"
+    result["config"]["records"] = "page-locked host memory, written by the launch" if zero_copy else \
+        "HBM + D2H copy" if not dist_on else "HBM + RCCL gather to rank 0"
+    if zero_copy:  # the host buffer holds exactly what the launch computed (after the last step's sync)
+        ctx.pack_records(out, dev_rec, stream)
+        torch.cuda.synchronize()
+        result["records_host_equal_device"] = bool(torch.equal(dev_rec.cpu(), host_rec[:S]))
     # PMC-measured HBM bytes per launch of the same kernel/workload (profiles/pmc_traffic.json)
     try:
         with open(args.traffic) as fh:

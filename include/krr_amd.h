@@ -129,7 +129,10 @@ int krr_simple_run(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
 /* krr_simple_run that also writes each object's 32-byte result record
  * (krr_pack_records layout: cpu bits, mem bits, cpu count | cpu flags << 48,
  * mem count | mem flags << 48) from the same launch — no separate pack pass.
- * records: device int64[4 * n_objects], or NULL (= krr_simple_run). */
+ * records: device-accessible int64[4 * n_objects] — HBM, or page-locked host memory
+ * (hipHostMalloc / a pinned torch tensor: mapped into the device's address space, so
+ * the launch writes the records to the host itself and no D2H copy follows) — or NULL
+ * (= krr_simple_run).  Host records are complete once the stream has synchronised. */
 int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
                            const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
                            uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,

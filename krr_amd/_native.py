@@ -303,7 +303,7 @@ class Context:
                       ("mem_value", "float64"), ("mem_count", "int64"), ("mem_flags", "int32")):
             _check_tensor(out[k], dt, n)
         if records is not None:
-            _check_tensor(records, "int64", 4 * n)
+            _check_tensor(records, "int64", 4 * n, host_pinned_ok=True)
         self._check(self._lib.krr_simple_run_records(
             self._h, ctypes.byref(cpu), ctypes.byref(mem), ctypes.byref(params),
             out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
@@ -469,11 +469,14 @@ def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectP
     return info
 
 
-def _check_tensor(t, dtype: str, numel: Optional[int] = None) -> None:
+def _check_tensor(t, dtype: str, numel: Optional[int] = None, host_pinned_ok: bool = False) -> None:
+    """host_pinned_ok: a page-locked host tensor is accepted too (the device writes it
+    through the mapping the pinned allocation has in its address space)."""
     import torch
 
     want = getattr(torch, dtype)
-    if not isinstance(t, torch.Tensor) or t.dtype != want or not t.is_cuda or not t.is_contiguous():
+    on_dev = isinstance(t, torch.Tensor) and (t.is_cuda or (host_pinned_ok and t.is_pinned()))
+    if not on_dev or t.dtype != want or not t.is_contiguous():
         raise TypeError(f"expected a contiguous {dtype} HIP-device tensor, got "
                         f"{getattr(t, 'dtype', type(t))} on {getattr(t, 'device', '?')}")
     if numel is not None and t.numel() < numel:

@@ -111,14 +111,27 @@ class SimpleEngine:
             e = np.zeros(0)
             return RawResults(e, e.astype(np.int64), e.astype(np.uint32), e, e.astype(np.int64),
                               e.astype(np.uint32))
+        from krr_amd.core.distributed import unpack_records
+
+        S = fleet.n_objects
         with torch.cuda.device(self.device):
             cv, co = self._to_device(fleet.cpu)
             mv, mo = self._to_device(fleet.mem)
-            out = self.run_device(cv, co, mv, mo, params, max(fleet.cpu.max_len, 1), max(fleet.mem.max_len, 1),
-                                  fleet.cpu.gaps_are_nan)
-            host = {k: v.cpu().numpy() for k, v in out.items()}  # synchronises the stream
-        return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"].view(np.uint32),
-                          host["mem_value"], host["mem_count"], host["mem_flags"].view(np.uint32))
+            # the launch writes the 32-B records straight into page-locked host memory
+            # (krr_simple_run_records with a mapped host buffer): one sync, no D2H copies
+            rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
+            ctx = self.context()
+            dev = cv.device
+            out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+                   (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+                    ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+            ctx.simple_run(ctx.series(cv, co, max(fleet.cpu.max_len, 1), fleet.cpu.gaps_are_nan),
+                           ctx.series(mv, mo, max(fleet.mem.max_len, 1), fleet.mem.gaps_are_nan),
+                           params, out, records=rec)
+            torch.cuda.current_stream(self.device).synchronize()
+        host = unpack_records(rec.numpy())
+        return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"], host["mem_value"],
+                          host["mem_count"], host["mem_flags"])
 
 
     def run_packed_records(self, fleet: PackedFleet, params: _native.KrrPercentileParams):
