@@ -5,7 +5,8 @@
 One "step" = one pass of the hot path over the rank's whole synthetic fleet
 shard, inputs resident in HBM: the CPU-percentile kernel over every CPU series,
 the max+count kernel over every memory series, and (N > 1) the RCCL gather of
-the 32-B per-container result records to rank 0, whose D2H copy ends the step.
+the 32-B per-container result records to rank 0 on the same stream, whose copy to
+host memory is done by rank 0's next launch (the last one's after the loop).
 
 Ranks: one process per GPU.  Under torchrun (WORLD_SIZE set) the world size must
 equal --gpus.  Without it, `--gpus N > 1` makes this process a launcher: it spawns
@@ -82,9 +83,10 @@ def parse():
     ap.add_argument("--parity-blocks", type=int, default=4, help="N > 1 parity: sampled blocks per shard")
     ap.add_argument("--parity-block", type=int, default=128, help="N > 1 parity: containers per sampled block")
     ap.add_argument("--separate", action="store_true", help="two launches (percentile, max) instead of the fused one")
-    ap.add_argument("--gather", choices=("pipelined", "blocking"), default="pipelined",
-                    help="N > 1 records path: pipelined = step k's gather overlaps step k+1's kernel; "
-                         "blocking = gather + host copy right after each kernel")
+    ap.add_argument("--gather", choices=("stream", "torch", "blocking"), default="stream",
+                    help="N > 1 records path: stream = RCCL send/recv through the C ABI on the launch stream "
+                         "(gloo: torch); torch = torch.distributed.gather on its own stream, step k's gather "
+                         "overlapping step k+1's kernel; blocking = torch gather + host copy after each kernel")
     ap.add_argument("--records", choices=("host", "device"), default="host",
                     help="N = 1: the fused launch writes the 32-B records straight into page-locked host "
                          "memory (host) or into HBM followed by a D2H copy (device)")
@@ -201,6 +203,13 @@ def main():
                      f"(launch one rank per GPU: torchrun --nproc-per-node {args.gpus}, or no torchrun)")
     elif args.gpus > 1:
         sys.exit(launch_ranks(args))
+    elif args.force_dist:  # a one-rank process group of its own
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     # Native libraries (RCCL's version banner, gloo's peer messages) write to fd 1:
     # point fd 1 at stderr and keep the real stdout for the ONE JSON line.
     global _JSON_OUT
@@ -267,16 +276,60 @@ def main():
     }
     stream = torch.cuda.current_stream()
     host_rec = torch.empty((containers_total if rank == 0 else S, 4), dtype=torch.int64, pin_memory=True)
-    # records go to the host on the compute stream: a copy stream overlapping the
-    # next step's kernel was measured to gain nothing (the blit slows the kernel)
-    dev_rec = torch.empty((S, 4), dtype=torch.int64, device=dev)
     counts = record_counts(S, coll_dev) if dist_on else None  # shard sizes are fixed: exchange once
+    gather_mode = args.gather if dist_on else None
+    if gather_mode == "stream" and args.separate:
+        gather_mode = "torch"
+    comm = None
+    if gather_mode == "stream":
+        # the RCCL communicator torch.distributed made (record_counts' all_gather created it)
+        comm = pg_comm(dev) if backend == "nccl" else None
+        if comm is None:
+            gather_mode = "torch"
+    # N > 1 over RCCL, "stream" (default): the gather is enqueued on the launch stream through
+    # the C ABI (krr_gather_results with torch's communicator), so a step is launch -> send/recv
+    # with no cross-stream dependency in the launch queue (each cost 20-30 us of idle queue,
+    # profiles/r02/fdtrace).  Rank 0's launch writes its own records into the head of the
+    # receive buffer (no self copy) and, as its first work items, forwards the PREVIOUS step's
+    # gathered records (N x 320 KB) into page-locked host memory (krr_simple_run_forward): no
+    # second stream, no separate D2H (on the launch stream 2.56 MB cost +60 us per step;
+    # scripts/d2h_overlap.py).  Two receive buffers alternate; the last step's records are
+    # copied after the loop, inside the timed region.
+    copy_stream = torch.cuda.Stream(device=dev) if dist_on and coll_dev.type == "cuda" else None
+    recv = [torch.empty((containers_total, 4), dtype=torch.int64, device=dev) for _ in range(2)] \
+        if gather_mode == "stream" and rank == 0 else []
+    # "torch": torch.distributed.gather on torch's RCCL stream, step k's gather waited for
+    # one step later; two send buffers alternate so it sends from the buffer the launch wrote
+    dev_recs = [torch.empty((S, 4), dtype=torch.int64, device=dev) for _ in range(2)]
+    dev_rec = dev_recs[0]
 
     # N = 1, fused: the launch can write its records straight into the page-locked host
     # buffer (mapped into the device's address space) instead of HBM + a D2H copy
     zero_copy = args.records == "host" and not dist_on and not args.separate
 
+    nstep = [0]
+
     def step(events=None):
+        k = nstep[0]
+        nstep[0] += 1
+        dev_rec = dev_recs[k % 2] if copy_stream is not None else dev_recs[0]
+        if gather_mode == "stream":
+            fwd = None
+            if rank == 0:
+                dev_rec = recv[k % 2][:S]
+                if k > 0:
+                    fwd = (recv[(k - 1) % 2], host_rec)
+            if events is not None:
+                events[0].record(stream)
+            ctx.simple_run(cs, ms, params, out, stream, records=dev_rec, forward=fwd)
+            if events is not None:
+                events[1].record(stream)
+            if rank == 0:
+                ctx.gather_results(comm, 0, dev_rec, counts=counts, out=recv[k % 2], stream=stream)
+                last[0] = recv[k % 2]
+            else:
+                ctx.gather_results(comm, 0, dev_rec, stream=stream)
+            return
         if events is not None:
             events[0].record(stream)
         if zero_copy:
@@ -300,10 +353,11 @@ def main():
         if not dist_on:
             host_rec.copy_(dev_rec, non_blocking=True)
             return
-        # N > 1: this step's gather stays in flight (RCCL stream) while the next
-        # step's kernel runs; it is waited for one step later (and by finish())
-        pend = gather_records(dev_rec.to(coll_dev), dst=0, counts=counts, async_op=True)
-        if args.gather == "blocking":  # no overlap: the step ends with its own gather
+        # this step's gather stays in flight (torch's RCCL stream) while the next step's
+        # kernel runs; it is waited for one step later (and by finish())
+        pend = gather_records(dev_rec.to(coll_dev), dst=0, counts=counts, async_op=True,
+                              copy_local=copy_stream is None)
+        if gather_mode == "blocking":  # no overlap: the step ends with its own gather
             inflight.append(pend)
             finish()
             return
@@ -311,12 +365,29 @@ def main():
         inflight.append(pend)
 
     inflight = []
+    last = [None]
 
     def finish():
+        if last[0] is not None:  # "stream": the last step's gathered records (no launch follows)
+            host_rec.copy_(last[0], non_blocking=True)
+            last[0] = None
         while inflight:
-            rec = inflight.pop().wait()
+            pend = inflight.pop()
+            if copy_stream is None:  # gloo (host tensors)
+                rec = pend.wait()
+                if rank == 0:
+                    host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+                continue
+            # the launch stream waits for the gather (done long since: it overlapped the
+            # launch just enqueued) before the NEXT launch rewrites the buffer it sent
+            rec = pend.wait()
             if rank == 0:
-                host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+                ready = torch.cuda.Event()
+                ready.record(stream)
+                copy_stream.wait_event(ready)
+                with torch.cuda.stream(copy_stream):
+                    host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
+                rec.record_stream(copy_stream)  # the receive buffer outlives the copy
 
     for _ in range(args.warmup):
         step()
@@ -393,7 +464,13 @@ def main():
         result["roofline"]["note"] = "compact REF_INDEX is one gather per segment: bytes count every slot anyway"
     result["config"]["records"] = "page-locked host memory, written by the launch" if zero_copy else \
         "HBM + D2H copy" if not dist_on else "HBM + RCCL gather to rank 0"
-    if zero_copy:  # the host buffer holds exactly what the launch computed (after the last step's sync)
+    if dist_on:
+        result["config"]["gather"] = {"stream": "RCCL send/recv on the launch stream (C ABI krr_gather_results)",
+                                      "torch": "torch.distributed.gather, overlapping the next launch",
+                                      "blocking": "torch.distributed.gather, waited for each step"}[gather_mode]
+    if zero_copy or (dist_on and rank == 0 and not args.separate):
+        # the host buffer holds exactly what the launch computed (after the last step's sync);
+        # N > 1: rank 0's own shard leads the gathered records
         ctx.pack_records(out, dev_rec, stream)
         torch.cuda.synchronize()
         result["records_host_equal_device"] = bool(torch.equal(dev_rec.cpu(), host_rec[:S]))
@@ -488,6 +565,18 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
+
+
+def pg_comm(dev):
+    """The ncclComm_t of torch.distributed's default "nccl" group on `dev` (as an int), or
+    None when this torch build does not expose it."""
+    import torch.distributed as dist
+
+    try:
+        fn = getattr(dist.group.WORLD._get_backend(dev), "_comm_ptr", None)
+        return int(fn()) if fn is not None else None
+    except (RuntimeError, AttributeError):
+        return None
 
 
 def parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed) -> dict:

@@ -138,6 +138,20 @@ int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series
                            uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
                            int64_t* records, void* stream);
 
+/* krr_simple_run_records whose launch also copies forward_bytes (a multiple of 16;
+ * 16-byte aligned pointers) from forward_src to forward_dst: device memory, or
+ * page-locked host memory mapped into the device's address space.  The copy runs as
+ * the first work items of the same launch, beside the HBM stream, instead of as a
+ * separate copy after it.  Multi-GPU step on the root: forward the previous step's
+ * gathered records (N x 32 B per object) to the host while this step's pass runs —
+ * no second stream, no cross-stream wait.  forward_bytes = 0: krr_simple_run_records.
+ * (Compact REF_INDEX, which is not fused, or zero objects: a stream-ordered copy.) */
+int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
+                           const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
+                           uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
+                           int64_t* records, const void* forward_src, void* forward_dst, int64_t forward_bytes,
+                           void* stream);
+
 /* Same as krr_simple_run, but every pointer (inputs and outputs) is a HOST
  * pointer; copies in, runs, copies out and synchronises.  Includes PCIe. */
 int krr_simple_run_host(krr_ctx* ctx, const double* cpu_values, const int64_t* cpu_offsets,

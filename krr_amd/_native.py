@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "krr_segmented_max",
     "krr_simple_run",
     "krr_simple_run_records",
+    "krr_simple_run_forward",
     "krr_simple_run_host",
     "krr_pack_records",
     "krr_synth_fill",
@@ -177,6 +178,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_simple_run.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_simple_run_records.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_simple_run_records.restype = ctypes.c_int
+        lib.krr_simple_run_forward.argtypes = [vp, sp, sp, pp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]
+        lib.krr_simple_run_forward.restype = ctypes.c_int
         lib.krr_simple_run.restype = ctypes.c_int
         lib.krr_simple_run_host.argtypes = [vp, vp, vp, vp, vp, i64, i32, pp, vp, vp, vp, vp, vp, vp]
         lib.krr_simple_run_host.restype = ctypes.c_int
@@ -294,21 +297,33 @@ class Context:
             self._stream(stream)))
 
     def simple_run(self, cpu: KrrSeries, mem: KrrSeries, params: KrrPercentileParams, out: dict,
-                   stream=None, records=None) -> None:
+                   stream=None, records=None, forward=None) -> None:
         """out: dict with cpu_value/cpu_count/cpu_flags/mem_value/mem_count/mem_flags tensors;
-        records (optional): int64 [S, 4] device tensor the same launch fills with the
-        32-B result records (krr_simple_run_records)."""
+        records (optional): int64 [S, 4] device (or page-locked host) tensor the same launch
+        fills with the 32-B result records (krr_simple_run_records); forward (optional):
+        (src, dst) tensors of equal byte size the same launch copies src -> dst
+        (krr_simple_run_forward; dst may be page-locked host memory)."""
         n = cpu.n_segments
         for k, dt in (("cpu_value", "float64"), ("cpu_count", "int64"), ("cpu_flags", "int32"),
                       ("mem_value", "float64"), ("mem_count", "int64"), ("mem_flags", "int32")):
             _check_tensor(out[k], dt, n)
         if records is not None:
             _check_tensor(records, "int64", 4 * n, host_pinned_ok=True)
-        self._check(self._lib.krr_simple_run_records(
+        fsrc = fdst = None
+        fbytes = 0
+        if forward is not None:
+            src, dst = forward
+            _check_tensor(src, "int64", host_pinned_ok=True)
+            _check_tensor(dst, "int64", host_pinned_ok=True)
+            fbytes = src.numel() * 8
+            if dst.numel() * 8 < fbytes:
+                raise ValueError(f"forward destination holds {dst.numel() * 8} bytes, need {fbytes}")
+            fsrc, fdst = src.data_ptr(), dst.data_ptr()
+        self._check(self._lib.krr_simple_run_forward(
             self._h, ctypes.byref(cpu), ctypes.byref(mem), ctypes.byref(params),
             out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
             out["mem_value"].data_ptr(), out["mem_count"].data_ptr(), out["mem_flags"].data_ptr(),
-            records.data_ptr() if records is not None else None, self._stream(stream)))
+            records.data_ptr() if records is not None else None, fsrc, fdst, fbytes, self._stream(stream)))
 
     def pack_records(self, out: dict, records, stream=None) -> None:
         """out: the six result tensors; records: int64 [S, 4] device tensor."""

@@ -2175,6 +2175,13 @@ struct MaxArgs {
     int64_t* out_n;
     uint32_t* out_f;
     int64_t* rec = nullptr;  // optional records, memory half
+    // optional forward copy done by the fused launch (krr_simple_run_forward): fwd_units
+    // 16-byte units from fwd_src to fwd_dst (device or mapped page-locked host memory),
+    // split over fwd_items work items that precede the segments
+    const double2* fwd_src = nullptr;
+    double2* fwd_dst = nullptr;
+    int64_t fwd_units = 0;
+    int64_t fwd_items = 0;
 };
 
 template <class Streamer>
@@ -2226,16 +2233,31 @@ __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
 // per kernel; one launch is also one roofline for the whole step.
 enum { CPU_SELECT = 0, CPU_REF_GAPS = 1, CPU_HSELECT = 2, CPU_HSELECT_LONG = 3 };  // HSELECT: window select
 
+// One forward work item: a contiguous kFwdItemUnits-unit share of the copy, 16 B per
+// lane per store (posted writes when the destination is host memory).
+constexpr int64_t kFwdItemUnits = 4096;  // 64 KiB per item
+__device__ __forceinline__ void forward_item(const MaxArgs& M, int64_t i, int lane) {
+    const int64_t a = i * kFwdItemUnits;
+    const int64_t e = a + kFwdItemUnits < M.fwd_units ? a + kFwdItemUnits : M.fwd_units;
+    for (int64_t u = a + lane; u < e; u += kWave) M.fwd_dst[u] = M.fwd_src[u];
+}
+
 template <int CPU_KIND>
 __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? window_waves(false)
                                 : CPU_KIND == CPU_HSELECT_LONG ? window_waves(true)
                                                                : KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t S_cpu = CPU_KIND == CPU_REF_GAPS ? R.S : A.S;
-    const int64_t total = S_cpu + M.S;
+    const int64_t F = M.fwd_items;  // forward-copy items first: short, done while the stream ramps up
+    const int64_t total = F + S_cpu + M.S;
     constexpr bool kWindow = CPU_KIND == CPU_HSELECT || CPU_KIND == CPU_HSELECT_LONG;
     if (kWindow && A.fail_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.fail_reset = 0;
-    for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+    for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {
+        if (bb < F) {
+            forward_item(M, bb, threadIdx.x);
+            continue;
+        }
+        const int64_t b = bb - F;  // F is a multiple of 8: blocks keep their XCD's eighth
         // remap within each resource's half, so the CPU items still all precede
         // the memory items in dispatch order
         if (b < S_cpu) {
@@ -3138,7 +3160,20 @@ int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series
                            const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
                            uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
                            int64_t* records, void* stream) {
+    return krr_simple_run_forward(ctx, cpu, mem, params, cpu_value, cpu_count, cpu_flags, mem_value, mem_count,
+                                  mem_flags, records, nullptr, nullptr, 0, stream);
+}
+
+int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series* mem,
+                           const krr_percentile_params* params, double* cpu_value, int64_t* cpu_count,
+                           uint32_t* cpu_flags, double* mem_value, int64_t* mem_count, uint32_t* mem_flags,
+                           int64_t* records, const void* forward_src, void* forward_dst, int64_t forward_bytes,
+                           void* stream) {
     if (!ctx) return KRR_E_INVALID;
+    if (forward_bytes < 0 || forward_bytes % 16 != 0 || (forward_bytes > 0 && (!forward_src || !forward_dst)))
+        return set_err(ctx, KRR_E_INVALID, "forward copy: a multiple of 16 bytes between non-null pointers%s", "");
+    if (forward_bytes > 0 && (((uintptr_t)forward_src | (uintptr_t)forward_dst) & 15))
+        return set_err(ctx, KRR_E_INVALID, "forward copy pointers must be 16-byte aligned%s", "");
     if (!cpu || !mem) return set_err(ctx, KRR_E_INVALID, "null series%s", "");
     if (cpu->n_segments != mem->n_segments)
         return set_err(ctx, KRR_E_INVALID, "cpu and mem need one segment per object each%s", "");
@@ -3147,9 +3182,17 @@ int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series
     if (!rc) rc = check_params(ctx, params);
     if (rc) return rc;
     const int64_t S = cpu->n_segments;
-    if (S == 0) return KRR_OK;
-    if (!cpu_value || !cpu_count || !cpu_flags || !mem_value || !mem_count || !mem_flags)
+    if (S > 0 && (!cpu_value || !cpu_count || !cpu_flags || !mem_value || !mem_count || !mem_flags))
         return set_err(ctx, KRR_E_INVALID, "null outputs%s", "");
+    const int64_t fwd_units = forward_bytes / 16;
+    if (fwd_units > 0 && (S == 0 || (params->mode == KRR_PCT_REF_INDEX && !cpu->gaps_are_nan))) {
+        // no fused launch to ride on: a plain copy on the stream
+        DeviceGuard g(ctx->device);
+        if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+        KRR_HIP(ctx, hipMemcpyAsync(forward_dst, forward_src, (size_t)forward_bytes, hipMemcpyDefault,
+                                    (hipStream_t)stream));
+    }
+    if (S == 0) return KRR_OK;
     if (params->mode == KRR_PCT_REF_INDEX && !cpu->gaps_are_nan) {
         // compact REF_INDEX is one gather per segment: nothing to fuse with
         rc = krr_segmented_percentile(ctx, cpu, params, cpu_value, cpu_count, cpu_flags, stream);
@@ -3163,19 +3206,26 @@ int krr_simple_run_records(krr_ctx* ctx, const krr_series* cpu, const krr_series
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     hipStream_t st = (hipStream_t)stream;
     MaxArgs M{mem->values, mem->offsets, S, mem->gaps_are_nan, mem_value, mem_count, mem_flags, records};
+    if (fwd_units > 0) {
+        M.fwd_src = (const double2*)forward_src;
+        M.fwd_dst = (double2*)forward_dst;
+        M.fwd_units = fwd_units;
+        M.fwd_items = ((fwd_units + kFwdItemUnits - 1) / kFwdItemUnits + 7) & ~(int64_t)7;
+    }
+    const int64_t items = M.fwd_items + 2 * S;
     RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags, records};
     SelectArgs A{};
     if (params->mode == KRR_PCT_REF_INDEX) {
-        hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(2 * S)), dim3(64), 0, st, A, R, M);
+        hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
     } else {
         size_t lds = 0;
         rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds);
         if (rc) return rc;
         A.rec = records;
-        if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
+        if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
         else if (A.wcap == kWselCapLong)
-            hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
-        else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(2 * S)), dim3(64), lds, st, A, R, M);
+            hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
+        else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
         KRR_HIP(ctx, hipGetLastError());
         return launch_fallback(ctx, A, S, st);
     }

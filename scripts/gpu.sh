@@ -35,7 +35,7 @@ for step in "$@"; do
   case "$kind" in
     tests)
       sel=()
-      [[ -n "$arg" ]] && sel=(-k "$arg")
+      [[ -n "$arg" ]] && sel=(-k "$args")
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${sel[@]}" \
         > "$OUT/pytest${n:+_$n}.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$OUT/pytest${n:+_$n}.log"; exit 1; }
       tail -3 "$OUT/pytest${n:+_$n}.log"

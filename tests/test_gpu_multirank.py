@@ -53,6 +53,30 @@ def test_bench_self_launches_ranks(cfg, extra):
     assert "cpu_baseline" not in r  # rank 0 at N = 1 only
 
 
+@pytest.mark.parametrize("gather", ["stream", "torch", "blocking"])
+def test_bench_rccl_path_one_rank(gather):
+    """The N > 1 step over RCCL at one rank (`--force-dist`): the C-ABI gather on the launch
+    stream with torch's communicator (rank 0's launch writing into the rotating receive
+    buffers) or torch.distributed.gather from two alternating send buffers; the gathered
+    records go to the host on the second stream, and the host copy after the timed steps
+    equals the records of the last launch."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), KRR_BENCH_BACKEND="nccl")
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist",
+                        "--containers", "400", "--steps", "5", "--warmup", "2", "--gather", gather,
+                        "--no-cpu-baseline"], capture_output=True, text=True, env=env, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["n_gpus"] == 1 and r["config"]["records"] == "HBM + RCCL gather to rank 0"
+    assert r["config"]["gather"].startswith("RCCL send/recv" if gather == "stream" else "torch.distributed")
+    assert r["records_host_equal_device"] is True, r
+
+
 @pytest.mark.parametrize("world,mode,pct", [(2, "linear", "99"), (3, "sorted_lower", "50"), (2, "linear", "95")])
 def test_bench_config5_time_sharded_ranks(world, mode, pct):
     """Config 5 through `bench.py --gpus N` (gloo ranks sharing the GPU): every series is
@@ -171,3 +195,53 @@ def test_c_abi_gather_with_torch_process_group_comm():
     finally:
         ctx.close()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,gaps", [("linear", True), ("sorted_lower", False), ("ref_index", True),
+                                       ("ref_index", False)])
+@pytest.mark.parametrize("units", [1, 1000, 4096, 4097, 40_000])
+def test_simple_run_forward_copy(mode, gaps, units):
+    """krr_simple_run_forward: the launch copies `units` x 16 B (device -> page-locked host and
+    device -> device) as its first work items, and its results and records equal those of the
+    plain launch (compact REF_INDEX, which is not fused, copies on the stream instead)."""
+    import torch
+
+    from decimal import Decimal
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+
+    ctx = _native.Context(0)
+    dev = torch.device("cuda:0")
+    S, L = 300, 3 * 10080
+    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    cpu = torch.empty(S * L, dtype=torch.float64, device=dev)
+    mem = torch.empty(S * L, dtype=torch.float64, device=dev)
+    ctx.synth_fill(cpu, offs, 11, 0, 10080 if gaps else 0, gaps)
+    ctx.synth_fill(mem, offs, 12, 1, 10080 if gaps else 0, gaps)
+    cs, ms = ctx.series(cpu, offs, L, gaps), ctx.series(mem, offs, L, gaps)
+    params = percentile_params(Decimal("95"), mode)
+
+    def outs():
+        return {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+                (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+                 ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+
+    src = _records(units // 2 + (units % 2), 7, dev).view(-1)[: 2 * units].contiguous()
+    host = torch.full((2 * units,), -1, dtype=torch.int64).pin_memory()
+    ddst = torch.full((2 * units,), -1, dtype=torch.int64, device=dev)
+    o0, o1, o2 = outs(), outs(), outs()
+    r0 = torch.empty((S, 4), dtype=torch.int64, device=dev)
+    r1 = torch.empty((S, 4), dtype=torch.int64, device=dev)
+    ctx.simple_run(cs, ms, params, o0, records=r0)
+    ctx.simple_run(cs, ms, params, o1, records=r1, forward=(src, host))
+    ctx.simple_run(cs, ms, params, o2, forward=(src, ddst))
+    torch.cuda.synchronize()
+    assert torch.equal(host, src.cpu()) and torch.equal(ddst, src)
+    assert torch.equal(r0, r1)
+    for k in o0:
+        assert torch.equal(o0[k].view(torch.int64) if o0[k].dtype == torch.float64 else o0[k],
+                           o2[k].view(torch.int64) if o2[k].dtype == torch.float64 else o2[k]), k
+    with pytest.raises(ValueError):
+        ctx.simple_run(cs, ms, params, o1, forward=(src, host[:-2]))
+    ctx.close()
