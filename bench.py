@@ -389,6 +389,22 @@ def main():
                     host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
                 rec.record_stream(copy_stream)  # the receive buffer outlives the copy
 
+    if gather_mode == "stream":
+        # first use of the C-ABI gather on torch's communicator: if it fails on any rank
+        # (an error return, not a hang), every rank falls back to torch.distributed.gather
+        ok = True
+        try:
+            step()
+            torch.cuda.synchronize()
+        except _native.NativeError as e:
+            print(f"bench.py rank {rank}: C-ABI gather failed ({e}); using torch.distributed.gather",
+                  file=sys.stderr)
+            ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            gather_mode = "torch"
+            last[0] = None
     for _ in range(args.warmup):
         step()
     finish()

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <dlfcn.h>
+#include <sched.h>
 #include <rccl/rccl.h>  // types only: RCCL is resolved with dlopen/dlsym (krr_comm_*)
 
 #include <new>
@@ -3559,6 +3560,7 @@ struct RcclApi {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;  // optional: nonblocking communicators
 };
 
 const RcclApi& rccl() {
@@ -3584,6 +3586,7 @@ const RcclApi& rccl() {
         sym(a.group_end, "ncclGroupEnd");
         sym(a.error_string, "ncclGetErrorString");
         a.ok = all;
+        a.async_error = reinterpret_cast<decltype(a.async_error)>(dlsym(h, "ncclCommGetAsyncError"));
         return a;
     }();
     return api;
@@ -3681,7 +3684,19 @@ int krr_gather_results(krr_ctx* ctx, void* comm, int root, const int64_t* record
     } else if (n_local > 0) {
         r = R.send(records, (size_t)n_local * kWords, ncclInt64, root, c, st);
     }
-    const ncclResult_t re = R.group_end();
+    ncclResult_t re = R.group_end();
+    // A nonblocking communicator (ncclCommInitRankConfig with blocking = 0, e.g. PyTorch's
+    // under TORCH_NCCL_USE_COMM_NONBLOCKING=1) may still be enqueueing when the group ends:
+    // wait for its state to settle before the caller's next call on it.
+    while (re == ncclInProgress && R.async_error) {
+        ncclResult_t st = ncclSuccess;
+        if (R.async_error(c, &st) != ncclSuccess) break;
+        if (st != ncclInProgress) {
+            re = st;
+            break;
+        }
+        sched_yield();
+    }
     if (he != hipSuccess) return set_err(ctx, KRR_E_HIP, "D2D copy failed: %s%lld", hipGetErrorString(he), 0);
     if (r != ncclSuccess) return nccl_err(ctx, "ncclSend/ncclRecv", r);
     if (re != ncclSuccess) return nccl_err(ctx, "ncclGroupEnd", re);
