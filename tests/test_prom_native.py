@@ -212,3 +212,29 @@ def test_timestamps_are_correctly_rounded():
     ps, ts = pack_query_range_bodies([[b]], want_timestamps=True)
     want = np.array([t for t, _ in samples])
     assert np.array_equal(ts.view(np.uint64), want.view(np.uint64))
+
+
+def test_near_midpoint_short_strings_are_correctly_rounded():
+    """The packer's fast path (one x87 extended multiply/divide, krr_pack.cpp fast_decimal)
+    must hand every string it cannot round safely to from_chars: 17-19 significant digits
+    lying within a few units of the last digit of a halfway point between two doubles, over
+    the magnitudes Prometheus values take (CPU cores, bytes), plus exact short midpoints."""
+    rng = np.random.default_rng(21)
+    strs = []
+    xs = np.concatenate([rng.gamma(2.0, 0.05, 1500), np.exp(rng.uniform(np.log(1e-12), np.log(1e18), 1500))])
+    for x in xs:
+        x = float(x)
+        mid = (Decimal(x) + Decimal(float(np.nextafter(x, np.inf)))) / 2
+        for sig in (17, 18, 19):
+            q = mid.scaleb(-mid.adjusted()).quantize(Decimal(1).scaleb(-(sig - 1)))  # sig digits
+            for d in (-2, -1, 0, 1, 2):
+                v = (q + d * Decimal(1).scaleb(-(sig - 1))).scaleb(mid.adjusted())
+                strs.append(format(v, "f"))
+    for k in range(1, 200, 2):  # short exact midpoints: (2^53 + k) / 2^s * 10^... as decimals
+        for s in (1, 2, 3):
+            strs.append(format(Decimal(2**53 + k) / Decimal(2**s), "f"))
+    b = body([(0.0, s) for s in strs])
+    ps = pack_query_range_bodies([[b]])
+    want = np.array([float(s) for s in strs])
+    bad = np.nonzero(ps.values.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, [strs[i] for i in bad[:10]]
