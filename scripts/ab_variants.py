@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--pods", type=int, default=5, help="config 2: pods per container")
+    ap.add_argument("--length", type=int, default=10080, help="config 4: slots per (compact) segment")
     a = ap.parse_args()
     import torch
 
@@ -51,8 +52,8 @@ def main():
     if a.config == 2:
         L, pod_len, gaps = a.pods * 10080, 10080, True
         offs_np = np.arange(n + 1, dtype=np.int64) * L
-    elif a.config == 4:  # 10,080-sample compact segments (one shard of config 4)
-        offs_np = np.arange(n + 1, dtype=np.int64) * 10080
+    elif a.config == 4:  # compact segments of --length samples (10,080: one shard of config 4)
+        offs_np = np.arange(n + 1, dtype=np.int64) * a.length
         pod_len, gaps = 0, False
     else:
         rng = np.random.default_rng(3)
