@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import decimal
 import enum
+import threading
 from decimal import Decimal
 from typing import Optional, Sequence
 
@@ -116,11 +117,40 @@ class SimpleStrategySettings(StrategySettings):
             return prom_decimal(float(raw.mem_value[i])) * buffer
 
 
+_COALESCER_LOCK = threading.Lock()
+
+
 class SimpleStrategy(BaseStrategy[SimpleStrategySettings]):
     __display_name__ = "simple"
 
     def run(self, history_data: HistoryData, object_data: K8sObjectData) -> RunResult:
-        return self.run_batch([history_data], [object_data])[0]
+        """One object (the reference's per-object call, runner.py:106).  Calls that overlap
+        in time — the reference Runner issues them from its executor threads — share one
+        kernel launch (krr_amd.core.coalesce.RunCoalescer); the result is this object's
+        alone, as run_batch([history_data])[0] would give it."""
+        raw, i = self.coalescer().submit(history_data)
+        return self.result_at(raw, i)
+
+    def coalescer(self):
+        c = self.__dict__.get("_coalescer")
+        if c is None:
+            from krr_amd.core.coalesce import RunCoalescer
+
+            with _COALESCER_LOCK:
+                c = self.__dict__.get("_coalescer")
+                if c is None:
+                    c = self.__dict__["_coalescer"] = RunCoalescer(
+                        lambda hs: self.settings.run_fleet(self.pack(hs)))
+        return c
+
+    def result_at(self, raw: RawResults, i: int, buffer: Optional[Decimal] = None) -> RunResult:
+        st = self.settings
+        cpu = st.cpu_from_raw(raw, i)
+        mem = st.memory_from_raw(raw, i, buffer)
+        return {
+            ResourceType.CPU: ResourceRecommendation(request=cpu, limit=None),
+            ResourceType.Memory: ResourceRecommendation(request=mem, limit=mem),
+        }
 
     def run_batch(self, histories: Sequence[HistoryData],
                   objects: Optional[Sequence[K8sObjectData]] = None) -> list[RunResult]:
@@ -144,14 +174,5 @@ class SimpleStrategy(BaseStrategy[SimpleStrategySettings]):
         return format_simple_batch(raw, self.settings, cpu_min_value, memory_min_value)
 
     def results_from_raw(self, raw: RawResults) -> list[RunResult]:
-        st = self.settings
-        buffer = st.memory_buffer()
-        out: list[RunResult] = []
-        for i in range(int(np.asarray(raw.cpu_value).size)):
-            cpu = st.cpu_from_raw(raw, i)
-            mem = st.memory_from_raw(raw, i, buffer)
-            out.append({
-                ResourceType.CPU: ResourceRecommendation(request=cpu, limit=None),
-                ResourceType.Memory: ResourceRecommendation(request=mem, limit=mem),
-            })
-        return out
+        buffer = self.settings.memory_buffer()
+        return [self.result_at(raw, i, buffer) for i in range(int(np.asarray(raw.cpu_value).size))]

@@ -300,3 +300,35 @@ def test_concurrent_run_from_threads_matches_sequential():
         s = seq[i % len(seq)]
         for rt in ResourceType:
             assert _d(r[rt].request) == _d(s[rt].request) and _d(r[rt].limit) == _d(s[rt].limit)
+
+
+def test_concurrent_run_calls_share_launches_on_gpu():
+    """The reference Runner's per-object calls (runner.py:104-106: strategy.run in executor
+    threads) on the GPU: 16 threads calling SimpleStrategy.run() at once get the reference's
+    own strings (or its exception) per object, from fewer launches than calls."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from krr_amd.core.models.allocations import ResourceType
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    strat = SimpleStrategy(SimpleStrategySettings(**PATHS["cli_99_5"]))
+    cases = DOC["cases"] * 4
+
+    def one(case):
+        try:
+            return strat.run(_hist(case), _obj(case["name"]))
+        except decimal.DecimalException as e:
+            return e
+
+    with ThreadPoolExecutor(16) as ex:
+        results = list(ex.map(one, cases))
+    for case, res in zip(cases, results):
+        want = case["results"]["cli_99_5"]
+        if "error" in want:
+            assert isinstance(res, getattr(decimal, want["error"])), case["name"]
+            continue
+        got = {"cpu_request": _d(res[ResourceType.CPU].request), "cpu_limit": _d(res[ResourceType.CPU].limit),
+               "mem_request": _d(res[ResourceType.Memory].request), "mem_limit": _d(res[ResourceType.Memory].limit)}
+        assert got == want["raw"], case["name"]
+    co = strat.coalescer()
+    assert co.calls == len(cases) and co.launches < len(cases)
