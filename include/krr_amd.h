@@ -193,16 +193,17 @@ int krr_gather_results(krr_ctx* ctx, void* comm, int root, const int64_t* record
                        const int64_t* counts, int64_t* out, void* stream);
 
 /* ---- Launch plan (host only: no device, no ctx) ----
- * What krr_segmented_percentile / krr_simple_run choose for SORTED_LOWER / LINEAR
- * when the longest segment has max_segment_len slots. */
+ * What krr_segmented_percentile (and, in fused_hselect, krr_simple_run) chooses for
+ * SORTED_LOWER / LINEAR when the longest segment has max_segment_len slots.  The
+ * other fields describe the krr_segmented_percentile launch. */
 typedef struct {
-    int32_t hselect;      /* 1: histogram select (1-2 HBM passes); 0: single-pass LDS candidate buffer */
+    int32_t hselect;      /* 1: window select (wselect; hselect for its misses); 0: single-pass LDS candidate buffer */
     int32_t bottom;       /* 1: the smallest keys are kept (low percentiles) */
     int64_t tkeep;        /* keys a segment of max length must keep */
     int64_t cap_keys;     /* single-pass candidate capacity (0 with hselect) */
     int64_t lds_bytes;    /* dynamic LDS per workgroup */
     int32_t probe;        /* 1: a max-length segment starts at a probe-estimated threshold */
-    int32_t reserved;
+    int32_t fused_hselect; /* the same choice for krr_simple_run's fused launch */
 } krr_select_plan_info;
 
 int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params, krr_select_plan_info* out);

@@ -136,7 +136,7 @@ class KrrSelectPlanInfo(ctypes.Structure):
         ("cap_keys", ctypes.c_int64),
         ("lds_bytes", ctypes.c_int64),
         ("probe", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("fused_hselect", ctypes.c_int32),
     ]
 
 

@@ -2966,13 +2966,13 @@ int check_series(krr_ctx* ctx, const krr_series* s) {
 // longest segment, or (when that exceeds kSingleCapMax keys) the hselect path
 // for every segment (A->cap = 0), and the LDS bytes.
 int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_params* params,
-                hipStream_t st, double* ov, int64_t* on, uint32_t* of, SelectArgs* A, size_t* lds) {
+                hipStream_t st, double* ov, int64_t* on, uint32_t* of, SelectArgs* A, size_t* lds, bool fused) {
     int64_t Lmax = 0;
     int rc = resolve_maxlen(ctx, series, st, &Lmax);
     if (rc) return rc;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom);  // every segment through hselect
+    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom, fused);  // every segment through wselect
     const uint32_t cap = hsel ? 0u : need;
     *A = SelectArgs{};
     A->vals = series->values;
@@ -3124,7 +3124,7 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
 
     SelectArgs A;
     size_t lds = 0;
-    rc = plan_select(ctx, series, params, st, out_value, out_count, out_flags, &A, &lds);
+    rc = plan_select(ctx, series, params, st, out_value, out_count, out_flags, &A, &lds, false);
     if (rc) return rc;
     if (A.cap) hipLaunchKernelGGL(k_select<SEL_SINGLE>, dim3(grid_for(S)), dim3(64), lds, st, A);
     else if (A.wcap == kWselCapLong) hipLaunchKernelGGL(k_select<SEL_WINDOW_LONG>, dim3(grid_for(S)), dim3(64), lds, st, A);
@@ -3220,7 +3220,7 @@ int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series
         hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
     } else {
         size_t lds = 0;
-        rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds);
+        rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds, true);
         if (rc) return rc;
         A.rec = records;
         if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
@@ -3528,8 +3528,9 @@ int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params
     const int64_t Lmax = max_segment_len > 0 ? max_segment_len : 1;
     const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
     const uint32_t need = capacity_for(sp.tkeep);
-    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom);
+    const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom, false);
     out->hselect = hsel ? 1 : 0;
+    out->fused_hselect = window_select(need, sp.tkeep, Lmax, sp.bottom, true) ? 1 : 0;
     out->bottom = (int32_t)sp.bottom;
     out->tkeep = sp.tkeep;
     out->cap_keys = hsel ? 0 : need;

@@ -159,15 +159,36 @@ KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L, uint
 // launch (profiles/r02/ab18, ab19): config 2 p94 1.288 -> 1.220 ms, p95 1.221 -> 1.180,
 // p96 1.189 -> 1.184; config 3 p95 2.56 -> 2.44, p96 2.46 -> 2.43; p97 and up (<= 3%
 // kept) and the 10,080-slot config-4 shape equal or better on the single pass.
+//
+// Round 2, v21 (profiles/r02/q, same-process A/B of the percentile pass alone and of the
+// fused launch): a percentile-only launch (krr_segmented_percentile) gains from the window
+// down to 0.5% kept — 30d@15s (172,800 slots) p99 4.42 -> 4.23 ms, 50,400-slot p98 0.684 ->
+// 0.646, p97 0.797 -> 0.625, 100,800-slot p97 4.46 -> 3.66 — while in the fused launch the
+// window kernel's 2 waves per SIMD also carry the memory half, so there it only pays against
+// the probe-backed big buffers (more than KRR_WSEL_FUSED_NEED keys: 100,800-slot p97 fused
+// 7.71 -> 7.13 ms; 172,800-slot p99 8.09 vs 8.30 and 50,400-slot p97 / p98 1.170 / 1.162 vs
+// 1.192 / 1.188 stay on the single pass).
 #ifndef KRR_WSEL_KEEP_PERMILLE
 #define KRR_WSEL_KEEP_PERMILLE 35
+#endif
+#ifndef KRR_WSEL_KEEP_PERMILLE_SOLO
+#define KRR_WSEL_KEEP_PERMILLE_SOLO 5
+#endif
+#ifndef KRR_WSEL_FUSED_NEED
+#define KRR_WSEL_FUSED_NEED 2560
+#endif
+#ifndef KRR_WSEL_SOLO_NEED
+#define KRR_WSEL_SOLO_NEED 1600  // the measured gains: buffers of 1,664 keys and more
 #endif
 #ifndef KRR_WSEL_MIN_NEED
 #define KRR_WSEL_MIN_NEED 1200
 #endif
-KRR_HD inline bool window_select(uint32_t need, uint32_t tkeep, int64_t L, uint32_t bottom) {
+KRR_HD inline bool window_select(uint32_t need, uint32_t tkeep, int64_t L, uint32_t bottom, bool fused) {
     if (!single_pass_ok(need, tkeep, L, bottom)) return true;
-    return need > (uint32_t)KRR_WSEL_MIN_NEED && (int64_t)tkeep * 1000 > (int64_t)KRR_WSEL_KEEP_PERMILLE * L;
+    const int64_t kept = (int64_t)tkeep * 1000;  // vs permille of L
+    if (need > (uint32_t)KRR_WSEL_MIN_NEED && kept > (int64_t)KRR_WSEL_KEEP_PERMILLE * L) return true;
+    if (fused) return need > (uint32_t)KRR_WSEL_FUSED_NEED;
+    return need > (uint32_t)KRR_WSEL_SOLO_NEED && kept > (int64_t)KRR_WSEL_KEEP_PERMILLE_SOLO * L;
 }
 
 // hselect LDS after kSelectLdsFixed: histogram + collect buffer.

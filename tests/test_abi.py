@@ -122,38 +122,40 @@ def _plan(L, p, mode="linear"):
     return _native.select_plan(L, percentile_params(Decimal(p), mode))
 
 
-@pytest.mark.parametrize("L,p,hselect,probe,bottom", [
-    (50400, "99", 0, 1, 0),    # headline: ~507 kept keys; the start-threshold probe saves compactions
-    (50400, "97", 0, 1, 0),    # 1,515 kept keys (3%): single pass behind the probe
-    (50400, "96", 1, 0, 0),    # 4% kept: window select (krr_plan.h window_select, A/B r02 ab18/ab19)
-    (50400, "94", 1, 0, 0),
-    (50400, "50", 1, 0, 0),    # mid percentile: window select
-    (50400, "93", 1, 0, 0),    # 4,224 keys would be needed
-    (50400, "5", 1, 0, 1),     # low percentiles keep the bottom side, which has no probe
-    (50400, "6", 1, 0, 1),
-    (50400, "3", 1, 0, 1),     # 1,515 bottom keys: just past the 3% kept-fraction rule of the 2,560-key cap
-    (50400, "2", 0, 0, 1),     # 1,012 bottom keys: single pass, no probe on the bottom side
-    (50400, "1", 0, 0, 1),
-    (100800, "97", 0, 1, 0),   # 3,027 kept keys: the probe-backed big buffer (3,712 keys)
-    (100800, "96", 1, 0, 0),
-    (20160, "97", 0, 1, 0),    # config 3's longest segment: 608 kept keys
-    (20160, "96", 1, 0, 0),    # 810 kept keys, 4%: window select
-    (20160, "95", 1, 0, 0),
-    (10080, "95", 0, 1, 0),    # a 1,152-key buffer: the single pass never loses there
-    (172800, "99", 0, 1, 0),   # 30d@15s p99: 1% kept
+@pytest.mark.parametrize("L,p,hselect,probe,bottom,fused", [
+    (50400, "99", 0, 1, 0, 0),    # headline: ~507 kept keys; the start-threshold probe saves compactions
+    (50400, "98", 1, 0, 0, 0),    # 2% kept, a 1,664-key buffer: window select alone, single pass fused (r02/q)
+    (50400, "97", 1, 0, 0, 0),    # 1,515 kept keys (3%): the same split
+    (50400, "96", 1, 0, 0, 1),    # 4% kept: window select (krr_plan.h window_select, A/B r02 ab18/ab19)
+    (50400, "94", 1, 0, 0, 1),
+    (50400, "50", 1, 0, 0, 1),    # mid percentile: window select
+    (50400, "93", 1, 0, 0, 1),    # 4,224 keys would be needed
+    (50400, "5", 1, 0, 1, 1),     # low percentiles keep the bottom side, which has no probe
+    (50400, "6", 1, 0, 1, 1),
+    (50400, "3", 1, 0, 1, 1),     # 1,515 bottom keys: just past the 3% kept-fraction rule of the 2,560-key cap
+    (50400, "2", 1, 0, 1, 0),     # 1,012 bottom keys: the p98 split mirrored (no probe on the bottom side)
+    (50400, "1", 0, 0, 1, 0),
+    (100800, "97", 1, 0, 0, 1),   # 3,027 kept keys: the window beats the probe-backed 3,712-key buffer both ways
+    (100800, "96", 1, 0, 0, 1),
+    (20160, "97", 0, 1, 0, 0),    # config 3's longest segment: 608 kept keys, a 1,280-key buffer
+    (20160, "96", 1, 0, 0, 1),    # 810 kept keys, 4%: window select
+    (20160, "95", 1, 0, 0, 1),
+    (10080, "95", 0, 1, 0, 0),    # a 1,152-key buffer: the single pass never loses there
+    (172800, "99", 1, 0, 0, 0),   # 30d@15s p99, 1% kept: window alone (4.42 -> 4.23 ms), single pass fused
+    (172800, "99.9", 0, 1, 0, 0),
 ])
-def test_select_plan_decisions(lib, L, p, hselect, probe, bottom):
-    """krr_select_plan reports the path the launch takes (krr_plan.h single_pass_ok /
-    window_select), so the big-buffer boundary, the kept-fraction rule of the window select
-    and the top-side-only probe are pinned without a GPU."""
+def test_select_plan_decisions(lib, L, p, hselect, probe, bottom, fused):
+    """krr_select_plan reports the path each launch takes (krr_plan.h single_pass_ok /
+    window_select) — the percentile-only launch and, in fused_hselect, krr_simple_run's —
+    so the big-buffer boundary, the kept-fraction rules of the window select and the
+    top-side-only probe are pinned without a GPU."""
     info = _plan(L, p)
-    assert (info.hselect, info.probe, info.bottom) == (hselect, probe, bottom), (p, info.tkeep, info.cap_keys)
+    assert (info.hselect, info.probe, info.bottom, info.fused_hselect) == (hselect, probe, bottom, fused), \
+        (p, info.tkeep, info.cap_keys)
     if hselect:
         assert info.cap_keys == 0
     else:
         assert info.tkeep < info.cap_keys <= 3712 and info.lds_bytes == 1536 + 8 * info.cap_keys
-    if (L, p) == (100800, "97"):
-        assert info.cap_keys == 3712
 
 
 def test_select_plan_ref_index_is_not_a_selection(lib):

@@ -44,6 +44,27 @@ def _run_gpu(ctx, values, offsets, mode, p_num, p_den, gaps=False, maxlen=0):
     return ov.cpu().numpy(), on.cpu().numpy(), of.cpu().numpy().astype(np.uint32)
 
 
+def _run_gpu_fused(ctx, values, offsets, mode, p_num, p_den, gaps=False):
+    """The CPU half of krr_simple_run's fused launch (the memory half gets the same series)."""
+    import torch
+
+    from krr_amd import _native
+
+    dev = torch.device("cuda:0")
+    dv = torch.from_numpy(np.ascontiguousarray(values, np.float64)).to(dev)
+    do = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).to(dev)
+    S = offsets.size - 1
+    out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+           (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+            ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+    q = float(p_num) / float(p_den) / 100.0
+    ser = ctx.series(dv, do, 0, gaps)
+    ctx.simple_run(ser, ser, _native.KrrPercentileParams(MODES[mode], 0, p_num, p_den, q), out)
+    torch.cuda.synchronize()
+    return (out["cpu_value"].cpu().numpy(), out["cpu_count"].cpu().numpy(),
+            out["cpu_flags"].cpu().numpy().astype(np.uint32))
+
+
 def _oracle(values, offsets, mode, p_num, p_den, gaps=False):
     if mode == "max":
         return oracle.seg_max(values, offsets, gaps)
@@ -404,16 +425,17 @@ def test_select_probe_start_threshold(ctx, mode):
                 _assert_same(one[0], one[1], mode, f"probe {nm} gaps={gaps} {mode} p={pct}")
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
 @pytest.mark.parametrize("L", [50400, 100800])
-def test_select_probe_large_buffer(ctx, mode, L):
-    """Long launches run p97 single-pass behind the start-threshold probe with a buffer of
-    up to 3,712 keys (100,800 slots: 3,027 kept keys; 50,400: 1,515), and p94-p96 (4-6%
-    kept) through the window select (krr_plan.h single_pass_ok / window_select; the plan
-    itself is pinned by tests/test_abi.py::test_select_plan_decisions): hits, a probe that
-    sees only huge values (re-stream), only tiny values, gaps, and a short segment sharing
-    the launch.  p5 / p6 keep the BOTTOM keys, for which there is no probe: window select
-    (ADVICE r1)."""
+def test_select_probe_large_buffer(ctx, mode, L, fused):
+    """Long launches at tail percentiles: the fused launch runs 50,400-slot p97 single-pass
+    behind the start-threshold probe (1,515 kept keys, a 2,176-key buffer), the percentile-only
+    launch and 100,800-slot p97 (3,027 kept keys) take the window select, and p94-p96 (4-6%
+    kept) the window select everywhere (krr_plan.h single_pass_ok / window_select; the plan is
+    pinned by tests/test_abi.py::test_select_plan_decisions): hits, a probe that sees only huge
+    values (re-stream), only tiny values, gaps, and a short segment sharing the launch.  p5 / p6
+    keep the BOTTOM keys, for which there is no probe: window select."""
     rng = np.random.default_rng(97)
     ps = _select_probe_slots(L)
     segs = [("gamma", rng.gamma(2.0, 0.05, size=L), False), ("short", rng.gamma(2.0, 0.05, size=3000), False)]
@@ -437,8 +459,32 @@ def test_select_probe_large_buffer(ctx, mode, L):
         vals = np.concatenate([v for _, v in chosen])
         offs = np.concatenate([[0], np.cumsum([v.size for _, v in chosen])]).astype(np.int64)
         for pct in [(94, 1), (95, 1), (96, 1), (97, 1), (9549, 100), (5, 1), (6, 1)]:
-            got = _run_gpu(ctx, vals, offs, mode, *pct, gaps=gaps)
+            got = (_run_gpu_fused if fused else _run_gpu)(ctx, vals, offs, mode, *pct, gaps=gaps)
             want = _oracle(vals, offs, mode, *pct, gaps=gaps)
             for i, (nm, _) in enumerate(chosen):
                 one = tuple(a[i:i + 1] for a in got), tuple(a[i:i + 1] for a in want)
                 _assert_same(one[0], one[1], mode, f"probe-large {nm} gaps={gaps} {mode} p={pct}")
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+def test_select_probe_biggest_buffer(ctx, mode):
+    """A 500,000-slot series at p99.6 (2,001 kept keys, 0.4%): the percentile-only launch keeps
+    the single pass behind the probe with a buffer above 2,560 keys (the biggest buffers the
+    window-select rules still leave to it); parity with a probe that sees only huge values."""
+    from decimal import Decimal
+
+    from krr_amd import _native
+    from krr_amd.core.engine import percentile_params
+
+    L = 500_000
+    info = _native.select_plan(L, percentile_params(Decimal("99.6"), mode))
+    assert info.hselect == 0 and info.probe == 1 and 2560 < info.cap_keys <= 3712, (info.tkeep, info.cap_keys)
+    rng = np.random.default_rng(996)
+    a = rng.gamma(2.0, 0.05, size=L)
+    b = rng.random(L)
+    b[_select_probe_slots(L)] = 1e6 + rng.random(_select_probe_slots(L).size)
+    vals = np.concatenate([a, b])
+    offs = np.array([0, L, 2 * L], dtype=np.int64)
+    got = _run_gpu(ctx, vals, offs, mode, 996, 10)
+    want = _oracle(vals, offs, mode, 996, 10)
+    _assert_same(got, want, mode, f"biggest buffer {mode}")
