@@ -92,6 +92,9 @@ def parse():
                          "memory (host) or into HBM followed by a D2H copy (device)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N > 1 path (process group + pipelined RCCL gather) even with one rank (testing)")
+    ap.add_argument("--chunk-gib", type=float, default=8.0,
+                    help="fleets of more than twice this many GiB of values per resource run as chunks of "
+                         "about this size, in buffers of their own, one launch per chunk")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -140,6 +143,20 @@ def workload(cfg: int, rank: int, world: int, override: int, pods: int = 5):
         return offs, 0, False, f"config3: {n} containers/rank x 1 pod, 1..14 days @1m, compact CSR", total, g0
     return offs, 0, False, (f"config4: {total} containers x 10080 samples (7d@1m) over {world} ranks, "
                             f"compact CSR"), total, g0
+
+
+def fleet_chunks(offs_np: np.ndarray, chunk_gib: float) -> list[tuple[int, int]]:
+    """Contiguous object ranges of about chunk_gib GiB of values each (one range when the
+    fleet holds at most twice that), cut by sample-balanced prefix sums."""
+    from krr_amd.core.distributed import shard_bounds
+
+    S = offs_np.size - 1
+    nbytes = 8 * int(offs_np[-1])
+    limit = max(chunk_gib, 1e-3) * 2**30
+    if S == 0 or nbytes <= 2 * limit:
+        return [(0, S)]
+    n = int(np.ceil(nbytes / limit))
+    return [(lo, hi) for lo, hi in shard_bounds(np.diff(offs_np), n) if hi > lo]
 
 
 def cpu_lease() -> dict:
@@ -255,17 +272,37 @@ def main():
     N = int(offs_np[-1])
     maxlen = int(np.max(np.diff(offs_np))) if S else 0
     ctx = _native.Context(local)
-    offs = torch.from_numpy(offs_np).to(dev)
-    cpu = torch.empty(N, dtype=torch.float64, device=dev)
-    mem = torch.empty(N, dtype=torch.float64, device=dev)
     seed = 1000003 * (args.config + 1)  # one fleet: containers are generated from their global index
-    ctx.synth_fill(cpu, offs, seed, 0, pod_len, gaps, seg_base=g0)
-    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, pod_len, gaps, seg_base=g0)
+    params = percentile_params(Decimal(args.percentile), args.mode)
+    # A fleet of more than 2 chunks' values per resource lives in buffers of about
+    # --chunk-gib each, one launch per chunk (config 4 at N <= 2): at 700k containers one
+    # 113 GB launch streamed at 79.8% of peak and 7 launches over buffers of their own at
+    # 84.3%, on a box where 125k containers in one launch ran at 83.6% (same process,
+    # scripts/footprint_ab.py, profiles/r02/footprint)
+    chunks = fleet_chunks(offs_np, args.chunk_gib)
+    parts = []
+    for lo, hi in chunks:
+        o_np = (offs_np[lo:hi + 1] - offs_np[lo]).astype(np.int64)
+        o = torch.from_numpy(o_np).to(dev)
+        c = torch.empty(int(o_np[-1]), dtype=torch.float64, device=dev)
+        m = torch.empty(int(o_np[-1]), dtype=torch.float64, device=dev)
+        ctx.synth_fill(c, o, seed, 0, pod_len, gaps, seg_base=g0 + lo)
+        ctx.synth_fill(m, o, seed ^ 0x5A5A, 1, pod_len, gaps, seg_base=g0 + lo)
+        ml = int(np.max(np.diff(o_np))) if hi > lo else 0
+        parts.append((lo, hi, c, m, ctx.series(c, o, ml, gaps), ctx.series(m, o, ml, gaps)))
     torch.cuda.synchronize()
 
-    params = percentile_params(Decimal(args.percentile), args.mode)
-    cs = ctx.series(cpu, offs, maxlen, gaps)
-    ms = ctx.series(mem, offs, maxlen, gaps)
+    def host_values(end):
+        """The first `end` slots of both resources on the host (parity / CPU baseline)."""
+        cs_, ms_ = [], []
+        for lo, hi, c, m, _, _ in parts:
+            a = int(offs_np[lo])
+            if a >= end:
+                break
+            k = min(end, int(offs_np[hi])) - a
+            cs_.append(c[:k].cpu().numpy())
+            ms_.append(m[:k].cpu().numpy())
+        return np.concatenate(cs_), np.concatenate(ms_)
     out = {
         "cpu_value": torch.empty(S, dtype=torch.float64, device=dev),
         "cpu_count": torch.empty(S, dtype=torch.int64, device=dev),
@@ -307,6 +344,13 @@ def main():
     # buffer (mapped into the device's address space) instead of HBM + a D2H copy
     zero_copy = args.records == "host" and not dist_on and not args.separate
 
+    def run_all(records, fwd=None):
+        """The fused launch over every chunk (one chunk: one launch); records rows follow
+        the containers; the forward copy rides the first launch."""
+        for j, (lo, hi, _, _, cs, ms) in enumerate(parts):
+            ctx.simple_run(cs, ms, params, {key: v[lo:hi] for key, v in out.items()}, stream,
+                           records=records[lo:hi], forward=fwd if j == 0 else None)
+
     nstep = [0]
 
     def step(events=None):
@@ -321,7 +365,7 @@ def main():
                     fwd = (recv[(k - 1) % 2], host_rec)
             if events is not None:
                 events[0].record(stream)
-            ctx.simple_run(cs, ms, params, out, stream, records=dev_rec, forward=fwd)
+            run_all(dev_rec, fwd)
             if events is not None:
                 events[1].record(stream)
             if rank == 0:
@@ -333,21 +377,25 @@ def main():
         if events is not None:
             events[0].record(stream)
         if zero_copy:
-            ctx.simple_run(cs, ms, params, out, stream, records=host_rec)
+            run_all(host_rec)
             if events is not None:
                 events[1].record(stream)
             return
         if args.separate:
-            ctx.segmented_percentile(cs, params, out["cpu_value"], out["cpu_count"], out["cpu_flags"], stream)
+            for lo, hi, _, _, cs, _ in parts:
+                ctx.segmented_percentile(cs, params, out["cpu_value"][lo:hi], out["cpu_count"][lo:hi],
+                                         out["cpu_flags"][lo:hi], stream)
             if events is not None:
                 events[1].record(stream)
-            ctx.segmented_max(ms, out["mem_value"], out["mem_count"], out["mem_flags"], stream)
+            for lo, hi, _, _, _, ms in parts:
+                ctx.segmented_max(ms, out["mem_value"][lo:hi], out["mem_count"][lo:hi], out["mem_flags"][lo:hi],
+                                  stream)
             if events is not None:
                 events[2].record(stream)
         if args.separate:
             ctx.pack_records(out, dev_rec, stream)  # one launch: 32-B records
-        else:  # ONE launch: CPU percentile + memory max for every container, records included
-            ctx.simple_run(cs, ms, params, out, stream, records=dev_rec)
+        else:  # ONE launch per chunk: CPU percentile + memory max for every container, records included
+            run_all(dev_rec)
             if events is not None:
                 events[1].record(stream)
         if not dist_on:
@@ -463,6 +511,7 @@ def main():
             "parallelism": f"shard{world} (contiguous container ranges, RCCL gather of 32-B records)",
         },
         "samples_per_s": 2 * N * world / step_s,
+        "launches_per_step": len(parts),
         "hbm_frac_step": step_bytes_all / step_s / (HBM_PEAK * world),
         "kernels_ms": kernels,
         "roofline": {
@@ -508,8 +557,7 @@ def main():
         m = S if args.cpu_sample <= 0 else max(1, min(args.cpu_sample, S))
         m = max(1, min(m, int(np.searchsorted(offs_np, 1_100_000_000, side="right")) - 1))
         end = int(offs_np[m])
-        c_host = cpu[:end].cpu().numpy()
-        m_host = mem[:end].cpu().numpy()
+        c_host, m_host = host_values(end)
         o_host = offs_np[: m + 1].copy()
         lease = cpu_lease()
         threads = args.cpu_threads or lease["threads"]
@@ -689,18 +737,29 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     t0, t1 = (T * rank) // world, (T * (rank + 1)) // world
     Lr = t1 - t0
     ctx = _native.Context(local)
-    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * Lr
-    cpu = torch.empty(S * Lr, dtype=torch.float64, device=dev)
     seed = 1000003 * 6
-    ctx.synth_fill_window(cpu, offs, seed, 0, 0, False, t0, T)
-    torch.cuda.synchronize()
-    ser = ctx.series(cpu, offs, Lr, False)
     cfg = sketch.SketchConfig(mantissa_bits=args.sketch_bits)
     params = percentile_params(Decimal(args.percentile), params_mode(args))
     exact = not args.sketch_only
     # N = 1 holds every series whole: the exact answer is ONE single-window select pass;
     # time sharding (sketch merge + refinement) is what N > 1 needs (or --c5-refine)
     direct = exact and world == 1 and not args.c5_refine
+    # the direct pass over 138 GB runs per chunk of series in buffers of their own (as
+    # configs 2-4, fleet_chunks); the sketch path keeps one buffer per rank
+    chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.chunk_gib) if direct else [(0, S)]
+    parts = []
+    for lo, hi in chunks:
+        o = torch.arange(hi - lo + 1, dtype=torch.int64, device=dev) * Lr
+        c = torch.empty((hi - lo) * Lr, dtype=torch.float64, device=dev)
+        ctx.synth_fill_window(c, o, seed, 0, 0, False, t0, T, seg_base=lo)
+        parts.append((lo, hi, c, ctx.series(c, o, Lr, False)))
+    torch.cuda.synchronize()
+    cpu, ser = parts[0][2], parts[0][3]  # the whole rank when it is one chunk (the sketch path)
+
+    def first_rows(k):
+        """[k, Lr] device view/copy of the first k series."""
+        rows = [c.view(hi - lo, Lr)[: max(0, min(k, hi) - lo)] for lo, hi, c, _ in parts if lo < k]
+        return rows[0] if len(rows) == 1 else torch.cat(rows)
     stream = torch.cuda.current_stream()
     dres = None
     if direct:
@@ -718,7 +777,9 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         if ev is not None:
             ev[0].record(stream)
         if direct:
-            ctx.segmented_percentile(ser, params, dres["value"], dres["count"], dres["flags"], stream)
+            for lo, hi, _, ser_c in parts:
+                ctx.segmented_percentile(ser_c, params, dres["value"][lo:hi], dres["count"][lo:hi],
+                                         dres["flags"][lo:hi], stream)
             if ev is not None:
                 ev[1].record(stream)
             rec = torch.stack([dres["value"].view(torch.int64),
@@ -799,6 +860,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                            f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
         },
         "samples_per_s": S * T / step_s,
+        "launches_per_step": len(parts),
         "kernels_ms": kernels_ms,
         "roofline": {"kernel": kname, "bound": "hbm", "achieved": kbytes / (kms * 1e-3) / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kbytes / (kms * 1e-3) / HBM_PEAK,
@@ -819,7 +881,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         pass
     # rank error of the sketch answers against the exact path on a sample of series
     m = max(1, min(args.error_sample, S))
-    piece = cpu.view(S, Lr)[:m].contiguous()
+    piece = first_rows(m).contiguous()
     if world > 1:
         width = (T + world - 1) // world
         pad = torch.full((m, width), float("nan"), dtype=torch.float64, device=dev)
@@ -871,7 +933,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             from oracle import oracle
 
             cs = max(1, min(args.cpu_sample * 5 if args.cpu_sample else 4096, S))  # ~10 s on 16 cores
-            host = cpu.view(S, Lr)[:cs].cpu().numpy().ravel()
+            host = first_rows(cs).cpu().numpy().ravel()
             ho = (np.arange(cs + 1) * Lr).astype(np.int64)
             threads = args.cpu_threads or cpu_lease()["threads"]
             ta = time.perf_counter()

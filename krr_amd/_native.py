@@ -465,12 +465,14 @@ class Context:
                                                  self._stream(stream)))
 
     def synth_fill_window(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, t0: int,
-                          total_len: int, stream=None) -> None:
+                          total_len: int, stream=None, seg_base: int = 0) -> None:
+        """Time window [t0, t0 + len) of series of total_len slots; segment s is global
+        segment seg_base + s."""
         _check_tensor(values, "float64")
         _check_tensor(offsets, "int64")
-        self._check(self._lib.krr_synth_fill_window(
+        self._check(self._lib.krr_synth_fill_global(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
-            int(kind), int(pod_len), int(bool(gaps)), int(t0), int(total_len), self._stream(stream)))
+            int(kind), int(pod_len), int(bool(gaps)), int(seg_base), int(t0), int(total_len), self._stream(stream)))
 
 
 def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectPlanInfo:

@@ -245,3 +245,31 @@ def test_simple_run_forward_copy(mode, gaps, units):
     with pytest.raises(ValueError):
         ctx.simple_run(cs, ms, params, o1, forward=(src, host[:-2]))
     ctx.close()
+
+
+@pytest.mark.parametrize("args", [["--config", "4", "--containers", "3000", "--chunk-gib", "0.05"],
+                                  ["--config", "2", "--containers", "400", "--chunk-gib", "0.05", "--mode", "ref_index"],
+                                  ["--config", "4", "--containers", "3000", "--chunk-gib", "0.05", "--separate"]])
+def test_bench_chunked_fleet_one_rank(args):
+    """A fleet cut into chunks (buffers of their own, one launch per chunk, records rows per
+    chunk written into the host buffer): parity with the oracle on every container and the
+    host records equal to the device results."""
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), *args,
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["launches_per_step"] > 1 and r["parity_vs_oracle_on_sample"] is True, r
+    assert r["parity_sample_containers"] == r["config"]["containers"]
+    if "--separate" not in args:
+        assert r["records_host_equal_device"] is True
+
+
+def test_bench_config5_direct_chunked():
+    """Config 5 at N = 1 (exact single-window select per chunk of series): equal bits to the
+    select over the regathered series."""
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5",
+                        "--containers", "600", "--chunk-gib", "0.2", "--steps", "2", "--warmup", "1",
+                        "--error-sample", "600", "--no-cpu-baseline"], capture_output=True, text=True, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["parity_vs_single_window_select"] is True and r["parity_sample_series"] == 600, r
