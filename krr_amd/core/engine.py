@@ -115,19 +115,10 @@ class SimpleEngine:
 
         S = fleet.n_objects
         with torch.cuda.device(self.device):
-            cv, co = self._to_device(fleet.cpu)
-            mv, mo = self._to_device(fleet.mem)
             # the launch writes the 32-B records straight into page-locked host memory
             # (krr_simple_run_records with a mapped host buffer): one sync, no D2H copies
             rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
-            ctx = self.context()
-            dev = cv.device
-            out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
-                   (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
-                    ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
-            ctx.simple_run(ctx.series(cv, co, max(fleet.cpu.max_len, 1), fleet.cpu.gaps_are_nan),
-                           ctx.series(mv, mo, max(fleet.mem.max_len, 1), fleet.mem.gaps_are_nan),
-                           params, out, records=rec)
+            self._run_chunks(fleet, params, rec)
             torch.cuda.current_stream(self.device).synchronize()
         host = unpack_records(rec.numpy())
         return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"], host["mem_value"],
@@ -149,18 +140,42 @@ class SimpleEngine:
         if S == 0:
             return rec
         with torch.cuda.device(self.device):
-            cv, co = self._to_device(fleet.cpu)
-            mv, mo = self._to_device(fleet.mem)
-            out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
-                   (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
-                    ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
-            ctx = self.context()
-            ctx.simple_run(ctx.series(cv, co, max(fleet.cpu.max_len, 1), fleet.cpu.gaps_are_nan),
-                           ctx.series(mv, mo, max(fleet.mem.max_len, 1), fleet.mem.gaps_are_nan),
-                           params, out, records=rec)
+            self._run_chunks(fleet, params, rec)
             # the host buffers may be pinned and released by the caller: finish the copies
             torch.cuda.current_stream(self.device).synchronize()
         return rec
+
+    # a fleet of more than 2 chunks of values runs as chunks of about this many bytes
+    # (both resources), each uploaded into buffers of its own and launched on its own:
+    # HBM holds one chunk at a time, and big single launches stream slower
+    # (profiles/r02/footprint)
+    chunk_bytes = 16 << 30
+
+    def _run_chunks(self, fleet: PackedFleet, params: _native.KrrPercentileParams, rec) -> None:
+        """Upload + fused launch per chunk of objects, records rows into ``rec`` (device or
+        page-locked host), all on the current stream: a chunk's device buffers are released
+        to the caching allocator after its launch is enqueued, which reuses them in stream
+        order for the next chunk."""
+        import torch
+
+        from krr_amd.core.distributed import fleet_shard_bounds, slice_fleet
+
+        S = fleet.n_objects
+        nbytes = 8 * (int(fleet.cpu.offsets[-1]) + int(fleet.mem.offsets[-1]))
+        n = 1 if nbytes <= 2 * self.chunk_bytes else -(-nbytes // self.chunk_bytes)
+        bounds = [(0, S)] if n == 1 else [(lo, hi) for lo, hi in fleet_shard_bounds(fleet, n) if hi > lo]
+        ctx = self.context()
+        dev = torch.device("cuda", self.device)
+        out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+               (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+                ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+        for lo, hi in bounds:
+            part = fleet if (lo, hi) == (0, S) else slice_fleet(fleet, lo, hi)
+            cv, co = self._to_device(part.cpu)
+            mv, mo = self._to_device(part.mem)
+            ctx.simple_run(ctx.series(cv, co, max(part.cpu.max_len, 1), part.cpu.gaps_are_nan),
+                           ctx.series(mv, mo, max(part.mem.max_len, 1), part.mem.gaps_are_nan),
+                           params, {k: v[lo:hi] for k, v in out.items()}, records=rec[lo:hi])
 
 
 def pinned_alloc(n: int) -> np.ndarray:

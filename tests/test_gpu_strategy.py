@@ -332,3 +332,30 @@ def test_concurrent_run_calls_share_launches_on_gpu():
         assert got == want["raw"], case["name"]
     co = strat.coalescer()
     assert co.calls == len(cases) and co.launches < len(cases)
+
+
+def test_engine_chunks_large_fleets(monkeypatch):
+    """SimpleEngine runs a fleet of more than two chunks as chunks (uploads and launches of
+    their own, records rows per chunk): with a 256-KiB chunk the golden cases come back
+    identical to the one-launch run, through run_batch (host records) and the device-records
+    path of the multi-GPU shard."""
+    from krr_amd.core.distributed import unpack_records
+    from krr_amd.core.engine import SimpleEngine
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    strat = SimpleStrategy(SimpleStrategySettings(**PATHS["cli_99_5"]))
+    ok_cases = [c for c in DOC["cases"] if "error" not in c["results"]["cli_99_5"]] * 40
+    fleet = strat.pack([_hist(c) for c in ok_cases])
+    one = strat.settings.run_fleet(fleet)
+    rec_one = strat.settings.run_fleet_records(fleet).cpu().numpy()
+    assert 8 * (fleet.cpu.offsets[-1] + fleet.mem.offsets[-1]) > 6 * (256 << 10)
+    monkeypatch.setattr(SimpleEngine, "chunk_bytes", 256 << 10)
+    many = strat.settings.run_fleet(fleet)
+    rec_many = strat.settings.run_fleet_records(fleet).cpu().numpy()
+    for f in ("cpu_value", "mem_value"):
+        assert np.array_equal(getattr(one, f).view(np.uint64), getattr(many, f).view(np.uint64)), f
+    for f in ("cpu_count", "cpu_flags", "mem_count", "mem_flags"):
+        assert np.array_equal(getattr(one, f), getattr(many, f)), f
+    assert np.array_equal(rec_one, rec_many)
+    u = unpack_records(rec_many)
+    assert np.array_equal(u["cpu_value"].view(np.uint64), many.cpu_value.view(np.uint64))
