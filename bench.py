@@ -270,7 +270,6 @@ def main():
                                                                    args.pods)
     S = offs_np.size - 1
     N = int(offs_np[-1])
-    maxlen = int(np.max(np.diff(offs_np))) if S else 0
     ctx = _native.Context(local)
     seed = 1000003 * (args.config + 1)  # one fleet: containers are generated from their global index
     params = percentile_params(Decimal(args.percentile), args.mode)
