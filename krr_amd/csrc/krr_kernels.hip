@@ -58,10 +58,10 @@
 #define KRR_HSEL_WAVES_PER_SIMD 2  // ... and for hselect (LDS allows ~9 waves per CU)
 #endif
 #ifndef KRR_WSEL_WAVES_PER_SIMD
-#define KRR_WSEL_WAVES_PER_SIMD 3  // ... and for the window select (wselect)
+#define KRR_WSEL_WAVES_PER_SIMD 4  // ... and for the window select (wselect) of short segments
 #endif
 #ifndef KRR_WSEL_CAP
-#define KRR_WSEL_CAP 1472  // wselect's LDS keys: 1.5 + 11.5 KiB per wave -> 12 waves per CU
+#define KRR_WSEL_CAP 1088  // wselect's LDS keys: 1.5 + 8.5 KiB per wave -> 16 waves per CU (v23)
 #endif
 #ifndef KRR_WSEL_CAP_LONG
 #define KRR_WSEL_CAP_LONG 2304  // ... for launches of long segments (1.5 + 18 KiB -> 8 waves per CU)
@@ -1607,7 +1607,10 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
 // (k_hselect_list), so the window kernel's LDS and registers are its own.
 constexpr uint32_t kWselCap = (uint32_t)KRR_WSEL_CAP & ~63u;
 constexpr uint32_t kWselCapLong = (uint32_t)KRR_WSEL_CAP_LONG & ~63u;
-static_assert(kWselCap >= kChunkElems + 256 && kWselCapLong >= kWselCap,
+#ifndef KRR_WSEL_CAP_MIN_SLACK
+#define KRR_WSEL_CAP_MIN_SLACK 64  // the first chunk (every present sample) fits an empty window
+#endif
+static_assert(kWselCap >= kChunkElems + KRR_WSEL_CAP_MIN_SLACK && kWselCapLong >= kWselCap,
               "the window buffer takes a chunk before its first shrink");
 // Per launch: more waves per CU for shorter segments (their fixed per-segment work
 // needs the overlap), a larger window for long ones (fewer shrinks).
@@ -2240,23 +2243,32 @@ constexpr int64_t kFwdItemUnits = 4096;  // 64 KiB per item
 __device__ __forceinline__ void forward_item(const MaxArgs& M, int64_t i, int lane) {
     const int64_t a = i * kFwdItemUnits;
     const int64_t e = a + kFwdItemUnits < M.fwd_units ? a + kFwdItemUnits : M.fwd_units;
+    // not unrolled: an unrolled copy keeps many 16-B loads in flight and lifts the fused
+    // kernel's VGPR count (and so its occupancy) for every launch, forward or not
+#pragma unroll 1
     for (int64_t u = a + lane; u < e; u += kWave) M.fwd_dst[u] = M.fwd_src[u];
 }
 
-template <int CPU_KIND>
+// FWD: the launch also runs a forward copy (krr_simple_run_forward) as its first items.  A
+// template parameter, not a runtime branch: the forward arguments would otherwise take
+// scalar registers in every launch (SGPR spills into VGPR lanes: the CPU_SELECT kernel went
+// from 126 to 131 VGPRs, the short window kernel from 129 to 133).
+template <int CPU_KIND, bool FWD = false>
 __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? window_waves(false)
                                 : CPU_KIND == CPU_HSELECT_LONG ? window_waves(true)
                                                                : KRR_SELECT_WAVES_PER_SIMD) void k_simple(SelectArgs A, RefArgs R, MaxArgs M) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t S_cpu = CPU_KIND == CPU_REF_GAPS ? R.S : A.S;
-    const int64_t F = M.fwd_items;  // forward-copy items first: short, done while the stream ramps up
+    const int64_t F = FWD ? M.fwd_items : 0;  // forward-copy items first: short, done while the stream ramps up
     const int64_t total = F + S_cpu + M.S;
     constexpr bool kWindow = CPU_KIND == CPU_HSELECT || CPU_KIND == CPU_HSELECT_LONG;
     if (kWindow && A.fail_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.fail_reset = 0;
     for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {
-        if (bb < F) {
-            forward_item(M, bb, threadIdx.x);
-            continue;
+        if constexpr (FWD) {
+            if (bb < F) {
+                forward_item(M, bb, threadIdx.x);
+                continue;
+            }
         }
         const int64_t b = bb - F;  // F is a multiple of 8: blocks keep their XCD's eighth
         // remap within each resource's half, so the CPU items still all precede
@@ -3075,7 +3087,9 @@ int krr_create(int device, krr_ctx** out_ctx) {
 
     for (const void* f : {(const void*)k_select<SEL_SINGLE>, (const void*)k_select<SEL_WINDOW>,
                           (const void*)k_select<SEL_WINDOW_LONG>, (const void*)k_simple<CPU_SELECT>,
-                          (const void*)k_simple<CPU_HSELECT>, (const void*)k_simple<CPU_HSELECT_LONG>})
+                          (const void*)k_simple<CPU_HSELECT>, (const void*)k_simple<CPU_HSELECT_LONG>,
+                          (const void*)k_simple<CPU_SELECT, true>, (const void*)k_simple<CPU_HSELECT, true>,
+                          (const void*)k_simple<CPU_HSELECT_LONG, true>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     (void)hipFuncSetAttribute((const void*)k_sketch_build, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
@@ -3216,17 +3230,26 @@ int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series
     const int64_t items = M.fwd_items + 2 * S;
     RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags, records};
     SelectArgs A{};
+    const bool fwd = M.fwd_items > 0;
     if (params->mode == KRR_PCT_REF_INDEX) {
-        hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
+        if (fwd) hipLaunchKernelGGL((k_simple<CPU_REF_GAPS, true>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
+        else hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
     } else {
         size_t lds = 0;
         rc = plan_select(ctx, cpu, params, st, cpu_value, cpu_count, cpu_flags, &A, &lds, true);
         if (rc) return rc;
         A.rec = records;
-        if (A.cap) hipLaunchKernelGGL((k_simple<CPU_SELECT>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
-        else if (A.wcap == kWselCapLong)
-            hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
-        else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), dim3(grid_for(items)), dim3(64), lds, st, A, R, M);
+        const dim3 g(grid_for(items)), b(64);
+        if (A.cap) {
+            if (fwd) hipLaunchKernelGGL((k_simple<CPU_SELECT, true>), g, b, lds, st, A, R, M);
+            else hipLaunchKernelGGL((k_simple<CPU_SELECT>), g, b, lds, st, A, R, M);
+        } else if (A.wcap == kWselCapLong) {
+            if (fwd) hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG, true>), g, b, lds, st, A, R, M);
+            else hipLaunchKernelGGL((k_simple<CPU_HSELECT_LONG>), g, b, lds, st, A, R, M);
+        } else {
+            if (fwd) hipLaunchKernelGGL((k_simple<CPU_HSELECT, true>), g, b, lds, st, A, R, M);
+            else hipLaunchKernelGGL((k_simple<CPU_HSELECT>), g, b, lds, st, A, R, M);
+        }
         KRR_HIP(ctx, hipGetLastError());
         return launch_fallback(ctx, A, S, st);
     }
