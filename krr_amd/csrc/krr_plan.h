@@ -79,8 +79,11 @@ constexpr uint32_t kChunkElems = 2u * kUnroll * 64u;
 // chunk always fits; the 128-key margin above tkeep is what a histogram cut may
 // keep beyond tkeep before the exact fallback is needed.  The first chunk of a
 // segment (every sample a candidate) must fit an empty buffer.
+#ifndef KRR_CAP_MARGIN
+#define KRR_CAP_MARGIN 128
+#endif
 KRR_HD inline uint32_t capacity_for(uint32_t tkeep_max) {
-    uint64_t c = (uint64_t)tkeep_max + kChunkElems / 2 + 128;
+    uint64_t c = (uint64_t)tkeep_max + kChunkElems / 2 + KRR_CAP_MARGIN;
     if (c < kChunkElems + 64) c = kChunkElems + 64;
     c = (c + 63) & ~63ull;
     return (uint32_t)c;
