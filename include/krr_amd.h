@@ -201,7 +201,7 @@ typedef struct {
     int32_t bottom;       /* 1: the smallest keys are kept (low percentiles) */
     int64_t tkeep;        /* keys a segment of max length must keep */
     int64_t cap_keys;     /* single-pass candidate capacity (0 with hselect) */
-    int64_t lds_bytes;    /* dynamic LDS per workgroup */
+    int64_t lds_bytes;    /* dynamic LDS per workgroup (compact layout; a gapped one keeps the short-segment window) */
     int32_t probe;        /* 1: a max-length segment starts at a probe-estimated threshold */
     int32_t fused_hselect; /* the same choice for krr_simple_run's fused launch */
 } krr_select_plan_info;

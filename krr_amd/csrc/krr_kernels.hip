@@ -1614,7 +1614,15 @@ static_assert(kWselCap >= kChunkElems + KRR_WSEL_CAP_MIN_SLACK && kWselCapLong >
               "the window buffer takes a chunk before its first shrink");
 // Per launch: more waves per CU for shorter segments (their fixed per-segment work
 // needs the overlap), a larger window for long ones (fewer shrinks).
-KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax) { return Lmax >= KRR_WSEL_LONG ? kWselCapLong : kWselCap; }
+// Gapped (NaN-masked) layouts keep the 16-waves/CU kernel at any length: config 2 (50,400
+// gapped slots) p50 fused 1.183 -> 1.163 ms, p95 1.183 -> 1.166, while 50,400 compact slots
+// p50 lose 2% without the long window (profiles/r02/z, v24).
+#ifndef KRR_WSEL_LONG_GAPS
+#define KRR_WSEL_LONG_GAPS 0  // 1: gapped layouts take the long-segment kernel too
+#endif
+KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax, bool gaps = false) {
+    return Lmax >= KRR_WSEL_LONG && (KRR_WSEL_LONG_GAPS || !gaps) ? kWselCapLong : kWselCap;
+}
 
 enum { WIN_GENERAL = 0, WIN_FAST = 1, WIN_FULL = 2 };  // window classify modes (WindowProc::classify)
 
@@ -3000,7 +3008,7 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->out_n = on;
     A->out_f = of;
     A->stats = ctx->d_tmp + 1;
-    A->wcap = wsel_cap_for(Lmax);
+    A->wcap = wsel_cap_for(Lmax, series->gaps_are_nan != 0);
     if (hsel && KRR_WSEL && A->wcap != kWselCapLong) {  // misses: a list for the hselect launch that follows
         if (ctx->fail_cap < series->n_segments) {
             if (ctx->d_fail_list) KRR_HIP(ctx, hipFree(ctx->d_fail_list));
