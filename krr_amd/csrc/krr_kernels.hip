@@ -1614,11 +1614,13 @@ static_assert(kWselCap >= kChunkElems + KRR_WSEL_CAP_MIN_SLACK && kWselCapLong >
               "the window buffer takes a chunk before its first shrink");
 // Per launch: more waves per CU for shorter segments (their fixed per-segment work
 // needs the overlap), a larger window for long ones (fewer shrinks).
-// Gapped (NaN-masked) layouts keep the 16-waves/CU kernel at any length: config 2 (50,400
-// gapped slots) p50 fused 1.183 -> 1.163 ms, p95 1.183 -> 1.166, while 50,400 compact slots
-// p50 lose 2% without the long window (profiles/r02/z, v24).
+// Long segments take the long-segment kernel in every layout: its rare window misses run
+// hselect inline, beside the other waves.  (Gapped 50,400-slot segments on the 16-waves/CU
+// kernel were 1.5% faster at p50/p95 in the A/B, profiles/r02/z, but a miss there goes to the
+// separate miss pass, where ONE wave streams the whole segment twice: on the bench's data one
+// miss per launch cost config 2 p97 +150 us.)
 #ifndef KRR_WSEL_LONG_GAPS
-#define KRR_WSEL_LONG_GAPS 0  // 1: gapped layouts take the long-segment kernel too
+#define KRR_WSEL_LONG_GAPS 1  // 0: gapped layouts keep the 16-waves/CU kernel at any length
 #endif
 KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax, bool gaps = false) {
     return Lmax >= KRR_WSEL_LONG && (KRR_WSEL_LONG_GAPS || !gaps) ? kWselCapLong : kWselCap;

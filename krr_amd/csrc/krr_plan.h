@@ -163,6 +163,11 @@ KRR_HD inline bool single_pass_ok(uint32_t need, uint32_t tkeep, int64_t L, uint
 // p96 1.189 -> 1.184; config 3 p95 2.56 -> 2.44, p96 2.46 -> 2.43; p97 and up (<= 3%
 // kept) and the 10,080-slot config-4 shape equal or better on the single pass.
 //
+// (Tried in round 2: every fused buffer above 1,200 keys to the window, with gapped long
+// segments on the 16-waves/CU kernel — faster in the A/B (config 2 p97 1.206 -> 1.186 ms),
+// but on the bench's data one 50,400-slot segment per launch missed the window, and a miss
+// there is finished by ONE wave in the separate miss pass: +150 us, config 2 p97 1.29 ms.
+// Long segments keep the kernel whose misses run inline, beside the other waves.)
 // Round 2, v21 (profiles/r02/q, same-process A/B of the percentile pass alone and of the
 // fused launch): a percentile-only launch (krr_segmented_percentile) gains from the window
 // down to 0.5% kept — 30d@15s (172,800 slots) p99 4.42 -> 4.23 ms, 50,400-slot p98 0.684 ->

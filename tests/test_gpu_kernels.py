@@ -429,13 +429,12 @@ def test_select_probe_start_threshold(ctx, mode):
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
 @pytest.mark.parametrize("L", [50400, 100800])
 def test_select_probe_large_buffer(ctx, mode, L, fused):
-    """Long launches at tail percentiles: the fused launch runs 50,400-slot p97 single-pass
-    behind the start-threshold probe (1,515 kept keys, a 2,176-key buffer), the percentile-only
-    launch and 100,800-slot p97 (3,027 kept keys) take the window select, and p94-p96 (4-6%
-    kept) the window select everywhere (krr_plan.h single_pass_ok / window_select; the plan is
-    pinned by tests/test_abi.py::test_select_plan_decisions): hits, a probe that sees only huge
-    values (re-stream), only tiny values, gaps, and a short segment sharing the launch.  p5 / p6
-    keep the BOTTOM keys, for which there is no probe: window select."""
+    """Long launches at tail percentiles through both launch kinds: p94-p97 and p95.49
+    (1,515-3,027 kept keys) take the window select (krr_plan.h single_pass_ok / window_select; the plan is pinned by
+    tests/test_abi.py::test_select_plan_decisions; the biggest probe-backed buffers by
+    test_select_probe_biggest_buffer): hits, a probe that sees only huge values (re-stream),
+    only tiny values, gaps, and a short segment sharing the launch.  p5 / p6 keep the BOTTOM
+    keys, for which there is no probe: window select."""
     rng = np.random.default_rng(97)
     ps = _select_probe_slots(L)
     segs = [("gamma", rng.gamma(2.0, 0.05, size=L), False), ("short", rng.gamma(2.0, 0.05, size=3000), False)]

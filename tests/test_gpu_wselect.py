@@ -142,13 +142,12 @@ def test_adversarial_orders_exact_with_fallback(ctx, mode):
 
 @pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
 @pytest.mark.parametrize("lens", [(50400, 0, 30000, 50400, 17000, 50400), (20160, 0, 12000, 20160, 7000, 20160)],
-                         ids=["long_lengths", "short_lengths"])
+                         ids=["long_kernel", "short_kernel"])
 def test_gaps_nan_and_empty(ctx, mode, lens):
     """Gapped segments (incl. negative NaN gaps, all-gap and empty segments) and a real
-    NaN sample in the compact layout (flagged) through the window select.  Gapped layouts
-    run the 16-waves/CU kernel at any length (v24), whose scalar counts recount every chunk
-    holding a NaN and take negative NaNs back out of "below"; the compact long lengths run
-    the long-segment kernel (per-lane counts)."""
+    NaN sample in the compact layout (flagged) through the window select: the long-segment
+    kernel (per-lane counts) and the 16-waves/CU kernel, whose scalar counts recount every
+    chunk holding a NaN and take negative NaNs back out of "below"."""
     rng = np.random.default_rng(77)
     lens = np.array(lens, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
