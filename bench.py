@@ -477,16 +477,20 @@ def main():
 
     # algorithmic bytes per launch: every stored slot once, offsets, outputs
     seg_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S  # one resource
+    # compact REF_INDEX reads one sample per CPU segment (an index into the unsorted list),
+    # not the segment: offsets + the gathered sample + outputs
+    dense_ref = args.mode == "ref_index" and not gaps
+    cpu_bytes = 8 * (S + 1) + 8 * S + (8 + 8 + 4) * S if dense_ref else seg_bytes
     if args.separate:
         kname = "k_select" if args.mode != "ref_index" else ("k_refindex_gaps" if gaps else "k_refindex_dense")
-        kbytes, kms = seg_bytes, k1_ms
+        kbytes, kms = cpu_bytes, k1_ms
         kernels = {kname: k1_ms, "k_max": k2_ms}
     else:
-        kname = "k_simple" if not (args.mode == "ref_index" and not gaps) else "k_refindex_dense+k_max"
-        kbytes, kms = 2 * seg_bytes, k1_ms
+        kname = "k_simple" if not dense_ref else "k_refindex_dense+k_max"
+        kbytes, kms = cpu_bytes + seg_bytes, k1_ms
         kernels = {kname: k1_ms}
     achieved = kbytes / (kms * 1e-3)
-    step_bytes_all = 2 * seg_bytes * world
+    step_bytes_all = (cpu_bytes + seg_bytes) * world
     result = {
         "metric": METRIC,
         "value": containers_total / step_s,
@@ -525,7 +529,8 @@ def main():
         },
     }
     if args.mode == "ref_index" and not gaps:
-        result["roofline"]["note"] = "compact REF_INDEX is one gather per segment: bytes count every slot anyway"
+        result["roofline"]["note"] = ("compact REF_INDEX: the CPU half is one gather per segment (offsets + one "
+                                      "sample + outputs), the memory half streams every slot")
     result["config"]["records"] = "page-locked host memory, written by the launch" if zero_copy else \
         "HBM + D2H copy" if not dist_on else "HBM + RCCL gather to rank 0"
     if dist_on:
