@@ -273,3 +273,13 @@ def test_bench_config5_direct_chunked():
     assert p.returncode == 0, p.stderr[-4000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert r["parity_vs_single_window_select"] is True and r["parity_sample_series"] == 600, r
+
+
+def test_bench_four_ranks_chunked_shards():
+    """Four gloo ranks sharing the GPU, config 4 cut into shards that are each chunked (buffers
+    of their own, one launch per chunk): the gathered records equal the oracle and rank 0's
+    kernel on samples from every shard."""
+    r = _bench(["--gpus", "4", "--config", "4", "--containers", "2000", "--chunk-gib", "0.03", "--steps", "2",
+                "--warmup", "1", "--parity-block", "64"], timeout=300)
+    assert r["n_gpus"] == 4 and r["launches_per_step"] > 1
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_gathered_vs_rank0_kernel"] is True, r
