@@ -1598,7 +1598,7 @@ __device__ __forceinline__ void hselect_segment(const SelectArgs& A, int64_t s, 
 #define KRR_WSEL 1
 #endif
 #ifndef KRR_WSEL_Z
-#define KRR_WSEL_Z 4.5
+#define KRR_WSEL_Z 5.0  // v26: 4.5 left ~1 statistical miss per 100k short segments (a ~40 us serial tail)
 #endif
 #ifndef KRR_WSEL_BINS
 #define KRR_WSEL_BINS 1  // shrink to histogram-bin edges (one pass) instead of exact keys (0)
