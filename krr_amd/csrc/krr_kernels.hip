@@ -33,6 +33,9 @@
 #ifndef KRR_STREAM_DEPTH
 #define KRR_STREAM_DEPTH 2  // chunks in flight per wave
 #endif
+#ifndef KRR_WSEL_LONG_DEPTH
+#define KRR_WSEL_LONG_DEPTH 2  // chunks in flight beyond the one processed, long-segment window kernels (v27)
+#endif
 #ifndef KRR_ONE_SITE_DEPTH
 #define KRR_ONE_SITE_DEPTH 1  // chunks in flight beyond the one processed, single-call-site streaming loop
 #endif
@@ -158,7 +161,7 @@ __device__ __forceinline__ void load_chunk(double2 (&c)[kUnroll], const double2*
     for (int u = 0; u < kUnroll; ++u) c[u] = load16(p + u * kWave);
 }
 
-template <bool ONE_SITE, class Proc>
+template <bool ONE_SITE, class Proc, int DEPTH = KRR_ONE_SITE_DEPTH>
 __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ vals, int64_t beg,
                                                    int64_t end, Proc& proc, int lane) {
     int64_t a0 = (beg + 1) & ~(int64_t)1;
@@ -236,7 +239,7 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
         // KRR_ONE_SITE_DEPTH > 1: a ring of that many chunks in flight (for launches
         // whose LDS budget leaves few waves per CU to cover HBM latency).
         double2 cur[kUnroll];
-        if constexpr (KRR_ONE_SITE_DEPTH <= 1) {
+        if constexpr (DEPTH <= 1) {
             double2 nxt[kUnroll];
             fill_u(nxt, 0);
 #pragma unroll
@@ -259,7 +262,7 @@ __device__ __forceinline__ uint32_t stream_segment(const double* __restrict__ va
             // before that copy leaves the D - 1 newer chunks' loads outstanding.
             // (Register shifting would wait for every load.)  D call sites of
             // proc.chunk.
-            constexpr int D = KRR_ONE_SITE_DEPTH;
+            constexpr int D = DEPTH;
             double2 ring[D][kUnroll];
             {
                 double2 first[kUnroll];
@@ -1950,7 +1953,9 @@ __device__ __forceinline__ void wselect_segment(const SelectArgs& A, int64_t s, 
     // opaque bounds (see select_segment): no address set-up hoisted across the pass
     int64_t b = beg, e = end;
     asm volatile("" : "+s"(b), "+s"(e));
-    const uint32_t pad = stream_segment<true>(A.vals, b, e, W, lane);
+    const uint32_t pad =
+        stream_segment<true, WindowProc<INLINE_FALLBACK>, INLINE_FALLBACK ? KRR_WSEL_LONG_DEPTH : KRR_ONE_SITE_DEPTH>(
+            A.vals, b, e, W, lane);
     __syncthreads();
     const uint64_t nnan = W.nan_total() - pad;
     const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;
