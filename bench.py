@@ -66,8 +66,12 @@ def parse():
     ap.add_argument("--sketch-only", action="store_true",
                     help="config 5: stop at the sketch answer (approximate) instead of the exact refinement")
     ap.add_argument("--c5-refine", action="store_true",
-                    help="config 5 at N=1: run the time-sharded sketch + exact-refinement path instead of the "
-                         "direct single-window select (N>1 always uses it)")
+                    help="config 5 at N=1: run the time-sharded exact path (--c5-method) instead of the direct "
+                         "single-window select (N>1 always uses it)")
+    ap.add_argument("--c5-method", choices=("window", "sketch"), default="window",
+                    help="config 5 time-sharded exact path: window = one HBM pass (window export + all-to-all + "
+                         "merge, misses regathered); sketch = sketch build + reduce-scatter + locate + collect "
+                         "(a second HBM pass) + refine")
     ap.add_argument("--error-sample", type=int, default=256, help="config 5: series checked against the exact path")
     ap.add_argument("--mode", default="linear", choices=["linear", "sorted_lower", "ref_index"])
     ap.add_argument("--percentile", default="99")
@@ -96,7 +100,19 @@ def parse():
                     help="fleets of more than twice this many GiB of values per resource run as chunks of "
                          "about this size, in buffers of their own, one launch per chunk")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--deadline", type=float, default=float(os.environ.get("KRR_BENCH_DEADLINE", "540")),
+                    help="--gpus N > 1 launcher: seconds before every rank is stopped (SIGTERM, then SIGKILL) and "
+                         "one JSON line with status 'timeout' and each rank's last phase is printed")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds torch.distributed waits in a collective / rendezvous before failing")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-path measurements (H2D, native packer, end-to-end from JSON bodies)")
     return ap.parse_args()
+
+
+def phase(name: str) -> None:
+    """This rank's progress on stderr (the launcher keeps each rank's last phase)."""
+    print(f"KRR_PHASE rank={os.environ.get('RANK', '0')} {name}", file=sys.stderr, flush=True)
 
 
 def _splitmix(x: np.ndarray) -> np.ndarray:
@@ -176,22 +192,49 @@ def cpu_lease() -> dict:
 
 def launch_ranks(args) -> int:
     """--gpus N > 1 without torchrun: spawn N ranks (fresh interpreters, nothing here
-    touches the GPU), stream their output through, return the first failing exit code."""
+    touches the GPU), forward their output, return the first failing exit code.
+
+    Every rank reports its phase on stderr (init, synth, warmup, step k, gather, report);
+    the launcher keeps each rank's last one.  If the ranks are still running after
+    --deadline seconds (e.g. one hangs in a rendezvous or a collective), they are all
+    stopped (SIGTERM, then SIGKILL) and ONE JSON line with status "timeout" and every
+    rank's last phase is printed, exit code 124."""
     import signal
     import socket
     import subprocess
+    import threading
 
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    procs = []
+    procs, phases = [], {}
+    lock = threading.Lock()
+
+    def pump(r, pipe):
+        for raw in iter(pipe.readline, b""):
+            line = raw.decode(errors="replace")
+            if line.startswith("KRR_PHASE "):
+                with lock:
+                    phases[r] = line.split(" ", 2)[2].strip()
+            sys.stderr.write(line)
+            sys.stderr.flush()
+
+    pumps = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                             stderr=subprocess.PIPE)
+        procs.append(p)
+        phases[r] = "started"
+        t = threading.Thread(target=pump, args=(r, p.stderr), daemon=True)
+        t.start()
+        pumps.append(t)
     rc = 0
     alive = set(range(args.gpus))
-    deadline = None
+    kill_at = None
+    t_end = time.time() + args.deadline
+    timed_out = False
     while alive:
         for r in sorted(alive):
             c = procs[r].poll()
@@ -203,12 +246,27 @@ def launch_ranks(args) -> int:
                 print(f"bench.py launcher: rank {r} exited with {c}; stopping the others", file=sys.stderr)
                 for q in alive:
                     procs[q].send_signal(signal.SIGTERM)
-                deadline = time.time() + 20
-        if deadline is not None and time.time() > deadline:
+                kill_at = time.time() + 20
+        if alive and not timed_out and time.time() > t_end:
+            timed_out = True
+            with lock:
+                last = {str(q): phases.get(q) for q in range(args.gpus)}
+            print(f"bench.py launcher: deadline of {args.deadline:.0f} s passed; stopping ranks {sorted(alive)}",
+                  file=sys.stderr)
+            for q in alive:
+                procs[q].send_signal(signal.SIGTERM)
+            kill_at = time.time() + 10
+            print(json.dumps({"metric": METRIC, "n_gpus": args.gpus, "status": "timeout",
+                              "deadline_s": args.deadline, "ranks_running": sorted(alive), "rank_phases": last}),
+                  file=_JSON_OUT, flush=True)
+            rc = 124
+        if kill_at is not None and time.time() > kill_at:
             for q in alive:
                 procs[q].kill()
-            deadline = None
+            kill_at = None
         time.sleep(0.1)
+    for t in pumps:
+        t.join(timeout=5)
     return rc
 
 
@@ -227,6 +285,10 @@ def main():
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if os.environ.get("KRR_BENCH_TEST_HANG"):  # tests: a rank that never finishes (launcher deadline)
+        phase("init")
+        while True:
+            time.sleep(1)
     # Native libraries (RCCL's version banner, gloo's peer messages) write to fd 1:
     # point fd 1 at stderr and keep the real stdout for the ONE JSON line.
     global _JSON_OUT
@@ -258,10 +320,14 @@ def main():
     # N>1 path with several ranks on ONE GPU (RCCL refuses duplicate devices).
     backend = os.environ.get("KRR_BENCH_BACKEND", "nccl")
     if dist_on:
+        import datetime
+
+        phase("init")
+        tmo = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
     if args.config == 5:
         return run_config5(args, world, rank, local, dev, coll_dev)
@@ -279,6 +345,7 @@ def main():
     # 84.3%, on a box where 125k containers in one launch ran at 83.6% (same process,
     # scripts/footprint_ab.py, profiles/r02/footprint)
     chunks = fleet_chunks(offs_np, args.chunk_gib)
+    phase("synth")
     parts = []
     for lo, hi in chunks:
         o_np = (offs_np[lo:hi + 1] - offs_np[lo]).astype(np.int64)
@@ -372,6 +439,8 @@ def main():
                 last[0] = recv[k % 2]
             else:
                 ctx.gather_results(comm, 0, dev_rec, stream=stream)
+            if events is not None:
+                events[2].record(stream)
             return
         if events is not None:
             events[0].record(stream)
@@ -452,6 +521,7 @@ def main():
         if int(flag.item()) == 0:
             gather_mode = "torch"
             last[0] = None
+    phase("warmup")
     for _ in range(args.warmup):
         step()
     finish()
@@ -460,6 +530,7 @@ def main():
         dist.barrier()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     torch.cuda.synchronize()
+    phase(f"timed {args.steps} steps")
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
@@ -468,12 +539,22 @@ def main():
     if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
+    phase("report")
     dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=coll_dev)
     if dist_on:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())
     k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs])) if args.separate else 0.0
+    # N > 1: where each rank's step goes (kernel on the launch stream; the RCCL gather
+    # enqueued after it on the same stream, "stream" mode only)
+    per_rank = None
+    if dist_on:
+        g_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs])) if gather_mode == "stream" else float("nan")
+        mine = torch.tensor([k1_ms, g_ms], dtype=torch.float64, device=coll_dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[float(x) for x in t.cpu().tolist()] for t in allr]
 
     # algorithmic bytes per launch: every stored slot once, offsets, outputs
     seg_bytes = 8 * N + 8 * (S + 1) + (8 + 8 + 4) * S  # one resource
@@ -533,6 +614,12 @@ def main():
                                       "sample + outputs), the memory half streams every slot")
     result["config"]["records"] = "page-locked host memory, written by the launch" if zero_copy else \
         "HBM + D2H copy" if not dist_on else "HBM + RCCL gather to rank 0"
+    if per_rank is not None:
+        result["per_rank_kernel_ms"] = [r[0] for r in per_rank]
+        result["kernel_ms_max"] = max(r[0] for r in per_rank)
+        if gather_mode == "stream":
+            result["per_rank_gather_ms"] = [r[1] for r in per_rank]
+            result["gather_ms_max"] = max(r[1] for r in per_rank)
     if dist_on:
         result["config"]["gather"] = {"stream": "RCCL send/recv on the launch stream (C ABI krr_gather_results)",
                                       "torch": "torch.distributed.gather, overlapping the next launch",
@@ -621,6 +708,9 @@ def main():
             "value": 492.0, "unit": "container-series/s", "cores": 1,
             "source": "BASELINE.md (SimpleStrategy.run + _format_result, config 1)"}
 
+    if rank == 0 and world == 1 and not args.no_host_path:
+        phase("host path")
+        result.update(host_path(args, dev, c_host_sample=parts[0][2]))
     if world > 1:
         result["config"]["backend"] = backend
         if backend != "nccl":
@@ -633,6 +723,91 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()
+
+
+def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, distinct: int = 48) -> dict:
+    """The host side of the path, measured after the timed region (never part of `value`):
+
+    * h2d_GBps: page-locked chunks of this run's own CPU series copied to HBM (the PCIe leg a
+      caller holding host buffers pays; krr_simple_run_host / SimpleEngine.run_packed);
+    * pack_samples_per_s: the native query_range JSON -> CSR packer (include/krr_pack.h) on
+      config-1-shaped bodies (objects x pods x 10,080 samples, both resources), the lease's
+      threads — the reference's loader does this with json + Decimal(value)
+      (robusta_krr/core/integrations/prometheus.py:150-155);
+    * e2e_objects_per_s: BatchedRunner.recommend_from_bodies on the same bodies: pack ->
+      H2D -> fused kernel -> exact-decimal rounding -> RunResults.
+    Bodies are Prometheus-formatted (shortest-repr sample strings); `distinct` random pod
+    series per resource are reused across the fleet (the packer's cost is per byte)."""
+    import torch
+
+    from krr_amd.core.prom_native import pack_query_range_bodies
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    out = {}
+    # --- H2D of the run's own data, 1 GiB in 256 MiB pinned chunks
+    n = min(c_host_sample.numel(), 1 << 27)
+    host = torch.empty(n, dtype=torch.float64, pin_memory=True)
+    host.copy_(c_host_sample[:n])
+    dst = torch.empty(n, dtype=torch.float64, device=dev)
+    chunk = 1 << 25
+    torch.cuda.synchronize()
+    reps = 4
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for a in range(0, n, chunk):
+            dst[a:a + chunk].copy_(host[a:a + chunk], non_blocking=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    out["h2d_GBps"] = reps * n * 8 / (t1 - t0) / 1e9
+    del host, dst
+    # --- config-1-shaped query_range bodies
+    rng = np.random.default_rng(0)
+    L = SLOTS_7D
+    ts = [repr(1.7e9 + 60.0 * i) for i in range(L)]
+
+    def body(xs):
+        vals = ",".join(f'[{t},"{x!r}"]' for t, x in zip(ts, xs.tolist()))
+        return ('{"status":"success","data":{"resultType":"matrix","result":[{"metric":{"pod":"p"},"values":['
+                + vals + ']}]}}').encode()
+
+    t_g = time.perf_counter()
+    cpu_pool = [body(rng.gamma(2.0, 0.05, L)) for _ in range(distinct)]
+    mem_pool = [body(np.floor(rng.normal(2e8, 2e7, L))) for _ in range(distinct)]
+    t_g = time.perf_counter() - t_g
+    cpu_b = [[cpu_pool[(o * pods + i) % distinct] for i in range(pods)] for o in range(objects)]
+    mem_b = [[mem_pool[(o * pods + i * 7) % distinct] for i in range(pods)] for o in range(objects)]
+    json_bytes = sum(len(b) for bs in cpu_b for b in bs) + sum(len(b) for bs in mem_b for b in bs)
+    threads = args.cpu_threads or cpu_lease()["threads"]
+    samples = 2 * objects * pods * L
+    pack_query_range_bodies(cpu_b[:4], threads=threads)  # warm-up (library load)
+    best = float("inf")
+    for _ in range(2):
+        t0 = time.perf_counter()
+        pack_query_range_bodies(cpu_b, threads=threads)
+        pack_query_range_bodies(mem_b, threads=threads)
+        best = min(best, time.perf_counter() - t0)
+    out["pack_samples_per_s"] = samples / best
+    runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(cpu_percentile=99, memory_buffer_percentage=5)))
+    runner.recommend_from_bodies(cpu_b[:8], mem_b[:8], threads=threads)  # warm-up (context, modules)
+    best_e = float("inf")
+    for _ in range(2):
+        t0 = time.perf_counter()
+        res = runner.recommend_from_bodies(cpu_b, mem_b, threads=threads)
+        best_e = min(best_e, time.perf_counter() - t0)
+    assert len(res) == objects
+    out["e2e_objects_per_s"] = objects / best_e
+    out["host_path"] = {
+        "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",
+        "bodies": f"{objects} objects x {pods} pods x {L} samples x 2 resources = {samples} samples, "
+                  f"{json_bytes / 1e9:.2f} GB of query_range JSON ({distinct} distinct pod series per resource, "
+                  f"generated in {t_g:.1f} s)",
+        "pack_s": best, "e2e_s": best_e, "threads": threads,
+        "pack_GBps_json": json_bytes / best / 1e9,
+        "definition": "pack = krr_pack_parse/copy of every body (CPU + memory); e2e = "
+                      "BatchedRunner.recommend_from_bodies: pack -> H2D -> fused kernel -> native exact-decimal "
+                      "rounding -> RunResults (best of 2)"}
+    return out
 
 
 def pg_comm(dev):
@@ -722,11 +897,15 @@ def _cpu_model() -> str:
 def run_config5(args, world, rank, local, dev, coll_dev):
     """Config 5: time-sharded 30d@15s series (see krr_amd/core/sketch.py).
 
-    step = per-slice sketch build (one HBM pass) -> reduce-scatter of the sketches
-    (RCCL, N > 1) -> exact refinement: locate the needed ranks' bins in the merged
-    sketches, all-gather them, collect every rank's samples in those bins (second
-    HBM pass), all-to-all them to the owners, select exactly -> results gathered to
-    rank 0.  ``--sketch-only`` stops at the interpolated sketch answer.
+    N = 1 (default): every series whole on the GPU: ONE exact select pass per chunk of
+    series, consecutive chunks' launches alternating between two streams so one's drain
+    overlaps the next one's start.
+    Time-sharded (N > 1, or --c5-refine at N = 1), exact, --c5-method window (default):
+    ONE HBM pass per rank (window export) -> one all-to-all of the windows to each series'
+    owner (RCCL) -> merge (exact counts decide; misses regathered and selected whole) ->
+    results gathered to rank 0.  --c5-method sketch: sketch build -> reduce-scatter ->
+    locate -> collect (a second HBM pass) -> all-to-all -> refine.  --sketch-only stops at
+    the interpolated sketch answer (value error <= 2^-m; rank error measured, not bounded).
     """
     import torch
     import torch.distributed as dist
@@ -745,12 +924,12 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     cfg = sketch.SketchConfig(mantissa_bits=args.sketch_bits)
     params = percentile_params(Decimal(args.percentile), params_mode(args))
     exact = not args.sketch_only
-    # N = 1 holds every series whole: the exact answer is ONE single-window select pass;
-    # time sharding (sketch merge + refinement) is what N > 1 needs (or --c5-refine)
     direct = exact and world == 1 and not args.c5_refine
+    method = "direct" if direct else (args.c5_method if exact else "sketch-only")
     # the direct pass over 138 GB runs per chunk of series in buffers of their own (as
-    # configs 2-4, fleet_chunks); the sketch path keeps one buffer per rank
+    # configs 2-4, fleet_chunks); the time-sharded paths keep one buffer per rank
     chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.chunk_gib) if direct else [(0, S)]
+    phase("synth")
     parts = []
     for lo, hi in chunks:
         o = torch.arange(hi - lo + 1, dtype=torch.int64, device=dev) * Lr
@@ -758,13 +937,16 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         ctx.synth_fill_window(c, o, seed, 0, 0, False, t0, T, seg_base=lo)
         parts.append((lo, hi, c, ctx.series(c, o, Lr, False)))
     torch.cuda.synchronize()
-    cpu, ser = parts[0][2], parts[0][3]  # the whole rank when it is one chunk (the sketch path)
+    ser = parts[0][3]  # the whole rank when it is one chunk (the time-sharded paths)
 
     def first_rows(k):
         """[k, Lr] device view/copy of the first k series."""
         rows = [c.view(hi - lo, Lr)[: max(0, min(k, hi) - lo)] for lo, hi, c, _ in parts if lo < k]
         return rows[0] if len(rows) == 1 else torch.cat(rows)
     stream = torch.cuda.current_stream()
+    # direct, several chunks: consecutive launches alternate between two streams (each
+    # launch of ~5,900 whole series is ~3 wave lifetimes long: its drain is a large share)
+    side = torch.cuda.Stream(device=dev) if direct and len(parts) > 1 else None
     dres = None
     if direct:
         dres = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
@@ -775,15 +957,24 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     else:
         counts = None
     host_rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
-    state = {}
+    state = {"misses": 0, "steps": 0}
 
     def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        if direct:
-            for lo, hi, _, ser_c in parts:
+        if method == "direct":
+            if ev is not None:
+                ev[0].record(stream)
+            if side is not None:
+                fork = torch.cuda.Event()
+                fork.record(stream)
+                side.wait_event(fork)
+            for j, (lo, hi, _, ser_c) in enumerate(parts):
+                st = side if (side is not None and j % 2) else stream
                 ctx.segmented_percentile(ser_c, params, dres["value"][lo:hi], dres["count"][lo:hi],
-                                         dres["flags"][lo:hi], stream)
+                                         dres["flags"][lo:hi], st)
+            if side is not None:
+                join = torch.cuda.Event()
+                join.record(side)
+                stream.wait_event(join)
             if ev is not None:
                 ev[1].record(stream)
             rec = torch.stack([dres["value"].view(torch.int64),
@@ -791,30 +982,45 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                                torch.zeros_like(dres["count"]), torch.zeros_like(dres["count"])], dim=1)
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
             return
-        sk = sketch.build(ctx, ser, cfg, stream)
-        if ev is not None:
-            ev[1].record(stream)
-        merged = sketch.merge_time_sharded(sk)
-        if exact:
-            res = sketch.exact_time_sharded(ctx, ser, sk, merged, cfg, params, stream=stream,
-                                            events=None if ev is None else ev[2:4])
-            state["collected"] = res["collected"]
+        if method == "window":
+            res = sketch.window_exact_time_sharded(ctx, ser, params, ext_slots=T - Lr, stream=stream,
+                                                   events=None if ev is None else ev[0:2])
+            state["misses"] += res["misses"]
+            state["key_cap"] = res["key_cap"]
+            state["exchanged_bytes"] = res["exchanged_bytes"]
+            state["hdr"] = res["hdr"]
         else:
-            res = sketch.query(ctx, merged, cfg, params, stream)
+            if ev is not None:
+                ev[0].record(stream)
+            sk = sketch.build(ctx, ser, cfg, stream)
+            if ev is not None:
+                ev[1].record(stream)
+            merged = sketch.merge_time_sharded(sk)
+            if exact:
+                res = sketch.exact_time_sharded(ctx, ser, sk, merged, cfg, params, stream=stream,
+                                                events=None if ev is None else ev[3:5])
+                state["collected"] = res["collected"]
+            else:
+                res = sketch.query(ctx, merged, cfg, params, stream)
+        if ev is not None:
+            ev[2].record(stream)
         rec = torch.stack([res["value"].view(torch.int64), res["count"] | (res["flags"].to(torch.int64) << 48),
                            torch.zeros_like(res["count"]), torch.zeros_like(res["count"])], dim=1)
         if world > 1:
             rec = gather_records(rec.to(coll_dev), dst=0, counts=counts)
         if rank == 0:
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
-        state["merged"] = merged
+        state["steps"] += 1
 
+    phase("warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    state["misses"] = state["steps"] = 0
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    phase(f"timed {args.steps} steps")
     t_a = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
@@ -822,23 +1028,50 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     if world > 1:
         dist.barrier()
     t_b = time.perf_counter()
+    phase("report")
     dt = torch.tensor([(t_b - t_a) / args.steps], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     step_s = float(dt.item())
     kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     N = S * Lr
-    kbytes = 8 * N + 8 * (S + 1) + S * (4 * cfg.width + 8 + 8 + 4)
-    kname = "k_sketch_build"
-    if direct:
+    kernels_ms = {}
+    if method == "direct":
         kname = "k_select"
         kbytes = 8 * N + 8 * (S + 1) + 20 * S
-    kernels_ms = {kname: kms}
-    if exact and not direct:
+    elif method == "window":
+        kname = "k_window_export"
+        hdr = state["hdr"]
+        cw = hdr[:, 4] & 0xFFFFFFFF
+        fl = hdr[:, 4] >> 32
+        stored = (fl & (_native.KRR_WIN_FAIL | _native.KRR_WIN_POINT)) == 0
+        keys_out = int(torch.where(stored, cw, torch.zeros_like(cw)).sum().item())
+        # every slot once + offsets + a 40-B header and the exported keys per series
+        kbytes = 8 * N + 8 * (S + 1) + 40 * S + 8 * keys_out
+        kernels_ms["merge_exchange_ms"] = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    else:
+        kname = "k_sketch_build"
+        kbytes = 8 * N + 8 * (S + 1) + S * (4 * cfg.width + 8 + 8 + 4)
+    kernels_ms = {kname: kms, **kernels_ms}
+    if method == "sketch":
         # collect: every slot read once + locations in, collected samples out
-        cms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+        cms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
         kernels_ms["k_sketch_collect"] = cms
         cbytes = 8 * N + 8 * (S + 1) + 56 * S + 8 * S + 8 * int(state.get("collected", 0))
+    kind = {"direct": (f"config5: {S} CPU series x {T} samples (30d@15s) on one GPU: exact single-window select, "
+                       f"one pass (no time sharding at N=1; {len(parts)} launches alternating on 2 streams)"),
+            "window": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
+                       f"samples/series/rank): exact, one HBM pass (window export -> all-to-all -> merge)"),
+            "sketch": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
+                       f"samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave + exact "
+                       f"refinement (collect + select in the located bins; two HBM passes)"),
+            "sketch-only": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
+                            f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave, "
+                            f"approximate")}[method]
+    par = {"direct": "single GPU, whole series",
+           "window": f"time-shard{world} (all-to-all of per-slice windows to the series' owners, RCCL)",
+           "sketch": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
+           "sketch-only": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)"}[method]
     result = {
         "metric": METRIC,
         "value": S / step_s,
@@ -852,17 +1085,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device counter-hash: CPU ~ Gamma(2, 0.05) cores), generated per time slice",
-        "config": {
-            "workload": (f"config5: {S} CPU series x {T} samples (30d@15s) on one GPU: exact single-window "
-                         f"select, one pass (no time sharding at N=1)") if direct else
-                        (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
-                         f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave"
-                         + (" + exact refinement (collect + select in the located bins)" if exact else "")),
-            "percentile_mode": params_mode(args), "cpu_percentile": args.percentile,
-            "series": S, "slots_per_rank": N,
-            "parallelism": "single GPU, whole series" if direct else
-                           f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
-        },
+        "config": {"workload": kind, "percentile_mode": params_mode(args), "cpu_percentile": args.percentile,
+                   "series": S, "slots_per_rank": N, "parallelism": par, "method": method},
         "samples_per_s": S * T / step_s,
         "launches_per_step": len(parts),
         "kernels_ms": kernels_ms,
@@ -870,10 +1094,21 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kbytes / (kms * 1e-3) / HBM_PEAK,
                      "traffic": None, "algorithmic_bytes_per_launch": kbytes},
     }
-    if exact and not direct:
+    if method == "window":
+        result["window"] = {"key_cap": state["key_cap"], "keys_exported_per_series": keys_out / max(S, 1),
+                            "alltoall_bytes_sent_per_rank": state["exchanged_bytes"],
+                            "misses_per_step": state["misses"] / max(args.steps, 1),
+                            "hbm_passes_per_step": 1}
+    if method == "sketch":
         result["roofline_collect"] = {"kernel": "k_sketch_collect", "bound": "hbm",
                                       "achieved": cbytes / (cms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                                       "frac": cbytes / (cms * 1e-3) / HBM_PEAK, "algorithmic_bytes_per_launch": cbytes}
+    if world > 1:
+        mine = torch.tensor([kms], dtype=torch.float64, device=coll_dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        result["per_rank_kernel_ms"] = [float(t.item()) for t in allr]
+        result["kernel_ms_max"] = max(result["per_rank_kernel_ms"])
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
@@ -883,7 +1118,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             result["roofline"]["traffic_source"] = tr[key].get("source")
     except (OSError, ValueError):
         pass
-    # rank error of the sketch answers against the exact path on a sample of series
+    # parity / rank error on a sample of series, regathered whole on rank 0
+    phase("parity")
     m = max(1, min(args.error_sample, S))
     piece = first_rows(m).contiguous()
     if world > 1:
@@ -897,10 +1133,12 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                               for r, b in enumerate(bufs)], dim=1).contiguous()
     else:
         full = piece
-    sk_vals = None
     if rank == 0:
+        from oracle import oracle
+
         rec = host_rec[:m].numpy()
-        sk_vals = rec[:, 0].copy().view(np.float64)
+        got = rec[:, 0].copy().view(np.float64)
+        got_n = rec[:, 1] & ((1 << 48) - 1)  # config-5 records: value bits, count | flags << 48, 0, 0
         fo = torch.arange(m + 1, dtype=torch.int64, device=dev) * T
         fser = ctx.series(full.view(-1), fo, T, False)
         ev_ = torch.empty(m, dtype=torch.float64, device=dev)
@@ -910,44 +1148,72 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         ctx.segmented_percentile(fser, exact_params, ev_, en_, ef_)
         lt = torch.empty(m, dtype=torch.int64, device=dev)
         le = torch.empty(m, dtype=torch.int64, device=dev)
-        ctx.rank_of(fser, torch.from_numpy(sk_vals).to(dev), lt, le)
+        ctx.rank_of(fser, torch.from_numpy(got).to(dev), lt, le)
         torch.cuda.synchronize()
         n = en_.cpu().numpy().astype(np.float64)
         target = (n - 1) * float(args.percentile) / 100.0
         ltn, len_ = lt.cpu().numpy(), le.cpu().numpy()
         err = np.maximum(0.0, np.maximum(ltn - target, target - (len_ - 1))) / n
         exact_v = ev_.cpu().numpy()
-        if exact:
-            same = (sk_vals.view(np.uint64) == exact_v.view(np.uint64)) | (np.isnan(sk_vals) & np.isnan(exact_v))
+        threads = args.cpu_threads or cpu_lease()["threads"]
+
+        def same_bits(a, b):
+            ok = (a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))
             if params_mode(args) == "linear":  # zero sign of a LINEAR result is unspecified
-                same |= (sk_vals == exact_v)
-            result["parity_vs_single_window_select"] = bool(same.all())
+                ok |= (a == b)
+            return ok
+
+        if exact:
+            bad = ~same_bits(got, exact_v) | (got_n != en_.cpu().numpy())
+            result["parity_vs_single_window_select"] = bool(not bad.any())
+            if bad.any():
+                i = int(np.nonzero(bad)[0][0])
+                result["parity_mismatch"] = {"series": int(bad.sum()), "first": i, "got": float(got[i]),
+                                             "want": float(exact_v[i]), "got_n": int(got_n[i]),
+                                             "want_n": int(en_[i].item()), "got_flags": int(rec[i, 1] >> 48)}
             result["parity_sample_series"] = m
-            result["parity_definition"] = ("exact refinement result (bits) == k_select/hselect over the gathered "
-                                           "full 172,800-sample series, first sample series")
-            result["collected_samples_per_rank"] = int(state.get("collected", 0))
+            if world > 1:  # the oracle on the regathered series, beside k_select
+                full_h = full.cpu().numpy().ravel()
+                ov, on, _ = oracle.percentile(full_h, (np.arange(m + 1) * T).astype(np.int64), exact_params.mode,
+                                              exact_params.p_num, exact_params.p_den, exact_params.q, False, threads)
+                result["parity_vs_oracle_on_sample"] = bool(same_bits(got, ov).all() and np.array_equal(got_n, on))
+                result["parity_oracle_sample_series"] = m
+            result["parity_definition"] = ("answers gathered on rank 0 (bits, counts) == k_select over the full "
+                                           "172,800-sample series regathered from every rank"
+                                           + (" and == oracle/krr_oracle.c on the same series" if world > 1 else "")
+                                           + ", first sample series")
+            if method == "sketch":
+                result["collected_samples_per_rank"] = int(state.get("collected", 0))
         else:
-            rel = np.abs(sk_vals - exact_v) / np.abs(exact_v)
+            rel = np.abs(got - exact_v) / np.abs(exact_v)
             result["sketch_error"] = {
                 "sample_series": m, "rank_error_max": float(err.max()), "rank_error_mean": float(err.mean()),
                 "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
+                "value_rel_bound": 2.0 ** -cfg.mantissa_bits,
+                "guarantee": (f"value: |v - exact| / exact <= 2^-{cfg.mantissa_bits} when the needed ranks fall in "
+                              f"binned octaves (else KRR_FLAG_SKETCH_RANGE); rank: no data-independent bound (a "
+                              f"low-dispersion series can put most samples in one bin) - exact refinement is the "
+                              f"default at every N"),
                 "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
                               "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
         if not args.no_cpu_baseline and world == 1:
-            from oracle import oracle
-
             cs = max(1, min(args.cpu_sample * 5 if args.cpu_sample else 4096, S))  # ~10 s on 16 cores
             host = first_rows(cs).cpu().numpy().ravel()
             ho = (np.arange(cs + 1) * Lr).astype(np.int64)
-            threads = args.cpu_threads or cpu_lease()["threads"]
             ta = time.perf_counter()
-            oracle.percentile(host, ho, exact_params.mode, exact_params.p_num, exact_params.p_den, exact_params.q,
-                              False, threads)
+            ov, on, _ = oracle.percentile(host, ho, exact_params.mode, exact_params.p_num, exact_params.p_den,
+                                          exact_params.q, False, threads)
             tb = time.perf_counter()
             result["cpu_baseline"] = {
                 "value": cs / (tb - ta), "unit": "cpu-series/s (exact)", "cores": threads, "kind": "port",
                 "sample": f"first {cs} series ({cs * Lr} samples) copied D2H; oracle/krr_oracle.c exact "
                           f"{args.mode}, OpenMP {threads} threads on {_cpu_model()}"}
+            if exact:  # this run's answers on the same series against the oracle
+                recs = host_rec[:cs].numpy()
+                gv = recs[:, 0].copy().view(np.float64)
+                result["parity_vs_oracle_on_sample"] = bool(same_bits(gv, ov).all()
+                                                            and np.array_equal(recs[:, 1] & ((1 << 48) - 1), on))
+                result["parity_oracle_sample_series"] = cs
         print(json.dumps(result), file=_JSON_OUT, flush=True)
     if world > 1:
         dist.barrier()

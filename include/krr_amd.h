@@ -276,6 +276,51 @@ int krr_sketch_collect(krr_ctx* ctx, const krr_series* series, const krr_sketch_
 int krr_sketch_refine(krr_ctx* ctx, const krr_series* collected, const krr_sketch_loc* loc, double* out_value,
                       int64_t* out_count, uint32_t* out_flags, void* stream);
 
+/* ---- Exact time-sharded percentiles in ONE HBM pass (config 5, window export) ----
+ * A series too long for one GPU is time-sharded: rank r holds its r-th time slice.
+ *   1. every rank: krr_window_export streams each local slice ONCE and keeps, in LDS,
+ *      the exact contents of a key window that narrows around where the GLOBAL
+ *      percentile's ranks are expected to fall (the slice's samples are read as a
+ *      sample of the whole series: ext_slots = the other ranks' slots per series widen
+ *      the window by the uncertainty they add).  Per series it writes a krr_window_hdr
+ *      and the window's keys (order-preserving uint64 keys, -0 < +0) into a row of
+ *      key_cap keys;
+ *   2. the owner of a series receives every rank's header and row (RCCL all-to-all);
+ *   3. krr_window_merge intersects the ranks' windows [max lo, min hi]; the headers'
+ *      exact counts say whether the needed ranks lie inside it — then they are selected
+ *      there, bit-identical to krr_segmented_percentile on the whole series — or not
+ *      (a slice whose distribution differs from the series', e.g. a trend): then the
+ *      series is flagged KRR_FLAG_WINDOW_MISS and counted in *miss_count, and the caller
+ *      finishes it exactly (krr_amd.core.sketch: its slices regathered to the owner).
+ * Nothing statistical is trusted: a hit is decided by exact counts. */
+#define KRR_FLAG_WINDOW_MISS 16u  /* krr_window_merge: the needed ranks are not inside the
+                                     ranks' common window (value NaN): finish it elsewhere */
+#define KRR_WIN_FAIL 0x100u       /* krr_window_hdr.flags: no usable window (keys crowded the LDS) */
+#define KRR_WIN_POINT 0x200u      /* the window is one key (lo == hi): cnt copies of it, no keys stored */
+
+typedef struct {
+    uint64_t lo, hi;   /* inclusive key window */
+    int64_t below;     /* present samples of the slice with key < lo */
+    int64_t n;         /* present samples of the slice (compact layout: every slot) */
+    uint32_t cnt;      /* samples with key in [lo, hi]: the first cnt keys of the row */
+    uint32_t flags;    /* KRR_WIN_FAIL, KRR_WIN_POINT, KRR_FLAG_NAN (compact layout) */
+} krr_window_hdr;      /* 40 bytes */
+
+/* Keys per row for slices of up to max_slice_len slots with ext_slots slots elsewhere
+ * (host only; 0 for REF_INDEX or invalid arguments). */
+int64_t krr_window_key_cap(int64_t max_slice_len, int64_t ext_slots, const krr_percentile_params* params);
+/* hdr[S], keys[S * key_cap] (device).  SORTED_LOWER / LINEAR only. */
+int krr_window_export(krr_ctx* ctx, const krr_series* slices, const krr_percentile_params* params,
+                      int64_t ext_slots, int64_t key_cap, krr_window_hdr* hdr, uint64_t* keys, void* stream);
+/* n_series series, each with n_slices slices in time order: slice j of series i has
+ * header hdr[j * slice_stride + i] and keys keys[(j * slice_stride + i) * key_cap ...].
+ * Writes out_value / out_count / out_flags[n_series]; *miss_count (device uint32, may
+ * be NULL) is zeroed on the stream, then counts the KRR_FLAG_WINDOW_MISS series. */
+int krr_window_merge(krr_ctx* ctx, int64_t n_series, int32_t n_slices, int64_t slice_stride,
+                     const krr_window_hdr* hdr, const uint64_t* keys, int64_t key_cap,
+                     const krr_percentile_params* params, double* out_value, int64_t* out_count,
+                     uint32_t* out_flags, uint32_t* miss_count, void* stream);
+
 /* Per segment: out_lt[s] = #present samples < values[s], out_le[s] = #<= values[s]. */
 int krr_rank_of(krr_ctx* ctx, const krr_series* series, const double* values, int64_t* out_lt,
                 int64_t* out_le, void* stream);

@@ -32,6 +32,10 @@ KRR_FLAG_NAN = 1
 KRR_FLAG_CAPACITY = 2
 KRR_FLAG_EMPTY = 4
 KRR_FLAG_SKETCH_RANGE = 8
+KRR_FLAG_WINDOW_MISS = 16
+
+KRR_WIN_FAIL = 0x100
+KRR_WIN_POINT = 0x200
 
 # Every symbol include/krr_amd.h declares (tests/test_abi.py checks the export table).
 EXPORTED_SYMBOLS = (
@@ -58,6 +62,9 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_refine",
     "krr_rank_of",
     "krr_select_present",
+    "krr_window_key_cap",
+    "krr_window_export",
+    "krr_window_merge",
     "krr_select_plan",
     "krr_get_stats",
     "krr_comm_unique_id",
@@ -125,6 +132,22 @@ class KrrSketchLoc(ctypes.Structure):
 
 
 LOC_WORDS = ctypes.sizeof(KrrSketchLoc) // 8
+
+
+class KrrWindowHdr(ctypes.Structure):
+    """include/krr_amd.h krr_window_hdr (40 bytes): device arrays of it are int64 tensors
+    [S, HDR_WORDS] (lo, hi as key bits; cnt | flags << 32 in the last word)."""
+    _fields_ = [
+        ("lo", ctypes.c_uint64),
+        ("hi", ctypes.c_uint64),
+        ("below", ctypes.c_int64),
+        ("n", ctypes.c_int64),
+        ("cnt", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+HDR_WORDS = ctypes.sizeof(KrrWindowHdr) // 8
 
 
 class KrrSelectPlanInfo(ctypes.Structure):
@@ -222,6 +245,12 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_sketch_refine.restype = ctypes.c_int
         lib.krr_select_present.argtypes = [vp, sp, vp, vp, vp]
         lib.krr_select_present.restype = ctypes.c_int
+        lib.krr_window_key_cap.argtypes = [i64, i64, pp]
+        lib.krr_window_key_cap.restype = i64
+        lib.krr_window_export.argtypes = [vp, sp, pp, i64, i64, vp, vp, vp]
+        lib.krr_window_export.restype = ctypes.c_int
+        lib.krr_window_merge.argtypes = [vp, i64, i32, i64, vp, vp, i64, pp, vp, vp, vp, vp, vp]
+        lib.krr_window_merge.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
@@ -464,6 +493,32 @@ class Context:
         self._check(self._lib.krr_select_present(self._h, ctypes.byref(series), k.data_ptr(), out.data_ptr(),
                                                  self._stream(stream)))
 
+    # --- time-sharded exact percentiles in one pass (window export / merge) ---------
+    def window_export(self, series: KrrSeries, params: KrrPercentileParams, ext_slots: int, key_cap: int, hdr,
+                      keys, stream=None) -> None:
+        """hdr: int64 [>= S, HDR_WORDS]; keys: int64 [>= S, key_cap] (uint64 key bit patterns)."""
+        S = series.n_segments
+        _check_tensor(hdr, "int64", S * HDR_WORDS)
+        _check_tensor(keys, "int64", S * int(key_cap))
+        self._check(self._lib.krr_window_export(self._h, ctypes.byref(series), ctypes.byref(params), int(ext_slots),
+                                                int(key_cap), hdr.data_ptr(), keys.data_ptr(), self._stream(stream)))
+
+    def window_merge(self, n_series: int, n_slices: int, slice_stride: int, hdr, keys, key_cap: int,
+                     params: KrrPercentileParams, out_value, out_count, out_flags, miss_count=None,
+                     stream=None) -> None:
+        """Slice j of series i: hdr[j * slice_stride + i], keys row j * slice_stride + i.
+        miss_count: optional int32 [1] device tensor (zeroed, then counts the misses)."""
+        _check_tensor(hdr, "int64", ((n_slices - 1) * slice_stride + n_series) * HDR_WORDS if n_series else 0)
+        _check_tensor(keys, "int64", ((n_slices - 1) * slice_stride + n_series) * int(key_cap) if n_series else 0)
+        for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, n_series)
+        if miss_count is not None:
+            _check_tensor(miss_count, "int32", 1)
+        self._check(self._lib.krr_window_merge(
+            self._h, int(n_series), int(n_slices), int(slice_stride), hdr.data_ptr(), keys.data_ptr(), int(key_cap),
+            ctypes.byref(params), out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(),
+            miss_count.data_ptr() if miss_count is not None else None, self._stream(stream)))
+
     def synth_fill_window(self, values, offsets, seed: int, kind: int, pod_len: int, gaps: bool, t0: int,
                           total_len: int, stream=None, seg_base: int = 0) -> None:
         """Time window [t0, t0 + len) of series of total_len slots; segment s is global
@@ -484,6 +539,15 @@ def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectP
     if rc != KRR_OK:
         raise NativeError(rc, "krr_select_plan")
     return info
+
+
+def window_key_cap(max_slice_len: int, ext_slots: int, params: KrrPercentileParams) -> int:
+    """Keys per exported row (krr_window_key_cap; host only)."""
+    lib = load_library()
+    k = int(lib.krr_window_key_cap(int(max_slice_len), int(ext_slots), ctypes.byref(params)))
+    if k <= 0:
+        raise NativeError(KRR_E_INVALID, "krr_window_key_cap: REF_INDEX or invalid arguments")
+    return k
 
 
 def _check_tensor(t, dtype: str, numel: Optional[int] = None, host_pinned_ok: bool = False) -> None:

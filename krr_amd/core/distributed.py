@@ -185,13 +185,18 @@ def raw_from_records(rec):
     return RawResults(u["cpu_value"], u["cpu_count"], u["cpu_flags"], u["mem_value"], u["mem_count"], u["mem_flags"])
 
 
-def collective_device(group=None):
-    """Where a collective's tensors live: the rank's GPU for "nccl" (RCCL), host for gloo."""
+def collective_device(group=None, device: Optional[int] = None):
+    """Where a collective's tensors live: the rank's GPU for "nccl" (RCCL), host for gloo.
+
+    The rank's GPU is ``device`` (default: ``local_device()``), never the calling thread's
+    current device: HIP's current device is per host thread, and a worker thread (e.g.
+    ``asyncio.to_thread``) starts on device 0, which would put every rank's records on
+    GPU 0 and give RCCL duplicate devices."""
     import torch
     import torch.distributed as dist
 
     if dist.get_backend(group) == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cuda", local_device() if device is None else int(device))
     return torch.device("cpu")
 
 

@@ -99,6 +99,11 @@ class GroupQuery:
         return group_query(resource, self.namespace, self.container, self.pods)
 
 
+# history_duration 336 h / timeframe_duration 15 min + 1 (SimpleStrategySettings defaults,
+# robusta_krr/core/abstract/strategies.py:20-23; range query prometheus.py:124-126)
+DEFAULT_POINTS_PER_SERIES = 336 * 60 // 15 + 1
+
+
 @dataclass
 class FleetQueryPlan:
     """Grouping of a fleet's (object, pod) pairs into grouped range queries.
@@ -112,7 +117,10 @@ class FleetQueryPlan:
     """
     objects: Sequence
     max_query_chars: int = 6000
-    points_per_series: int = 0           # evaluation timestamps per series (0: no sample bound)
+    # evaluation timestamps per series.  Default: the reference's default settings (336 h
+    # at 15 min: 1,345 points), so a plan built without settings still respects Prometheus'
+    # sample limit; ``for_settings`` takes them from the strategy; 0 turns the bound off.
+    points_per_series: int = DEFAULT_POINTS_PER_SERIES
     max_query_samples: int = 50_000_000  # Prometheus' default --query.max-samples [external]
     series_per_pod: int = 4              # raw series the selector may match per pod (restarts, ids)
     groups: list[GroupQuery] = field(init=False)

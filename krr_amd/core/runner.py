@@ -87,9 +87,17 @@ class BatchedRunner:
         order, on ``dst``; None on the other ranks.  Collective: every rank calls it."""
         from krr_amd.core.distributed import collective_device, gather_records, local_device, raw_from_records
 
+        import torch
+
         self._require_packed()
-        rec = self.strategy.settings.run_fleet_records(local_fleet, local_device() if device is None else device)
-        full = gather_records(rec.to(collective_device(group)), dst=dst, group=group)
+        dev = local_device() if device is None else int(device)
+        rec = self.strategy.settings.run_fleet_records(local_fleet, dev)
+        coll = collective_device(group, dev)
+        if coll.type == "cuda":
+            # this may run on a worker thread (gather_objects_recommendations_sharded):
+            # its current device is 0 until set, and RCCL enqueues on the current device
+            torch.cuda.set_device(coll)
+        full = gather_records(rec.to(coll), dst=dst, group=group)
         if full is None:
             return None
         return self.strategy.format_raw(raw_from_records(full), self.cpu_min_value, self.memory_min_value)

@@ -13,7 +13,17 @@ r-th contiguous time slice of every series.
   contiguous block of series, which it queries (``krr_sketch_query``).  The value
   is interpolated inside the bin holding the rank (relative bin width 2^-m); the
   rank error is measured against the exact path, never assumed (bench.py).
-* Exact percentiles (``exact_time_sharded``): the merged counts are exact, so they
+* Exact percentiles, ONE HBM pass (``window_exact_time_sharded``, the default): every
+  rank streams its slice of each series once through the window select, with the
+  other slices' slots counted as unseen, and exports the window it kept (bounds,
+  exact count below, keys; ``krr_window_export``).  One all-to-all (RCCL) hands each
+  series' windows to its owner, which intersects them; the exact counts decide
+  whether the needed ranks lie inside, and then they are selected there
+  (``krr_window_merge``) — bit-identical to one select over the whole series.  A
+  miss (a slice whose distribution differs from the series', e.g. a trend) regathers
+  only that series' slices to its owner and selects it whole.
+* Exact percentiles, two passes (``exact_time_sharded``, kept as the reference
+  design and for comparison): the merged counts are exact, so they
   say exactly which bin holds each needed rank and how many samples lie below it
   (``krr_sketch_locate``).  One all-gather gives every rank those bins, each rank
   collects its samples inside them (``krr_sketch_collect``, a second HBM pass), an
@@ -379,3 +389,176 @@ def max_time_sharded(local_value, local_count, local_flags, group=None) -> dict:
     flags[count == 0] |= _native.KRR_FLAG_EMPTY
     best[(flags & _native.KRR_FLAG_NAN) != 0] = np.nan
     return {"value": best, "count": count, "flags": flags}
+
+
+# -------------------- one-pass exact time-sharded percentiles (window export) ---------------------
+
+def _max_len(series) -> int:
+    if series.max_segment_len > 0:
+        return int(series.max_segment_len)
+    offs = series._keep[1]
+    return int((offs[1:] - offs[:-1]).max().item()) if series.n_segments else 0
+
+
+def gather_segments(values, offs, ids):
+    """Segments ``ids`` (int64 tensor, any order) of a CSR -> (values, offsets) of a
+    new CSR holding them in that order (device-side index gather)."""
+    import torch
+
+    dev = values.device
+    k = int(ids.numel())
+    starts = offs[ids]
+    lens = offs[ids + 1] - starts
+    new_offs = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+    if k:
+        new_offs[1:] = torch.cumsum(lens, 0)
+    total = int(new_offs[-1].item()) if k else 0
+    if total == 0:
+        return torch.empty(1, dtype=values.dtype, device=dev), new_offs
+    seg = torch.repeat_interleave(torch.arange(k, device=dev), lens)
+    pos = torch.arange(total, device=dev) - new_offs[seg] + starts[seg]
+    return values[pos], new_offs
+
+
+def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, params: _native.KrrPercentileParams,
+                              ext_slots: Optional[int] = None, group=None, stream=None, events=None,
+                              key_cap: Optional[int] = None) -> dict:
+    """Exact SORTED_LOWER / LINEAR percentile of every time-sharded series in ONE pass over
+    this rank's slices (module docstring).  ``series``: this rank's slice of every series
+    (the same series on every rank, rank order = time order).  ``ext_slots``: slots of a
+    series held by the other ranks (default (world - 1) x the longest local slice); it
+    only sizes the windows, results are exact whatever it is.  Returns device tensors
+    value/count/flags for this rank's owner block (``owner_blocks``), plus 'block',
+    'misses' (series of the block finished by regathering their slices), 'key_cap' and
+    'exchanged_bytes' (what this rank sent in the all-to-all) and 'hdr' (this rank's
+    exported krr_window_hdr rows, int64 [S, HDR_WORDS]).  ``events``: optional pair
+    of HIP events recorded around the export pass (its HBM time)."""
+    import torch
+    import torch.distributed as dist
+
+    S = series.n_segments
+    dev = series._keep[0].device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    Lmax = _max_len(series)
+    if ext_slots is None:
+        ext_slots = (world - 1) * Lmax
+    kc = int(key_cap or _native.window_key_cap(max(Lmax, 1), ext_slots, params))
+    per = -(-S // world) if S else 0
+    rows = per * world
+    hdr = torch.empty((max(rows, 1), _native.HDR_WORDS), dtype=torch.int64, device=dev)
+    keys = torch.empty((max(rows, 1), kc), dtype=torch.int64, device=dev)
+    if events is not None:
+        events[0].record(stream)
+    if S:
+        ctx.window_export(series, params, ext_slots, kc, hdr, keys, stream)
+    if events is not None:
+        events[1].record(stream)
+    lo, hi = owner_blocks(S, world)[rank] if world > 1 else (0, S)
+    nb = hi - lo
+    if world > 1:
+        coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        hdr_r = torch.empty((rows, _native.HDR_WORDS), dtype=torch.int64, device=coll)
+        keys_r = torch.empty((rows, kc), dtype=torch.int64, device=coll)
+        if rows:
+            dist.all_to_all_single(hdr_r, hdr[:rows].to(coll), group=group)
+            dist.all_to_all_single(keys_r, keys[:rows].to(coll), group=group)
+        hdr_r, keys_r = hdr_r.to(dev), keys_r.to(dev)
+        stride = per
+        sent = (rows - per) * (_native.HDR_WORDS + kc) * 8
+    else:
+        hdr_r, keys_r, stride, sent = hdr, keys, max(S, 1), 0
+    out = {"value": torch.empty(max(nb, 1), dtype=torch.float64, device=dev)[:nb],
+           "count": torch.empty(max(nb, 1), dtype=torch.int64, device=dev)[:nb],
+           "flags": torch.empty(max(nb, 1), dtype=torch.int32, device=dev)[:nb]}
+    miss = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctx.window_merge(nb, world, stride, hdr_r, keys_r, kc, params, out["value"], out["count"], out["flags"], miss,
+                     stream)
+    nmiss = int(miss.item())
+    total = nmiss
+    if world > 1:
+        coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([nmiss], dtype=torch.int64, device=coll)
+        dist.all_reduce(t, group=group)
+        total = int(t.item())
+    if total:
+        finish_window_misses(ctx, series, params, out, (lo, hi), group, stream)
+    out.update(block=(lo, hi), misses=nmiss, key_cap=kc, exchanged_bytes=sent, hdr=hdr[:S])
+    return out
+
+
+def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params: _native.KrrPercentileParams,
+                         out: dict, block, group=None, stream=None) -> None:
+    """The series ``krr_window_merge`` flagged KRR_FLAG_WINDOW_MISS in ``out`` (this rank's
+    owner block): their slices are regathered to the owner (RCCL all-to-all) and selected
+    whole with ``krr_segmented_percentile``; ``out`` is updated in place.  Collective: every
+    rank calls it (with or without misses of its own)."""
+    import torch
+    import torch.distributed as dist
+
+    vals, offs = series._keep
+    dev = vals.device
+    S = series.n_segments
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    lo, _ = block
+    mine = torch.nonzero((out["flags"] & _native.KRR_FLAG_WINDOW_MISS) != 0).flatten()
+    if world == 1:
+        ids = mine
+        if ids.numel() == 0:
+            return
+        sv, so = gather_segments(vals, offs, ids)
+        sub = ctx.series(sv, so, 0, series.gaps_are_nan)
+        v = torch.empty(ids.numel(), dtype=torch.float64, device=dev)
+        n = torch.empty(ids.numel(), dtype=torch.int64, device=dev)
+        f = torch.empty(ids.numel(), dtype=torch.int32, device=dev)
+        ctx.segmented_percentile(sub, params, v, n, f, stream)
+        out["value"][ids], out["count"][ids], out["flags"][ids] = v, n, f
+        return
+    # every rank learns every owner's missed series (global ids, ascending)
+    lists = [None] * world
+    dist.all_gather_object(lists, (mine + lo).tolist(), group=group)
+    blocks = owner_blocks(S, world)
+    per_owner = [torch.tensor(sorted(x), dtype=torch.int64, device=dev) for x in lists]
+    ids_all = torch.cat(per_owner) if any(len(x) for x in lists) else torch.empty(0, dtype=torch.int64, device=dev)
+    if ids_all.numel() == 0:
+        return
+    # this rank's slices of them, grouped by owner (= ascending id)
+    sv, so = gather_segments(vals, offs, ids_all)
+    lens = (so[1:] - so[:-1])
+    coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    counts = [len(x) for x in lists]
+    send_sizes = [int(lens[sum(counts[:r]):sum(counts[:r + 1])].sum().item()) for r in range(world)]
+    # every rank's slice lengths of every missed series: [world, n_missed]
+    all_lens = [torch.empty_like(lens, device=coll) for _ in range(world)]
+    dist.all_gather(all_lens, lens.to(coll), group=group)
+    rank = dist.get_rank(group)
+    a, b = sum(counts[:rank]), sum(counts[:rank + 1])
+    recv_lens = torch.stack([x[a:b] for x in all_lens]).to(dev)  # [src, my missed series]
+    recv_sizes = [int(x) for x in recv_lens.sum(dim=1).tolist()]
+    recv = torch.empty(max(sum(recv_sizes), 1), dtype=torch.float64, device=coll)
+    dist.all_to_all_single(recv[:sum(recv_sizes)], sv[:int(so[-1].item())].to(coll), output_split_sizes=recv_sizes,
+                           input_split_sizes=send_sizes, group=group)
+    k = b - a
+    if k == 0:
+        return
+    recv = recv.to(dev)
+    # src-major pieces -> series-major, src (= time) order inside each series
+    flat = recv_lens.reshape(-1)
+    src_start = torch.cumsum(flat, 0) - flat
+    tot = recv_lens.sum(dim=0)
+    new_offs = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+    new_offs[1:] = torch.cumsum(tot, 0)
+    dst_start = (new_offs[:-1][None, :] + (torch.cumsum(recv_lens, 0) - recv_lens)).reshape(-1)
+    n_all = int(new_offs[-1].item())
+    whole = torch.empty(max(n_all, 1), dtype=torch.float64, device=dev)
+    if n_all:
+        piece = torch.repeat_interleave(torch.arange(flat.numel(), device=dev), flat)
+        pos = torch.arange(n_all, device=dev)
+        whole[dst_start[piece] + (pos - src_start[piece])] = recv[:n_all]
+    sub = ctx.series(whole, new_offs, 0, series.gaps_are_nan)
+    v = torch.empty(k, dtype=torch.float64, device=dev)
+    n = torch.empty(k, dtype=torch.int64, device=dev)
+    f = torch.empty(k, dtype=torch.int32, device=dev)
+    ctx.segmented_percentile(sub, params, v, n, f, stream)
+    loc = per_owner[rank] - blocks[rank][0]
+    out["value"][loc], out["count"][loc], out["flags"][loc] = v, n, f

@@ -95,6 +95,11 @@
 namespace krr {
 
 constexpr int kLdsBatch = KRR_LDS_BATCH;
+#ifdef KRR_WEXP_DEBUG
+__device__ unsigned long long g_wdbg[5 * 1024];
+__device__ unsigned int g_wdbg_n = 0;
+__device__ unsigned int g_wdbg_on = 1;
+#endif
 
 // Diagnostic build (-DKRR_DIAG): per-segment cycle and event counters written
 // to a buffer attached with krr_diag_attach(); never compiled into the product.
@@ -1628,13 +1633,24 @@ static_assert(kWselCap >= kChunkElems + KRR_WSEL_CAP_MIN_SLACK && kWselCapLong >
 KRR_HD inline uint32_t wsel_cap_for(int64_t Lmax, bool gaps = false) {
     return Lmax >= KRR_WSEL_LONG && (KRR_WSEL_LONG_GAPS || !gaps) ? kWselCapLong : kWselCap;
 }
+// Dynamic LDS past kSelectLdsFixed of a window launch: the window keys; the long
+// kernels finish their misses inline, so hselect's LDS too.
+KRR_HD inline size_t window_lds(uint32_t wcap) {
+    const size_t w = (size_t)wcap * 8;
+    return wcap == kWselCapLong && w < kHselectLds ? kHselectLds : w;
+}
 
 enum { WIN_GENERAL = 0, WIN_FAST = 1, WIN_FULL = 2 };  // window classify modes (WindowProc::classify)
 
 // LANE_COUNTS: below / NaN counts per lane in VALU (the long-segment kernels: their
 // gapped layouts put NaNs in many chunks, and at 2 waves per SIMD the stream, not
 // the vector unit, bounds them); otherwise scalar ballot popcounts (see classify).
-template <bool LANE_COUNTS>
+// EXPORT: the time-sharded window export (k_window_export): the segment is one time
+// slice of a longer series, so the other slices' ext_u slots count as unseen too.
+#ifndef KRR_WEXP_Z
+#define KRR_WEXP_Z 6.0  // export windows: a miss costs a regather of the series, not a second pass
+#endif
+template <bool LANE_COUNTS, bool EXPORT = false>
 struct WindowProc {
     SelectProc sp;            // buffer algebra (locate / kth / pair) over buf
     uint64_t* buf;
@@ -1652,6 +1668,7 @@ struct WindowProc {
     int64_t L;
     int64_t p_num, p_den;     // percentile p = p_num / p_den
     uint32_t fail;
+    double ext_u;             // EXPORT: slots of the series held by the other slices
 #ifdef KRR_DIAG
     unsigned long long diag[D_WORDS];
 #endif
@@ -1792,6 +1809,18 @@ struct WindowProc {
         const uint32_t incl = wave_scan32(vc, 0u, OpAdd32{});
         const uint32_t C = lane_bcast32(incl, kWave - 1);
         if (!point && cnt + C > cap) {
+            // EXPORT: a window crowded by ONE repeated key (a constant stretch whose
+            // window still reaches up to +inf) becomes that key's point window, and the
+            // chunk is counted against it; anything else fails (the series is a miss)
+#ifdef KRR_WEXP_DEBUG
+            dbg(3, seen, cnt, C, lo);
+#endif
+            if constexpr (EXPORT) {
+                if (point_rescue()) {
+                    point_chunk(c);
+                    return;
+                }
+            }
             fail = 1;
             return;
         }
@@ -1841,13 +1870,25 @@ struct WindowProc {
         below_extra += uni32(dropped_below);
     }
 
+#ifdef KRR_WEXP_DEBUG
+    __device__ void dbg(uint64_t tag, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+        if (lane == 0 && g_wdbg_on) {
+            const unsigned i = atomicAdd(&g_wdbg_n, 1u);
+            if (i < 1024) {
+                g_wdbg[5 * i] = tag; g_wdbg[5 * i + 1] = a; g_wdbg[5 * i + 2] = b; g_wdbg[5 * i + 3] = c;
+                g_wdbg[5 * i + 4] = d;
+            }
+        }
+    }
+#endif
     // Narrow the window around the target's estimated seen-rank (header comment).
     __device__ __forceinline__ void shrink() {
         if (point || cnt == 0) return;
         const uint64_t nanc = nan_total();
         const uint64_t below = below_total();
         const uint64_t S = seen - nanc;  // present samples seen
-        const double U = L > (int64_t)seen ? (double)(L - (int64_t)seen) : 0.0;
+        double U = L > (int64_t)seen ? (double)(L - (int64_t)seen) : 0.0;
+        if constexpr (EXPORT) U += ext_u;
         // q from the kernel's scalars here, not a per-segment value the compiler would
         // hoist to kernel entry and keep in registers for the whole launch
         int64_t pn = p_num, pd = p_den;
@@ -1856,7 +1897,7 @@ struct WindowProc {
         const double Sd = (double)S;
         const double c = qq * (Sd - 1.0);
         const double sig = (S > 0 && U > 0.0) ? sqrt(qq * (1.0 - qq) * Sd * U / (Sd + U)) : 0.0;
-        const double w = KRR_WSEL_Z * sig + 4.0;
+        const double w = (EXPORT ? KRR_WEXP_Z : KRR_WSEL_Z) * sig + 4.0;
         const int64_t jlo = (int64_t)floor(c - w);
         const int64_t jhi = (int64_t)ceil(c + w) + 1;
         int64_t ilo = jlo - (int64_t)below;  // ascending buffer indices
@@ -1891,8 +1932,20 @@ struct WindowProc {
                 keep_lo_side = bh.above;
             }
             __syncthreads();
-            // crowded bins leave too much: exact bounds instead
-            if (keep_hi_side - keep_lo_side > cap - kChunkElems / 2) {
+            // crowded bins leave too much: exact bounds instead.  EXPORT windows are also
+            // held to a few times the ranks they need: a bin can span most of the data
+            // when the keys straddle the sign (negatives and positives in one histogram),
+            // and such a window would overflow on the next chunk and fail the series.
+            uint32_t keep_limit = cap - kChunkElems / 2;
+            if constexpr (EXPORT) {
+                const uint32_t need = 2u * (uint32_t)(ihi - ilo + 1) + 256u;
+                keep_limit = need < keep_limit ? need : keep_limit;
+            }
+            // ... and so is a window that keeps so large a share of the keys that the next
+            // two chunks would overflow it (coarse bins: zeros in the data put the
+            // histogram's range over many octaves, one bin over several of them)
+            const uint64_t keep = keep_hi_side - keep_lo_side;
+            if (keep > keep_limit || keep * (uint64_t)(cnt + 2 * kChunkElems) > (uint64_t)cap * cnt) {
                 nl = ilo > 0 ? sp.kth_largest((uint32_t)(cnt - ilo), mn, mx) : lo;
                 nh = ihi < last ? sp.kth_largest((uint32_t)(cnt - ihi), mn, mx) : hi;
             }
@@ -1903,6 +1956,10 @@ struct WindowProc {
         nh = ihi < last ? sp.kth_largest((uint32_t)(cnt - ihi), mn, mx) : hi;
 #endif
         __syncthreads();
+#ifdef KRR_WEXP_DEBUG
+        dbg(1, seen, below, cnt, ((uint64_t)ilo << 32) | (uint64_t)ihi);
+        dbg(2, lo, hi, nl, nh);
+#endif
         if (sp.bad || nl > nh) {
             fail = 1;
             return;
@@ -1913,6 +1970,74 @@ struct WindowProc {
         diag[D_COMPACT] += __builtin_amdgcn_s_memtime() - t0;
         diag[D_NCOMPACT] += 1;
 #endif
+    }
+
+    // EXPORT: the buffer holds one distinct key v (and none below lo): the window becomes
+    // [v, v] (counted, not stored); later keys above v fall outside it.  Exact counts
+    // decide at the merge whether the target really is v.
+    __device__ __forceinline__ bool point_rescue() {
+        if (cnt == 0) return false;
+        __syncthreads();
+        uint64_t mn, mx;
+        sp.cnt = cnt;
+        sp.buf_minmax(mn, mx);
+        if (mn != mx) return false;
+        set_window(mn, mn);
+        return true;
+    }
+
+    // EXPORT: commit a chunk against a point window [lo, lo] (after point_rescue).
+    __device__ __forceinline__ void point_chunk(const double2 (&c)[kUnroll]) {
+        uint32_t bl = 0, nnc = 0, eq = 0;
+#pragma unroll
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+            const uint64_t x = dbits(slot_val(c, j));
+            const bool nan = is_nan_bits(x);
+            const uint64_t key = okey(x);
+            nnc += popc64(ballot(nan));
+            bl += popc64(ballot(!nan && key < lo));
+            eq += popc64(ballot(!nan && key == lo));
+        }
+        below_extra += bl;
+        if constexpr (LANE_COUNTS) nan_l += lane == 0 ? nnc : 0u;
+        else nan_u += nnc;
+        cnt = uni32(cnt + eq);
+        seen += kChunkElems;
+    }
+
+    // EXPORT, after the stream: narrow the window to the ranks the GLOBAL percentile can
+    // need (unseen = the other slices only) with exact key bounds, so that the row the
+    // series' owner receives holds at most key_cap keys.
+    __device__ __forceinline__ void export_shrink(uint32_t key_cap) {
+        if (point || cnt <= key_cap) return;
+        const uint64_t nanc = nan_total();
+        const uint64_t below = below_total();
+        const uint64_t S = seen - nanc;
+        const double qq = (double)p_num / (100.0 * (double)p_den);
+        const double Sd = (double)S, U = ext_u;
+        const double c = qq * (Sd - 1.0);
+        const double sig = (S > 0 && U > 0.0) ? sqrt(qq * (1.0 - qq) * Sd * U / (Sd + U)) : 0.0;
+        const double w = KRR_WEXP_Z * sig + 4.0;
+        const int64_t last = (int64_t)cnt - 1;
+        int64_t ilo = (int64_t)floor(c - w) - (int64_t)below;
+        int64_t ihi = (int64_t)ceil(c + w) + 1 - (int64_t)below;
+        ilo = ilo < 0 ? 0 : (ilo > last ? last : ilo);
+        ihi = ihi < 0 ? 0 : (ihi > last ? last : ihi);
+        __syncthreads();
+        sp.cnt = cnt;
+        sp.bad = 0;
+        uint64_t mn = lo, mx = hi;
+        if (shrinks == 0) sp.buf_minmax(mn, mx);
+        ++shrinks;
+        const uint64_t nl = ilo > 0 ? sp.kth_largest((uint32_t)(cnt - ilo), mn, mx) : lo;
+        const uint64_t nh = ihi < last ? sp.kth_largest((uint32_t)(cnt - ihi), mn, mx) : hi;
+        __syncthreads();
+        if (sp.bad || nl > nh) {
+            fail = 1;
+            return;
+        }
+        filter_window(nl, nh);
+        set_window(nl, nh);
     }
 };
 
@@ -2031,10 +2156,10 @@ __device__ __forceinline__ void mid_select_segment(const SelectArgs& A, int64_t 
 
 // The segments wselect missed, by hselect (launched right after the window kernel
 // on the same stream).  With no misses every workgroup reads the count and exits.
-// The last workgroup to finish resets the list for the next launch.
-// Launches alternate between two counters: the window kernel of launch k + 1
-// zeroes launch k's (its fallback pass has finished by then, same stream), which
-// launch k + 2 counts into — no extra memset or completion counter per launch.
+// Nothing here resets the list: launches alternate between two counters, and the
+// window kernel of launch k + 1 zeroes launch k's (this pass has finished by then:
+// same stream, or the ctx's event when k + 1 comes on another stream), which launch
+// k + 2 counts into — no extra memset or completion counter per launch.
 __global__ __launch_bounds__(64, KRR_HSEL_WAVES_PER_SIMD) void k_hselect_list(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const unsigned int n = __builtin_nontemporal_load(A.fail_count);
@@ -2058,6 +2183,215 @@ void k_select(SelectArgs A) {
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         if constexpr (KIND != SEL_SINGLE) mid_select_segment<KIND == SEL_WINDOW_LONG>(A, xcd_item(s, A.S), smem, threadIdx.x);
         else select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Time-sharded exact percentiles in one HBM pass (config 5; include/krr_amd.h
+// "window export").  Each rank streams its time slice of every series once through
+// the window select, with the other slices' slots counted as unseen (EXPORT), and
+// exports the window: its bounds, the exact count of present samples below it and
+// its keys.  The owner of a series intersects the ranks' windows; exact counts
+// decide whether the needed ranks lie inside, and if so they are selected there.
+// ---------------------------------------------------------------------------
+struct WindowExportArgs {
+    SelectArgs A;         // vals, offs, S, mode, gaps, p, q, wcap (outputs unused)
+    double ext;           // slots of each series held by the other slices
+    uint32_t key_cap;     // keys per row
+    krr_window_hdr* hdr;  // [S]
+    uint64_t* keys;       // [S][key_cap]
+};
+
+template <bool LONG>
+__device__ __forceinline__ void window_export_segment(const WindowExportArgs& X, int64_t s, unsigned char* smem,
+                                                      int lane) {
+    const SelectArgs& A = X.A;
+    const int64_t beg = A.offs[s], end = A.offs[s + 1];
+    const int64_t L = end - beg;
+    WindowProc<LONG, true> W;
+    W.buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+    W.sp.buf = W.buf;
+    W.sp.H = reinterpret_cast<uint32_t*>(smem);
+    W.sp.small = reinterpret_cast<uint64_t*>(smem + 1024);
+    W.sp.lane = lane;
+    W.sp.flip = 0;
+    W.sp.cnt = 0;
+    W.sp.bad = 0;
+    W.lane = lane;
+    W.cap = A.wcap;
+    W.shrinks = 0;
+    W.cnt = 0;
+    W.below_u = W.nan_u = 0;
+    W.below_l = W.nan_l = W.negnan_l = 0;
+    W.below_extra = 0;
+    W.seen = 0;
+    W.L = L;
+    W.p_num = A.p_num;
+    W.p_den = A.p_den;
+    W.fail = 0;
+    W.ext_u = X.ext;
+    W.set_window(kKeyNegInf, kKeyPosInf);
+    int64_t b = (int64_t)uni64((uint64_t)beg), e = (int64_t)uni64((uint64_t)end);
+    asm volatile("" : "+s"(b), "+s"(e));
+    const uint32_t pad = stream_segment<true, WindowProc<LONG, true>, LONG ? KRR_WSEL_LONG_DEPTH : KRR_ONE_SITE_DEPTH>(
+        A.vals, b, e, W, lane);
+    __syncthreads();
+    // a failed window stopped counting part-way: its counts mean nothing (no NaN flag)
+    const uint64_t nnan = W.fail ? 0 : W.nan_total() - pad;
+    const uint64_t n = A.gaps ? (uint64_t)L - nnan : (uint64_t)L;
+    const bool has_nan = nnan && !A.gaps;
+    if (!W.fail && n > 0 && !has_nan) W.export_shrink(X.key_cap);
+    uint32_t flags = 0;
+    if (W.fail || (!W.point && W.cnt > X.key_cap)) flags |= KRR_WIN_FAIL;
+    if (has_nan) flags |= KRR_FLAG_NAN;
+    if (W.point) flags |= KRR_WIN_POINT;
+    if (!(flags & (KRR_WIN_FAIL | KRR_WIN_POINT))) {
+        uint64_t* row = X.keys + (size_t)s * X.key_cap;
+        for (uint32_t i = lane; i < W.cnt; i += kWave) row[i] = W.buf[i];
+    }
+    const uint64_t below = W.below_total();  // a wave reduction (LANE_COUNTS): every lane takes part
+    if (lane == 0) {
+        krr_window_hdr h;
+        h.lo = W.lo;
+        h.hi = W.hi;
+        h.below = (int64_t)below;
+        h.n = (int64_t)n;
+        h.cnt = W.cnt;
+        h.flags = flags;
+        X.hdr[s] = h;
+    }
+    __syncthreads();
+}
+
+template <bool LONG>
+__global__ __launch_bounds__(64, window_waves(LONG)) void k_window_export(WindowExportArgs X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    for (int64_t s = blockIdx.x; s < X.A.S; s += gridDim.x) window_export_segment<LONG>(X, xcd_item(s, X.A.S), smem, threadIdx.x);
+}
+
+struct OpAdd64 {
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+};
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+    return lane_bcast64(wave_scan64(x, 0ull, OpAdd64{}), kWave - 1);
+}
+
+struct WindowMergeArgs {
+    SelectArgs A;                // mode, p, q; out_v / out_n / out_f; S = series
+    int32_t slices;
+    int64_t stride;              // header / row index of slice j of series i: j * stride + i
+    const krr_window_hdr* hdr;
+    const uint64_t* keys;
+    int64_t key_cap;
+    unsigned int* miss_count;    // may be null
+};
+
+// One wave per series: the slices' windows -> the exact result, or a miss.
+__global__ __launch_bounds__(64) void k_window_merge(WindowMergeArgs M) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const SelectArgs& A = M.A;
+    uint64_t* buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const bool has = lane < M.slices;
+        krr_window_hdr h;
+        if (has) {
+            h = M.hdr[(int64_t)lane * M.stride + s];
+        } else {
+            h.lo = 0;
+            h.hi = ~0ull;
+            h.below = h.n = 0;
+            h.cnt = h.flags = 0;
+        }
+        const uint64_t n = wave_sum_u64((uint64_t)h.n);
+        const uint64_t Lk = wave_max_u64(h.lo), Hk = wave_min_u64(h.hi);
+        const bool any_nan = ballot((h.flags & KRR_FLAG_NAN) != 0) != 0;
+        // a row longer than key_cap cannot come from krr_window_export: no window
+        const bool any_fail =
+            ballot((h.flags & KRR_WIN_FAIL) != 0 || (!(h.flags & KRR_WIN_POINT) && h.cnt > M.key_cap)) != 0;
+        uint32_t flags = 0;
+        double result = bitsd(kQuietNaN);
+        bool miss = false;
+        if (any_nan) {
+            flags = KRR_FLAG_NAN;  // a NaN sample (compact layout): NaN, as the whole-series select says
+        } else if (n == 0) {
+            flags = KRR_FLAG_EMPTY;
+        } else if (any_fail || Lk > Hk) {
+            miss = true;
+        } else {
+            const Ranks R = ranks_for(A, n);
+            uint64_t cb = wave_sum_u64((uint64_t)h.below);  // present samples below Lk, all slices
+            uint32_t inr = 0, inr_point = 0;
+#pragma unroll 1
+            for (int j = 0; j < M.slices; ++j) {
+                const uint64_t loj = lane_bcast64(h.lo, j);
+                const uint32_t cj = lane_bcast32(h.cnt, j), fj = lane_bcast32(h.flags, j);
+                if (fj & KRR_WIN_POINT) {  // cj copies of loj (Lk >= loj >= Hk when it is in range)
+                    if (loj < Lk) cb += cj;
+                    else if (loj <= Hk) inr_point += cj;
+                    continue;
+                }
+                const uint64_t* row = M.keys + ((int64_t)j * M.stride + s) * M.key_cap;
+                uint32_t lt = 0;
+                for (uint32_t base = 0; base < cj; base += kWave) {
+                    const uint32_t i = base + lane;
+                    const bool v = i < cj;
+                    const uint64_t k = v ? row[i] : 0ull;
+                    lt += popc64(ballot(v && k < Lk));
+                    const bool in = v && k >= Lk && k <= Hk;
+                    const uint64_t m = ballot(in);
+                    if (in) buf[inr + lane_prefix(m)] = k;
+                    inr += popc64(m);
+                }
+                cb += lt;
+            }
+            __syncthreads();
+            const uint64_t tot = (uint64_t)inr + inr_point;
+            if (cb <= (uint64_t)R.r0 && (uint64_t)R.r1 < cb + tot) {
+                uint64_t k0 = Lk, k1 = Lk;
+                bool bad = false;
+                if (Lk != Hk && inr_point == 0) {
+                    SelectProc sp;
+                    sp.buf = buf;
+                    sp.H = reinterpret_cast<uint32_t*>(smem);
+                    sp.small = reinterpret_cast<uint64_t*>(smem + 1024);
+                    sp.lane = lane;
+                    sp.flip = 0;
+                    sp.cnt = inr;
+                    sp.bad = 0;
+                    uint64_t mn, mx;
+                    sp.buf_minmax(mn, mx);
+                    const uint32_t Rt = (uint32_t)(inr - ((uint64_t)R.r0 - cb));  // R-th largest = rank r0
+                    if (R.r1 != R.r0) sp.kth_pair(Rt, -1, mn, mx, k0, k1);
+                    else k0 = k1 = sp.kth_largest(Rt, mn, mx);
+                    bad = sp.bad != 0;
+                }
+                const double a = bitsd(okey_inv(k0));
+                if (bad) {
+                    miss = true;
+                } else if (A.mode == KRR_PCT_SORTED_LOWER) {
+                    // a zero's sign is the (r0 - #negatives)-th zero's in time order (sorted()
+                    // is stable): not in the windows, so the whole series decides it
+                    if (is_zero_bits(dbits(a))) miss = true;
+                    else result = a;
+                } else {
+                    result = np_lerp(a, R.r1 != R.r0 ? bitsd(okey_inv(k1)) : a, R.gamma);
+                }
+            } else {
+                miss = true;
+            }
+        }
+        if (miss) {
+            flags = KRR_FLAG_WINDOW_MISS;
+            result = bitsd(kQuietNaN);
+        }
+        if (lane == 0) {
+            A.out_v[s] = result;
+            A.out_n[s] = (int64_t)n;
+            A.out_f[s] = flags;
+            if (miss && M.miss_count) atomicAdd(M.miss_count, 1u);
+        }
+        __syncthreads();
     }
 }
 
@@ -2924,9 +3258,15 @@ struct krr_ctx {
     size_t max_lds;
     unsigned long long* d_tmp;    // [0] scratch (max segment length), [1] stats: wselect fallbacks
     unsigned int* d_fail_count;   // wselect miss list lengths: [epoch & 1]
-    unsigned int fail_epoch;
+    unsigned int fail_epoch;      // advanced only after a window launch + its miss pass were enqueued
     int64_t* d_fail_list;         // segment ids (capacity fail_cap)
     int64_t fail_cap;
+    // The miss list and its counters are shared by every stream the ctx is used on:
+    // the miss pass of the last window launch is recorded here, and a window launch on
+    // another stream first waits for it (same stream: stream order already does).
+    hipEvent_t fail_ev;
+    hipStream_t fail_stream;
+    bool fail_ev_valid;
     char err[512];
 };
 
@@ -3024,26 +3364,35 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
             KRR_HIP(ctx, hipMalloc(&ctx->d_fail_list, (size_t)series->n_segments * sizeof(int64_t)));
             ctx->fail_cap = series->n_segments;
         }
+    }
+    *lds = kSelectLdsFixed + (hsel ? (KRR_WSEL ? window_lds(A->wcap) : kHselectLds) : (size_t)cap * 8);
+    if (*lds < (size_t)KRR_LDS_MIN) *lds = (size_t)KRR_LDS_MIN;
+    if (*lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "select needs %s%lld B of LDS", "", (long long)*lds);
+    if (hsel && KRR_WSEL && A->wcap != kWselCapLong) {
+        // launch k counts its misses into counter (k & 1) and zeroes counter ((k + 1) & 1),
+        // which launch k - 1's miss pass has read by then (stream order, or the event below);
+        // the epoch only advances once the launch is enqueued (commit_fail_list)
+        if (ctx->fail_ev_valid && ctx->fail_stream != st) KRR_HIP(ctx, hipStreamWaitEvent(st, ctx->fail_ev, 0));
         A->fail_list = ctx->d_fail_list;
-        const unsigned int e = ctx->fail_epoch++ & 1u;
+        const unsigned int e = ctx->fail_epoch & 1u;
         A->fail_count = ctx->d_fail_count + e;
         A->fail_reset = ctx->d_fail_count + (e ^ 1u);
     }
-    // the long kernels finish misses inline: hselect's LDS too
-    const size_t wlds = A->wcap == kWselCapLong ? ((size_t)A->wcap * 8 > kHselectLds ? (size_t)A->wcap * 8 : kHselectLds)
-                                                : (size_t)A->wcap * 8;
-    *lds = kSelectLdsFixed + (hsel ? (KRR_WSEL ? wlds : kHselectLds) : (size_t)cap * 8);
-    if (*lds < (size_t)KRR_LDS_MIN) *lds = (size_t)KRR_LDS_MIN;
-    if (*lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "select needs %s%lld B of LDS", "", (long long)*lds);
     return KRR_OK;
 }
 
 // After a window-select launch: hselect over the segments it missed (none, usually).
+// Only then does the miss list's epoch advance, and the pass is recorded for window
+// launches that come on another stream (plan_select).
 int launch_fallback(krr_ctx* ctx, const SelectArgs& A, int64_t S, hipStream_t st) {
     if (!A.fail_list) return KRR_OK;
     const int64_t g = S < (int64_t)KRR_FALLBACK_GRID ? S : (int64_t)KRR_FALLBACK_GRID;
     hipLaunchKernelGGL(k_hselect_list, dim3((unsigned)g), dim3(64), kSelectLdsFixed + kHselectLds, st, A);
     KRR_HIP(ctx, hipGetLastError());
+    ctx->fail_epoch++;
+    KRR_HIP(ctx, hipEventRecord(ctx->fail_ev, st));
+    ctx->fail_stream = st;
+    ctx->fail_ev_valid = true;
     return KRR_OK;
 }
 
@@ -3090,12 +3439,20 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->fail_epoch = 0;
     c->d_fail_list = nullptr;
     c->fail_cap = 0;
+    c->fail_ev = nullptr;
+    c->fail_stream = nullptr;
+    c->fail_ev_valid = false;
+    if (hipEventCreateWithFlags(&c->fail_ev, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return KRR_E_HIP;
+    }
     if (hipMalloc(&c->d_tmp, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_tmp, 0, 2 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_fail_count, 2 * sizeof(unsigned int)) != hipSuccess ||
         hipMemset(c->d_fail_count, 0, 2 * sizeof(unsigned int)) != hipSuccess) {
         if (c->d_tmp) (void)hipFree(c->d_tmp);
         if (c->d_fail_count) (void)hipFree(c->d_fail_count);
+        (void)hipEventDestroy(c->fail_ev);
         delete c;
         return KRR_E_HIP;
     }
@@ -3108,8 +3465,9 @@ int krr_create(int device, krr_ctx** out_ctx) {
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     (void)hipFuncSetAttribute((const void*)k_sketch_build, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
-    (void)hipFuncSetAttribute((const void*)k_hselect_list, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)c->max_lds);
+    for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
+                          (const void*)k_window_export<false>, (const void*)k_window_merge})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
 }
@@ -3120,6 +3478,7 @@ int krr_destroy(krr_ctx* ctx) {
     if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
     if (ctx->d_fail_count) (void)hipFree(ctx->d_fail_count);
     if (ctx->d_fail_list) (void)hipFree(ctx->d_fail_list);
+    if (ctx->fail_ev) (void)hipEventDestroy(ctx->fail_ev);
     delete ctx;
     return KRR_OK;
 }
@@ -3362,6 +3721,15 @@ int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value, c
     return KRR_OK;
 }
 
+#ifdef KRR_WEXP_DEBUG
+int krr_wexp_debug_read(unsigned long long* out, unsigned int* n) {
+    if (hipMemcpyFromSymbol(n, HIP_SYMBOL(krr::g_wdbg_n), sizeof(unsigned int)) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krr::g_wdbg), sizeof(unsigned long long) * 5 * 1024) != hipSuccess) return -2;
+    unsigned int z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(krr::g_wdbg_n), &z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 #ifdef KRR_DIAG
 int krr_diag_attach(void* dev_buffer) {
     return hipMemcpyToSymbol(HIP_SYMBOL(krr::g_diag), &dev_buffer, sizeof(void*)) == hipSuccess ? 0 : -2;
@@ -3546,6 +3914,105 @@ int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k,
     return KRR_OK;
 }
 
+int64_t krr_window_key_cap(int64_t max_slice_len, int64_t ext_slots, const krr_percentile_params* params) {
+    if (max_slice_len < 0 || ext_slots < 0 || check_params(nullptr, params) != KRR_OK ||
+        params->mode == KRR_PCT_REF_INDEX)
+        return 0;
+    const double q = (double)params->p_num / (100.0 * (double)params->p_den);
+    const double L = (double)max_slice_len, U = (double)ext_slots;
+    const double sig = (L > 0 && U > 0) ? sqrt(q * (1.0 - q) * L * U / (L + U)) : 0.0;
+    // export_shrink keeps ranks [c - w, c + w + 1] (w = z sig + 4): 2w + 2 keys, plus
+    // room for keys equal to the bounds
+    int64_t keys = 2 * (int64_t)ceil(KRR_WEXP_Z * sig + 4.0) + 2 + 64;
+    keys = (keys + 63) & ~(int64_t)63;
+    return keys;
+}
+
+int krr_window_export(krr_ctx* ctx, const krr_series* slices, const krr_percentile_params* params,
+                      int64_t ext_slots, int64_t key_cap, krr_window_hdr* hdr, uint64_t* keys, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, slices);
+    if (!rc) rc = check_params(ctx, params);
+    if (rc) return rc;
+    if (params->mode == KRR_PCT_REF_INDEX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no window form: use krr_select_present%s", "");
+    if (ext_slots < 0 || key_cap < 1 || key_cap > (int64_t)kWselCapLong)
+        return set_err(ctx, KRR_E_INVALID, "window export: ext_slots >= 0, 1 <= key_cap <= %s%lld", "",
+                       (long long)kWselCapLong);
+    const int64_t S = slices->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!hdr || !keys) return set_err(ctx, KRR_E_INVALID, "null outputs%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipStream_t st = (hipStream_t)stream;
+    int64_t Lmax = 0;
+    rc = resolve_maxlen(ctx, slices, st, &Lmax);
+    if (rc) return rc;
+    WindowExportArgs X{};
+    X.A.vals = slices->values;
+    X.A.offs = slices->offsets;
+    X.A.S = S;
+    X.A.mode = params->mode;
+    X.A.gaps = slices->gaps_are_nan;
+    X.A.p_num = params->p_num;
+    X.A.p_den = params->p_den;
+    X.A.q = params->q;
+    X.A.wcap = wsel_cap_for(Lmax, slices->gaps_are_nan != 0);
+    X.ext = (double)ext_slots;
+    X.key_cap = (uint32_t)key_cap;
+    X.hdr = hdr;
+    X.keys = keys;
+    const size_t lds = kSelectLdsFixed + (size_t)X.A.wcap * 8;
+    if (lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "window export needs %s%lld B of LDS", "", (long long)lds);
+    if (X.A.wcap == kWselCapLong) hipLaunchKernelGGL(k_window_export<true>, dim3(grid_for(S)), dim3(64), lds, st, X);
+    else hipLaunchKernelGGL(k_window_export<false>, dim3(grid_for(S)), dim3(64), lds, st, X);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_window_merge(krr_ctx* ctx, int64_t n_series, int32_t n_slices, int64_t slice_stride,
+                     const krr_window_hdr* hdr, const uint64_t* keys, int64_t key_cap,
+                     const krr_percentile_params* params, double* out_value, int64_t* out_count,
+                     uint32_t* out_flags, uint32_t* miss_count, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    if (params->mode == KRR_PCT_REF_INDEX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no window form: use krr_select_present%s", "");
+    if (n_series < 0 || n_slices < 1 || n_slices > kWave || slice_stride < n_series || key_cap < 1 ||
+        key_cap > (int64_t)kWselCapLong)
+        return set_err(ctx, KRR_E_INVALID, "window merge: 1 <= n_slices <= 64, slice_stride >= n_series, "
+                       "1 <= key_cap <= %s%lld", "", (long long)kWselCapLong);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipStream_t st = (hipStream_t)stream;
+    if (miss_count) KRR_HIP(ctx, hipMemsetAsync(miss_count, 0, sizeof(uint32_t), st));
+    if (n_series == 0) return KRR_OK;
+    if (!hdr || !keys || !out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    const size_t lds = kSelectLdsFixed + (size_t)n_slices * (size_t)key_cap * 8;
+    if (lds > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "window merge needs %s%lld B of LDS (n_slices x key_cap keys)", "",
+                       (long long)lds);
+    WindowMergeArgs M{};
+    M.A.S = n_series;
+    M.A.mode = params->mode;
+    M.A.p_num = params->p_num;
+    M.A.p_den = params->p_den;
+    M.A.q = params->q;
+    M.A.out_v = out_value;
+    M.A.out_n = out_count;
+    M.A.out_f = out_flags;
+    M.slices = n_slices;
+    M.stride = slice_stride;
+    M.hdr = hdr;
+    M.keys = keys;
+    M.key_cap = key_cap;
+    M.miss_count = miss_count;
+    hipLaunchKernelGGL(k_window_merge, dim3(grid_for(n_series)), dim3(64), lds, st, M);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
 int krr_get_stats(krr_ctx* ctx, int64_t* wselect_fallbacks) {
     if (!ctx || !wselect_fallbacks) return KRR_E_INVALID;
     DeviceGuard g(ctx->device);
@@ -3573,7 +4040,7 @@ int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params
     out->tkeep = sp.tkeep;
     out->cap_keys = hsel ? 0 : need;
     out->lds_bytes = (int64_t)kSelectLdsFixed +
-                     (int64_t)(hsel ? (KRR_WSEL ? (size_t)wsel_cap_for(Lmax) * 8 : kHselectLds) : (size_t)need * 8);
+                     (int64_t)(hsel ? (KRR_WSEL ? window_lds(wsel_cap_for(Lmax)) : kHselectLds) : (size_t)need * 8);
 #if KRR_SELECT_PROBE
     out->probe = (!hsel && !sp.bottom && select_probe_pays(Lmax, sp.tkeep, need)) ? 1 : 0;
 #endif

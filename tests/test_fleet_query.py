@@ -254,7 +254,7 @@ def test_sample_bounded_groups_keep_the_per_pod_csr(resource, max_samples):
     exp = pack_query_range_bodies(per_pod_bodies(objects, prom, resource))
     np.testing.assert_array_equal(got.offsets, exp.offsets)
     assert got.values.tobytes() == exp.values.tobytes()
-    unbounded = FleetQueryPlan(objects)
+    unbounded = FleetQueryPlan(objects, points_per_series=0)
     assert len(plan.groups) >= len(unbounded.groups)
 
 
@@ -270,3 +270,6 @@ def test_plan_for_settings_counts_points():
     assert max(pods_per_group) == 50_000_000 // (1345 * 4) and sum(pods_per_group) == 20_000
     with pytest.raises(ValueError):
         FleetQueryPlan(objects, points_per_series=-1)
+    # without settings the plan still bounds samples, at the reference's default settings
+    default = FleetQueryPlan(big, max_query_chars=10**9)
+    assert default.points_per_series == 1345 and max(len(g.pods) for g in default.groups) == max(pods_per_group)

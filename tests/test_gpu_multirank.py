@@ -77,18 +77,39 @@ def test_bench_rccl_path_one_rank(gather):
     assert r["records_host_equal_device"] is True, r
 
 
-@pytest.mark.parametrize("world,mode,pct", [(2, "linear", "99"), (3, "sorted_lower", "50"), (2, "linear", "95")])
-def test_bench_config5_time_sharded_ranks(world, mode, pct):
+@pytest.mark.parametrize("world,mode,pct,method", [(2, "linear", "99", "window"), (3, "sorted_lower", "50", "window"),
+                                                   (2, "linear", "95", "window"), (3, "linear", "99", "sketch"),
+                                                   (2, "sorted_lower", "50", "sketch")])
+def test_bench_config5_time_sharded_ranks(world, mode, pct, method):
     """Config 5 through `bench.py --gpus N` (gloo ranks sharing the GPU): every series is
-    time-sharded over N ranks, the per-slice sketches are reduce-scattered, the needed
-    ranks' bins located, the samples in them all-to-all'd to the owners and selected
-    exactly; rank 0 checks the gathered answers bit for bit against one k_select/hselect
-    pass over the full 172,800-sample series (regathered from every rank)."""
+    time-sharded over N ranks.  window (default): each rank streams its slices once and
+    exports its windows, one all-to-all hands them to the owners, which merge them;
+    sketch: per-slice sketches reduce-scattered, the needed bins located, the samples in
+    them collected (second pass), all-to-all'd and selected.  Rank 0 checks the gathered
+    answers bit for bit against one k_select/hselect pass AND the C oracle over the full
+    172,800-sample series (regathered from every rank)."""
     r = _bench(["--gpus", str(world), "--config", "5", "--containers", "600", "--steps", "2", "--warmup", "1",
-                "--mode", mode, "--percentile", pct, "--error-sample", "600"], timeout=300)
+                "--mode", mode, "--percentile", pct, "--error-sample", "600", "--c5-method", method], timeout=300)
     assert r["n_gpus"] == world and r["config"]["parallelism"].startswith(f"time-shard{world}")
+    assert r["config"]["method"] == method
     assert r["parity_vs_single_window_select"] is True and r["parity_sample_series"] == 600, r
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_oracle_sample_series"] == 600, r
     assert "cpu_baseline" not in r
+    if method == "window":
+        assert r["roofline"]["kernel"] == "k_window_export" and r["window"]["hbm_passes_per_step"] == 1
+        assert r["window"]["misses_per_step"] == 0, r["window"]
+
+
+def test_bench_config5_window_refine_one_rank():
+    """--c5-refine at N = 1: the time-sharded one-pass path on one rank; its answers equal the
+    oracle on the CPU-baseline sample and k_select on the error sample."""
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5",
+                        "--containers", "800", "--c5-refine", "--steps", "2", "--warmup", "1", "--error-sample", "300",
+                        "--cpu-sample", "100"], capture_output=True, text=True, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["config"]["method"] == "window" and r["parity_vs_single_window_select"] is True, r
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_oracle_sample_series"] == 500, r
 
 
 def test_bench_config5_sketch_only_two_ranks():
@@ -273,6 +294,19 @@ def test_bench_config5_direct_chunked():
     assert p.returncode == 0, p.stderr[-4000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert r["parity_vs_single_window_select"] is True and r["parity_sample_series"] == 600, r
+    assert r["launches_per_step"] > 1
+
+
+def test_bench_config5_direct_oracle_parity():
+    """Config 5 at N = 1 with the CPU baseline: the run's own answers on the baseline sample
+    equal the oracle (parity_vs_oracle_on_sample), beside the k_select check."""
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5",
+                        "--containers", "700", "--chunk-gib", "0.3", "--steps", "2", "--warmup", "1",
+                        "--error-sample", "200", "--cpu-sample", "60"], capture_output=True, text=True, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_oracle_sample_series"] == 300, r
+    assert r["cpu_baseline"]["kind"] == "port"
 
 
 def test_bench_four_ranks_chunked_shards():
