@@ -1113,7 +1113,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         with open(args.traffic) as fh:
             tr = json.load(fh)
         key = f"config5:{params_mode(args)}:p{args.percentile}:{kname}"
-        if key in tr and int(tr[key].get("containers_per_rank", -1)) == S:
+        if (key in tr and int(tr[key].get("containers_per_rank", -1)) == S
+                and int(tr[key].get("slots_per_rank", N)) == N):  # the same slice size per rank
             result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
             result["roofline"]["traffic_source"] = tr[key].get("source")
     except (OSError, ValueError):

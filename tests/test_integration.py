@@ -47,3 +47,25 @@ def test_reference_runner_results_equal_reference(path):
     assert r["custom_strategy_not_routed"]
     # the reference's _format_result clamps 7 B to the 10 MB memory floor (runner.py:49-77)
     assert r["custom_strategy_rows"] == [["99", "10000000", "10000000"]] * 3
+
+
+@pytest.mark.parametrize("loader", ["bodies", "grouped"])
+def test_reference_collect_result_native_loader_and_fleet_scan(loader):
+    """install(Runner, loader=..., scan="fleet"): the reference's whole _collect_result against
+    a fake Prometheus session.  The per-pod (or grouped) bodies go to the native packer —
+    the reference's gather_data (Decimal per sample) never runs — and the Result built by
+    scan_fleet out of the reference's own models equals the unpatched reference's, scan
+    for scan and in score, every severity included.  The same run first takes the real
+    engine through it: the bodies are packed natively, then the kernel call raises
+    NativeUnavailable on this GPU-less host (no CPU fallback anywhere)."""
+    r = _check("--engine", "oracle", "--loader", loader, "--scan", "fleet", "--objects", "30")
+    assert r["raised"] == "NativeUnavailable" and r["native_packer_used_before_raise"], r
+    assert r["collect_patched"] and r["equals_reference_result"], r
+    assert r["types"] == ["robusta_krr.core.models.result.ResourceScan", "robusta_krr.core.models.result.Result"]
+    assert r["severities"] == ["CRITICAL", "GOOD", "OK", "UNKNOWN", "WARNING"]
+    assert r["n_scans"] == 32 and r["gather_data_calls"] == 0 and r["native_packer_used"]
+    assert r["same_window_and_step"]
+    if loader == "bodies":  # the reference's own per-pod requests, one for one
+        assert r["http_requests"]["patched"] == r["http_requests"]["reference"] == 2 * (30 * 3 + 2)
+    else:  # one grouped query per (namespace, container) and resource
+        assert r["http_requests"]["patched"] == 2
