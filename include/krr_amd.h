@@ -28,6 +28,9 @@
  *                                runs in Runner._gather_objects_recommendations,
  *                                robusta_krr/core/runner.py:88-120)
  *   krr_simple_run_host       <- same, for callers holding host buffers (PCIe-inclusive)
+ *   krr_json_parse / _compact <- PrometheusLoader.gather_data's per-pod value parse,
+ *                                robusta_krr/core/integrations/prometheus.py:147-155,
+ *                                on response bodies in HBM (device packer)
  *
  * Ownership: the caller owns every buffer; no allocation crosses the ABI.
  * Device pointers are HIP device pointers on the ctx's device; `stream` is a
@@ -354,6 +357,45 @@ int krr_synth_fill_window(krr_ctx* ctx, double* values, const int64_t* offsets, 
 int krr_synth_fill_global(krr_ctx* ctx, double* values, const int64_t* offsets, int64_t n_segments,
                           uint64_t seed, int32_t kind, int64_t pod_len, int32_t gaps, int64_t seg_base,
                           int64_t t0, int64_t total_len, void* stream);
+
+/* ---- Device packer: Prometheus query_range bodies -> CSR in HBM (round 3) ----
+ * Replaces, for bodies already copied to HBM, the host packer krr_pack_parse
+ * (include/krr_pack.h), i.e. the reference's per-pod
+ *   [Decimal(value) for _, value in pod_result[0]["values"]] + the empty-pod drop
+ * of PrometheusLoader.gather_data, robusta_krr/core/integrations/prometheus.py:147-155.
+ * One wave per body.  A body whose bytes lie outside the canonical query_range form
+ * Prometheus writes (whitespace inside the values array, escapes in keys or values,
+ * spellings of NaN/Inf other than "NaN"/"Inf", more than 19 significant digits,
+ * status != "success", malformed JSON) is NOT an error here: its status is
+ * KRR_JSON_HOST and the caller parses that batch with krr_pack_parse, which returns
+ * the host packer's result or error.  Whatever this packer accepts it parses to the
+ * bits krr_pack_parse produces.
+ *
+ * Two steps on `stream`:
+ *   krr_json_parse    every body of [first, first + n): status[b], counts[b] (samples
+ *                     kept; 0 unless KRR_JSON_OK), values (and timestamps) written to
+ *                     scratch slot (body_offsets[b] / 8) + i;
+ *   krr_json_compact  each KRR_JSON_OK body's run to values[out_pos[b] ..) — out_pos
+ *                     the exclusive prefix sum of counts (the CSR of the caller's
+ *                     objects follows from the counts, bodies in fleet order).
+ * Buffers: bodies 16-byte aligned with 64 readable bytes past the last body;
+ * scratch_values / scratch_ts hold body_offsets[n_bodies] / 8 + 1 doubles. */
+#define KRR_JSON_OK 0        /* parsed: counts[b] samples */
+#define KRR_JSON_DROPPED 1   /* data.result is empty: the pod is dropped (prometheus.py:154) */
+#define KRR_JSON_HOST 2      /* outside the device grammar: parse the batch with krr_pack_parse */
+
+typedef struct krr_json_bodies {
+    const char* bodies;           /* device: the response bodies back to back */
+    const int64_t* body_offsets;  /* device: [n_bodies + 1] byte offsets, body_offsets[0] == 0 */
+    int64_t n_bodies;
+    int64_t total_bytes;          /* body_offsets[n_bodies] (host copy) */
+} krr_json_bodies;
+
+int krr_json_parse(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, int32_t want_timestamps,
+                   double* scratch_values, double* scratch_ts, int64_t* counts, int32_t* status, void* stream);
+int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scratch_values,
+                     const double* scratch_ts, const int64_t* counts, const int32_t* status,
+                     const int64_t* out_pos, double* values, double* timestamps, void* stream);
 
 #ifdef __cplusplus
 }

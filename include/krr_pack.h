@@ -101,6 +101,12 @@ int krr_pack_parse_grouped(const char* const* bodies, const int64_t* body_lens, 
                            const int64_t* obj_of_slot, int64_t n_slots, int64_t n_objects, int32_t want_timestamps,
                            int32_t threads, krr_pack** out);
 
+/* Staging for the device packer (include/krr_amd.h krr_json_parse): body b's bytes to
+ * dst[dst_offsets[b] - dst_offsets[0] ..) for b in [0, n_bodies), on up to `threads`
+ * host threads (dst typically page-locked memory the H2D copy reads by DMA). */
+int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                    const int64_t* dst_offsets, char* dst, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

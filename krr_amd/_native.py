@@ -40,6 +40,8 @@ KRR_WIN_POINT = 0x200
 # Every symbol include/krr_amd.h declares (tests/test_abi.py checks the export table).
 EXPORTED_SYMBOLS = (
     "krr_abi_version",
+    "krr_json_parse",
+    "krr_json_compact",
     "krr_create",
     "krr_destroy",
     "krr_last_error",
@@ -163,6 +165,18 @@ class KrrSelectPlanInfo(ctypes.Structure):
     ]
 
 
+class KrrJsonBodies(ctypes.Structure):
+    """include/krr_amd.h krr_json_bodies."""
+    _fields_ = [
+        ("bodies", ctypes.c_void_p),
+        ("body_offsets", ctypes.c_void_p),
+        ("n_bodies", ctypes.c_int64),
+        ("total_bytes", ctypes.c_int64),
+    ]
+
+
+KRR_JSON_OK, KRR_JSON_DROPPED, KRR_JSON_HOST = 0, 1, 2
+
 NCCL_UNIQUE_ID_BYTES = 128
 
 _lib = None
@@ -251,6 +265,11 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_window_export.restype = ctypes.c_int
         lib.krr_window_merge.argtypes = [vp, i64, i32, i64, vp, vp, i64, pp, vp, vp, vp, vp, vp]
         lib.krr_window_merge.restype = ctypes.c_int
+        jb = ctypes.POINTER(KrrJsonBodies)
+        lib.krr_json_parse.argtypes = [vp, jb, i64, i64, i32, vp, vp, vp, vp, vp]
+        lib.krr_json_parse.restype = ctypes.c_int
+        lib.krr_json_compact.argtypes = [vp, jb, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_json_compact.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
@@ -528,6 +547,47 @@ class Context:
         self._check(self._lib.krr_synth_fill_global(
             self._h, values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, int(seed) & (2**64 - 1),
             int(kind), int(pod_len), int(bool(gaps)), int(seg_base), int(t0), int(total_len), self._stream(stream)))
+
+    # --- device packer: query_range bodies in HBM -> CSR --------------------------------
+    def json_bodies(self, bodies, body_offsets, total_bytes: int) -> KrrJsonBodies:
+        """bodies: uint8 device tensor (16-B aligned, >= 64 bytes past the last body);
+        body_offsets: int64 device tensor [n_bodies + 1]."""
+        _check_tensor(bodies, "uint8", int(total_bytes) + 64)
+        _check_tensor(body_offsets, "int64")
+        if bodies.data_ptr() % 16:
+            raise ValueError("bodies must be 16-byte aligned")
+        jb = KrrJsonBodies(bodies.data_ptr(), body_offsets.data_ptr(), body_offsets.numel() - 1, int(total_bytes))
+        jb._keep = (bodies, body_offsets)
+        return jb
+
+    def json_parse(self, jb: KrrJsonBodies, first: int, n: int, want_timestamps: bool, scratch_values, scratch_ts,
+                   counts, status, stream=None) -> None:
+        slots = jb.total_bytes // 8 + 1
+        _check_tensor(scratch_values, "float64", slots)
+        if want_timestamps:
+            _check_tensor(scratch_ts, "float64", slots)
+        _check_tensor(counts, "int64", jb.n_bodies)
+        _check_tensor(status, "int32", jb.n_bodies)
+        self._check(self._lib.krr_json_parse(
+            self._h, ctypes.byref(jb), int(first), int(n), int(bool(want_timestamps)), scratch_values.data_ptr(),
+            scratch_ts.data_ptr() if want_timestamps else None, counts.data_ptr(), status.data_ptr(),
+            self._stream(stream)))
+
+    def json_compact(self, jb: KrrJsonBodies, scratch_values, scratch_ts, counts, status, out_pos, values,
+                     timestamps=None, stream=None) -> None:
+        n = jb.n_bodies
+        _check_tensor(counts, "int64", n)
+        _check_tensor(status, "int32", n)
+        _check_tensor(out_pos, "int64", n)
+        _check_tensor(values, "float64")
+        if timestamps is not None:
+            _check_tensor(timestamps, "float64", values.numel())
+            _check_tensor(scratch_ts, "float64")
+        self._check(self._lib.krr_json_compact(
+            self._h, ctypes.byref(jb), scratch_values.data_ptr(),
+            scratch_ts.data_ptr() if timestamps is not None else None, counts.data_ptr(), status.data_ptr(),
+            out_pos.data_ptr(), values.data_ptr(), timestamps.data_ptr() if timestamps is not None else None,
+            self._stream(stream)))
 
 
 def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectPlanInfo:

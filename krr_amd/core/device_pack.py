@@ -1,0 +1,175 @@
+"""Device packer: Prometheus query_range response bodies -> CSR float64 in HBM.
+
+The host packer (``krr_amd.core.prom_native.pack_query_range_bodies``, libkrr_host.so)
+restates the reference's per-pod ``[Decimal(value) for _, value in
+pod_result[0]["values"]]`` + empty-pod drop (robusta_krr/core/integrations/prometheus.py:
+147-155) on the host's cores; end to end from bodies it was the limiter.
+Here the raw bodies cross PCIe instead and the MI355X parses them (include/krr_amd.h
+``krr_json_parse`` / ``krr_json_compact``, krr_amd/csrc/krr_json.h):
+
+  1. bodies are gathered into page-locked staging memory by the host runtime's parallel
+     copy (``krr_pack_concat``), chunk by chunk;
+  2. each chunk goes to HBM on a copy stream while the previous chunk is parsed: one wave
+     per body, the values array by all 64 lanes, values to a scratch slot per body;
+  3. one synchronisation reads the bodies' statuses and the CSR size; the counts' prefix
+     sums (bodies are in fleet order) give the segment offsets and each body's place, and
+     ``krr_json_compact`` writes the CSR.
+
+A body outside the canonical form Prometheus writes (KRR_JSON_HOST: whitespace in the
+values array, escapes, other NaN/Inf spellings, > 19 significant digits, an error status,
+malformed JSON) is not decided here: the whole batch is then parsed by the host packer,
+which returns the host's result or raises its error — the outcome is the host packer's
+either way (``DevicePacked.via`` says which ran).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from krr_amd import _native
+from krr_amd.core.packing import PackedSeries
+from krr_amd.core.prom_native import KRR_PACK_OK, PrometheusResponseError, load_library, pack_query_range_bodies
+
+
+@dataclass
+class DevicePacked:
+    series: PackedSeries            # values / offsets: torch tensors in HBM (via == "device") or numpy (host)
+    via: str                        # "device" | "host"
+    host_bodies: int = 0            # bodies the device left to the host (KRR_JSON_HOST)
+    pod_counts: Optional[object] = None  # per body: samples kept, -1 dropped (return_pod_counts)
+    timestamps: Optional[object] = None
+
+
+class DevicePacker:
+    """One per (thread, device): owns the page-locked staging buffer and a copy stream.
+
+    ``chunk_bytes``: bodies are staged and copied in chunks of about this size, each
+    parsed as soon as it is in HBM."""
+
+    def __init__(self, ctx: _native.Context, chunk_bytes: int = 256 << 20, threads: int = 0):
+        import torch
+
+        self.ctx = ctx
+        self.device = torch.device("cuda", ctx.device)
+        self.chunk_bytes = int(chunk_bytes)
+        self.threads = int(threads)
+        self._stage = None
+        self._copy_stream = torch.cuda.Stream(device=self.device)
+        self._lock = threading.Lock()
+
+    def _staging(self, nbytes: int):
+        import torch
+
+        if self._stage is None or self._stage.numel() < nbytes:
+            self._stage = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+        return self._stage
+
+    def pack(self, per_object_bodies: Sequence[Sequence[bytes]], *, want_timestamps: bool = False,
+             return_pod_counts: bool = False, stream=None) -> DevicePacked:
+        """per_object_bodies[o][i] = the raw query_range body of pod i of object o, for ONE
+        resource (as ``pack_query_range_bodies``).  Returns a DevicePacked whose series is
+        the host packer's CSR, bit for bit, in HBM."""
+        with self._lock:
+            return self._pack(per_object_bodies, want_timestamps, return_pod_counts, stream)
+
+    def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:
+        import torch
+
+        flat: list = []
+        obj: list = []
+        for o, bodies in enumerate(per_object_bodies):
+            for b in bodies:
+                flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
+                obj.append(o)
+        n_obj, nb = len(per_object_bodies), len(flat)
+        dev = self.device
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        if nb == 0:
+            offs = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
+            return DevicePacked(PackedSeries(torch.empty(0, dtype=torch.float64, device=dev), offs, 0), "device", 0,
+                                torch.empty(0, dtype=torch.int64, device=dev) if want_counts else None,
+                                torch.empty(0, dtype=torch.float64, device=dev) if want_ts else None)
+        lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=nb)
+        boffs = np.zeros(nb + 1, dtype=np.int64)
+        np.cumsum(lens, out=boffs[1:])
+        total = int(boffs[-1])
+        stage = self._staging(total + 64)
+        d_bodies = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        d_boffs = torch.from_numpy(boffs).to(dev)
+        slots = total // 8 + 1
+        tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
+        tmp_t = torch.empty(slots, dtype=torch.float64, device=dev) if want_ts else None
+        counts = torch.empty(nb, dtype=torch.int64, device=dev)
+        status = torch.empty(nb, dtype=torch.int32, device=dev)
+        jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
+        ptrs = (ctypes.c_char_p * nb)(*flat)
+        host = load_library()
+        cs = self._copy_stream
+        cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        # chunks of bodies: stage (host threads) -> H2D (copy stream) -> parse (st)
+        a = 0
+        while a < nb:
+            b = int(np.searchsorted(boffs, boffs[a] + self.chunk_bytes, side="left"))
+            b = min(max(b, a + 1), nb)
+            lo, hi = int(boffs[a]), int(boffs[b])
+            rc = host.krr_pack_concat(ctypes.addressof(ptrs) + a * ctypes.sizeof(ctypes.c_char_p),
+                                      lens[a:].ctypes.data, b - a, boffs[a:].ctypes.data,
+                                      stage.data_ptr() + lo, self.threads)
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_concat failed")
+            with torch.cuda.stream(cs):
+                d_bodies[lo:hi].copy_(stage[lo:hi], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            st.wait_event(ev)
+            self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
+            a = b
+        with torch.cuda.stream(st):
+            obj_t = torch.from_numpy(np.asarray(obj, dtype=np.int64)).to(dev, non_blocking=False)
+            seg = torch.zeros(n_obj, dtype=torch.int64, device=dev).index_add_(0, obj_t, counts)
+            offsets = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(seg, 0, out=offsets[1:])
+            summary = torch.stack([status.max().to(torch.int64), offsets[-1], seg.max()]).cpu()  # the one sync
+        worst, n_vals, max_len = (int(x) for x in summary)
+        if worst == _native.KRR_JSON_HOST:
+            n_host = int((status == _native.KRR_JSON_HOST).sum().item())
+            res = pack_query_range_bodies(per_object_bodies, want_timestamps=want_ts, threads=self.threads,
+                                          return_pod_counts=want_counts)
+            if not isinstance(res, tuple):
+                res = (res,)
+            series = res[0]
+            rest = list(res[1:])
+            ts = rest.pop(0) if want_ts else None
+            pc = rest.pop(0) if want_counts else None
+            return DevicePacked(series, "host", n_host, pc, ts)
+        with torch.cuda.stream(st):
+            out_pos = torch.cumsum(counts, 0) - counts
+            values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
+            ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
+            self.ctx.json_compact(jb, tmp_v, tmp_t, counts, status, out_pos, values, ts, stream=st)
+            pc = torch.where(status == _native.KRR_JSON_DROPPED, torch.full_like(counts, -1), counts) \
+                if want_counts else None
+        # the staging buffer is reused by the next call: its copies must be done (they are:
+        # the parse launches waited for them before the summary synchronised)
+        return DevicePacked(PackedSeries(values[:n_vals], offsets, max_len), "device", 0, pc,
+                            ts[:n_vals] if ts is not None else None)
+
+
+_packers: dict = {}
+_packers_lock = threading.Lock()
+
+
+def default_packer(ctx: _native.Context) -> DevicePacker:
+    key = (threading.get_ident(), id(ctx))
+    with _packers_lock:
+        p = _packers.get(key)
+        if p is None:
+            p = _packers[key] = DevicePacker(ctx)
+        return p
+
+
+__all__ = ["DevicePacked", "DevicePacker", "default_packer"]

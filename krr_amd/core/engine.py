@@ -71,6 +71,8 @@ class SimpleEngine:
         import torch
 
         dev = torch.device("cuda", self.device)
+        if isinstance(ps.values, torch.Tensor) and ps.values.is_cuda:  # already in HBM (device packer)
+            return ps.values, ps.offsets
         host = torch.from_numpy(np.ascontiguousarray(ps.values, dtype=np.float64))
         # page-locked values (pinned_alloc) go by DMA without blocking the host; the
         # caller synchronises before the host buffer is released
@@ -162,7 +164,8 @@ class SimpleEngine:
 
         S = fleet.n_objects
         nbytes = 8 * (int(fleet.cpu.offsets[-1]) + int(fleet.mem.offsets[-1]))
-        n = 1 if nbytes <= 2 * self.chunk_bytes else -(-nbytes // self.chunk_bytes)
+        resident = isinstance(fleet.cpu.values, torch.Tensor) and fleet.cpu.values.is_cuda
+        n = 1 if resident or nbytes <= 2 * self.chunk_bytes else -(-nbytes // self.chunk_bytes)
         bounds = [(0, S)] if n == 1 else [(lo, hi) for lo, hi in fleet_shard_bounds(fleet, n) if hi > lo]
         ctx = self.context()
         dev = torch.device("cuda", self.device)

@@ -132,20 +132,44 @@ class BatchedRunner:
         return None if res is None else [to_allocations(r) for r in res]
 
     def recommend_from_bodies(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
-                              threads: int = 0) -> list[RunResult]:
+                              threads: int = 0, parser: str = "device") -> list[RunResult]:
         """The whole loader -> strategy -> rounding path from raw Prometheus query_range
         response bodies: bodies[o][i] = pod i of object o (K8sObjectData.pods order),
         as PrometheusLoader.gather_data would fetch them (prometheus.py:118-143).
-        Native JSON packing (no Decimal lists), one kernel pass, native rounding."""
+        ``parser="device"`` (default): the bodies cross PCIe raw and the MI355X parses them
+        (krr_amd.core.device_pack; a batch with bodies outside Prometheus' canonical form
+        goes to the host packer); ``"host"``: the native host packer (libkrr_host.so).
+        No Decimal lists either way; one kernel pass, native rounding."""
         from krr_amd.core.packing import PackedFleet
         from krr_amd.core.prom_native import pack_query_range_bodies
 
         if len(cpu_bodies) != len(mem_bodies):
             raise ValueError("cpu and memory bodies need one entry per object each")
-        alloc = _pinned_alloc_or_none()
-        fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
-                            pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
+        if parser not in ("device", "host"):
+            raise ValueError("parser must be 'device' or 'host'")
+        if parser == "device":
+            fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads)
+        else:
+            alloc = _pinned_alloc_or_none()
+            fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
+                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
         return self.recommend_packed(fleet)
+
+    def pack_bodies_device(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None):
+        """PackedFleet in HBM from raw bodies, parsed on the device (krr_amd.core.device_pack)."""
+        from krr_amd.core.device_pack import default_packer
+        from krr_amd.core.engine import default_engine
+        from krr_amd.core.packing import PackedFleet
+
+        dev = getattr(self.strategy.settings, "device", 0) if device is None else int(device)
+        ctx = default_engine(dev).context()  # NativeUnavailable without a GPU
+        packer = default_packer(ctx)
+        if threads:
+            packer.threads = int(threads)
+        cpu = packer.pack(cpu_bodies)
+        mem = packer.pack(mem_bodies)
+        self.last_pack_via = (cpu.via, mem.via)
+        return PackedFleet(cpu.series, mem.series)
 
     def recommend_from_grouped(self, plan, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes],
                                threads: int = 0) -> list[RunResult]:

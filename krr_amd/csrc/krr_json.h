@@ -1,0 +1,205 @@
+// krr_json.h — the Prometheus query_range packer on the device (round 3).
+//
+// The host packer (krr_pack.cpp, include/krr_pack.h) parses response bodies at
+// ~12 GB/s of JSON on 16 cores; the end-to-end path from bodies was bound by it
+// (DESIGN.md §9).  Here the raw bodies go to HBM instead (PCIe moves ~55 GB/s) and
+// every body is parsed by one wave:
+//   * lane 0 reads the envelope up to data.result[0]["values"] (krr_json_parse.h
+//     envelope_head: status, data, result, the series' other keys, validated);
+//   * the values array — nearly all of the body — is parsed by all 64 lanes at once:
+//     each lane owns 32 bytes of a 2-KiB block, parses the sample elements that start
+//     in them (`[<time>,"<value>"]`, value -> float64 by Eisel-Lemire), and a wave
+//     prefix sum over the lanes' element counts places each value;
+//   * lane 0 validates the rest of the body (envelope_tail).
+// Values land in a scratch array at slot (body byte offset / 8) + element index (an
+// element takes at least 8 bytes, so bodies' slots never overlap); k_json_compact then
+// moves each kept body's run to its place in the CSR (exclusive prefix of the counts).
+// A body outside the canonical grammar is reported KRR_JSON_HOST, never as an error:
+// the caller parses that batch with the host packer, which gives the reference's
+// result or error for it (krr_json_parse.h header).
+#pragma once
+
+#include "krr_device.h"
+#include "krr_json_parse.h"
+
+namespace krr {
+namespace json {
+
+constexpr int kLaneBytes = 32;                  // bytes of a block each lane scans for '['
+constexpr int kBlockBytes = kLaneBytes * kWave;  // 2 KiB per block
+constexpr int kMaxPerLane = 4;                   // an element spans >= 8 bytes: <= 4 start in 32
+
+struct JsonArgs {
+    const char* bodies;      // device: the bodies back to back (16-B aligned base)
+    const int64_t* offs;     // device: [n_bodies + 1] byte offsets
+    int64_t first;           // first body of this launch
+    int64_t n;               // bodies in this launch
+    int32_t want_ts;
+    double* tmp_v;           // scratch [total_bytes / 8 + 1]
+    double* tmp_t;           // scratch for timestamps (want_ts) or null
+    int64_t* counts;         // [n_bodies] samples kept per body
+    int32_t* status;         // [n_bodies] KRR_JSON_OK / DROPPED / HOST
+};
+
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
+struct ByteLoad {
+    __device__ char operator()(const char* p) const { return *p; }
+};
+
+// positions are >= 0 (INT64_MAX: none)
+__device__ __forceinline__ int64_t wave_min_pos(int64_t x) { return (int64_t)wave_min_u64((uint64_t)x); }
+
+// The values array from its first '[' (vs): returns false when the body goes to the
+// host; else *count samples written at tv/tt[0 ..), *vend = one past the array's ']'.
+__device__ bool values_array(const JsonArgs& A, const char* vs, const char* e, double* tv, double* tt, int lane,
+                             int64_t* count, const char** vend) {
+    const char* const buf = A.bodies;
+    const int64_t lo_abs = vs - buf, hi_abs = e - buf;
+    int64_t blk = lo_abs & ~(int64_t)(kLaneBytes - 1);
+    int64_t cnt = 0;
+    const bool want_ts = A.want_ts != 0;
+    for (; blk < hi_abs; blk += kBlockBytes) {
+        const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
+        double v[kMaxPerLane], t[kMaxPerLane];
+        int64_t st[kMaxPerLane];
+        int nok = 0;
+        int64_t fail_min = INT64_MAX, last_start = INT64_MAX, last_next = 0;
+        if (r0 + kLaneBytes > lo_abs && r0 < hi_abs) {
+            // the lane's 32 bytes: two aligned 16-B loads (the buffer base is 16-B aligned)
+            const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0);
+            const v4u32 a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+            const uint32_t w[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#pragma unroll
+            for (int k = 0; k < kLaneBytes; ++k) {
+                const int64_t x = r0 + k;
+                if (((w[k >> 2] >> (8 * (k & 3))) & 0xFF) != '[' || x < lo_abs || x >= hi_abs) continue;
+                double vv = 0.0, tt2 = 0.0;
+                const char* next;
+                bool last;
+                if (!sample_element(buf + x, e, want_ts, &vv, &tt2, &next, &last, ByteLoad{})) {
+                    fail_min = x < fail_min ? x : fail_min;
+                    continue;
+                }
+                if (nok == kMaxPerLane) {  // cannot happen for elements (>= 8 bytes each)
+                    fail_min = x < fail_min ? x : fail_min;
+                    continue;
+                }
+                v[nok] = vv;
+                t[nok] = tt2;
+                st[nok] = x;
+                ++nok;
+                if (last && x < last_start) {
+                    last_start = x;
+                    last_next = next - buf;
+                }
+            }
+        }
+        // the array's last element is the first one followed by ']'
+        const int64_t end_start = wave_min_pos(last_start);
+        if (wave_min_pos(fail_min) < (end_start == INT64_MAX ? INT64_MAX : end_start + 1)) return false;
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < kMaxPerLane; ++j) mine += (j < nok && st[j] <= end_start) ? 1 : 0;
+        const uint32_t incl = wave_scan32((uint32_t)mine, 0u, OpAdd32{});
+        const int64_t base = cnt + (int64_t)(incl - (uint32_t)mine);
+#pragma unroll
+        for (int j = 0; j < kMaxPerLane; ++j) {
+            if (j < mine) {
+                tv[base + j] = v[j];
+                if (want_ts) tt[base + j] = t[j];
+            }
+        }
+        cnt += (int64_t)lane_bcast32(incl, kWave - 1);
+        if (end_start != INT64_MAX) {
+            // the lane that holds the last element knows where the array ends
+            const uint64_t nx = ballot(last_start == end_start);
+            const int src = (int)__builtin_ctzll(nx);
+            *vend = buf + (int64_t)lane_bcast64((uint64_t)last_next, src);
+            *count = cnt;
+            return true;
+        }
+    }
+    return false;  // no closing ']'
+}
+
+// One body per wave (grid-stride over the launch's bodies).
+__global__ __launch_bounds__(64) void k_json_parse(JsonArgs A) {
+    const int lane = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < A.n; i += gridDim.x) {
+        const int64_t bi = A.first + i;
+        const int64_t ob = A.offs[bi], oe = A.offs[bi + 1];
+        const char* s = A.bodies + ob;
+        const char* e = A.bodies + oe;
+        // phase 1 (lane 0): the envelope up to result[0]["values"]
+        int code = 0;
+        int64_t at = 0;
+        Envelope env{0, 0};
+        if (lane == 0) {
+            Reader r{s, e};
+            const char* p = nullptr;
+            code = envelope_head(r, env, &p);
+            if (code == 1) at = p - s;
+        }
+        code = (int)__builtin_amdgcn_readfirstlane(code);
+        at = (int64_t)uni64((uint64_t)at);
+        int32_t status = JSON_HOST;
+        int64_t count = 0;
+        if (code == 2) {
+            status = JSON_DROPPED;
+        } else if (code == 1) {
+            const char* vs = s + at;
+            const char* vend = nullptr;
+            bool ok = false;
+            if (vs < e && *vs == ']') {  // "values": []
+                ok = true;
+                vend = vs + 1;
+            } else if (vs < e && *vs == '[') {
+                // phase 2 (all lanes): the samples
+                ok = values_array(A, vs, e, A.tmp_v + (ob >> 3), A.tmp_t ? A.tmp_t + (ob >> 3) : nullptr, lane,
+                                  &count, &vend);
+            }
+            // phase 3 (lane 0): the rest of the body
+            if (ok) {
+                int tail_ok = 0;
+                if (lane == 0) {
+                    Reader r{vend, e};
+                    tail_ok = envelope_tail(r, env) ? 1 : 0;
+                }
+                ok = __builtin_amdgcn_readfirstlane(tail_ok) != 0;
+            }
+            if (ok) status = JSON_OK;
+        }
+        if (lane == 0) {
+            A.status[bi] = status;
+            A.counts[bi] = status == JSON_OK ? count : 0;
+        }
+    }
+}
+
+struct CompactArgs {
+    const int64_t* offs;     // body byte offsets (scratch slot = offs[b] / 8)
+    const int64_t* counts;
+    const int32_t* status;
+    const int64_t* out_pos;  // exclusive prefix of counts
+    const double* tmp_v;
+    const double* tmp_t;
+    double* values;
+    double* ts;
+    int64_t n;
+};
+
+// Each kept body's run of values from its scratch slot to its CSR place.
+__global__ __launch_bounds__(256) void k_json_compact(CompactArgs C) {
+    for (int64_t b = blockIdx.x; b < C.n; b += gridDim.x) {
+        if (C.status[b] != JSON_OK) continue;
+        const int64_t n = C.counts[b], src = C.offs[b] >> 3, dst = C.out_pos[b];
+        for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+            C.values[dst + j] = C.tmp_v[src + j];
+            if (C.ts) C.ts[dst + j] = C.tmp_t[src + j];
+        }
+    }
+}
+
+}  // namespace json
+}  // namespace krr

@@ -1,0 +1,570 @@
+// krr_json_parse.h — Prometheus query_range parsing shared by the device packer
+// (krr_json.h, one wave per response body) and its host-compiled checks.
+//
+// What the reference does per pod (robusta_krr/core/integrations/prometheus.py:147-155):
+// keep ONLY data.result[0]["values"], drop a pod whose result list is empty, parse each
+// sample's value string with Decimal().  The host packer (krr_pack.cpp) restates that
+// with a recursive-descent reader and std::from_chars.  This header holds the pieces the
+// device restates it with:
+//   * decimal -> binary64, correctly rounded: Eisel-Lemire over a 128-bit table of
+//     powers of five (krr_pow5.inc, scripts/gen_pow5.py).  With the decimal significand
+//     exact in 64 bits (<= 19 significant digits) the 128-bit product always suffices
+//     (N. Mushtak and D. Lemire, "Fast number parsing without fallback", Software:
+//     Practice and Experience 53(6), 2023), so no big-integer path exists here; a
+//     string with more significant digits is handed back to the host packer.
+//   * one sample element `[<time>,"<value>"]` of the canonical (whitespace-free)
+//     values array Prometheus writes;
+//   * a small JSON reader for the envelope around that array.
+// Contract with the host packer: whatever this code ACCEPTS it parses to exactly the
+// bits krr_pack.cpp produces; anything else (whitespace inside the values array,
+// escapes, "nan"/"infinity" spellings, > 19 digits, status != "success", a malformed
+// body ...) is reported as JSON_HOST and the caller re-parses the batch on the host,
+// which yields the host's own result or error.  So the device never invents an error.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define KRR_JHD __host__ __device__
+#else
+#define KRR_JHD
+#endif
+
+namespace krr {
+namespace json {
+
+enum : int32_t { JSON_OK = 0, JSON_DROPPED = 1, JSON_HOST = 2 };
+enum : int { NUM_OK = 0, NUM_HOST = 1 };
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ static const uint64_t kPow5[] = {
+#include "krr_pow5.inc"
+};
+#else
+static const uint64_t kPow5[] = {
+#include "krr_pow5.inc"
+};
+#endif
+
+KRR_JHD inline uint64_t mul_hi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+KRR_JHD inline int clz64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __clzll((long long)x);
+#else
+    return __builtin_clzll(x);
+#endif
+}
+
+KRR_JHD inline double from_bits(uint64_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double((long long)u);
+#else
+    double d;
+    __builtin_memcpy(&d, &u, 8);
+    return d;
+#endif
+}
+
+// w * 10^q correctly rounded to binary64 (ties to even), w != 0 exact, as IEEE bits
+// without the sign.  Eisel-Lemire (fast_float's compute_float restated).
+KRR_JHD inline uint64_t eisel_lemire(uint64_t w, int64_t q) {
+    if (w == 0 || q < -342) return 0;
+    if (q > 308) return 0x7FF0000000000000ull;
+    const int lz = clz64(w);
+    w <<= lz;
+    const int idx = 2 * (int)(q + 342);
+    uint64_t hi = mul_hi64(w, kPow5[idx]);
+    uint64_t lo = w * kPow5[idx];
+    if ((hi & 0x1FF) == 0x1FF) {  // the 64-bit product leaves the rounding bits unsure
+        const uint64_t hi2 = mul_hi64(w, kPow5[idx + 1]);
+        lo += hi2;
+        if (hi2 > lo) ++hi;
+    }
+    const int upper = (int)(hi >> 63);
+    const int shift = upper + 9;
+    uint64_t m = hi >> shift;
+    // power(q) = floor(q * log2(10)) + 63
+    int32_t p2 = (int32_t)((((152170 + 65536) * (int64_t)q) >> 16) + 63) + upper - lz + 1023;
+    if (p2 <= 0) {  // subnormal (or zero)
+        if (-p2 + 1 >= 64) return 0;
+        m >>= -p2 + 1;
+        m += m & 1;
+        m >>= 1;
+        p2 = m < (1ull << 52) ? 0 : 1;
+        return ((uint64_t)p2 << 52) | (m & ((1ull << 52) - 1));
+    }
+    // an exact halfway case rounds to even (possible only for q in [-4, 23])
+    if (lo <= 1 && q >= -4 && q <= 23 && (m & 3) == 1 && (m << shift) == hi) m &= ~1ull;
+    m += m & 1;
+    m >>= 1;
+    if (m >= (2ull << 52)) {
+        m = 1ull << 52;
+        ++p2;
+    }
+    m &= ~(1ull << 52);
+    if (p2 >= 0x7FF) return 0x7FF0000000000000ull;
+    return ((uint64_t)p2 << 52) | m;
+}
+
+KRR_JHD inline bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
+
+// Digits [p, e) of `int[.frac][(e|E)[+-]exp]` (grammar already checked by the caller,
+// or checked here when `strict_json`) -> IEEE bits of the magnitude.  NUM_HOST when the
+// significand needs more than 19 digits or the exponent more than 6.
+KRR_JHD inline int decimal_bits(const char* p, const char* e, uint64_t* bits) {
+    uint64_t w = 0;
+    int nd = 0;             // significant digits taken into w
+    int64_t drop = 0;       // exponent adjustment: digits not taken (zeros) / fraction digits
+    bool nonzero_lost = false;
+    bool any = false;
+    while (p < e && is_digit((unsigned char)*p)) {
+        const unsigned d = (unsigned)(*p - '0');
+        any = true;
+        if (nd == 0 && d == 0) {
+            // leading zero
+        } else if (nd < 19) {
+            w = w * 10 + d;
+            ++nd;
+        } else {
+            ++drop;  // integer digit beyond 19: scale up
+            if (d) nonzero_lost = true;
+        }
+        ++p;
+    }
+    if (p < e && *p == '.') {
+        ++p;
+        while (p < e && is_digit((unsigned char)*p)) {
+            const unsigned d = (unsigned)(*p - '0');
+            any = true;
+            if (nd == 0 && d == 0) {
+                --drop;  // leading fraction zero
+            } else if (nd < 19) {
+                w = w * 10 + d;
+                ++nd;
+                --drop;
+            } else if (d) {
+                nonzero_lost = true;
+            }
+            ++p;
+        }
+    }
+    if (!any) return NUM_HOST;
+    int64_t ex = 0;
+    if (p < e && (*p == 'e' || *p == 'E')) {
+        ++p;
+        bool eneg = false;
+        if (p < e && (*p == '+' || *p == '-')) {
+            eneg = *p == '-';
+            ++p;
+        }
+        int ne = 0;
+        while (p < e && is_digit((unsigned char)*p)) {
+            ex = ex * 10 + (*p - '0');
+            if (++ne > 6) return NUM_HOST;
+            ++p;
+        }
+        if (ne == 0) return NUM_HOST;
+        if (eneg) ex = -ex;
+    }
+    if (p != e || nonzero_lost) return NUM_HOST;
+    *bits = eisel_lemire(w, drop + ex);
+    return NUM_OK;
+}
+
+// A JSON number (the sample's timestamp), grammar as the host reader's Reader::num:
+// -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?  Returns the end, or nullptr.
+KRR_JHD inline const char* json_number_end(const char* p, const char* e) {
+    if (p < e && *p == '-') ++p;
+    if (p >= e) return nullptr;
+    if (*p == '0') {
+        ++p;
+    } else if (*p >= '1' && *p <= '9') {
+        while (p < e && is_digit((unsigned char)*p)) ++p;
+    } else {
+        return nullptr;
+    }
+    if (p < e && *p == '.') {
+        ++p;
+        if (p >= e || !is_digit((unsigned char)*p)) return nullptr;
+        while (p < e && is_digit((unsigned char)*p)) ++p;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+        ++p;
+        if (p < e && (*p == '+' || *p == '-')) ++p;
+        if (p >= e || !is_digit((unsigned char)*p)) return nullptr;
+        while (p < e && is_digit((unsigned char)*p)) ++p;
+    }
+    return p;
+}
+
+KRR_JHD inline int json_number_value(const char* b, const char* e, double* out) {
+    const bool neg = *b == '-';
+    uint64_t bits;
+    if (decimal_bits(b + (neg ? 1 : 0), e, &bits) != NUM_OK) return NUM_HOST;
+    *out = from_bits(bits | (neg ? 0x8000000000000000ull : 0));
+    return NUM_OK;
+}
+
+// A sample value string (between the quotes) -> float64, as krr_pack.cpp parse_value:
+// an optional sign, then std::from_chars' decimal form.  Accepted here: digits with an
+// optional fraction and exponent, "NaN" and "Inf" (Prometheus' spellings); the host
+// decides every other spelling.
+KRR_JHD inline int value_bits(const char* b, const char* e, double* out) {
+    bool neg = false;
+    if (b < e && (*b == '+' || *b == '-')) {
+        neg = *b == '-';
+        ++b;
+    }
+    if (b >= e) return NUM_HOST;
+    const uint64_t sign = neg ? 0x8000000000000000ull : 0;
+    if (e - b == 3 && b[0] == 'N' && b[1] == 'a' && b[2] == 'N') {
+        *out = from_bits(0x7FF8000000000000ull | sign);
+        return NUM_OK;
+    }
+    if (e - b == 3 && b[0] == 'I' && b[1] == 'n' && b[2] == 'f') {
+        *out = from_bits(0x7FF0000000000000ull | sign);
+        return NUM_OK;
+    }
+    if (!is_digit((unsigned char)*b)) return NUM_HOST;  // ".5", "inf", a second sign: the host's call
+    // digits [. digits] [e [+-] digits] — a fraction needs a digit after the point
+    const char* p = b;
+    while (p < e && is_digit((unsigned char)*p)) ++p;
+    if (p < e && *p == '.') {
+        ++p;
+        if (p >= e || !is_digit((unsigned char)*p)) return NUM_HOST;
+        while (p < e && is_digit((unsigned char)*p)) ++p;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+        ++p;
+        if (p < e && (*p == '+' || *p == '-')) ++p;
+        if (p >= e || !is_digit((unsigned char)*p)) return NUM_HOST;
+        while (p < e && is_digit((unsigned char)*p)) ++p;
+    }
+    if (p != e) return NUM_HOST;
+    uint64_t bits;
+    if (decimal_bits(b, e, &bits) != NUM_OK) return NUM_HOST;
+    *out = from_bits(bits | sign);
+    return NUM_OK;
+}
+
+// One element of a canonical values array at p (which must be '['):
+// `[<json number>,"<value>"]` followed by ',' + '[' (more follow) or ']' (the last one).
+// On success: *next = the following element's '[' or one past the array's ']', *last set.
+// Returns false for anything else (the caller hands the body to the host).
+template <class Load>
+KRR_JHD inline bool sample_element(const char* p, const char* e, bool want_ts, double* value, double* ts,
+                                   const char** next, bool* last, Load ld) {
+    if (p >= e || ld(p) != '[') return false;
+    ++p;
+    // timestamp
+    const char* tb = p;
+    {
+        if (p < e && ld(p) == '-') ++p;
+        if (p >= e) return false;
+        const char c0 = ld(p);
+        if (c0 == '0') {
+            ++p;
+        } else if (c0 >= '1' && c0 <= '9') {
+            while (p < e && is_digit((unsigned char)ld(p))) ++p;
+        } else {
+            return false;
+        }
+        if (p < e && ld(p) == '.') {
+            ++p;
+            if (p >= e || !is_digit((unsigned char)ld(p))) return false;
+            while (p < e && is_digit((unsigned char)ld(p))) ++p;
+        }
+        if (p < e && (ld(p) == 'e' || ld(p) == 'E')) {
+            ++p;
+            if (p < e && (ld(p) == '+' || ld(p) == '-')) ++p;
+            if (p >= e || !is_digit((unsigned char)ld(p))) return false;
+            while (p < e && is_digit((unsigned char)ld(p))) ++p;
+        }
+    }
+    const char* te = p;
+    if (p + 1 >= e || ld(p) != ',' || ld(p + 1) != '"') return false;
+    p += 2;
+    const char* vb = p;
+    while (p < e) {
+        const unsigned char c = (unsigned char)ld(p);
+        if (c == '"') break;
+        if (c == '\\' || c < 0x20) return false;
+        ++p;
+    }
+    if (p + 2 >= e || ld(p + 1) != ']') return false;
+    const char* ve = p;
+    p += 2;
+    const char d = ld(p);
+    if (d == ',') {
+        if (p + 1 >= e || ld(p + 1) != '[') return false;
+        *last = false;
+        *next = p + 1;
+    } else if (d == ']') {
+        *last = true;
+        *next = p + 1;
+    } else {
+        return false;
+    }
+    if (value_bits(vb, ve, value) != NUM_OK) return false;
+    if (want_ts && json_number_value(tb, te, ts) != NUM_OK) return false;
+    return true;
+}
+
+// ---- the envelope: a small JSON reader ----------------------------------------
+// Keys and the status value may not hold escapes here (the host decides those).
+struct Reader {
+    const char* p;
+    const char* e;
+
+    KRR_JHD void ws() {
+        while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+    }
+    KRR_JHD bool lit(char c) {
+        ws();
+        if (p < e && *p == c) {
+            ++p;
+            return true;
+        }
+        return false;
+    }
+    KRR_JHD bool peek(char c) {
+        ws();
+        return p < e && *p == c;
+    }
+    // A string; [*b, *n) = its raw bytes; *esc: it holds escapes.  Grammar as the host's.
+    KRR_JHD bool str(const char** b, int64_t* n, bool* esc) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        const char* s = ++p;
+        bool any = false;
+        while (p < e && *p != '"') {
+            const unsigned char c = (unsigned char)*p;
+            if (c < 0x20) return false;
+            if (c == '\\') {
+                any = true;
+                if (++p >= e) return false;
+                if (*p == 'u') {
+                    if (e - p < 5) return false;
+                    for (int k = 1; k <= 4; ++k) {
+                        const char h = p[k];
+                        if (!((h >= '0' && h <= '9') || (h >= 'a' && h <= 'f') || (h >= 'A' && h <= 'F'))) return false;
+                    }
+                    p += 4;
+                } else {
+                    const char c2 = *p;
+                    if (!(c2 == '"' || c2 == '\\' || c2 == '/' || c2 == 'b' || c2 == 'f' || c2 == 'n' || c2 == 'r' ||
+                          c2 == 't'))
+                        return false;
+                }
+            }
+            ++p;
+        }
+        if (p >= e) return false;
+        if (b) *b = s;
+        if (n) *n = p - s;
+        if (esc) *esc = any;
+        ++p;
+        return true;
+    }
+    // A key equal to k (no escapes): 1; another key without escapes: 0; escapes or a
+    // malformed key: -1 (the host's call).
+    KRR_JHD int key(const char* k) {
+        const char* b;
+        int64_t n;
+        bool esc;
+        if (!str(&b, &n, &esc) || esc) return -1;
+        if (!lit(':')) return -1;
+        int64_t i = 0;
+        for (; k[i]; ++i)
+            if (i >= n || b[i] != k[i]) return 0;
+        return i == n ? 1 : 0;
+    }
+    KRR_JHD bool word(const char* w) {
+        ws();
+        int64_t n = 0;
+        while (w[n]) ++n;
+        if (e - p < n) return false;
+        for (int64_t i = 0; i < n; ++i)
+            if (p[i] != w[i]) return false;
+        p += n;
+        return true;
+    }
+    // Skip one JSON value, validating it (iterative: an explicit stack of up to 256
+    // open containers, the host reader's depth bound).
+    KRR_JHD bool skip() {
+        uint64_t stk[5] = {0, 0, 0, 0, 0};  // bit d: container d is an object
+        int d = 0;
+        for (;;) {
+            // a value
+            ws();
+            if (p >= e || d > 256) return false;
+            const char c = *p;
+            bool opened = false;
+            if (c == '{' || c == '[') {
+                ++p;
+                const bool obj = c == '{';
+                if (obj) stk[d >> 6] |= 1ull << (d & 63);
+                else stk[d >> 6] &= ~(1ull << (d & 63));
+                ++d;
+                if (lit(obj ? '}' : ']')) {
+                    --d;
+                } else {
+                    if (obj && (!str(nullptr, nullptr, nullptr) || !lit(':'))) return false;
+                    opened = true;
+                }
+            } else if (c == '"') {
+                if (!str(nullptr, nullptr, nullptr)) return false;
+            } else if (c == 't') {
+                if (!word("true")) return false;
+            } else if (c == 'f') {
+                if (!word("false")) return false;
+            } else if (c == 'n') {
+                if (!word("null")) return false;
+            } else {
+                const char* q = json_number_end(p, e);
+                if (!q) return false;
+                p = q;
+            }
+            if (opened) continue;  // its first member / element
+            // after a value: close containers or move to the next member / element
+            for (;;) {
+                if (d == 0) return true;
+                const bool obj = (stk[(d - 1) >> 6] >> ((d - 1) & 63)) & 1;
+                if (lit(',')) {
+                    if (obj && (!str(nullptr, nullptr, nullptr) || !lit(':'))) return false;
+                    break;
+                }
+                if (!lit(obj ? '}' : ']')) return false;
+                --d;
+            }
+        }
+    }
+};
+
+// Where the envelope parse stands when it reaches result[0]'s "values" array.
+struct Envelope {
+    int32_t have_status, ok_status;
+};
+
+// From the body start to just inside result[0]["values"]'s '[' (returns 1, *at = that
+// position), or through the whole body when the result list is empty (returns 2: a
+// dropped pod, everything validated), or 0: the host decides.
+KRR_JHD inline int envelope_head(Reader& r, Envelope& env, const char** at) {
+    env.have_status = env.ok_status = 0;
+    bool have_result = false, dropped = false;
+    if (!r.lit('{') || r.peek('}')) return 0;
+    for (;;) {
+        const char* kb;
+        int64_t kn;
+        bool kesc;
+        if (!r.str(&kb, &kn, &kesc) || kesc || !r.lit(':')) return 0;
+        const bool is_status = kn == 6 && kb[0] == 's' && kb[1] == 't' && kb[2] == 'a' && kb[3] == 't' &&
+                               kb[4] == 'u' && kb[5] == 's';
+        const bool is_data = kn == 4 && kb[0] == 'd' && kb[1] == 'a' && kb[2] == 't' && kb[3] == 'a';
+        if (is_status) {
+            const char* vb;
+            int64_t vn;
+            bool vesc;
+            if (!r.str(&vb, &vn, &vesc) || vesc) return 0;
+            env.have_status = 1;
+            env.ok_status = vn == 7 && vb[0] == 's' && vb[1] == 'u' && vb[2] == 'c' && vb[3] == 'c' && vb[4] == 'e' &&
+                            vb[5] == 's' && vb[6] == 's';
+        } else if (is_data) {
+            if (have_result || dropped || !r.lit('{')) return 0;
+            if (!r.lit('}')) {
+                for (;;) {
+                    const int k = r.key("result");
+                    if (k < 0) return 0;
+                    if (k == 0) {
+                        if (!r.skip()) return 0;
+                    } else {
+                        if (have_result || !r.lit('[')) return 0;
+                        have_result = true;
+                        if (r.lit(']')) {
+                            dropped = true;
+                        } else {
+                            if (!r.lit('{') || r.peek('}')) return 0;
+                            for (;;) {
+                                const int sk = r.key("values");
+                                if (sk < 0) return 0;
+                                if (sk == 1) {
+                                    if (!r.lit('[')) return 0;
+                                    *at = r.p;
+                                    return 1;
+                                }
+                                if (!r.skip() || !r.lit(',')) return 0;  // no "values" in result[0]: host
+                            }
+                        }
+                    }
+                    if (r.lit(',')) continue;
+                    if (!r.lit('}')) return 0;
+                    break;
+                }
+            }
+        } else if (!r.skip()) {
+            return 0;
+        }
+        if (r.lit(',')) continue;
+        if (!r.lit('}')) return 0;
+        break;
+    }
+    r.ws();
+    if (r.p != r.e || !dropped || !env.have_status || !env.ok_status) return 0;
+    return 2;
+}
+
+// From one past the values array's ']' to the end of the body: the rest of result[0],
+// further series (validated, never read), the rest of data and of the response.
+KRR_JHD inline bool envelope_tail(Reader& r, Envelope env) {
+    // rest of result[0]
+    while (r.lit(',')) {
+        const int k = r.key("values");
+        if (k != 0 || !r.skip()) return false;  // a second "values": the host's call
+    }
+    if (!r.lit('}')) return false;
+    // further series
+    while (r.lit(','))
+        if (!r.skip()) return false;
+    if (!r.lit(']')) return false;
+    // rest of data
+    while (r.lit(',')) {
+        const int k = r.key("result");
+        if (k != 0 || !r.skip()) return false;
+    }
+    if (!r.lit('}')) return false;
+    // rest of the response
+    while (r.lit(',')) {
+        const char* kb;
+        int64_t kn;
+        bool kesc;
+        if (!r.str(&kb, &kn, &kesc) || kesc || !r.lit(':')) return false;
+        const bool is_status = kn == 6 && kb[0] == 's' && kb[1] == 't' && kb[2] == 'a' && kb[3] == 't' &&
+                               kb[4] == 'u' && kb[5] == 's';
+        const bool is_data = kn == 4 && kb[0] == 'd' && kb[1] == 'a' && kb[2] == 't' && kb[3] == 'a';
+        if (is_data) return false;
+        if (is_status) {
+            const char* vb;
+            int64_t vn;
+            bool vesc;
+            if (!r.str(&vb, &vn, &vesc) || vesc) return false;
+            env.have_status = 1;
+            env.ok_status = vn == 7 && vb[0] == 's' && vb[1] == 'u' && vb[2] == 'c' && vb[3] == 'c' && vb[4] == 'e' &&
+                            vb[5] == 's' && vb[6] == 's';
+        } else if (!r.skip()) {
+            return false;
+        }
+    }
+    if (!r.lit('}')) return false;
+    r.ws();
+    return r.p == r.e && env.have_status && env.ok_status;
+}
+
+}  // namespace json
+}  // namespace krr

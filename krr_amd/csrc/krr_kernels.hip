@@ -29,6 +29,7 @@
 #include "krr_amd.h"
 #include "krr_device.h"
 #include "krr_plan.h"
+#include "krr_json.h"
 
 #ifndef KRR_STREAM_DEPTH
 #define KRR_STREAM_DEPTH 2  // chunks in flight per wave
@@ -4021,6 +4022,43 @@ int krr_get_stats(krr_ctx* ctx, int64_t* wselect_fallbacks) {
     KRR_HIP(ctx, hipDeviceSynchronize());
     KRR_HIP(ctx, hipMemcpy(&h, ctx->d_tmp + 1, sizeof(h), hipMemcpyDeviceToHost));
     *wselect_fallbacks = (int64_t)h;
+    return KRR_OK;
+}
+
+int krr_json_parse(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, int32_t want_timestamps,
+                   double* scratch_values, double* scratch_ts, int64_t* counts, int32_t* status, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!b || b->n_bodies < 0 || first < 0 || n < 0 || first + n > b->n_bodies)
+        return set_err(ctx, KRR_E_INVALID, "json: bad body range%s", "");
+    if (n == 0) return KRR_OK;
+    if (!b->bodies || !b->body_offsets || !scratch_values || !counts || !status || (want_timestamps && !scratch_ts))
+        return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    if (((uintptr_t)b->bodies & 15) != 0) return set_err(ctx, KRR_E_INVALID, "json: bodies not 16-byte aligned%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    json::JsonArgs A{b->bodies, b->body_offsets, first, n, want_timestamps ? 1 : 0, scratch_values,
+                     want_timestamps ? scratch_ts : nullptr, counts, status};
+    hipLaunchKernelGGL(json::k_json_parse, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scratch_values,
+                     const double* scratch_ts, const int64_t* counts, const int32_t* status,
+                     const int64_t* out_pos, double* values, double* timestamps, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!b || b->n_bodies < 0) return set_err(ctx, KRR_E_INVALID, "json: bad bodies%s", "");
+    if (b->n_bodies == 0) return KRR_OK;
+    if (!b->body_offsets || !scratch_values || !counts || !status || !out_pos || !values ||
+        (timestamps && !scratch_ts))
+        return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    json::CompactArgs C{b->body_offsets, counts, status, out_pos, scratch_values, timestamps ? scratch_ts : nullptr,
+                        values, timestamps, b->n_bodies};
+    const int64_t grid = b->n_bodies < 65536 ? b->n_bodies : 65536;
+    hipLaunchKernelGGL(json::k_json_compact, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, C);
+    KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
 

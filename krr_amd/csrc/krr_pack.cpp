@@ -722,4 +722,18 @@ const char* krr_series_error(const krr_series_set* h) { return h ? h->set.err.c_
 
 void krr_series_free(krr_series_set* h) { delete h; }
 
+int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                    const int64_t* dst_offsets, char* dst, int32_t threads) {
+    if (n_bodies < 0 || (n_bodies > 0 && (!bodies || !body_lens || !dst_offsets || !dst))) return KRR_PACK_E_INVALID;
+    for (int64_t b = 0; b < n_bodies; ++b)
+        if (body_lens[b] < 0 || (body_lens[b] > 0 && !bodies[b]) ||
+            dst_offsets[b + 1] - dst_offsets[b] != body_lens[b])
+            return KRR_PACK_E_INVALID;
+    const int64_t base = n_bodies > 0 ? dst_offsets[0] : 0;
+    parallel_for(n_bodies, threads, [&](int64_t b) {
+        if (body_lens[b]) memcpy(dst + (dst_offsets[b] - base), bodies[b], (size_t)body_lens[b]);
+    });
+    return KRR_PACK_OK;
+}
+
 }  // extern "C"

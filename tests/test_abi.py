@@ -61,6 +61,8 @@ def test_abi_version_and_null_handling(lib):
     assert lib.krr_segmented_percentile(None, None, None, None, None, None, None) == -1
     assert lib.krr_segmented_max(None, None, None, None, None, None) == -1
     assert lib.krr_destroy(None) == 0
+    assert lib.krr_json_parse(None, None, 0, 0, 0, None, None, None, None, None) == -1
+    assert lib.krr_json_compact(None, None, None, None, None, None, None, None, None, None) == -1
     h = ctypes.c_void_p()
     assert lib.krr_create(0, None) == -1
 
@@ -71,6 +73,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.KrrSeries) == 8 * 5 + 4 * 2
     assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 3
     assert ctypes.sizeof(_native.KrrSketchLoc) == 8 * 5 + 4 * 4 and _native.LOC_WORDS == 7
+    assert ctypes.sizeof(_native.KrrJsonBodies) == 8 * 4
 
 
 def _declared_host():

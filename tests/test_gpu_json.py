@@ -1,0 +1,176 @@
+"""Device packer (include/krr_amd.h krr_json_parse / krr_json_compact, krr_amd/csrc/krr_json.h)
+against the host packer (krr_pack_parse, itself pinned to json + Decimal by
+tests/test_prom_native.py): values, offsets, pod drops and timestamps bit for bit.
+
+Canonical bodies (what Prometheus writes: compact JSON) must be parsed on the device
+(``via == "device"``); a batch holding a body outside that form goes to the host packer
+and gives exactly the host's result or error."""
+import json
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def packer():
+    from krr_amd import _native
+    from krr_amd.core.device_pack import DevicePacker
+
+    ctx = _native.Context(0)
+    yield DevicePacker(ctx, chunk_bytes=1 << 20)
+    ctx.close()
+
+
+def _compact(doc) -> bytes:
+    return json.dumps(doc, separators=(",", ":")).encode()
+
+
+def _host(per_obj, want_ts=True):
+    from krr_amd.core.prom_native import pack_query_range_bodies
+
+    return pack_query_range_bodies(per_obj, want_timestamps=want_ts, return_pod_counts=True)
+
+
+def _same(dp, per_obj, want_ts=True):
+    ps, ts, counts = _host(per_obj, want_ts)
+    got = dp.series
+    v = got.values.cpu().numpy() if hasattr(got.values, "cpu") else got.values
+    o = got.offsets.cpu().numpy() if hasattr(got.offsets, "cpu") else got.offsets
+    assert np.array_equal(o, ps.offsets)
+    assert np.array_equal(v.view(np.uint64), ps.values.view(np.uint64))
+    assert got.max_len == ps.max_len
+    pc = dp.pod_counts.cpu().numpy() if hasattr(dp.pod_counts, "cpu") else dp.pod_counts
+    assert np.array_equal(pc, counts)
+    if want_ts:
+        t = dp.timestamps.cpu().numpy() if hasattr(dp.timestamps, "cpu") else dp.timestamps
+        assert np.array_equal(t.view(np.uint64), ts.view(np.uint64))
+
+
+def _fleet(seed, n_obj=80, max_samples=3000):
+    from krr_amd.utils.prom_decimal import prom_format
+
+    rng = np.random.default_rng(seed)
+    per_obj = []
+    for o in range(n_obj):
+        pods = []
+        for p in range(int(rng.integers(0, 5))):
+            if rng.random() < 0.12:
+                pods.append(_compact({"status": "success", "data": {"resultType": "matrix", "result": []}}))
+                continue
+            n = int(rng.integers(0, max_samples))
+            xs = rng.gamma(2.0, 0.05, n)
+            sp = rng.random(n)
+            xs[sp < 0.01] = np.nan
+            xs[(sp >= 0.01) & (sp < 0.015)] = np.inf
+            xs[(sp >= 0.015) & (sp < 0.02)] = -np.inf
+            m = (sp >= 0.02) & (sp < 0.1)
+            xs[m] = np.floor(rng.normal(2e8, 2e7, int(m.sum())))
+            m = (sp >= 0.1) & (sp < 0.105)
+            xs[m] = 1e-300 * rng.random(int(m.sum()))
+            m = (sp >= 0.105) & (sp < 0.11)
+            xs[m] = 1e300 * rng.random(int(m.sum()))  # 300-digit strings: elements longer than a block's lane
+            ts = 1.7e9 + 60.0 * np.arange(n) + 0.781
+            res = [{"metric": {"pod": f"p{o}-{p}", "container": "c"},
+                    "values": [[float(t), prom_format(float(x))] for t, x in zip(ts, xs)]}]
+            if rng.random() < 0.3:
+                res.append({"metric": {"pod": "x"}, "values": [[1.0, "7"]]})
+            pods.append(_compact({"status": "success", "data": {"resultType": "matrix", "result": res}}))
+        per_obj.append(pods)
+    return per_obj
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_canonical_fleet_parsed_on_device(packer, seed):
+    per_obj = _fleet(seed)
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "device" and dp.host_bodies == 0
+    _same(dp, per_obj)
+
+
+def test_prom_native_vectors_compacted(packer):
+    """tests/test_prom_native.py's fleet (escaped label values, non-ASCII keys, extra
+    series, NaN/Inf, subnormals), re-serialised compactly as Prometheus writes it."""
+    from test_prom_native import _fleet as pn_fleet
+
+    per_obj = [[json.dumps(json.loads(b), separators=(",", ":")).encode() for b in bodies]
+               for bodies in pn_fleet(1)]
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "device"
+    _same(dp, per_obj)
+
+
+def test_prom_native_vectors_as_is_go_to_the_host(packer):
+    """The same vectors as json.dumps writes them (spaces inside the values array): the
+    device hands the batch to the host packer, and the result is the host's."""
+    from test_prom_native import _fleet as pn_fleet
+
+    per_obj = pn_fleet(1)
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "host" and dp.host_bodies > 0
+    _same(dp, per_obj)
+
+
+def test_config2_sized_bodies_many_chunks(packer):
+    """10,080-sample bodies (7d@1m), many per chunk and chunks of 1 MiB: the staged copy /
+    parse pipeline and the block loop over long values arrays."""
+    from krr_amd.utils.prom_decimal import prom_format
+
+    rng = np.random.default_rng(5)
+    per_obj = []
+    for o in range(40):
+        pods = []
+        for p in range(3):
+            xs = rng.gamma(2.0, 0.05, 10080)
+            vals = ",".join(f'[{1700000000 + 60 * i},"{prom_format(float(x))}"]' for i, x in enumerate(xs))
+            pods.append(('{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},"values":['
+                         + vals + ']}]}}').encode())
+        per_obj.append(pods)
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "device"
+    _same(dp, per_obj)
+
+
+@pytest.mark.parametrize("bad", [b'{"status":"error","errorType":"bad_data","error":"x"}', b'{"status":"success"',
+                                 b'not json'])
+def test_error_bodies_raise_the_host_error(packer, bad):
+    from krr_amd.core.prom_native import PrometheusResponseError
+
+    per_obj = _fleet(3, n_obj=10)
+    per_obj[4] = per_obj[4] + [bad]
+    with pytest.raises(PrometheusResponseError) as dev_err:
+        packer.pack(per_obj)
+    with pytest.raises(PrometheusResponseError) as host_err:
+        _host(per_obj)
+    assert str(dev_err.value) == str(host_err.value) and dev_err.value.code == host_err.value.code
+
+
+def test_empty_and_odd_layouts(packer):
+    per_obj = [[], [_compact({"status": "success", "data": {"result": [{"metric": {}, "values": []}]}})],
+               [_compact({"data": {"result": [{"values": [[1, "1"], [2, "2"]], "metric": {"a": "b"}}],
+                                   "resultType": "matrix"}, "status": "success", "warnings": ["w"]})],
+               []]
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "device"
+    _same(dp, per_obj)
+    dp = packer.pack([], want_timestamps=False, return_pod_counts=True)
+    assert dp.series.offsets.numel() == 1
+
+
+def test_recommend_from_bodies_device_equals_host():
+    """The whole path from bodies: device parse -> kernel -> rounding equals the host
+    packer's path, result for result."""
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    cpu = _fleet(7, n_obj=60, max_samples=2000)
+    mem = _fleet(8, n_obj=60, max_samples=2000)
+    # memory bodies without NaN (the reference raises on a NaN memory sample)
+    mem = [[b.replace(b'"NaN"', b'"1"') for b in bodies] for bodies in mem]
+    runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(cpu_percentile="99", memory_buffer_percentage="5")))
+    a = runner.recommend_from_bodies(cpu, mem, parser="device")
+    assert runner.last_pack_via == ("device", "device")
+    b = runner.recommend_from_bodies(cpu, mem, parser="host")
+    assert [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in a] == \
+           [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in b]

@@ -163,3 +163,82 @@ def test_gaps_nan_and_empty(ctx, mode, lens):
     c[offs[4] + 1234] = np.nan  # a real NaN sample: KRR_FLAG_NAN
     got, _ = _run(ctx, c, offs, mode, 50, 1, gaps=False)
     _check(got, c, offs, mode, 50, 1, False, "compact with a NaN")
+
+
+def _missing_fleet(L, rng, copies=6):
+    """Short segments (the 16-waves/CU window kernel, whose misses go through the separate
+    miss list + k_hselect_list) that the window cannot hold: monotone trends and regime
+    changes, interleaved with exchangeable series that do not miss."""
+    segs = []
+    for _ in range(copies):
+        segs.append(np.arange(L, dtype=np.float64) + rng.random())           # increasing
+        r = rng.random(L)
+        r[int(0.6 * L):] += 10.0
+        segs.append(r)                                                      # regime change
+        segs.append(rng.gamma(2.0, 0.05, size=L))                            # exchangeable
+    return np.concatenate(segs), (np.arange(len(segs) + 1) * L).astype(np.int64)
+
+
+@pytest.mark.parametrize("mode", ["sorted_lower", "linear"])
+@pytest.mark.parametrize("L", [20160, 7000])
+def test_short_segment_miss_list_across_consecutive_launches(ctx, mode, L):
+    """The miss-list path (segments < 32,768 slots): every launch misses some segments, and
+    consecutive launches on one ctx alternate between the list's two counters (launch k
+    zeroes launch k-1's) — five launches in a row, different data and percentiles each
+    time, no sync in between; every one exact against the oracle and every one with misses."""
+    import torch
+
+    from krr_amd import _native
+
+    rng = np.random.default_rng(L + MODES[mode])
+    dev = torch.device("cuda:0")
+    runs = []
+    before = ctx.wselect_fallbacks()
+    for i, pct in enumerate([(50, 1), (40, 1), (60, 1), (50, 1), (35, 1)]):
+        vals, offs = _missing_fleet(L, rng)
+        S = offs.size - 1
+        dv = torch.from_numpy(vals).to(dev)
+        do = torch.from_numpy(offs).to(dev)
+        ser = ctx.series(dv, do, L, False)
+        prm = _native.KrrPercentileParams(MODES[mode], 0, pct[0], pct[1], pct[0] / pct[1] / 100.0)
+        out = [torch.empty(S, dtype=dt, device=dev) for dt in (torch.float64, torch.int64, torch.int32)]
+        ctx.segmented_percentile(ser, prm, *out)
+        runs.append((vals, offs, pct, out, dv, do, ser))
+    torch.cuda.synchronize()
+    total = ctx.wselect_fallbacks() - before
+    assert total >= 5 * 2, f"only {total} misses over 5 launches of trend / regime-change series"
+    for vals, offs, pct, out, *_ in runs:
+        got = (out[0].cpu().numpy(), out[1].cpu().numpy(), out[2].cpu().numpy().astype(np.uint32))
+        _check(got, vals, offs, mode, *pct, False, f"L={L} p={pct}")
+
+
+def test_two_streams_share_one_ctx(ctx):
+    """One ctx, window launches with misses on two streams, issued back to back with no
+    host sync: the miss list and its counters are shared, so a launch on the other stream
+    waits for the previous launch's miss pass (the ctx's event) — both results exact."""
+    import torch
+
+    from krr_amd import _native
+
+    rng = np.random.default_rng(5)
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    runs = []
+    for i in range(6):
+        L = (20160, 7000)[i % 2]
+        vals, offs = _missing_fleet(L, rng, copies=4)
+        S = offs.size - 1
+        st = streams[i % 2]
+        with torch.cuda.stream(st):
+            dv = torch.from_numpy(vals).to(dev, non_blocking=False)
+            do = torch.from_numpy(offs).to(dev, non_blocking=False)
+            out = [torch.empty(S, dtype=dt, device=dev) for dt in (torch.float64, torch.int64, torch.int32)]
+        st.synchronize()  # inputs in place; the launches below are not synchronised with each other
+        runs.append((vals, offs, out, dv, do, st, ctx.series(dv, do, L, False)))
+    for i, (vals, offs, out, dv, do, st, ser) in enumerate(runs):
+        prm = _native.KrrPercentileParams(MODES["linear"], 0, 50, 1, 0.5)
+        ctx.segmented_percentile(ser, prm, *out, st)
+    torch.cuda.synchronize()
+    for vals, offs, out, *_ in runs:
+        got = (out[0].cpu().numpy(), out[1].cpu().numpy(), out[2].cpu().numpy().astype(np.uint32))
+        _check(got, vals, offs, "linear", 50, 1, False, "two streams")
