@@ -96,6 +96,10 @@ def parse():
                          "memory (host) or into HBM followed by a D2H copy (device)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N > 1 path (process group + pipelined RCCL gather) even with one rank (testing)")
+    ap.add_argument("--c5-chunk-gib", type=float, default=3.0,
+                    help="config 5 at N = 1 (direct): series per launch, in GiB of values, each chunk in buffers "
+                         "of its own; 2-4 GiB streamed at 83-85%% of peak, 8 GiB at 82%%, 16-32 GiB at 81-82%%, "
+                         "one 138-GB buffer at 77%% (profiles/r03/f, profiles/r03/g)")
     ap.add_argument("--chunk-gib", type=float, default=8.0,
                     help="fleets of more than twice this many GiB of values per resource run as chunks of "
                          "about this size, in buffers of their own, one launch per chunk")
@@ -734,8 +738,11 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
       config-1-shaped bodies (objects x pods x 10,080 samples, both resources), the lease's
       threads — the reference's loader does this with json + Decimal(value)
       (robusta_krr/core/integrations/prometheus.py:150-155);
-    * e2e_objects_per_s: BatchedRunner.recommend_from_bodies on the same bodies: pack ->
-      H2D -> fused kernel -> exact-decimal rounding -> RunResults.
+    * device_pack_samples_per_s: the device packer (krr_amd.core.device_pack: bodies staged,
+      copied to HBM raw and parsed there, one wave per body) on the same bodies;
+    * e2e_objects_per_s: BatchedRunner.recommend_from_bodies on the same bodies (device
+      parse -> fused kernel -> exact-decimal rounding -> RunResults); e2e_objects_per_s_host_parse
+      the same with the host packer.
     Bodies are Prometheus-formatted (shortest-repr sample strings); `distinct` random pod
     series per resource are reused across the fleet (the packer's cost is per byte)."""
     import torch
@@ -789,24 +796,47 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         best = min(best, time.perf_counter() - t0)
     out["pack_samples_per_s"] = samples / best
     runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(cpu_percentile=99, memory_buffer_percentage=5)))
-    runner.recommend_from_bodies(cpu_b[:8], mem_b[:8], threads=threads)  # warm-up (context, modules)
-    best_e = float("inf")
-    for _ in range(2):
+    e2e = {}
+    for parser in ("host", "device"):
+        runner.recommend_from_bodies(cpu_b[:8], mem_b[:8], threads=threads, parser=parser)  # warm-up
+        best_e = float("inf")
+        for _ in range(3 if parser == "device" else 2):
+            t0 = time.perf_counter()
+            res = runner.recommend_from_bodies(cpu_b, mem_b, threads=threads, parser=parser)
+            best_e = min(best_e, time.perf_counter() - t0)
+        assert len(res) == objects
+        e2e[parser] = (best_e, [(str(r[k].request), str(r[k].limit)) for r in res[:64] for k in r])
+    assert runner.last_pack_via == ("device", "device"), runner.last_pack_via
+    out["e2e_objects_per_s"] = objects / e2e["device"][0]
+    out["e2e_objects_per_s_host_parse"] = objects / e2e["host"][0]
+    out["e2e_device_equals_host"] = e2e["device"][1] == e2e["host"][1]
+    # the device packer alone: staging copy -> H2D -> parse -> CSR in HBM, both resources
+    from krr_amd.core.device_pack import default_packer
+    from krr_amd.core.engine import default_engine
+
+    packer = default_packer(default_engine(dev.index or 0).context())
+    best_d = float("inf")
+    for _ in range(3):
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        res = runner.recommend_from_bodies(cpu_b, mem_b, threads=threads)
-        best_e = min(best_e, time.perf_counter() - t0)
-    assert len(res) == objects
-    out["e2e_objects_per_s"] = objects / best_e
+        packer.pack(cpu_b)
+        packer.pack(mem_b)
+        torch.cuda.synchronize()
+        best_d = min(best_d, time.perf_counter() - t0)
+    out["device_pack_samples_per_s"] = samples / best_d
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",
         "bodies": f"{objects} objects x {pods} pods x {L} samples x 2 resources = {samples} samples, "
                   f"{json_bytes / 1e9:.2f} GB of query_range JSON ({distinct} distinct pod series per resource, "
                   f"generated in {t_g:.1f} s)",
-        "pack_s": best, "e2e_s": best_e, "threads": threads,
-        "pack_GBps_json": json_bytes / best / 1e9,
-        "definition": "pack = krr_pack_parse/copy of every body (CPU + memory); e2e = "
-                      "BatchedRunner.recommend_from_bodies: pack -> H2D -> fused kernel -> native exact-decimal "
-                      "rounding -> RunResults (best of 2)"}
+        "pack_s": best, "device_pack_s": best_d, "e2e_s": e2e["device"][0], "e2e_host_parse_s": e2e["host"][0],
+        "threads": threads,
+        "pack_GBps_json": json_bytes / best / 1e9, "device_pack_GBps_json": json_bytes / best_d / 1e9,
+        "definition": "pack = krr_pack_parse/copy of every body on the host (CPU + memory); device_pack = "
+                      "krr_amd.core.device_pack: staging copy into page-locked memory -> H2D -> krr_json_parse "
+                      "(one wave per body) -> CSR in HBM; e2e = BatchedRunner.recommend_from_bodies (default "
+                      "parser='device'; e2e_host_parse: parser='host'): pack -> fused kernel -> native "
+                      "exact-decimal rounding -> RunResults (best of 2-3)"}
     return out
 
 
@@ -928,7 +958,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     method = "direct" if direct else (args.c5_method if exact else "sketch-only")
     # the direct pass over 138 GB runs per chunk of series in buffers of their own (as
     # configs 2-4, fleet_chunks); the time-sharded paths keep one buffer per rank
-    chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.chunk_gib) if direct else [(0, S)]
+    chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.c5_chunk_gib) if direct else [(0, S)]
     phase("synth")
     parts = []
     for lo, hi in chunks:

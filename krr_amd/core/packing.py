@@ -36,7 +36,7 @@ class PackedSeries:
 
     @property
     def n_segments(self) -> int:
-        return int(self.offsets.size - 1)
+        return len(self.offsets) - 1  # numpy array, or a torch tensor in HBM (device packer)
 
     def segment(self, s: int) -> np.ndarray:
         return self.values[self.offsets[s]:self.offsets[s + 1]]

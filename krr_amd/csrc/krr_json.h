@@ -28,6 +28,7 @@ namespace json {
 constexpr int kLaneBytes = 32;                  // bytes of a block each lane scans for '['
 constexpr int kBlockBytes = kLaneBytes * kWave;  // 2 KiB per block
 constexpr int kMaxPerLane = 4;                   // an element spans >= 8 bytes: <= 4 start in 32
+constexpr int kStageBytes = 2 * kBlockBytes;     // LDS copy: the block and the next one
 
 struct JsonArgs {
     const char* bodies;      // device: the bodies back to back (16-B aligned base)
@@ -43,56 +44,97 @@ struct JsonArgs {
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
-struct ByteLoad {
-    __device__ char operator()(const char* p) const { return *p; }
-};
-
 // positions are >= 0 (INT64_MAX: none)
 __device__ __forceinline__ int64_t wave_min_pos(int64_t x) { return (int64_t)wave_min_u64((uint64_t)x); }
 
+// Element bytes come from the wave's LDS copy of [blk, blk + kStageBytes) — an element
+// starting in the block's first 2 KiB and shorter than 2 KiB lies inside it — and from
+// global memory past it (long value strings only).
+struct StagedLoad {
+    const char* buf;           // the bodies buffer
+    const unsigned char* lds;  // its bytes [blk, blk + kStageBytes)
+    int64_t blk;
+    __device__ char operator()(const char* p) const {
+        const int64_t o = (p - buf) - blk;
+        return (uint64_t)o < (uint64_t)kStageBytes ? (char)lds[o] : *p;
+    }
+};
+
 // The values array from its first '[' (vs): returns false when the body goes to the
 // host; else *count samples written at tv/tt[0 ..), *vend = one past the array's ']'.
+// Per 2-KiB block: the wave stages the block and the next one in LDS (each lane 2 x 32
+// bytes, 16-B loads; 64 readable bytes past every body make the loads safe), each lane
+// finds the '[' in its own 32 bytes (a bit mask from registers) and parses the elements
+// starting there from LDS, one at a time.
 __device__ bool values_array(const JsonArgs& A, const char* vs, const char* e, double* tv, double* tt, int lane,
-                             int64_t* count, const char** vend) {
+                             unsigned char* lds, int64_t* count, const char** vend) {
     const char* const buf = A.bodies;
     const int64_t lo_abs = vs - buf, hi_abs = e - buf;
     int64_t blk = lo_abs & ~(int64_t)(kLaneBytes - 1);
     int64_t cnt = 0;
     const bool want_ts = A.want_ts != 0;
     for (; blk < hi_abs; blk += kBlockBytes) {
+        // stage [blk, blk + 4 KiB): lane l's 32 bytes at 32 l and at 2 KiB + 32 l
         const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
+        uint32_t mine_w[8];
+        {
+            v4u32 x0 = {0, 0, 0, 0}, x1 = x0, y0 = x0, y1 = x0;
+            if (r0 < hi_abs) {
+                const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0);
+                x0 = q[0];
+                x1 = q[1];
+            }
+            if (r0 + kBlockBytes < hi_abs) {
+                const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0 + kBlockBytes);
+                y0 = q[0];
+                y1 = q[1];
+            }
+            v4u32* d = reinterpret_cast<v4u32*>(lds + lane * kLaneBytes);
+            d[0] = x0;
+            d[1] = x1;
+            v4u32* d2 = reinterpret_cast<v4u32*>(lds + kBlockBytes + lane * kLaneBytes);
+            d2[0] = y0;
+            d2[1] = y1;
+            mine_w[0] = x0[0], mine_w[1] = x0[1], mine_w[2] = x0[2], mine_w[3] = x0[3];
+            mine_w[4] = x1[0], mine_w[5] = x1[1], mine_w[6] = x1[2], mine_w[7] = x1[3];
+        }
+        __syncthreads();
+        // '[' in this lane's 32 bytes that lie inside the array's span
+        uint32_t starts = 0;
+#pragma unroll
+        for (int k = 0; k < kLaneBytes; ++k)
+            starts |= (((mine_w[k >> 2] >> (8 * (k & 3))) & 0xFF) == '[' ? 1u : 0u) << k;
+        if (r0 < lo_abs) {
+            const int64_t d = lo_abs - r0;
+            starts = d >= kLaneBytes ? 0u : (starts >> d) << d;
+        }
+        if (r0 + kLaneBytes > hi_abs) {
+            const int64_t d = hi_abs - r0;
+            starts = d <= 0 ? 0u : starts & (0xFFFFFFFFu >> (kLaneBytes - d));
+        }
         double v[kMaxPerLane], t[kMaxPerLane];
         int64_t st[kMaxPerLane];
         int nok = 0;
         int64_t fail_min = INT64_MAX, last_start = INT64_MAX, last_next = 0;
-        if (r0 + kLaneBytes > lo_abs && r0 < hi_abs) {
-            // the lane's 32 bytes: two aligned 16-B loads (the buffer base is 16-B aligned)
-            const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0);
-            const v4u32 a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
-            const uint32_t w[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-#pragma unroll
-            for (int k = 0; k < kLaneBytes; ++k) {
-                const int64_t x = r0 + k;
-                if (((w[k >> 2] >> (8 * (k & 3))) & 0xFF) != '[' || x < lo_abs || x >= hi_abs) continue;
-                double vv = 0.0, tt2 = 0.0;
-                const char* next;
-                bool last;
-                if (!sample_element(buf + x, e, want_ts, &vv, &tt2, &next, &last, ByteLoad{})) {
-                    fail_min = x < fail_min ? x : fail_min;
-                    continue;
-                }
-                if (nok == kMaxPerLane) {  // cannot happen for elements (>= 8 bytes each)
-                    fail_min = x < fail_min ? x : fail_min;
-                    continue;
-                }
-                v[nok] = vv;
-                t[nok] = tt2;
-                st[nok] = x;
-                ++nok;
-                if (last && x < last_start) {
-                    last_start = x;
-                    last_next = next - buf;
-                }
+        const StagedLoad ld{buf, lds, blk};
+        while (starts) {
+            const int k = __builtin_ctz(starts);
+            starts &= starts - 1;
+            const int64_t x = r0 + k;
+            double vv = 0.0, tt2 = 0.0;
+            const char* next = nullptr;
+            bool last = false;
+            if (nok == kMaxPerLane || !sample_element(buf + x, e, want_ts, &vv, &tt2, &next, &last, ld)) {
+                fail_min = x < fail_min ? x : fail_min;  // (more than 4 starts: elements are >= 8 bytes)
+                continue;
+            }
+            v[nok] = vv;
+            t[nok] = tt2;
+            st[nok] = x;
+            ++nok;
+            if (last && x < last_start) {
+                last_start = x;
+                last_next = next - buf;
             }
         }
         // the array's last element is the first one followed by ']'
@@ -119,12 +161,14 @@ __device__ bool values_array(const JsonArgs& A, const char* vs, const char* e, d
             *count = cnt;
             return true;
         }
+        __syncthreads();  // every lane is done with the staged bytes
     }
     return false;  // no closing ']'
 }
 
 // One body per wave (grid-stride over the launch's bodies).
 __global__ __launch_bounds__(64) void k_json_parse(JsonArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
     const int lane = threadIdx.x;
     for (int64_t i = blockIdx.x; i < A.n; i += gridDim.x) {
         const int64_t bi = A.first + i;
@@ -157,7 +201,7 @@ __global__ __launch_bounds__(64) void k_json_parse(JsonArgs A) {
             } else if (vs < e && *vs == '[') {
                 // phase 2 (all lanes): the samples
                 ok = values_array(A, vs, e, A.tmp_v + (ob >> 3), A.tmp_t ? A.tmp_t + (ob >> 3) : nullptr, lane,
-                                  &count, &vend);
+                                  lds, &count, &vend);
             }
             // phase 3 (lane 0): the rest of the body
             if (ok) {

@@ -115,71 +115,109 @@ KRR_JHD inline uint64_t eisel_lemire(uint64_t w, int64_t q) {
 
 KRR_JHD inline bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
 
-// Digits [p, e) of `int[.frac][(e|E)[+-]exp]` (grammar already checked by the caller,
-// or checked here when `strict_json`) -> IEEE bits of the magnitude.  NUM_HOST when the
-// significand needs more than 19 digits or the exponent more than 6.
-KRR_JHD inline int decimal_bits(const char* p, const char* e, uint64_t* bits) {
-    uint64_t w = 0;
-    int nd = 0;             // significant digits taken into w
-    int64_t drop = 0;       // exponent adjustment: digits not taken (zeros) / fraction digits
-    bool nonzero_lost = false;
-    bool any = false;
-    while (p < e && is_digit((unsigned char)*p)) {
-        const unsigned d = (unsigned)(*p - '0');
-        any = true;
-        if (nd == 0 && d == 0) {
-            // leading zero
-        } else if (nd < 19) {
-            w = w * 10 + d;
-            ++nd;
-        } else {
-            ++drop;  // integer digit beyond 19: scale up
-            if (d) nonzero_lost = true;
+// One pass over a number at p (advanced past it): a JSON number (the sample's timestamp;
+// grammar of the host reader's Reader::num, -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?)
+// or, with value_form, a sample value string's contents (krr_pack.cpp parse_value: an
+// optional sign, then digits with an optional fraction and exponent, or "NaN" / "Inf" —
+// Prometheus' spellings; std::from_chars' other spellings are the host's call).  The
+// digits are read once: grammar, significand and exponent together.  false: not
+// accepted here (more than 19 significant digits or 6 exponent digits included).
+template <class Load>
+KRR_JHD inline bool scan_number(const char*& p, const char* e, Load ld, bool value_form, uint64_t* out_bits) {
+    uint64_t sign = 0;
+    if (p < e) {
+        const char c = ld(p);
+        if (c == '-') {
+            sign = 0x8000000000000000ull;
+            ++p;
+        } else if (c == '+' && value_form) {
+            ++p;
         }
-        ++p;
     }
-    if (p < e && *p == '.') {
+    if (p >= e) return false;
+    char c = ld(p);
+    if (value_form && (c == 'N' || c == 'I')) {
+        if (e - p < 3) return false;
+        const char c1 = ld(p + 1), c2 = ld(p + 2);
+        if (c == 'N' && c1 == 'a' && c2 == 'N') {
+            *out_bits = 0x7FF8000000000000ull | sign;
+        } else if (c == 'I' && c1 == 'n' && c2 == 'f') {
+            *out_bits = 0x7FF0000000000000ull | sign;
+        } else {
+            return false;
+        }
+        p += 3;
+        return true;
+    }
+    if (!is_digit((unsigned char)c)) return false;
+    uint64_t w = 0;
+    int nd = 0;          // significant digits taken into w
+    int64_t drop = 0;    // power of ten of w's last digit
+    bool lost = false;   // a nonzero digit beyond the 19th
+    if (!value_form && c == '0') {  // JSON: a lone leading zero
         ++p;
-        while (p < e && is_digit((unsigned char)*p)) {
-            const unsigned d = (unsigned)(*p - '0');
-            any = true;
+        if (p < e && is_digit((unsigned char)ld(p))) return false;
+    } else {
+        for (; p < e; ++p) {
+            c = ld(p);
+            if (!is_digit((unsigned char)c)) break;
+            const unsigned d = (unsigned)(c - '0');
+            if (nd == 0 && d == 0) continue;  // leading zero
+            if (nd < 19) {
+                w = w * 10 + d;
+                ++nd;
+            } else {
+                ++drop;
+                lost |= d != 0;
+            }
+        }
+    }
+    if (p < e && ld(p) == '.') {
+        ++p;
+        if (p >= e || !is_digit((unsigned char)ld(p))) return false;
+        for (; p < e; ++p) {
+            c = ld(p);
+            if (!is_digit((unsigned char)c)) break;
+            const unsigned d = (unsigned)(c - '0');
             if (nd == 0 && d == 0) {
-                --drop;  // leading fraction zero
+                --drop;
             } else if (nd < 19) {
                 w = w * 10 + d;
                 ++nd;
                 --drop;
-            } else if (d) {
-                nonzero_lost = true;
+            } else {
+                lost |= d != 0;
             }
-            ++p;
         }
     }
-    if (!any) return NUM_HOST;
     int64_t ex = 0;
-    if (p < e && (*p == 'e' || *p == 'E')) {
+    if (p < e && (ld(p) == 'e' || ld(p) == 'E')) {
         ++p;
         bool eneg = false;
-        if (p < e && (*p == '+' || *p == '-')) {
-            eneg = *p == '-';
+        if (p < e && (ld(p) == '+' || ld(p) == '-')) {
+            eneg = ld(p) == '-';
             ++p;
         }
         int ne = 0;
-        while (p < e && is_digit((unsigned char)*p)) {
-            ex = ex * 10 + (*p - '0');
-            if (++ne > 6) return NUM_HOST;
-            ++p;
+        for (; p < e; ++p) {
+            c = ld(p);
+            if (!is_digit((unsigned char)c)) break;
+            ex = ex * 10 + (c - '0');
+            if (++ne > 6) return false;
         }
-        if (ne == 0) return NUM_HOST;
+        if (ne == 0) return false;
         if (eneg) ex = -ex;
     }
-    if (p != e || nonzero_lost) return NUM_HOST;
-    *bits = eisel_lemire(w, drop + ex);
-    return NUM_OK;
+    if (lost) return false;
+    *out_bits = eisel_lemire(w, drop + ex) | sign;
+    return true;
 }
 
-// A JSON number (the sample's timestamp), grammar as the host reader's Reader::num:
-// -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?  Returns the end, or nullptr.
+struct PlainLoad {
+    KRR_JHD char operator()(const char* q) const { return *q; }
+};
+
+// A JSON number's end (grammar only), or nullptr.
 KRR_JHD inline const char* json_number_end(const char* p, const char* e) {
     if (p < e && *p == '-') ++p;
     if (p >= e) return nullptr;
@@ -204,102 +242,32 @@ KRR_JHD inline const char* json_number_end(const char* p, const char* e) {
     return p;
 }
 
-KRR_JHD inline int json_number_value(const char* b, const char* e, double* out) {
-    const bool neg = *b == '-';
-    uint64_t bits;
-    if (decimal_bits(b + (neg ? 1 : 0), e, &bits) != NUM_OK) return NUM_HOST;
-    *out = from_bits(bits | (neg ? 0x8000000000000000ull : 0));
-    return NUM_OK;
-}
-
-// A sample value string (between the quotes) -> float64, as krr_pack.cpp parse_value:
-// an optional sign, then std::from_chars' decimal form.  Accepted here: digits with an
-// optional fraction and exponent, "NaN" and "Inf" (Prometheus' spellings); the host
-// decides every other spelling.
+// A whole sample value string [b, e) -> float64 (NUM_OK), else NUM_HOST.
 KRR_JHD inline int value_bits(const char* b, const char* e, double* out) {
-    bool neg = false;
-    if (b < e && (*b == '+' || *b == '-')) {
-        neg = *b == '-';
-        ++b;
-    }
-    if (b >= e) return NUM_HOST;
-    const uint64_t sign = neg ? 0x8000000000000000ull : 0;
-    if (e - b == 3 && b[0] == 'N' && b[1] == 'a' && b[2] == 'N') {
-        *out = from_bits(0x7FF8000000000000ull | sign);
-        return NUM_OK;
-    }
-    if (e - b == 3 && b[0] == 'I' && b[1] == 'n' && b[2] == 'f') {
-        *out = from_bits(0x7FF0000000000000ull | sign);
-        return NUM_OK;
-    }
-    if (!is_digit((unsigned char)*b)) return NUM_HOST;  // ".5", "inf", a second sign: the host's call
-    // digits [. digits] [e [+-] digits] — a fraction needs a digit after the point
     const char* p = b;
-    while (p < e && is_digit((unsigned char)*p)) ++p;
-    if (p < e && *p == '.') {
-        ++p;
-        if (p >= e || !is_digit((unsigned char)*p)) return NUM_HOST;
-        while (p < e && is_digit((unsigned char)*p)) ++p;
-    }
-    if (p < e && (*p == 'e' || *p == 'E')) {
-        ++p;
-        if (p < e && (*p == '+' || *p == '-')) ++p;
-        if (p >= e || !is_digit((unsigned char)*p)) return NUM_HOST;
-        while (p < e && is_digit((unsigned char)*p)) ++p;
-    }
-    if (p != e) return NUM_HOST;
     uint64_t bits;
-    if (decimal_bits(b, e, &bits) != NUM_OK) return NUM_HOST;
-    *out = from_bits(bits | sign);
+    if (!scan_number(p, e, PlainLoad{}, true, &bits) || p != e) return NUM_HOST;
+    *out = from_bits(bits);
     return NUM_OK;
 }
 
 // One element of a canonical values array at p (which must be '['):
 // `[<json number>,"<value>"]` followed by ',' + '[' (more follow) or ']' (the last one).
 // On success: *next = the following element's '[' or one past the array's ']', *last set.
-// Returns false for anything else (the caller hands the body to the host).
+// Returns false for anything else (the caller hands the body to the host).  One pass:
+// every byte is read once through ld.
 template <class Load>
 KRR_JHD inline bool sample_element(const char* p, const char* e, bool want_ts, double* value, double* ts,
                                    const char** next, bool* last, Load ld) {
     if (p >= e || ld(p) != '[') return false;
     ++p;
-    // timestamp
-    const char* tb = p;
-    {
-        if (p < e && ld(p) == '-') ++p;
-        if (p >= e) return false;
-        const char c0 = ld(p);
-        if (c0 == '0') {
-            ++p;
-        } else if (c0 >= '1' && c0 <= '9') {
-            while (p < e && is_digit((unsigned char)ld(p))) ++p;
-        } else {
-            return false;
-        }
-        if (p < e && ld(p) == '.') {
-            ++p;
-            if (p >= e || !is_digit((unsigned char)ld(p))) return false;
-            while (p < e && is_digit((unsigned char)ld(p))) ++p;
-        }
-        if (p < e && (ld(p) == 'e' || ld(p) == 'E')) {
-            ++p;
-            if (p < e && (ld(p) == '+' || ld(p) == '-')) ++p;
-            if (p >= e || !is_digit((unsigned char)ld(p))) return false;
-            while (p < e && is_digit((unsigned char)ld(p))) ++p;
-        }
-    }
-    const char* te = p;
+    uint64_t tb;
+    if (!scan_number(p, e, ld, false, &tb)) return false;
     if (p + 1 >= e || ld(p) != ',' || ld(p + 1) != '"') return false;
     p += 2;
-    const char* vb = p;
-    while (p < e) {
-        const unsigned char c = (unsigned char)ld(p);
-        if (c == '"') break;
-        if (c == '\\' || c < 0x20) return false;
-        ++p;
-    }
-    if (p + 2 >= e || ld(p + 1) != ']') return false;
-    const char* ve = p;
+    uint64_t vb;
+    if (!scan_number(p, e, ld, true, &vb)) return false;
+    if (p + 2 >= e || ld(p) != '"' || ld(p + 1) != ']') return false;
     p += 2;
     const char d = ld(p);
     if (d == ',') {
@@ -312,8 +280,8 @@ KRR_JHD inline bool sample_element(const char* p, const char* e, bool want_ts, d
     } else {
         return false;
     }
-    if (value_bits(vb, ve, value) != NUM_OK) return false;
-    if (want_ts && json_number_value(tb, te, ts) != NUM_OK) return false;
+    *value = from_bits(vb);
+    if (want_ts) *ts = from_bits(tb);
     return true;
 }
 

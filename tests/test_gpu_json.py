@@ -166,8 +166,13 @@ def test_recommend_from_bodies_device_equals_host():
 
     cpu = _fleet(7, n_obj=60, max_samples=2000)
     mem = _fleet(8, n_obj=60, max_samples=2000)
-    # memory bodies without NaN (the reference raises on a NaN memory sample)
-    mem = [[b.replace(b'"NaN"', b'"1"') for b in bodies] for bodies in mem]
+    # finite samples only: the reference's rounding raises on +-Inf (math.ceil) and on a NaN
+    # memory sample (max over Decimals) — both paths would raise the same there
+    def finite(b):
+        return b.replace(b'"NaN"', b'"1"').replace(b'"+Inf"', b'"2"').replace(b'"-Inf"', b'"3"')
+
+    cpu = [[finite(b) for b in bodies] for bodies in cpu]
+    mem = [[finite(b) for b in bodies] for bodies in mem]
     runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(cpu_percentile="99", memory_buffer_percentage="5")))
     a = runner.recommend_from_bodies(cpu, mem, parser="device")
     assert runner.last_pack_via == ("device", "device")

@@ -289,7 +289,7 @@ def test_bench_config5_direct_chunked():
     """Config 5 at N = 1 (exact single-window select per chunk of series): equal bits to the
     select over the regathered series."""
     p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5",
-                        "--containers", "600", "--chunk-gib", "0.2", "--steps", "2", "--warmup", "1",
+                        "--containers", "600", "--c5-chunk-gib", "0.2", "--steps", "2", "--warmup", "1",
                         "--error-sample", "600", "--no-cpu-baseline"], capture_output=True, text=True, timeout=270)
     assert p.returncode == 0, p.stderr[-4000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
@@ -301,7 +301,7 @@ def test_bench_config5_direct_oracle_parity():
     """Config 5 at N = 1 with the CPU baseline: the run's own answers on the baseline sample
     equal the oracle (parity_vs_oracle_on_sample), beside the k_select check."""
     p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5",
-                        "--containers", "700", "--chunk-gib", "0.3", "--steps", "2", "--warmup", "1",
+                        "--containers", "700", "--c5-chunk-gib", "0.3", "--steps", "2", "--warmup", "1",
                         "--error-sample", "200", "--cpu-sample", "60"], capture_output=True, text=True, timeout=270)
     assert p.returncode == 0, p.stderr[-4000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
