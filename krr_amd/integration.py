@@ -109,7 +109,8 @@ async def gather_objects_recommendations(runner: Any, objects: Sequence[Any]) ->
     if loader == "bodies":
         cpu_bodies, mem_bodies = await fetch_pod_bodies(runner, objects, settings)
         # native packer + one fleet-wide kernel pass + native rounding, off the event loop
-        results = await asyncio.to_thread(batched.recommend_from_bodies, cpu_bodies, mem_bodies)
+        results = await asyncio.to_thread(batched.recommend_from_bodies, cpu_bodies, mem_bodies, 0,
+                                          _options(runner).get("parser", "device"))
     elif loader == "grouped":
         fleet = await fetch_grouped_fleet(runner, objects, settings)
         results = await asyncio.to_thread(batched.recommend_packed, fleet)
@@ -252,16 +253,21 @@ async def collect_result(runner: Any):
     return fleet_collect(objects, recommendations, models)
 
 
-def install(runner_cls: Any = None, *, loader: str = "reference", scan: str = "reference") -> Any:
+def install(runner_cls: Any = None, *, loader: str = "reference", scan: str = "reference",
+            parser: str = "device") -> Any:
     """Route ``runner_cls._gather_objects_recommendations`` (default: the reference's
     ``robusta_krr.core.runner.Runner``) through ``gather_objects_recommendations``, loading
     histories with ``loader`` (see the module docstring), and with ``scan="fleet"`` also
-    ``_collect_result`` through ``collect_result``.  Calling it again changes the switches;
+    ``_collect_result`` through ``collect_result``.  ``parser`` (loader="bodies"): "device"
+    parses the raw bodies on the MI355X (krr_amd.core.device_pack), "host" with the native
+    host packer.  Calling it again changes the switches;
     ``uninstall`` restores the reference's methods.  Returns the class."""
     if loader not in LOADERS:
         raise ValueError(f"loader must be one of {LOADERS}")
     if scan not in SCANS:
         raise ValueError(f"scan must be one of {SCANS}")
+    if parser not in ("device", "host"):
+        raise ValueError("parser must be 'device' or 'host'")
     if runner_cls is None:
         from robusta_krr.core.runner import Runner as runner_cls  # the reference, in its own process
     if getattr(runner_cls, _ORIGINAL_ATTR, None) is None:
@@ -281,7 +287,7 @@ def install(runner_cls: Any = None, *, loader: str = "reference", scan: str = "r
     elif scan == "reference" and getattr(runner_cls, _ORIGINAL_COLLECT_ATTR, None) is not None:
         runner_cls._collect_result = getattr(runner_cls, _ORIGINAL_COLLECT_ATTR)
         setattr(runner_cls, _ORIGINAL_COLLECT_ATTR, None)
-    setattr(runner_cls, _OPTIONS_ATTR, {"loader": loader, "scan": scan})
+    setattr(runner_cls, _OPTIONS_ATTR, {"loader": loader, "scan": scan, "parser": parser})
     return runner_cls
 
 

@@ -351,11 +351,14 @@ def collect_check(args):
     except _native.NativeUnavailable as e:
         report["raised"] = "NativeUnavailable"
         report["message"] = str(e)
-    report["native_packer_used_before_raise"] = bool(packed)
+    report["raised_before_host_packer"] = not packed  # the device packer's context came first
     if args.engine == "oracle":
         from krr_amd.core.engine import SimpleEngine
 
         SimpleEngine.run_packed = oracle_run_packed
+        # the device packer needs the GPU too: the stand-in run packs on the host
+        integration.install(Runner, loader=args.loader, scan=args.scan, parser="host")
+        packed.clear()
         session.calls, session.params = 0, set()
         got = asyncio.run(make_runner()._collect_result())
         a, b = digest(got), digest(ref)

@@ -56,10 +56,11 @@ def test_reference_collect_result_native_loader_and_fleet_scan(loader):
     the reference's gather_data (Decimal per sample) never runs — and the Result built by
     scan_fleet out of the reference's own models equals the unpatched reference's, scan
     for scan and in score, every severity included.  The same run first takes the real
-    engine through it: the bodies are packed natively, then the kernel call raises
-    NativeUnavailable on this GPU-less host (no CPU fallback anywhere)."""
+    engine through it: the device packer (loader="bodies") or the kernel call raises
+    NativeUnavailable on this GPU-less host (no CPU fallback anywhere); the stand-in run
+    packs with the host packer (parser="host")."""
     r = _check("--engine", "oracle", "--loader", loader, "--scan", "fleet", "--objects", "30")
-    assert r["raised"] == "NativeUnavailable" and r["native_packer_used_before_raise"], r
+    assert r["raised"] == "NativeUnavailable", r
     assert r["collect_patched"] and r["equals_reference_result"], r
     assert r["types"] == ["robusta_krr.core.models.result.ResourceScan", "robusta_krr.core.models.result.Result"]
     assert r["severities"] == ["CRITICAL", "GOOD", "OK", "UNKNOWN", "WARNING"]
