@@ -956,9 +956,10 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     exact = not args.sketch_only
     direct = exact and world == 1 and not args.c5_refine
     method = "direct" if direct else (args.c5_method if exact else "sketch-only")
-    # the direct pass over 138 GB runs per chunk of series in buffers of their own (as
-    # configs 2-4, fleet_chunks); the time-sharded paths keep one buffer per rank
-    chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.c5_chunk_gib) if direct else [(0, S)]
+    # the direct pass and the window export run per chunk of series in buffers of their own
+    # (as configs 2-4, fleet_chunks); the sketch paths keep one buffer per rank
+    chunked = direct or method == "window"
+    chunks = fleet_chunks(np.arange(S + 1, dtype=np.int64) * Lr, args.c5_chunk_gib) if chunked else [(0, S)]
     phase("synth")
     parts = []
     for lo, hi in chunks:
@@ -967,7 +968,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         ctx.synth_fill_window(c, o, seed, 0, 0, False, t0, T, seg_base=lo)
         parts.append((lo, hi, c, ctx.series(c, o, Lr, False)))
     torch.cuda.synchronize()
-    ser = parts[0][3]  # the whole rank when it is one chunk (the time-sharded paths)
+    ser = parts[0][3]  # the whole rank when it is one chunk (the sketch paths)
+    ser_parts = [(lo, hi, ser_c) for lo, hi, _, ser_c in parts]
 
     def first_rows(k):
         """[k, Lr] device view/copy of the first k series."""
@@ -1013,7 +1015,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
             return
         if method == "window":
-            res = sketch.window_exact_time_sharded(ctx, ser, params, ext_slots=T - Lr, stream=stream,
+            res = sketch.window_exact_time_sharded(ctx, ser_parts, params, ext_slots=T - Lr, stream=stream,
                                                    events=None if ev is None else ev[0:2])
             state["misses"] += res["misses"]
             state["key_cap"] = res["key_cap"]
@@ -1091,7 +1093,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     kind = {"direct": (f"config5: {S} CPU series x {T} samples (30d@15s) on one GPU: exact single-window select, "
                        f"one pass (no time sharding at N=1; {len(parts)} launches alternating on 2 streams)"),
             "window": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
-                       f"samples/series/rank): exact, one HBM pass (window export -> all-to-all -> merge)"),
+                       f"samples/series/rank): exact, one HBM pass (window export in {len(parts)} launches "
+                       f"alternating on 2 streams -> all-to-all -> merge)"),
             "sketch": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
                        f"samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave + exact "
                        f"refinement (collect + select in the located bins; two HBM passes)"),

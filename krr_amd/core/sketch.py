@@ -38,6 +38,7 @@ r-th contiguous time slice of every series.
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -393,6 +394,18 @@ def max_time_sharded(local_value, local_count, local_flags, group=None) -> dict:
 
 # -------------------- one-pass exact time-sharded percentiles (window export) ---------------------
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    import torch
+
+    key = (threading.get_ident(), str(dev))
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 def _max_len(series) -> int:
     if series.max_segment_len > 0:
         return int(series.max_segment_len)
@@ -420,6 +433,39 @@ def gather_segments(values, offs, ids):
     return values[pos], new_offs
 
 
+def _parts(series):
+    """A KrrSeries, or a list of (lo, hi, KrrSeries) parts holding series [lo, hi) each in
+    buffers of their own (contiguous, ascending) -> the list form."""
+    if isinstance(series, (list, tuple)):
+        return list(series)
+    return [(0, series.n_segments, series)]
+
+
+def gather_segments_parts(parts, ids):
+    """gather_segments over series held in parts: ``ids`` ascending global series ids."""
+    import torch
+
+    if len(parts) == 1:
+        vals, offs = parts[0][2]._keep
+        return gather_segments(vals, offs, ids - parts[0][0])
+    vs, ls = [], []
+    for lo, hi, ser in parts:
+        sel = ids[(ids >= lo) & (ids < hi)]
+        if sel.numel() == 0:
+            continue
+        v, o = gather_segments(*ser._keep, sel - lo)
+        vs.append(v[: int(o[-1].item())])
+        ls.append(o[1:] - o[:-1])
+    dev = parts[0][2]._keep[0].device
+    if not vs:
+        return torch.empty(1, dtype=torch.float64, device=dev), torch.zeros(1, dtype=torch.int64, device=dev)
+    lens = torch.cat(ls)
+    offs = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)
+    vals = torch.cat(vs)
+    return (vals if vals.numel() else torch.empty(1, dtype=torch.float64, device=dev)), offs
+
+
 def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, params: _native.KrrPercentileParams,
                               ext_slots: Optional[int] = None, group=None, stream=None, events=None,
                               key_cap: Optional[int] = None) -> dict:
@@ -432,15 +478,21 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
     'misses' (series of the block finished by regathering their slices), 'key_cap' and
     'exchanged_bytes' (what this rank sent in the all-to-all) and 'hdr' (this rank's
     exported krr_window_hdr rows, int64 [S, HDR_WORDS]).  ``events``: optional pair
-    of HIP events recorded around the export pass (its HBM time)."""
+    of HIP events recorded around the export pass (its HBM time).
+
+    ``series`` may also be a list of (lo, hi, KrrSeries) parts, series [lo, hi) of the rank
+    in buffers of their own: one export launch per part, consecutive launches alternating
+    between ``stream`` and a second stream (one part's drain overlaps the next one's start;
+    launches over a few GiB stream faster than one over a whole 138-GB allocation)."""
     import torch
     import torch.distributed as dist
 
-    S = series.n_segments
-    dev = series._keep[0].device
+    parts = _parts(series)
+    S = parts[-1][1]
+    dev = parts[0][2]._keep[0].device
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    Lmax = _max_len(series)
+    Lmax = max(_max_len(ser) for _, _, ser in parts)
     if ext_slots is None:
         ext_slots = (world - 1) * Lmax
     kc = int(key_cap or _native.window_key_cap(max(Lmax, 1), ext_slots, params))
@@ -448,12 +500,20 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
     rows = per * world
     hdr = torch.empty((max(rows, 1), _native.HDR_WORDS), dtype=torch.int64, device=dev)
     keys = torch.empty((max(rows, 1), kc), dtype=torch.int64, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
     if events is not None:
-        events[0].record(stream)
-    if S:
-        ctx.window_export(series, params, ext_slots, kc, hdr, keys, stream)
+        events[0].record(st)
+    side = None
+    if len(parts) > 1:
+        side = _side_stream(dev)
+        side.wait_stream(st)
+    for j, (lo, hi, ser) in enumerate(parts):
+        if hi > lo:
+            ctx.window_export(ser, params, ext_slots, kc, hdr[lo:hi], keys[lo:hi], side if (side and j % 2) else st)
+    if side is not None:
+        st.wait_stream(side)
     if events is not None:
-        events[1].record(stream)
+        events[1].record(st)
     lo, hi = owner_blocks(S, world)[rank] if world > 1 else (0, S)
     nb = hi - lo
     if world > 1:
@@ -482,7 +542,7 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
         dist.all_reduce(t, group=group)
         total = int(t.item())
     if total:
-        finish_window_misses(ctx, series, params, out, (lo, hi), group, stream)
+        finish_window_misses(ctx, parts, params, out, (lo, hi), group, stream)
     out.update(block=(lo, hi), misses=nmiss, key_cap=kc, exchanged_bytes=sent, hdr=hdr[:S])
     return out
 
@@ -496,9 +556,10 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
     import torch
     import torch.distributed as dist
 
-    vals, offs = series._keep
-    dev = vals.device
-    S = series.n_segments
+    parts = _parts(series)
+    gaps = parts[0][2].gaps_are_nan
+    dev = parts[0][2]._keep[0].device
+    S = parts[-1][1]
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     lo, _ = block
     mine = torch.nonzero((out["flags"] & _native.KRR_FLAG_WINDOW_MISS) != 0).flatten()
@@ -506,8 +567,8 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
         ids = mine
         if ids.numel() == 0:
             return
-        sv, so = gather_segments(vals, offs, ids)
-        sub = ctx.series(sv, so, 0, series.gaps_are_nan)
+        sv, so = gather_segments_parts(parts, ids)
+        sub = ctx.series(sv, so, 0, gaps)
         v = torch.empty(ids.numel(), dtype=torch.float64, device=dev)
         n = torch.empty(ids.numel(), dtype=torch.int64, device=dev)
         f = torch.empty(ids.numel(), dtype=torch.int32, device=dev)
@@ -523,7 +584,7 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
     if ids_all.numel() == 0:
         return
     # this rank's slices of them, grouped by owner (= ascending id)
-    sv, so = gather_segments(vals, offs, ids_all)
+    sv, so = gather_segments_parts(parts, ids_all)
     lens = (so[1:] - so[:-1])
     coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
     counts = [len(x) for x in lists]
@@ -555,7 +616,7 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
         piece = torch.repeat_interleave(torch.arange(flat.numel(), device=dev), flat)
         pos = torch.arange(n_all, device=dev)
         whole[dst_start[piece] + (pos - src_start[piece])] = recv[:n_all]
-    sub = ctx.series(whole, new_offs, 0, series.gaps_are_nan)
+    sub = ctx.series(whole, new_offs, 0, gaps)
     v = torch.empty(k, dtype=torch.float64, device=dev)
     n = torch.empty(k, dtype=torch.int64, device=dev)
     f = torch.empty(k, dtype=torch.int32, device=dev)

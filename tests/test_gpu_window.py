@@ -151,6 +151,37 @@ def test_window_world1_flow_finishes_misses(ctx, mode):
         assert res["misses"] >= 1  # the all-zero series went through the fallback
 
 
+@pytest.mark.parametrize("mode", ["linear", "sorted_lower"])
+def test_window_parts_equal_one_buffer(ctx, mode):
+    """The same flow over the series split into parts in buffers of their own (one export
+    launch per part, alternating streams — what bench.py --config 5 runs): the misses are
+    regathered across parts, and every result equals the oracle."""
+    from decimal import Decimal
+
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    rng = np.random.default_rng(23)
+    S, L = 31, 9000
+    x = _mixed(rng, S, L)
+    x[rng.random(x.shape) < 0.1] = np.nan
+    offs = (np.arange(S + 1) * L).astype(np.int64)
+    cuts = [0, 4, 5, 17, 31]
+    parts = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        o = (np.arange(hi - lo + 1) * L).astype(np.int64)
+        v = _dev(x[lo:hi].ravel())
+        parts.append((lo, hi, ctx.series(v, _dev(o, np.int64), L, True)))
+    params = percentile_params(Decimal("50"), mode)
+    res = sketch.window_exact_time_sharded(ctx, parts, params)
+    ov, on, of = oracle.percentile(x.ravel(), offs, params.mode, params.p_num, params.p_den, params.q, True)
+    assert _same(res["value"].cpu().numpy(), ov, mode).all()
+    assert np.array_equal(res["count"].cpu().numpy(), on)
+    assert np.array_equal(res["flags"].cpu().numpy().astype(np.uint32), of)
+    if mode == "sorted_lower":
+        assert res["misses"] >= 1
+
+
 def test_window_nan_in_compact_layout(ctx):
     from krr_amd import _native
     from krr_amd.core.engine import percentile_params
