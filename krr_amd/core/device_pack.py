@@ -47,8 +47,9 @@ class DevicePacked:
 class DevicePacker:
     """One per (thread, device): owns the page-locked staging buffer and a copy stream.
 
-    ``chunk_bytes``: bodies are staged and copied in chunks of about this size, each
-    parsed as soon as it is in HBM."""
+    ``chunk_bytes``: bodies are staged and copied in chunks of up to this size (the first
+    ones smaller, doubling from 16 MiB, so the copy engine starts early), each parsed as
+    soon as it is in HBM."""
 
     def __init__(self, ctx: _native.Context, chunk_bytes: int = 256 << 20, threads: int = 0):
         import torch
@@ -112,8 +113,10 @@ class DevicePacker:
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
         # chunks of bodies: stage (host threads) -> H2D (copy stream) -> parse (st)
         a = 0
+        step = min(self.chunk_bytes, 16 << 20)  # small first chunks: the DMA starts early
         while a < nb:
-            b = int(np.searchsorted(boffs, boffs[a] + self.chunk_bytes, side="left"))
+            b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
+            step = min(2 * step, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
             lo, hi = int(boffs[a]), int(boffs[b])
             rc = host.krr_pack_concat(ctypes.addressof(ptrs) + a * ctypes.sizeof(ctypes.c_char_p),
