@@ -120,14 +120,21 @@ enum { D_TOTAL, D_COMPACT, D_FINAL, D_NCOMPACT, D_NFALLBACK, D_ACTIVE_SLOTS, D_I
 #ifndef KRR_XCD_REMAP
 #define KRR_XCD_REMAP 1  // per-XCD contiguous segment ranges (0: block i -> segment i)
 #endif
+// ... for launches whose longest segment is shorter than this (a per-launch flag): with
+// segments of 172,800 slots (config 5) block i -> segment i streamed 3.7% faster in a
+// same-process A/B (scripts/ab_variants.py, profiles/r03/l), with 50,400 ones 2.5% slower
+#ifndef KRR_XCD_REMAP_MAXLEN
+#define KRR_XCD_REMAP_MAXLEN 100000
+#endif
 // Workgroups are dispatched round-robin over the 8 XCDs (block i on XCD i % 8),
 // so block i -> segment i leaves every XCD's L2 fetching a fresh offsets line
 // per segment start.  Remap so that the blocks of one XCD (i, i+8, i+16, …)
 // walk one contiguous eighth of the items: their offsets (and result records)
 // share L2 lines.  A bijection of [0, n): the n % 8 trailing items map to
 // themselves.
-__device__ __forceinline__ int64_t xcd_item(int64_t i, int64_t n) {
+__device__ __forceinline__ int64_t xcd_item(int64_t i, int64_t n, int32_t remap) {
     if constexpr (!KRR_XCD_REMAP) return i;
+    if (!remap) return i;
     const int64_t q = n >> 3;
     if (i >= (q << 3)) return i;
     return (i & 7) * q + (i >> 3);
@@ -961,6 +968,7 @@ struct SelectArgs {
     int64_t* fail_list = nullptr;
     unsigned int* fail_count = nullptr;   // this launch's list length
     unsigned int* fail_reset = nullptr;   // the previous launch's counter: zeroed for the next one
+    int32_t remap = 1;   // xcd_item: per-XCD segment ranges (KRR_XCD_REMAP_MAXLEN)
 };
 
 // One half of an object's 32-B record (k_pack_records layout): half 0 = CPU, 1 = memory.
@@ -2182,8 +2190,8 @@ void k_select(SelectArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if (KIND != SEL_SINGLE && A.fail_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.fail_reset = 0;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        if constexpr (KIND != SEL_SINGLE) mid_select_segment<KIND == SEL_WINDOW_LONG>(A, xcd_item(s, A.S), smem, threadIdx.x);
-        else select_segment(A, xcd_item(s, A.S), smem, threadIdx.x);
+        if constexpr (KIND != SEL_SINGLE) mid_select_segment<KIND == SEL_WINDOW_LONG>(A, xcd_item(s, A.S, A.remap), smem, threadIdx.x);
+        else select_segment(A, xcd_item(s, A.S, A.remap), smem, threadIdx.x);
     }
 }
 
@@ -2267,7 +2275,7 @@ __device__ __forceinline__ void window_export_segment(const WindowExportArgs& X,
 template <bool LONG>
 __global__ __launch_bounds__(64, window_waves(LONG)) void k_window_export(WindowExportArgs X) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    for (int64_t s = blockIdx.x; s < X.A.S; s += gridDim.x) window_export_segment<LONG>(X, xcd_item(s, X.A.S), smem, threadIdx.x);
+    for (int64_t s = blockIdx.x; s < X.A.S; s += gridDim.x) window_export_segment<LONG>(X, xcd_item(s, X.A.S, X.A.remap), smem, threadIdx.x);
 }
 
 struct OpAdd64 {
@@ -2476,7 +2484,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
 }
 
 __global__ __launch_bounds__(64) void k_refindex_gaps(RefArgs A) {
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment<false>(A, xcd_item(s, A.S), threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) refindex_gaps_segment<false>(A, xcd_item(s, A.S, 1), threadIdx.x);
 }
 
 // Compact CSR (every slot is a sample, NaN included): X[k] is one gather.
@@ -2536,6 +2544,7 @@ struct MaxArgs {
     double2* fwd_dst = nullptr;
     int64_t fwd_units = 0;
     int64_t fwd_items = 0;
+    int32_t remap = 1;  // xcd_item: per-XCD segment ranges (KRR_XCD_REMAP_MAXLEN)
 };
 
 template <class Streamer>
@@ -2576,7 +2585,7 @@ __device__ __forceinline__ void max_segment(const MaxArgs& A, int64_t s, int lan
 }
 
 __global__ __launch_bounds__(64) void k_max(MaxArgs A) {
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) max_segment<false>(A, xcd_item(s, A.S), threadIdx.x);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) max_segment<false>(A, xcd_item(s, A.S, A.remap), threadIdx.x);
 }
 
 // ------------------------------ FUSED --------------------------------------
@@ -2624,12 +2633,12 @@ __global__ __launch_bounds__(64, CPU_KIND == CPU_HSELECT ? window_waves(false)
         // remap within each resource's half, so the CPU items still all precede
         // the memory items in dispatch order
         if (b < S_cpu) {
-            const int64_t s = xcd_item(b, S_cpu);
+            const int64_t s = xcd_item(b, S_cpu, A.remap);
             if constexpr (CPU_KIND == CPU_SELECT) select_segment(A, s, smem, threadIdx.x);
             else if constexpr (kWindow) mid_select_segment<CPU_KIND == CPU_HSELECT_LONG>(A, s, smem, threadIdx.x);
             else refindex_gaps_segment<true>(R, s, threadIdx.x);
         } else {
-            max_segment<true>(M, xcd_item(b - S_cpu, M.S), threadIdx.x);
+            max_segment<true>(M, xcd_item(b - S_cpu, M.S, M.remap), threadIdx.x);
         }
     }
 }
@@ -3357,6 +3366,7 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->out_f = of;
     A->stats = ctx->d_tmp + 1;
     A->wcap = wsel_cap_for(Lmax, series->gaps_are_nan != 0);
+    A->remap = Lmax < KRR_XCD_REMAP_MAXLEN ? 1 : 0;
     if (hsel && KRR_WSEL && A->wcap != kWselCapLong) {  // misses: a list for the hselect launch that follows
         if (ctx->fail_cap < series->n_segments) {
             if (ctx->d_fail_list) KRR_HIP(ctx, hipFree(ctx->d_fail_list));
@@ -3533,6 +3543,7 @@ int krr_segmented_max(krr_ctx* ctx, const krr_series* series, double* out_value,
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     MaxArgs A{series->values, series->offsets, S, series->gaps_are_nan, out_value, out_count, out_flags};
+    A.remap = series->max_segment_len > 0 && series->max_segment_len >= KRR_XCD_REMAP_MAXLEN ? 0 : 1;
     hipLaunchKernelGGL(k_max, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
@@ -3596,6 +3607,7 @@ int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     hipStream_t st = (hipStream_t)stream;
     MaxArgs M{mem->values, mem->offsets, S, mem->gaps_are_nan, mem_value, mem_count, mem_flags, records};
+    M.remap = mem->max_segment_len > 0 && mem->max_segment_len >= KRR_XCD_REMAP_MAXLEN ? 0 : 1;
     if (fwd_units > 0) {
         M.fwd_src = (const double2*)forward_src;
         M.fwd_dst = (double2*)forward_dst;
@@ -3953,6 +3965,7 @@ int krr_window_export(krr_ctx* ctx, const krr_series* slices, const krr_percenti
     X.A.vals = slices->values;
     X.A.offs = slices->offsets;
     X.A.S = S;
+    X.A.remap = Lmax < KRR_XCD_REMAP_MAXLEN ? 1 : 0;
     X.A.mode = params->mode;
     X.A.gaps = slices->gaps_are_nan;
     X.A.p_num = params->p_num;
