@@ -114,9 +114,36 @@ def parse():
     return ap.parse_args()
 
 
+_LAST_PHASE = ["started"]
+
+
 def phase(name: str) -> None:
     """This rank's progress on stderr (the launcher keeps each rank's last phase)."""
+    _LAST_PHASE[0] = name
     print(f"KRR_PHASE rank={os.environ.get('RANK', '0')} {name}", file=sys.stderr, flush=True)
+
+
+def start_rank_watchdog(args, rank: int, world: int) -> None:
+    """Under an external launcher (torchrun: the driver's N > 1 runs) nothing stops a rank
+    that hangs in a rendezvous or a collective before the launcher's own limit, and the run
+    would end with no JSON line.  After --deadline seconds this thread ends the rank:
+    rank 0 first prints ONE JSON line with status "timeout" and its last phase, then every
+    rank exits with 124 (os._exit: nothing the hung main thread holds is waited for)."""
+    import threading
+
+    def watch():
+        time.sleep(args.deadline)
+        print(f"bench.py rank {rank}: deadline of {args.deadline:.0f} s passed in phase {_LAST_PHASE[0]!r}",
+              file=sys.stderr, flush=True)
+        if rank == 0 and _JSON_OUT is not None:
+            try:
+                print(json.dumps({"metric": METRIC, "n_gpus": world, "status": "timeout", "deadline_s": args.deadline,
+                                  "rank_phases": {"0": _LAST_PHASE[0]}}), file=_JSON_OUT, flush=True)
+            except (OSError, ValueError):
+                pass
+        os._exit(124)
+
+    threading.Thread(target=watch, daemon=True, name="krr-bench-watchdog").start()
 
 
 def _splitmix(x: np.ndarray) -> np.ndarray:
@@ -226,7 +253,8 @@ def launch_ranks(args) -> int:
     pumps = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   KRR_BENCH_LAUNCHED="1")
         p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
                              stderr=subprocess.PIPE)
         procs.append(p)
@@ -289,16 +317,18 @@ def main():
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if os.environ.get("KRR_BENCH_TEST_HANG"):  # tests: a rank that never finishes (launcher deadline)
-        phase("init")
-        while True:
-            time.sleep(1)
     # Native libraries (RCCL's version banner, gloo's peer messages) write to fd 1:
     # point fd 1 at stderr and keep the real stdout for the ONE JSON line.
     global _JSON_OUT
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if "WORLD_SIZE" in os.environ and not os.environ.get("KRR_BENCH_LAUNCHED"):
+        start_rank_watchdog(args, int(os.environ.get("RANK", "0")), int(os.environ["WORLD_SIZE"]))
+    if os.environ.get("KRR_BENCH_TEST_HANG"):  # tests: a rank that never finishes (deadlines)
+        phase("init")
+        while True:
+            time.sleep(1)
     import torch
     import torch.distributed as dist
 
