@@ -397,6 +397,25 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
                      const double* scratch_ts, const int64_t* counts, const int32_t* status,
                      const int64_t* out_pos, double* values, double* timestamps, void* stream);
 
+/* Grouped bodies (`sum by (pod) (...)`, one series per pod; the host packer's
+ * krr_pack_parse_grouped, include/krr_pack.h): every series of every body in
+ * [first, first + n) is parsed (values to scratch slot values_at / 8) and described by
+ * one record of 6 int64 appended at records[*n_records ...] (device counter, zeroed by
+ * the caller; order: any — (body, index) restores it):
+ *   {body, index in data.result, label value byte offset in `bodies` (-1: the metric has
+ *    no `label`), label length, scratch slot of the first value, sample count}.
+ * status[b] as krr_json_parse (KRR_JSON_HOST also when the records outgrow rec_cap).
+ * The caller routes slots to series by label (krr_pack_match_grouped, include/krr_pack.h)
+ * and moves the kept runs into the CSR with krr_json_gather. */
+int krr_json_parse_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, const char* label,
+                          int32_t want_timestamps, double* scratch_values, double* scratch_ts, int64_t* records,
+                          int64_t rec_cap, uint64_t* n_records, int32_t* status, void* stream);
+/* values[dst[j] ..) = scratch_values[src[j] ..), count[j] values (count < 0: none); the same
+ * for timestamps when both pointers are given. */
+int krr_json_gather(krr_ctx* ctx, int64_t n_items, const int64_t* src, const int64_t* count, const int64_t* dst,
+                    const double* scratch_values, const double* scratch_ts, double* values, double* timestamps,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,8 @@ EXPORTED_SYMBOLS = (
     "krr_abi_version",
     "krr_json_parse",
     "krr_json_compact",
+    "krr_json_parse_series",
+    "krr_json_gather",
     "krr_create",
     "krr_destroy",
     "krr_last_error",
@@ -270,6 +272,10 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse.restype = ctypes.c_int
         lib.krr_json_compact.argtypes = [vp, jb, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_compact.restype = ctypes.c_int
+        lib.krr_json_parse_series.argtypes = [vp, jb, i64, i64, ctypes.c_char_p, i32, vp, vp, vp, i64, vp, vp, vp]
+        lib.krr_json_parse_series.restype = ctypes.c_int
+        lib.krr_json_gather.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.krr_json_gather.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
@@ -588,6 +594,35 @@ class Context:
             scratch_ts.data_ptr() if timestamps is not None else None, counts.data_ptr(), status.data_ptr(),
             out_pos.data_ptr(), values.data_ptr(), timestamps.data_ptr() if timestamps is not None else None,
             self._stream(stream)))
+
+    def json_parse_series(self, jb: KrrJsonBodies, first: int, n: int, label: str, want_timestamps: bool,
+                          scratch_values, scratch_ts, records, n_records, status, stream=None) -> None:
+        """records: int64 [rec_cap, 6]; n_records: int64 [1] device counter (zeroed by the caller)."""
+        slots = jb.total_bytes // 8 + 1
+        _check_tensor(scratch_values, "float64", slots)
+        if want_timestamps:
+            _check_tensor(scratch_ts, "float64", slots)
+        _check_tensor(records, "int64")
+        _check_tensor(n_records, "int64", 1)
+        _check_tensor(status, "int32", jb.n_bodies)
+        self._check(self._lib.krr_json_parse_series(
+            self._h, ctypes.byref(jb), int(first), int(n), label.encode(), int(bool(want_timestamps)),
+            scratch_values.data_ptr(), scratch_ts.data_ptr() if want_timestamps else None, records.data_ptr(),
+            records.numel() // 6, n_records.data_ptr(), status.data_ptr(), self._stream(stream)))
+
+    def json_gather(self, src, count, dst, scratch_values, scratch_ts, values, timestamps=None, stream=None) -> None:
+        n = src.numel()
+        for t in (src, count, dst):
+            _check_tensor(t, "int64", n)
+        _check_tensor(scratch_values, "float64")
+        _check_tensor(values, "float64")
+        if timestamps is not None:
+            _check_tensor(timestamps, "float64", values.numel())
+            _check_tensor(scratch_ts, "float64")
+        self._check(self._lib.krr_json_gather(
+            self._h, n, src.data_ptr(), count.data_ptr(), dst.data_ptr(), scratch_values.data_ptr(),
+            scratch_ts.data_ptr() if timestamps is not None else None, values.data_ptr(),
+            timestamps.data_ptr() if timestamps is not None else None, self._stream(stream)))
 
 
 def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectPlanInfo:

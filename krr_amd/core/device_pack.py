@@ -77,23 +77,14 @@ class DevicePacker:
         with self._lock:
             return self._pack(per_object_bodies, want_timestamps, return_pod_counts, stream)
 
-    def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:
+    def _upload(self, flat, want_ts, st, launch):
+        """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
+        copy stream and call ``launch(jb, a, b, tmp_v, tmp_t)`` on ``st`` for bodies [a, b)
+        once the chunk is there."""
         import torch
 
-        flat: list = []
-        obj: list = []
-        for o, bodies in enumerate(per_object_bodies):
-            for b in bodies:
-                flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
-                obj.append(o)
-        n_obj, nb = len(per_object_bodies), len(flat)
         dev = self.device
-        st = stream if stream is not None else torch.cuda.current_stream(dev)
-        if nb == 0:
-            offs = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
-            return DevicePacked(PackedSeries(torch.empty(0, dtype=torch.float64, device=dev), offs, 0), "device", 0,
-                                torch.empty(0, dtype=torch.int64, device=dev) if want_counts else None,
-                                torch.empty(0, dtype=torch.float64, device=dev) if want_ts else None)
+        nb = len(flat)
         lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=nb)
         boffs = np.zeros(nb + 1, dtype=np.int64)
         np.cumsum(lens, out=boffs[1:])
@@ -104,14 +95,11 @@ class DevicePacker:
         slots = total // 8 + 1
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
         tmp_t = torch.empty(slots, dtype=torch.float64, device=dev) if want_ts else None
-        counts = torch.empty(nb, dtype=torch.int64, device=dev)
-        status = torch.empty(nb, dtype=torch.int32, device=dev)
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
         ptrs = (ctypes.c_char_p * nb)(*flat)
         host = load_library()
         cs = self._copy_stream
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
-        # chunks of bodies: stage (host threads) -> H2D (copy stream) -> parse (st)
         a = 0
         step = min(self.chunk_bytes, 16 << 20)  # small first chunks: the DMA starts early
         while a < nb:
@@ -129,8 +117,108 @@ class DevicePacker:
                 ev = torch.cuda.Event()
                 ev.record(cs)
             st.wait_event(ev)
-            self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
+            launch(jb, a, b, tmp_v, tmp_t)
             a = b
+        self._last = (d_bodies, stage)
+        return lens, boffs, total, jb, tmp_v, tmp_t
+
+    def pack_grouped(self, plan, bodies: Sequence[bytes], *, want_timestamps: bool = False,
+                     return_pod_counts: bool = False, stream=None, label: str = "pod") -> DevicePacked:
+        """``plan`` a krr_amd.core.fleet_query.FleetQueryPlan, bodies[g] the response to its
+        g-th grouped query (one resource): the CSR ``plan.pack(bodies)`` builds on the host,
+        bit for bit, with the bodies parsed on the device (krr_json_parse_series) and routed
+        by pod label (krr_pack_match_grouped)."""
+        with self._lock:
+            return self._pack_grouped(plan, bodies, want_timestamps, return_pod_counts, stream, label)
+
+    def _pack_grouped(self, plan, bodies, want_ts, want_counts, stream, label) -> DevicePacked:
+        import torch
+
+        if len(bodies) != len(plan.groups):
+            raise ValueError(f"expected {len(plan.groups)} bodies (one per group query), got {len(bodies)}")
+        flat = [b if isinstance(b, (bytes, bytearray)) else bytes(b) for b in bodies]
+        dev = self.device
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        n_obj, nb, ns = plan.n_objects, len(flat), plan.n_slots
+
+        def host_fallback(n_host):
+            res = plan.pack(bodies, want_timestamps=want_ts, threads=self.threads, return_pod_counts=want_counts)
+            res = res if isinstance(res, tuple) else (res,)
+            rest = list(res[1:])
+            ts = rest.pop(0) if want_ts else None
+            pc = rest.pop(0) if want_counts else None
+            return DevicePacked(res[0], "host", n_host, pc, ts)
+
+        if nb == 0 or ns == 0:
+            return host_fallback(0)
+        total_guess = sum(len(b) for b in flat)
+        rec_cap = max(1024, total_guess // 256)
+        recs = torch.empty((rec_cap, 6), dtype=torch.int64, device=dev)
+        n_recs = torch.zeros(1, dtype=torch.int64, device=dev)
+        status = torch.empty(nb, dtype=torch.int32, device=dev)
+
+        def launch(jb, a, b, tmp_v, tmp_t):
+            self.ctx.json_parse_series(jb, a, b - a, label, want_ts, tmp_v, tmp_t, recs, n_recs, status, stream=st)
+
+        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
+        with torch.cuda.stream(st):
+            summary = torch.stack([status.max().to(torch.int64), n_recs[0]]).cpu()  # the one sync
+        worst, nr = (int(x) for x in summary)
+        if worst == _native.KRR_JSON_HOST or nr > rec_cap:
+            return host_fallback(int((status == _native.KRR_JSON_HOST).sum().item()))
+        rec_h = recs[:nr].cpu().numpy()
+        slot_src = np.empty(ns, dtype=np.int64)
+        slot_cnt = np.empty(ns, dtype=np.int64)
+        host = load_library()
+        stage = self._last[1]
+        rc = host.krr_pack_match_grouped(rec_h.ctypes.data, nr, stage.data_ptr(), nb, plan.slot_group.ctypes.data,
+                                         plan._names or b"\0", plan._name_offsets.ctypes.data, ns,
+                                         slot_src.ctypes.data, slot_cnt.ctypes.data, self.threads)
+        if rc != KRR_PACK_OK:
+            raise PrometheusResponseError(rc, "krr_pack_match_grouped failed")
+        kept = np.maximum(slot_cnt, 0)
+        dst = np.zeros(ns, dtype=np.int64)
+        if ns > 1:
+            np.cumsum(kept[:-1], out=dst[1:])
+        seg = np.zeros(n_obj, dtype=np.int64)
+        np.add.at(seg, plan.slot_obj, kept)
+        offsets = np.zeros(n_obj + 1, dtype=np.int64)
+        np.cumsum(seg, out=offsets[1:])
+        n_vals = int(offsets[-1])
+        with torch.cuda.stream(st):
+            values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
+            ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
+            d = [torch.from_numpy(x).to(dev) for x in (slot_src, kept, dst)]
+            self.ctx.json_gather(d[0], d[1], d[2], tmp_v, tmp_t, values, ts, stream=st)
+            offs_d = torch.from_numpy(offsets).to(dev)
+        series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
+        return DevicePacked(series, "device", 0, torch.from_numpy(slot_cnt) if want_counts else None,
+                            ts[:n_vals] if ts is not None else None)
+
+    def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:
+        import torch
+
+        flat: list = []
+        obj: list = []
+        for o, bodies in enumerate(per_object_bodies):
+            for b in bodies:
+                flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
+                obj.append(o)
+        n_obj, nb = len(per_object_bodies), len(flat)
+        dev = self.device
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        if nb == 0:
+            offs = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
+            return DevicePacked(PackedSeries(torch.empty(0, dtype=torch.float64, device=dev), offs, 0), "device", 0,
+                                torch.empty(0, dtype=torch.int64, device=dev) if want_counts else None,
+                                torch.empty(0, dtype=torch.float64, device=dev) if want_ts else None)
+        counts = torch.empty(nb, dtype=torch.int64, device=dev)
+        status = torch.empty(nb, dtype=torch.int32, device=dev)
+
+        def launch(jb, a, b, tmp_v, tmp_t):
+            self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
+
+        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
         with torch.cuda.stream(st):
             obj_t = torch.from_numpy(np.asarray(obj, dtype=np.int64)).to(dev, non_blocking=False)
             seg = torch.zeros(n_obj, dtype=torch.int64, device=dev).index_add_(0, obj_t, counts)

@@ -157,27 +157,45 @@ class BatchedRunner:
 
     def pack_bodies_device(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None):
         """PackedFleet in HBM from raw bodies, parsed on the device (krr_amd.core.device_pack)."""
-        from krr_amd.core.device_pack import default_packer
-        from krr_amd.core.engine import default_engine
         from krr_amd.core.packing import PackedFleet
 
-        dev = getattr(self.strategy.settings, "device", 0) if device is None else int(device)
-        ctx = default_engine(dev).context()  # NativeUnavailable without a GPU
-        packer = default_packer(ctx)
-        if threads:
-            packer.threads = int(threads)
+        packer = self._device_packer(threads, device)
         cpu = packer.pack(cpu_bodies)
         mem = packer.pack(mem_bodies)
         self.last_pack_via = (cpu.via, mem.via)
         return PackedFleet(cpu.series, mem.series)
 
     def recommend_from_grouped(self, plan, cpu_bodies: Sequence[bytes], mem_bodies: Sequence[bytes],
-                               threads: int = 0) -> list[RunResult]:
+                               threads: int = 0, parser: str = "device") -> list[RunResult]:
         """As recommend_from_bodies, from fleet-batched responses: ``plan`` is a
         krr_amd.core.fleet_query.FleetQueryPlan and bodies[g] answers its g-th grouped
-        ``sum by (pod)`` query (one per (namespace, container), not one per pod)."""
-        return self.recommend_packed(plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads,
-                                                     alloc=_pinned_alloc_or_none()))
+        ``sum by (pod)`` query (one per (namespace, container), not one per pod).
+        ``parser="device"``: the MI355X parses the bodies and the host routes series to
+        pods by label (krr_amd.core.device_pack); ``"host"``: krr_pack_parse_grouped."""
+        return self.recommend_packed(self.pack_grouped(plan, cpu_bodies, mem_bodies, threads=threads, parser=parser))
+
+    def pack_grouped(self, plan, cpu_bodies, mem_bodies, threads: int = 0, parser: str = "device"):
+        from krr_amd.core.packing import PackedFleet
+
+        if parser not in ("device", "host"):
+            raise ValueError("parser must be 'device' or 'host'")
+        if parser == "host":
+            return plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads, alloc=_pinned_alloc_or_none())
+        packer = self._device_packer(threads)
+        cpu = packer.pack_grouped(plan, cpu_bodies)
+        mem = packer.pack_grouped(plan, mem_bodies)
+        self.last_pack_via = (cpu.via, mem.via)
+        return PackedFleet(cpu.series, mem.series)
+
+    def _device_packer(self, threads: int = 0, device: Optional[int] = None):
+        from krr_amd.core.device_pack import default_packer
+        from krr_amd.core.engine import default_engine
+
+        dev = getattr(self.strategy.settings, "device", 0) if device is None else int(device)
+        packer = default_packer(default_engine(dev).context())  # NativeUnavailable without a GPU
+        if threads:
+            packer.threads = int(threads)
+        return packer
 
     def allocations(self, objects: Sequence[K8sObjectData],
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:

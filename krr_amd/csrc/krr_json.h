@@ -66,13 +66,11 @@ struct StagedLoad {
 // bytes, 16-B loads; 64 readable bytes past every body make the loads safe), each lane
 // finds the '[' in its own 32 bytes (a bit mask from registers) and parses the elements
 // starting there from LDS, one at a time.
-__device__ bool values_array(const JsonArgs& A, const char* vs, const char* e, double* tv, double* tt, int lane,
-                             unsigned char* lds, int64_t* count, const char** vend) {
-    const char* const buf = A.bodies;
+__device__ bool values_array(const char* const buf, bool want_ts, const char* vs, const char* e, double* tv, double* tt,
+                             int lane, unsigned char* lds, int64_t* count, const char** vend) {
     const int64_t lo_abs = vs - buf, hi_abs = e - buf;
     int64_t blk = lo_abs & ~(int64_t)(kLaneBytes - 1);
     int64_t cnt = 0;
-    const bool want_ts = A.want_ts != 0;
     for (; blk < hi_abs; blk += kBlockBytes) {
         // stage [blk, blk + 4 KiB): lane l's 32 bytes at 32 l and at 2 KiB + 32 l
         const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
@@ -200,8 +198,8 @@ __global__ __launch_bounds__(64) void k_json_parse(JsonArgs A) {
                 vend = vs + 1;
             } else if (vs < e && *vs == '[') {
                 // phase 2 (all lanes): the samples
-                ok = values_array(A, vs, e, A.tmp_v + (ob >> 3), A.tmp_t ? A.tmp_t + (ob >> 3) : nullptr, lane,
-                                  lds, &count, &vend);
+                ok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (ob >> 3),
+                                  A.tmp_t ? A.tmp_t + (ob >> 3) : nullptr, lane, lds, &count, &vend);
             }
             // phase 3 (lane 0): the rest of the body
             if (ok) {
@@ -241,6 +239,114 @@ __global__ __launch_bounds__(256) void k_json_compact(CompactArgs C) {
         for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
             C.values[dst + j] = C.tmp_v[src + j];
             if (C.ts) C.ts[dst + j] = C.tmp_t[src + j];
+        }
+    }
+}
+
+
+// ---- grouped bodies ("sum by (pod) (...)"): every series, routed by a label later ----
+constexpr int kSeriesRecWords = 6;  // body, index in data.result, label offset (-1: none), label length,
+                                    // scratch slot of its values, count
+constexpr int kMaxLabel = 64;
+
+struct SeriesArgs {
+    const char* bodies;
+    const int64_t* offs;
+    int64_t first, n;
+    int32_t want_ts;
+    int32_t label_len;
+    const char* label;              // device copy of the routing label key
+    double* tmp_v;
+    double* tmp_t;
+    int64_t* recs;                  // [rec_cap][kSeriesRecWords]
+    int64_t rec_cap;
+    unsigned long long* rec_count;  // appended with atomics (order restored by (body, index))
+    int32_t* status;
+};
+
+// One body per wave: lane 0 walks the envelope and every series (GroupedWalker), all 64
+// lanes parse each values array (values_array, scratch slot = the array's byte offset / 8),
+// lane 0 appends one record per series.
+__global__ __launch_bounds__(64) void k_json_series(SeriesArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
+    const int lane = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < A.n; i += gridDim.x) {
+        const int64_t bi = A.first + i;
+        const int64_t ob = A.offs[bi], oe = A.offs[bi + 1];
+        const char* s = A.bodies + ob;
+        const char* e = A.bodies + oe;
+        GroupedWalker W;
+        if (lane == 0) W.init(s, e, A.label, A.label_len);
+        int32_t status = JSON_HOST;
+        for (;;) {
+            int ev = W_HOST;
+            int64_t at = 0;
+            if (lane == 0) {
+                ev = W.step();
+                if (ev == W_VALUES) at = W.values_at - A.bodies;
+            }
+            ev = (int)__builtin_amdgcn_readfirstlane(ev);
+            at = (int64_t)uni64((uint64_t)at);
+            if (ev == W_HOST) break;
+            if (ev == W_DONE) {
+                status = JSON_OK;
+                break;
+            }
+            if (ev == W_SERIES) {
+                int ok = 1;
+                if (lane == 0) {
+                    const unsigned long long k = atomicAdd(A.rec_count, 1ull);
+                    if ((int64_t)k < A.rec_cap) {
+                        int64_t* r = A.recs + (int64_t)k * kSeriesRecWords;
+                        r[0] = bi;
+                        r[1] = W.index;
+                        r[2] = W.lab ? (int64_t)(W.lab - A.bodies) : -1;
+                        r[3] = W.lab_len;
+                        r[4] = (W.values_at - A.bodies) >> 3;
+                        r[5] = W.count;
+                    } else {
+                        ok = 0;  // more series than the table holds: the host's call
+                    }
+                }
+                if (!__builtin_amdgcn_readfirstlane(ok)) break;
+                continue;
+            }
+            // W_VALUES: the array's first byte is at `at`
+            const char* vs = A.bodies + at;
+            const char* vend = nullptr;
+            int64_t count = 0;
+            bool ok = false;
+            if (vs < e && *vs == ']') {
+                ok = true;
+                vend = vs + 1;
+            } else if (vs < e && *vs == '[') {
+                ok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (at >> 3),
+                                  A.tmp_t ? A.tmp_t + (at >> 3) : nullptr, lane, lds, &count, &vend);
+            }
+            if (!ok) break;
+            if (lane == 0) W.values_done(vend, count);
+        }
+        if (lane == 0) A.status[bi] = status;
+    }
+}
+
+struct GatherArgs {
+    const int64_t* src;    // scratch slot of item j's first value
+    const int64_t* count;  // its values (< 0: nothing)
+    const int64_t* dst;    // its place in the CSR
+    const double* tmp_v;
+    const double* tmp_t;
+    double* values;
+    double* ts;
+    int64_t n;
+};
+
+__global__ __launch_bounds__(256) void k_json_gather(GatherArgs G) {
+    for (int64_t j = blockIdx.x; j < G.n; j += gridDim.x) {
+        const int64_t n = G.count[j], src = G.src[j], dst = G.dst[j];
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+            G.values[dst + k] = G.tmp_v[src + k];
+            if (G.ts) G.ts[dst + k] = G.tmp_t[src + k];
         }
     }
 }

@@ -534,5 +534,182 @@ KRR_JHD inline bool envelope_tail(Reader& r, Envelope env) {
     return r.p == r.e && env.have_status && env.ok_status;
 }
 
+
+// ---- grouped responses: every series of data.result, routed by a metric label ----
+// ("sum by (pod) (...)" bodies, krr_amd.core.fleet_query; the host restatement is
+// krr_pack.cpp parse_series_set).  A resumable walk over the envelope: step() runs until
+// the next values array starts (W_VALUES: the caller parses it, then values_done()), a
+// series ends (W_SERIES: its label span and values are final), or the body ends
+// (W_DONE) / leaves the device grammar (W_HOST).
+enum : int { W_HOST = 0, W_VALUES = 1, W_SERIES = 2, W_DONE = 3 };
+
+struct GroupedWalker {
+    enum : int { TOP_OPEN, TOP_KEY, TOP_NEXT, DATA_KEY, DATA_NEXT, SERIES_OPEN, SERIES_KEY, SERIES_NEXT, RESULT_NEXT };
+    Reader r;
+    const char* label;   // the routing label key (no escapes)
+    int64_t label_len;
+    int state;
+    bool have_status, ok_status, have_result, have_data;
+    // the current series
+    int64_t index;        // 0-based position in data.result
+    const char* lab;      // its label value (raw bytes, no escapes) or nullptr
+    int64_t lab_len;
+    bool have_values, have_metric;
+    const char* values_at;  // its values array's first byte after '['
+    int64_t count;
+
+    KRR_JHD void init(const char* s, const char* e, const char* lbl, int64_t lbl_len) {
+        r.p = s;
+        r.e = e;
+        label = lbl;
+        label_len = lbl_len;
+        state = TOP_OPEN;
+        have_status = ok_status = have_result = have_data = false;
+        index = -1;
+    }
+    KRR_JHD bool key_is(const char* kb, int64_t kn, const char* k, int64_t n) const {
+        if (kn != n) return false;
+        for (int64_t i = 0; i < n; ++i)
+            if (kb[i] != k[i]) return false;
+        return true;
+    }
+    KRR_JHD void values_done(const char* vend, int64_t n) {
+        r.p = vend;
+        count = n;
+        state = SERIES_NEXT;
+    }
+    KRR_JHD int step() {
+        for (;;) {
+            switch (state) {
+                case TOP_OPEN:
+                    if (!r.lit('{') || r.peek('}')) return W_HOST;
+                    state = TOP_KEY;
+                    break;
+                case TOP_KEY: {
+                    const char* kb;
+                    int64_t kn;
+                    bool kesc;
+                    if (!r.str(&kb, &kn, &kesc) || kesc || !r.lit(':')) return W_HOST;
+                    if (key_is(kb, kn, "status", 6)) {
+                        const char* vb;
+                        int64_t vn;
+                        bool vesc;
+                        if (!r.str(&vb, &vn, &vesc) || vesc) return W_HOST;
+                        have_status = true;
+                        ok_status = key_is(vb, vn, "success", 7);
+                        state = TOP_NEXT;
+                    } else if (key_is(kb, kn, "data", 4)) {
+                        if (have_data || !r.lit('{')) return W_HOST;
+                        have_data = true;
+                        state = r.lit('}') ? TOP_NEXT : DATA_KEY;
+                    } else {
+                        if (!r.skip()) return W_HOST;
+                        state = TOP_NEXT;
+                    }
+                    break;
+                }
+                case TOP_NEXT:
+                    if (r.lit(',')) {
+                        state = TOP_KEY;
+                        break;
+                    }
+                    if (!r.lit('}')) return W_HOST;
+                    r.ws();
+                    return (r.p == r.e && have_status && ok_status && have_result) ? W_DONE : W_HOST;
+                case DATA_KEY: {
+                    const int k = r.key("result");
+                    if (k < 0) return W_HOST;
+                    if (k == 0) {
+                        if (!r.skip()) return W_HOST;
+                        state = DATA_NEXT;
+                        break;
+                    }
+                    if (have_result || !r.lit('[')) return W_HOST;
+                    have_result = true;
+                    state = r.lit(']') ? DATA_NEXT : SERIES_OPEN;
+                    break;
+                }
+                case DATA_NEXT:
+                    if (r.lit(',')) {
+                        state = DATA_KEY;
+                        break;
+                    }
+                    if (!r.lit('}')) return W_HOST;
+                    state = TOP_NEXT;
+                    break;
+                case SERIES_OPEN:
+                    if (!r.lit('{') || r.peek('}')) return W_HOST;  // a series without values: the host's error
+                    ++index;
+                    lab = nullptr;
+                    lab_len = 0;
+                    have_values = have_metric = false;
+                    values_at = nullptr;
+                    count = 0;
+                    state = SERIES_KEY;
+                    break;
+                case SERIES_KEY: {
+                    const char* kb;
+                    int64_t kn;
+                    bool kesc;
+                    if (!r.str(&kb, &kn, &kesc) || kesc || !r.lit(':')) return W_HOST;
+                    if (key_is(kb, kn, "metric", 6)) {
+                        if (have_metric || !r.lit('{')) return W_HOST;
+                        have_metric = true;
+                        if (!r.lit('}')) {
+                            for (;;) {
+                                const char* lb;
+                                int64_t ln;
+                                bool lesc;
+                                if (!r.str(&lb, &ln, &lesc) || lesc || !r.lit(':')) return W_HOST;
+                                if (key_is(lb, ln, label, label_len)) {
+                                    const char* vb;
+                                    int64_t vn;
+                                    bool vesc;
+                                    if (!r.str(&vb, &vn, &vesc) || vesc) return W_HOST;
+                                    lab = vb;  // the last one, as the host keeps it
+                                    lab_len = vn;
+                                } else if (!r.skip()) {
+                                    return W_HOST;
+                                }
+                                if (r.lit(',')) continue;
+                                if (!r.lit('}')) return W_HOST;
+                                break;
+                            }
+                        }
+                        state = SERIES_NEXT;
+                    } else if (key_is(kb, kn, "values", 6)) {
+                        if (have_values || !r.lit('[')) return W_HOST;
+                        have_values = true;
+                        values_at = r.p;
+                        return W_VALUES;  // the caller parses the array, then values_done()
+                    } else {
+                        if (!r.skip()) return W_HOST;
+                        state = SERIES_NEXT;
+                    }
+                    break;
+                }
+                case SERIES_NEXT:
+                    if (r.lit(',')) {
+                        state = SERIES_KEY;
+                        break;
+                    }
+                    if (!r.lit('}') || !have_values) return W_HOST;
+                    state = RESULT_NEXT;
+                    return W_SERIES;
+                case RESULT_NEXT:
+                    if (r.lit(',')) {
+                        state = SERIES_OPEN;
+                        break;
+                    }
+                    if (!r.lit(']')) return W_HOST;
+                    state = DATA_NEXT;
+                    break;
+                default:
+                    return W_HOST;
+            }
+        }
+    }
+};
+
 }  // namespace json
 }  // namespace krr

@@ -3277,6 +3277,7 @@ struct krr_ctx {
     hipEvent_t fail_ev;
     hipStream_t fail_stream;
     bool fail_ev_valid;
+    char* d_label;                // krr_json_parse_series: the routing label key (device copy)
     char err[512];
 };
 
@@ -3453,6 +3454,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->fail_ev = nullptr;
     c->fail_stream = nullptr;
     c->fail_ev_valid = false;
+    c->d_label = nullptr;
     if (hipEventCreateWithFlags(&c->fail_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return KRR_E_HIP;
@@ -3489,6 +3491,7 @@ int krr_destroy(krr_ctx* ctx) {
     if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
     if (ctx->d_fail_count) (void)hipFree(ctx->d_fail_count);
     if (ctx->d_fail_list) (void)hipFree(ctx->d_fail_list);
+    if (ctx->d_label) (void)hipFree(ctx->d_label);
     if (ctx->fail_ev) (void)hipEventDestroy(ctx->fail_ev);
     delete ctx;
     return KRR_OK;
@@ -4071,6 +4074,60 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
                         values, timestamps, b->n_bodies};
     const int64_t grid = b->n_bodies < 65536 ? b->n_bodies : 65536;
     hipLaunchKernelGGL(json::k_json_compact, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, C);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_json_parse_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, const char* label,
+                          int32_t want_timestamps, double* scratch_values, double* scratch_ts, int64_t* records,
+                          int64_t rec_cap, uint64_t* n_records, int32_t* status, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!b || b->n_bodies < 0 || first < 0 || n < 0 || first + n > b->n_bodies || rec_cap < 0)
+        return set_err(ctx, KRR_E_INVALID, "json: bad body range%s", "");
+    if (!label) return set_err(ctx, KRR_E_INVALID, "json: null label%s", "");
+    const size_t ll = strlen(label);
+    if (ll >= (size_t)json::kMaxLabel) return set_err(ctx, KRR_E_INVALID, "json: label longer than 63 bytes%s", "");
+    if (n == 0) return KRR_OK;
+    if (!b->bodies || !b->body_offsets || !scratch_values || !records || !n_records || !status ||
+        (want_timestamps && !scratch_ts))
+        return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    if (((uintptr_t)b->bodies & 15) != 0) return set_err(ctx, KRR_E_INVALID, "json: bodies not 16-byte aligned%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    json::SeriesArgs A{};
+    A.bodies = b->bodies;
+    A.offs = b->body_offsets;
+    A.first = first;
+    A.n = n;
+    A.want_ts = want_timestamps ? 1 : 0;
+    if (!ctx->d_label) KRR_HIP(ctx, hipMalloc(&ctx->d_label, json::kMaxLabel));
+    KRR_HIP(ctx, hipMemcpyAsync(ctx->d_label, label, ll + 1, hipMemcpyHostToDevice, (hipStream_t)stream));
+    A.label_len = (int32_t)ll;
+    A.label = ctx->d_label;
+    A.tmp_v = scratch_values;
+    A.tmp_t = want_timestamps ? scratch_ts : nullptr;
+    A.recs = records;
+    A.rec_cap = rec_cap;
+    A.rec_count = (unsigned long long*)n_records;
+    A.status = status;
+    hipLaunchKernelGGL(json::k_json_series, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_json_gather(krr_ctx* ctx, int64_t n_items, const int64_t* src, const int64_t* count, const int64_t* dst,
+                    const double* scratch_values, const double* scratch_ts, double* values, double* timestamps,
+                    void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (n_items < 0) return set_err(ctx, KRR_E_INVALID, "json: negative item count%s", "");
+    if (n_items == 0) return KRR_OK;
+    if (!src || !count || !dst || !scratch_values || !values || (timestamps && !scratch_ts))
+        return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    json::GatherArgs G{src, count, dst, scratch_values, timestamps ? scratch_ts : nullptr, values, timestamps, n_items};
+    const int64_t grid = n_items < 65536 ? n_items : 65536;
+    hipLaunchKernelGGL(json::k_json_gather, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, G);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -112,7 +112,8 @@ async def gather_objects_recommendations(runner: Any, objects: Sequence[Any]) ->
         results = await asyncio.to_thread(batched.recommend_from_bodies, cpu_bodies, mem_bodies, 0,
                                           _options(runner).get("parser", "device"))
     elif loader == "grouped":
-        fleet = await fetch_grouped_fleet(runner, objects, settings)
+        fleet = await fetch_grouped_fleet(runner, objects, settings, _options(runner).get("parser", "device"),
+                                          batched)
         results = await asyncio.to_thread(batched.recommend_packed, fleet)
     else:
         async def history(obj):  # runner.py:88-102, with the reference's own loaders
@@ -188,7 +189,7 @@ async def fetch_pod_bodies(runner: Any, objects: Sequence[Any], settings) -> tup
     return tuple(await asyncio.gather(cpu, mem))  # type: ignore[return-value]
 
 
-async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings):
+async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings, parser: str = "host", batched=None):
     """The fleet's PackedFleet from grouped ``sum by (pod)`` queries: one FleetQueryPlan per
     cluster (each cluster has its own Prometheus), packed natively, then the clusters'
     segments put back in fleet order for ONE kernel pass."""
@@ -205,8 +206,12 @@ async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings):
         plan = FleetQueryPlan.for_settings([objects[i] for i in idx], settings)
         q = query_range_fn(runner._get_prometheus_loader(cluster).prometheus, start, end, step)
         bodies = await asyncio.to_thread(plan.fetch, q)
-        fleet = await asyncio.to_thread(plan.pack_fleet, bodies[HipResourceType.CPU],
-                                        bodies[HipResourceType.Memory])
+        if parser == "device" and batched is not None:  # parsed on the MI355X, routed by pod label
+            fleet = await asyncio.to_thread(batched.pack_grouped, plan, bodies[HipResourceType.CPU],
+                                            bodies[HipResourceType.Memory], 0, "device")
+        else:
+            fleet = await asyncio.to_thread(plan.pack_fleet, bodies[HipResourceType.CPU],
+                                            bodies[HipResourceType.Memory])
         parts.append((idx, fleet))
     if len(parts) == 1 and parts[0][0] == list(range(len(objects))):
         return parts[0][1]
@@ -218,9 +223,26 @@ async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings):
 
 def _reorder(series: list, order: list, alloc=None):
     """Concatenate PackedSeries whose segments are objects ``order`` and permute the segments
-    into object order 0..n-1."""
+    into object order 0..n-1 (numpy on the host, or torch for series already in HBM)."""
     from krr_amd.core.packing import PackedSeries
 
+    if series and not isinstance(series[0].values, np.ndarray):  # device packer output (torch, HBM)
+        import torch
+
+        dev = series[0].values.device
+        lens = torch.cat([s.offsets[1:] - s.offsets[:-1] for s in series])
+        bases = torch.tensor(np.cumsum([0] + [int(s.values.numel()) for s in series])[:-1], device=dev)
+        srcs = torch.cat([s.offsets[:-1] + b for s, b in zip(series, bases)])
+        flat = torch.cat([s.values for s in series])
+        inv = torch.empty(len(order), dtype=torch.int64, device=dev)
+        inv[torch.tensor(order, dtype=torch.int64, device=dev)] = torch.arange(len(order), device=dev)
+        lens_o, srcs_o = lens[inv], srcs[inv]
+        offsets = torch.zeros(len(order) + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens_o, 0, out=offsets[1:])
+        total = int(offsets[-1].item())
+        seg = torch.repeat_interleave(torch.arange(len(order), device=dev), lens_o)
+        pos = torch.arange(total, device=dev) - offsets[:-1][seg] + srcs_o[seg]
+        return PackedSeries(flat[pos], offsets, max(s.max_len for s in series))
     lens = np.concatenate([np.diff(s.offsets) for s in series]) if series else np.zeros(0, np.int64)
     srcs = np.concatenate([s.offsets[:-1] + base for s, base in
                            zip(series, np.cumsum([0] + [s.values.size for s in series])[:-1])]) \

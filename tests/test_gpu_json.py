@@ -179,3 +179,67 @@ def test_recommend_from_bodies_device_equals_host():
     b = runner.recommend_from_bodies(cpu, mem, parser="host")
     assert [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in a] == \
            [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in b]
+
+
+# ---- grouped bodies (fleet PromQL batching): krr_json_parse_series + krr_pack_match_grouped ----
+
+def _recompact(b: bytes) -> bytes:
+    return json.dumps(json.loads(b), separators=(",", ":")).encode()
+
+
+@pytest.mark.parametrize("max_chars", [6000, 40, 1])
+@pytest.mark.parametrize("resource", ["cpu", "memory"])
+def test_grouped_bodies_on_device_equal_host_plan(packer, resource, max_chars):
+    """tests/test_fleet_query.py's fleet (regex-metacharacter pod names, restarts summed per
+    pod, decoy series, shuffled series order, duplicated and ghost pods): the device parse
+    routed by pod label gives plan.pack's CSR, timestamps and pod counts bit for bit."""
+    from test_fleet_query import make_fleet
+
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.core.models.allocations import ResourceType
+
+    objects, prom = make_fleet()
+    plan = FleetQueryPlan(objects, max_query_chars=max_chars)
+    rt = ResourceType(resource)
+    bodies = [_recompact(prom.query_range(q)) for q in plan.queries(rt)]
+    want, want_ts, want_counts = plan.pack(bodies, want_timestamps=True, return_pod_counts=True)
+    dp = packer.pack_grouped(plan, bodies, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "device"
+    assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+    assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+    assert np.array_equal(dp.timestamps.cpu().numpy().view(np.uint64), want_ts.view(np.uint64))
+    assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+    assert dp.series.max_len == want.max_len
+    # as json.dumps wrote them (spaces): the host decides, same result
+    raw = [prom.query_range(q) for q in plan.queries(rt)]
+    dh = packer.pack_grouped(plan, raw, want_timestamps=True, return_pod_counts=True)
+    assert dh.via == "host" and np.array_equal(dh.series.values.view(np.uint64), want.values.view(np.uint64))
+
+
+def test_grouped_large_bodies(packer):
+    """Groups of 40 pods x 10,080 samples per body (several MB per body, many blocks per
+    series), pods listed in another order than the series."""
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.utils.prom_decimal import prom_format
+
+    class Obj:
+        def __init__(self, ns, c, pods):
+            self.namespace, self.container, self.pods = ns, c, pods
+
+    rng = np.random.default_rng(12)
+    objects = [Obj(f"ns{g}", "app", [f"pod-{g}-{k}" for k in range(int(rng.integers(1, 4)))]) for g in range(40)]
+    plan = FleetQueryPlan(objects, max_query_chars=400)
+    bodies = []
+    for grp in plan.groups:
+        res = []
+        for pod in reversed(grp.pods):
+            xs = rng.gamma(2.0, 0.05, 10080)
+            res.append({"metric": {"pod": pod}, "values": [[1700000000 + 60 * k, prom_format(float(x))]
+                                                           for k, x in enumerate(xs)]})
+        bodies.append(_compact({"status": "success", "data": {"resultType": "matrix", "result": res}}))
+    want, want_counts = plan.pack(bodies, return_pod_counts=True)
+    dp = packer.pack_grouped(plan, bodies, return_pod_counts=True)
+    assert dp.via == "device"
+    assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+    assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+    assert np.array_equal(np.asarray(dp.pod_counts), want_counts)

@@ -108,3 +108,26 @@ def test_install_rejects_unknown_switches():
     assert R._collect_result.__qualname__.endswith("R._collect_result")
     integration.uninstall(R)
     assert R._gather_objects_recommendations.__qualname__.endswith("R._gather_objects_recommendations")
+
+
+def test_reorder_of_tensor_series_equals_numpy():
+    """_reorder on series held as torch tensors (the device packer's output lives in HBM;
+    here CPU tensors) gives the numpy path's CSR."""
+    import torch
+
+    from krr_amd.core.packing import PackedSeries
+
+    rng = np.random.default_rng(4)
+    parts = []
+    for k in range(3):
+        lens = rng.integers(0, 7, size=int(rng.integers(1, 6)))
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        parts.append(PackedSeries(rng.random(int(offs[-1])), offs, int(lens.max(initial=0))))
+    n = sum(p.n_segments for p in parts)
+    order = list(rng.permutation(n))
+    want = integration._reorder(parts, order)
+    tparts = [PackedSeries(torch.from_numpy(p.values), torch.from_numpy(p.offsets), p.max_len) for p in parts]
+    got = integration._reorder(tparts, order)
+    assert np.array_equal(got.offsets.numpy(), want.offsets)
+    assert np.array_equal(got.values.numpy(), want.values)
+    assert got.max_len == want.max_len

@@ -209,3 +209,72 @@ def test_non_canonical_bodies_go_to_the_host(lib, kind):
         pack_query_range_bodies([[b]])
     except PrometheusResponseError:
         pass
+
+
+def _grouped(lib, b, label="pod", want_ts=1):
+    cap = len(b) // 8 + 1
+    ms = len(b) // 20 + 2
+    lo = np.empty(ms, np.int64)
+    ll = np.empty(ms, np.int64)
+    cn = np.empty(ms, np.int64)
+    v = np.empty(cap)
+    t = np.empty(cap)
+    ns = ctypes.c_int64()
+    lib.json_check_grouped.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int] + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                 ctypes.POINTER(ctypes.c_int64)]
+    rc = lib.json_check_grouped(b, len(b), label.encode(), want_ts, lo.ctypes.data, ll.ctypes.data, cn.ctypes.data,
+                                ms, v.ctypes.data, t.ctypes.data, cap, ctypes.byref(ns))
+    n = ns.value
+    return rc, [(None if lo[i] < 0 else b[lo[i]:lo[i] + ll[i]].decode(), int(cn[i])) for i in range(n)], v, t
+
+
+def test_grouped_bodies_walk_like_the_host_packer(lib):
+    """Every series of grouped (`sum by (pod)`) bodies, in order, with its pod label and
+    values — against the host packer's parse_series (krr_pack_parse_series)."""
+    from krr_amd.core.prom_native import parse_series
+
+    rng = np.random.default_rng(9)
+    for i in range(60):
+        res = []
+        for j in range(int(rng.integers(0, 6))):
+            m = int(rng.integers(0, 50))
+            xs = rng.gamma(2.0, 0.05, m)
+            metric = {"pod": f"p{i}-{j % 3}", "namespace": "n"} if rng.random() < 0.85 else {"namespace": "n"}
+            if rng.random() < 0.2:
+                metric = {"zz": {"nested": [1, 2, {"a": None}]}, **metric}
+            ser = {"metric": metric, "values": [[1.7e9 + 15 * k, go_format(float(x))] for k, x in enumerate(xs)]}
+            if rng.random() < 0.2:
+                ser = {"values": ser["values"], "metric": metric, "extra": True}
+            res.append(ser)
+        doc = {"status": "success", "data": {"resultType": "matrix", "result": res}}
+        b = _compact(doc)
+        rc, got, v, t = _grouped(lib, b)
+        assert rc == JSON_OK, b[:300]
+        want = parse_series(b, "pod", want_timestamps=True)
+        assert [(g[0], g[1]) for g in got] == [(w[0], len(w[1])) for w in want]
+        flat_v = np.concatenate([w[1] for w in want]) if want else np.zeros(0)
+        flat_t = np.concatenate([w[2] for w in want]) if want else np.zeros(0)
+        k = flat_v.size
+        assert np.array_equal(v[:k].view(np.uint64), flat_v.view(np.uint64))
+        assert np.array_equal(t[:k].view(np.uint64), flat_t.view(np.uint64))
+
+
+@pytest.mark.parametrize("kind", ["escaped_label", "dup_metric", "dup_values", "no_values", "spaces", "status",
+                                  "escaped_label_key", "empty_series"])
+def test_grouped_non_canonical_go_to_the_host(lib, kind):
+    base = {"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {"pod": "a"}, "values": [[1, "1"]]}, {"metric": {"pod": "b"}, "values": [[1, "2"]]}]}}
+    b = _compact(base)
+    b = {
+        "escaped_label": b.replace(b'"pod":"a"', b'"pod":"\\u0061"'),
+        "dup_metric": b.replace(b'{"metric":{"pod":"a"},', b'{"metric":{"pod":"a"},"metric":{},'),
+        "dup_values": b.replace(b'"values":[[1,"1"]]}', b'"values":[[1,"1"]],"values":[]}'),
+        "no_values": b.replace(b',"values":[[1,"1"]]', b''),
+        "spaces": json.dumps(base).encode(),
+        "status": b.replace(b'"success"', b'"error"'),
+        "escaped_label_key": b.replace(b'{"pod":"a"}', b'{"p\\u006fd":"a"}'),
+        "empty_series": b.replace(b'{"metric":{"pod":"a"},"values":[[1,"1"]]}', b'{}'),
+    }[kind]
+    rc, _, _, _ = _grouped(lib, b)
+    assert rc == JSON_HOST
