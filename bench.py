@@ -772,7 +772,9 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
       copied to HBM raw and parsed there, one wave per body) on the same bodies;
     * e2e_objects_per_s: BatchedRunner.recommend_from_bodies on the same bodies (device
       parse -> fused kernel -> exact-decimal rounding -> RunResults); e2e_objects_per_s_host_parse
-      the same with the host packer.
+      the same with the host packer;
+    * e2e_grouped_objects_per_s(_host_parse): the same fleet as grouped `sum by (pod)` bodies
+      (20 namespaces; krr_amd.core.fleet_query), BatchedRunner.recommend_from_grouped.
     Bodies are Prometheus-formatted (shortest-repr sample strings); `distinct` random pod
     series per resource are reused across the fleet (the packer's cost is per byte)."""
     import torch
@@ -808,9 +810,15 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         return ('{"status":"success","data":{"resultType":"matrix","result":[{"metric":{"pod":"p"},"values":['
                 + vals + ']}]}}').encode()
 
+    def values_part(xs):
+        return ",".join(f'[{t},"{x!r}"]' for t, x in zip(ts, xs.tolist()))
+
     t_g = time.perf_counter()
-    cpu_pool = [body(rng.gamma(2.0, 0.05, L)) for _ in range(distinct)]
-    mem_pool = [body(np.floor(rng.normal(2e8, 2e7, L))) for _ in range(distinct)]
+    cpu_vals = [values_part(rng.gamma(2.0, 0.05, L)) for _ in range(distinct)]
+    mem_vals = [values_part(np.floor(rng.normal(2e8, 2e7, L))) for _ in range(distinct)]
+    head = '{"status":"success","data":{"resultType":"matrix","result":['
+    cpu_pool = [(head + '{"metric":{"pod":"p"},"values":[' + v + ']}]}}').encode() for v in cpu_vals]
+    mem_pool = [(head + '{"metric":{"pod":"p"},"values":[' + v + ']}]}}').encode() for v in mem_vals]
     t_g = time.perf_counter() - t_g
     cpu_b = [[cpu_pool[(o * pods + i) % distinct] for i in range(pods)] for o in range(objects)]
     mem_b = [[mem_pool[(o * pods + i * 7) % distinct] for i in range(pods)] for o in range(objects)]
@@ -854,12 +862,48 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         torch.cuda.synchronize()
         best_d = min(best_d, time.perf_counter() - t0)
     out["device_pack_samples_per_s"] = samples / best_d
+    # --- the same fleet through fleet-batched queries: one `sum by (pod)` body per
+    # (namespace, container) group (krr_amd.core.fleet_query), 20 namespaces
+    from krr_amd.core.fleet_query import FleetQueryPlan
+
+    class _Obj:
+        def __init__(self, o):
+            self.namespace, self.container = f"ns{o % 20}", "main"
+            self.pods = [f"pod-{o}-{i}" for i in range(pods)]
+
+    fleet_objs = [_Obj(o) for o in range(objects)]
+    plan = FleetQueryPlan.for_settings(fleet_objs, runner.strategy.settings)
+
+    def grouped(vals, shift):
+        out_b = []
+        for gq in plan.groups:
+            parts = [f'{{"metric":{{"pod":"{pod}"}},"values":[{vals[(i + shift) % distinct]}]}}'
+                     for i, pod in enumerate(reversed(gq.pods))]
+            out_b.append((head + ",".join(parts) + ']}}').encode())
+        return out_b
+
+    g_cpu, g_mem = grouped(cpu_vals, 0), grouped(mem_vals, 7)
+    eg = {}
+    for parser in ("host", "device"):
+        best_g = float("inf")
+        for _ in range(2):
+            t0 = time.perf_counter()
+            res_g = runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)
+            best_g = min(best_g, time.perf_counter() - t0)
+        assert len(res_g) == objects
+        eg[parser] = (best_g, [(str(r[k].request), str(r[k].limit)) for r in res_g[:64] for k in r])
+    assert runner.last_pack_via == ("device", "device"), runner.last_pack_via
+    out["e2e_grouped_objects_per_s"] = objects / eg["device"][0]
+    out["e2e_grouped_objects_per_s_host_parse"] = objects / eg["host"][0]
+    out["e2e_grouped_device_equals_host"] = eg["device"][1] == eg["host"][1]
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",
         "bodies": f"{objects} objects x {pods} pods x {L} samples x 2 resources = {samples} samples, "
                   f"{json_bytes / 1e9:.2f} GB of query_range JSON ({distinct} distinct pod series per resource, "
                   f"generated in {t_g:.1f} s)",
         "pack_s": best, "device_pack_s": best_d, "e2e_s": e2e["device"][0], "e2e_host_parse_s": e2e["host"][0],
+        "grouped": f"{len(plan.groups)} grouped bodies per resource ({sum(len(b) for b in g_cpu) / 1e9:.2f} GB of "
+                   f"CPU JSON), e2e {eg['device'][0]:.3f} s device parse, {eg['host'][0]:.3f} s host parse",
         "threads": threads,
         "pack_GBps_json": json_bytes / best / 1e9, "device_pack_GBps_json": json_bytes / best_d / 1e9,
         "definition": "pack = krr_pack_parse/copy of every body on the host (CPU + memory); device_pack = "

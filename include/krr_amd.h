@@ -378,7 +378,7 @@ int krr_synth_fill_global(krr_ctx* ctx, double* values, const int64_t* offsets, 
  *   krr_json_compact  each KRR_JSON_OK body's run to values[out_pos[b] ..) — out_pos
  *                     the exclusive prefix sum of counts (the CSR of the caller's
  *                     objects follows from the counts, bodies in fleet order).
- * Buffers: bodies 16-byte aligned with 64 readable bytes past the last body;
+ * Buffers: bodies 16-byte aligned with 128 readable bytes past the last body;
  * scratch_values / scratch_ts hold body_offsets[n_bodies] / 8 + 1 doubles. */
 #define KRR_JSON_OK 0        /* parsed: counts[b] samples */
 #define KRR_JSON_DROPPED 1   /* data.result is empty: the pod is dropped (prometheus.py:154) */
@@ -397,19 +397,25 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
                      const double* scratch_ts, const int64_t* counts, const int32_t* status,
                      const int64_t* out_pos, double* values, double* timestamps, void* stream);
 
-/* Grouped bodies (`sum by (pod) (...)`, one series per pod; the host packer's
- * krr_pack_parse_grouped, include/krr_pack.h): every series of every body in
- * [first, first + n) is parsed (values to scratch slot values_at / 8) and described by
- * one record of 6 int64 appended at records[*n_records ...] (device counter, zeroed by
- * the caller; order: any — (body, index) restores it):
- *   {body, index in data.result, label value byte offset in `bodies` (-1: the metric has
- *    no `label`), label length, scratch slot of the first value, sample count}.
- * status[b] as krr_json_parse (KRR_JSON_HOST also when the records outgrow rec_cap).
- * The caller routes slots to series by label (krr_pack_match_grouped, include/krr_pack.h)
- * and moves the kept runs into the CSR with krr_json_gather. */
-int krr_json_parse_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, const char* label,
-                          int32_t want_timestamps, double* scratch_values, double* scratch_ts, int64_t* records,
-                          int64_t rec_cap, uint64_t* n_records, int32_t* status, void* stream);
+/* Grouped bodies (`sum by (pod) (...)`, one series per pod: the host packer's
+ * krr_pack_parse_grouped, include/krr_pack.h), one wave per SERIES:
+ *   krr_json_find_series    every `[{"metric":` / `,{"metric":` in the bodies: the absolute
+ *                           offset of its '{' appended at candidates[*n_candidates ..]
+ *                           (device counter, zeroed by the caller; any order; the count
+ *                           may exceed cap, then only cap are stored);
+ *   krr_json_parse_segments one series object per candidate (sorted starts, body_of[j] its
+ *                           body): segments[j] = 7 int64 {start, end (one past its '}', -1
+ *                           when it is not a series object), label value offset (-1: none),
+ *                           label length, scratch slot of its values (array offset / 8),
+ *                           count, ok}.
+ * The host then chains the segments from each body's envelope (krr_pack_route_grouped,
+ * include/krr_pack.h); a body whose series do not chain goes to the host packer.
+ * Bodies need 128 readable bytes past the last one. */
+int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t* candidates, int64_t cap,
+                         uint64_t* n_candidates, void* stream);
+int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
+                            int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
+                            double* scratch_ts, int64_t* segments, void* stream);
 /* values[dst[j] ..) = scratch_values[src[j] ..), count[j] values (count < 0: none); the same
  * for timestamps when both pointers are given. */
 int krr_json_gather(krr_ctx* ctx, int64_t n_items, const int64_t* src, const int64_t* count, const int64_t* dst,

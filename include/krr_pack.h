@@ -107,16 +107,21 @@ int krr_pack_parse_grouped(const char* const* bodies, const int64_t* body_lens, 
 int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
                     const int64_t* dst_offsets, char* dst, int32_t threads);
 
-/* Routing for the device packer's grouped bodies (include/krr_amd.h krr_json_parse_series):
- * records[r] = {body, index, label offset (-1: none), label length, scratch slot, count}
- * (any order), label bytes read from `bodies` (the staged host copy of the device buffer,
- * same offsets).  Slot s (body slot_body[s], pod name slot_names[slot_name_offsets[s] ..
- * slot_name_offsets[s+1])) takes the FIRST series of its body (lowest index) whose label
- * equals the name, as krr_pack_parse_grouped does: slot_src[s] / slot_count[s] = that
- * series' scratch slot and count, or -1 / -1 (dropped). */
-int krr_pack_match_grouped(const int64_t* records, int64_t n_records, const char* bodies, int64_t n_bodies,
-                           const int64_t* slot_body, const char* slot_names, const int64_t* slot_name_offsets,
-                           int64_t n_slots, int64_t* slot_src, int64_t* slot_count, int32_t threads);
+/* Routing for the device packer's grouped bodies (include/krr_amd.h krr_json_find_series /
+ * krr_json_parse_segments).  `bodies` is the staged host copy of the device buffer (same
+ * offsets).  Per body: the envelope is walked up to data.result's first series, the
+ * device's segments (n_segments x 7 int64 {start, end, label offset, label length,
+ * scratch slot, count, ok}, sorted by start) must chain from there, one series after
+ * the next, and the envelope's tail is walked (krr_json_parse.h chain_grouped);
+ * body_ok[b] = 0 when they do not (the caller parses the batch with
+ * krr_pack_parse_grouped).  Slot s (body slot_body[s], pod name slot_names[
+ * slot_name_offsets[s] .. slot_name_offsets[s+1])) takes the FIRST chained series of its
+ * body whose `label` equals the name, as krr_pack_parse_grouped does: slot_src[s] /
+ * slot_count[s] = its scratch slot and count, or -1 / -1 (dropped). */
+int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int64_t n_bodies, const char* label,
+                           const int64_t* segments, int64_t n_segments, const int64_t* slot_body,
+                           const char* slot_names, const int64_t* slot_name_offsets, int64_t n_slots,
+                           int64_t* slot_src, int64_t* slot_count, int32_t* body_ok, int32_t threads);
 
 #ifdef __cplusplus
 }

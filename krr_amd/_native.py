@@ -42,7 +42,8 @@ EXPORTED_SYMBOLS = (
     "krr_abi_version",
     "krr_json_parse",
     "krr_json_compact",
-    "krr_json_parse_series",
+    "krr_json_find_series",
+    "krr_json_parse_segments",
     "krr_json_gather",
     "krr_create",
     "krr_destroy",
@@ -272,8 +273,10 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse.restype = ctypes.c_int
         lib.krr_json_compact.argtypes = [vp, jb, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_compact.restype = ctypes.c_int
-        lib.krr_json_parse_series.argtypes = [vp, jb, i64, i64, ctypes.c_char_p, i32, vp, vp, vp, i64, vp, vp, vp]
-        lib.krr_json_parse_series.restype = ctypes.c_int
+        lib.krr_json_find_series.argtypes = [vp, jb, vp, i64, vp, vp]
+        lib.krr_json_find_series.restype = ctypes.c_int
+        lib.krr_json_parse_segments.argtypes = [vp, jb, vp, vp, i64, ctypes.c_char_p, i32, vp, vp, vp, vp]
+        lib.krr_json_parse_segments.restype = ctypes.c_int
         lib.krr_json_gather.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_gather.restype = ctypes.c_int
         if lib.krr_abi_version() != 1:
@@ -556,9 +559,9 @@ class Context:
 
     # --- device packer: query_range bodies in HBM -> CSR --------------------------------
     def json_bodies(self, bodies, body_offsets, total_bytes: int) -> KrrJsonBodies:
-        """bodies: uint8 device tensor (16-B aligned, >= 64 bytes past the last body);
+        """bodies: uint8 device tensor (16-B aligned, >= 128 bytes past the last body);
         body_offsets: int64 device tensor [n_bodies + 1]."""
-        _check_tensor(bodies, "uint8", int(total_bytes) + 64)
+        _check_tensor(bodies, "uint8", int(total_bytes) + 128)
         _check_tensor(body_offsets, "int64")
         if bodies.data_ptr() % 16:
             raise ValueError("bodies must be 16-byte aligned")
@@ -595,20 +598,26 @@ class Context:
             out_pos.data_ptr(), values.data_ptr(), timestamps.data_ptr() if timestamps is not None else None,
             self._stream(stream)))
 
-    def json_parse_series(self, jb: KrrJsonBodies, first: int, n: int, label: str, want_timestamps: bool,
-                          scratch_values, scratch_ts, records, n_records, status, stream=None) -> None:
-        """records: int64 [rec_cap, 6]; n_records: int64 [1] device counter (zeroed by the caller)."""
-        slots = jb.total_bytes // 8 + 1
-        _check_tensor(scratch_values, "float64", slots)
+    def json_find_series(self, jb: KrrJsonBodies, candidates, n_candidates, stream=None) -> None:
+        """candidates: int64 [cap]; n_candidates: int64 [1] device counter (zeroed by the caller)."""
+        _check_tensor(candidates, "int64")
+        _check_tensor(n_candidates, "int64", 1)
+        self._check(self._lib.krr_json_find_series(self._h, ctypes.byref(jb), candidates.data_ptr(),
+                                                   candidates.numel(), n_candidates.data_ptr(), self._stream(stream)))
+
+    def json_parse_segments(self, jb: KrrJsonBodies, starts, body_of, label: str, want_timestamps: bool,
+                            scratch_values, scratch_ts, segments, stream=None) -> None:
+        n = starts.numel()
+        _check_tensor(starts, "int64", n)
+        _check_tensor(body_of, "int64", n)
+        _check_tensor(segments, "int64", 7 * n)
+        _check_tensor(scratch_values, "float64", jb.total_bytes // 8 + 1)
         if want_timestamps:
-            _check_tensor(scratch_ts, "float64", slots)
-        _check_tensor(records, "int64")
-        _check_tensor(n_records, "int64", 1)
-        _check_tensor(status, "int32", jb.n_bodies)
-        self._check(self._lib.krr_json_parse_series(
-            self._h, ctypes.byref(jb), int(first), int(n), label.encode(), int(bool(want_timestamps)),
-            scratch_values.data_ptr(), scratch_ts.data_ptr() if want_timestamps else None, records.data_ptr(),
-            records.numel() // 6, n_records.data_ptr(), status.data_ptr(), self._stream(stream)))
+            _check_tensor(scratch_ts, "float64", jb.total_bytes // 8 + 1)
+        self._check(self._lib.krr_json_parse_segments(
+            self._h, ctypes.byref(jb), starts.data_ptr(), body_of.data_ptr(), n, label.encode(),
+            int(bool(want_timestamps)), scratch_values.data_ptr(), scratch_ts.data_ptr() if want_timestamps else None,
+            segments.data_ptr(), self._stream(stream)))
 
     def json_gather(self, src, count, dst, scratch_values, scratch_ts, values, timestamps=None, stream=None) -> None:
         n = src.numel()

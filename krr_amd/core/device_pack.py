@@ -89,8 +89,8 @@ class DevicePacker:
         boffs = np.zeros(nb + 1, dtype=np.int64)
         np.cumsum(lens, out=boffs[1:])
         total = int(boffs[-1])
-        stage = self._staging(total + 64)
-        d_bodies = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        stage = self._staging(total + 128)
+        d_bodies = torch.empty(total + 128, dtype=torch.uint8, device=dev)
         d_boffs = torch.from_numpy(boffs).to(dev)
         slots = total // 8 + 1
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
@@ -126,8 +126,9 @@ class DevicePacker:
                      return_pod_counts: bool = False, stream=None, label: str = "pod") -> DevicePacked:
         """``plan`` a krr_amd.core.fleet_query.FleetQueryPlan, bodies[g] the response to its
         g-th grouped query (one resource): the CSR ``plan.pack(bodies)`` builds on the host,
-        bit for bit, with the bodies parsed on the device (krr_json_parse_series) and routed
-        by pod label (krr_pack_match_grouped)."""
+        bit for bit, with the bodies parsed on the device one wave per series
+        (krr_json_find_series + krr_json_parse_segments) and chained and routed by pod label
+        on the host (krr_pack_route_grouped)."""
         with self._lock:
             return self._pack_grouped(plan, bodies, want_timestamps, return_pod_counts, stream, label)
 
@@ -151,31 +152,41 @@ class DevicePacker:
 
         if nb == 0 or ns == 0:
             return host_fallback(0)
-        total_guess = sum(len(b) for b in flat)
-        rec_cap = max(1024, total_guess // 256)
-        recs = torch.empty((rec_cap, 6), dtype=torch.int64, device=dev)
-        n_recs = torch.zeros(1, dtype=torch.int64, device=dev)
-        status = torch.empty(nb, dtype=torch.int32, device=dev)
+        status = None
 
-        def launch(jb, a, b, tmp_v, tmp_t):
-            self.ctx.json_parse_series(jb, a, b - a, label, want_ts, tmp_v, tmp_t, recs, n_recs, status, stream=st)
+        def launch(jb, a, b, tmp_v, tmp_t):  # the bodies are parsed once all are in HBM
+            pass
 
         lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
+        cap = max(1024, total // 4096)
+        cand = torch.empty(cap, dtype=torch.int64, device=dev)
+        n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ctx.json_find_series(jb, cand, n_cand, stream=st)
         with torch.cuda.stream(st):
-            summary = torch.stack([status.max().to(torch.int64), n_recs[0]]).cpu()  # the one sync
-        worst, nr = (int(x) for x in summary)
-        if worst == _native.KRR_JSON_HOST or nr > rec_cap:
-            return host_fallback(int((status == _native.KRR_JSON_HOST).sum().item()))
-        rec_h = recs[:nr].cpu().numpy()
+            nc = int(n_cand.item())  # sync
+        if nc > cap:
+            return host_fallback(nb)
+        starts = torch.sort(cand[:nc]).values
+        starts_h = starts.cpu().numpy()
+        body_of = np.searchsorted(boffs, starts_h, side="right") - 1
+        segs = torch.empty((max(nc, 1), 7), dtype=torch.int64, device=dev)
+        with torch.cuda.stream(st):
+            self.ctx.json_parse_segments(jb, starts, torch.from_numpy(body_of).to(dev), label, want_ts, tmp_v, tmp_t,
+                                         segs, stream=st)
+            segs_h = segs[:nc].cpu().numpy()  # sync
         slot_src = np.empty(ns, dtype=np.int64)
         slot_cnt = np.empty(ns, dtype=np.int64)
+        body_ok = np.empty(nb, dtype=np.int32)
         host = load_library()
         stage = self._last[1]
-        rc = host.krr_pack_match_grouped(rec_h.ctypes.data, nr, stage.data_ptr(), nb, plan.slot_group.ctypes.data,
+        rc = host.krr_pack_route_grouped(stage.data_ptr(), boffs.ctypes.data, nb, label.encode(),
+                                         np.ascontiguousarray(segs_h).ctypes.data, nc, plan.slot_group.ctypes.data,
                                          plan._names or b"\0", plan._name_offsets.ctypes.data, ns,
-                                         slot_src.ctypes.data, slot_cnt.ctypes.data, self.threads)
+                                         slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data, self.threads)
         if rc != KRR_PACK_OK:
-            raise PrometheusResponseError(rc, "krr_pack_match_grouped failed")
+            raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
+        if not body_ok.all():
+            return host_fallback(int((body_ok == 0).sum()))
         kept = np.maximum(slot_cnt, 0)
         dst = np.zeros(ns, dtype=np.int64)
         if ns > 1:
@@ -188,11 +199,11 @@ class DevicePacker:
         with torch.cuda.stream(st):
             values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
             ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
-            d = [torch.from_numpy(x).to(dev) for x in (slot_src, kept, dst)]
+            d = [torch.from_numpy(x).to(dev) for x in (np.maximum(slot_src, 0), kept, dst)]
             self.ctx.json_gather(d[0], d[1], d[2], tmp_v, tmp_t, values, ts, stream=st)
             offs_d = torch.from_numpy(offsets).to(dev)
         series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
-        return DevicePacked(series, "device", 0, torch.from_numpy(slot_cnt) if want_counts else None,
+        return DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
                             ts[:n_vals] if ts is not None else None)
 
     def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:

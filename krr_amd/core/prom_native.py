@@ -32,7 +32,7 @@ KRR_PACK_E_VALUE = -4
 EXPORTED_SYMBOLS = ("krr_pack_abi_version", "krr_pack_parse", "krr_pack_n_values", "krr_pack_max_len",
                     "krr_pack_copy", "krr_pack_error", "krr_pack_free", "krr_pack_parse_series", "krr_series_count",
                     "krr_series_label", "krr_series_len", "krr_series_copy", "krr_series_error", "krr_series_free",
-                    "krr_pack_parse_grouped", "krr_round_simple", "krr_pack_concat", "krr_pack_match_grouped")
+                    "krr_pack_parse_grouped", "krr_round_simple", "krr_pack_concat", "krr_pack_route_grouped")
 
 
 class PackerUnavailable(RuntimeError):
@@ -100,8 +100,9 @@ def load_library() -> ctypes.CDLL:
         lib.krr_round_simple.restype = ctypes.c_int
         lib.krr_pack_concat.argtypes = [vp, vp, i64, vp, vp, i32]
         lib.krr_pack_concat.restype = ctypes.c_int
-        lib.krr_pack_match_grouped.argtypes = [vp, i64, vp, i64, vp, ctypes.c_char_p, vp, i64, vp, vp, i32]
-        lib.krr_pack_match_grouped.restype = ctypes.c_int
+        lib.krr_pack_route_grouped.argtypes = [vp, vp, i64, ctypes.c_char_p, vp, i64, vp, ctypes.c_char_p, vp, i64,
+                                               vp, vp, vp, i32]
+        lib.krr_pack_route_grouped.restype = ctypes.c_int
         if lib.krr_pack_abi_version() != 1:
             raise PackerUnavailable("libkrr_host.so packer ABI version mismatch")
         _lib = lib

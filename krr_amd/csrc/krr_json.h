@@ -244,40 +244,87 @@ __global__ __launch_bounds__(256) void k_json_compact(CompactArgs C) {
 }
 
 
-// ---- grouped bodies ("sum by (pod) (...)"): every series, routed by a label later ----
-constexpr int kSeriesRecWords = 6;  // body, index in data.result, label offset (-1: none), label length,
-                                    // scratch slot of its values, count
+// ---- grouped bodies ("sum by (pod) (...)"): one wave per SERIES ----
+// A grouped body holds one series per pod (megabytes per body, a few bodies per fleet), so
+// a wave per body would leave the GPU idle.  Instead:
+//   k_json_find_series  every `[{"metric":` / `,{"metric":` in the bodies (a 32-bit window
+//                       compare at each byte, 64 bytes per lane): the candidate series starts;
+//   k_json_segments     one wave per candidate: the series object (GroupedWalker from
+//                       SERIES_OPEN) — label span, values by the whole wave into scratch slot
+//                       (array offset / 8), and where the object ends;
+// and the host chains the segments body by body from the envelope head to its tail
+// (krr_json_parse.h chain_grouped, in krr_pack_route_grouped): a candidate that is not a
+// real series start is never reached by the chain, and a real series that is not a
+// candidate (another key order, whitespace) breaks it — that body goes to the host packer.
+constexpr int kSegWords = 7;  // start, end (one past '}'), label offset (-1), label length, slot, count, ok
 constexpr int kMaxLabel = 64;
+constexpr uint32_t kMetricHead = (uint32_t)'{' | ((uint32_t)'"' << 8) | ((uint32_t)'m' << 16) | ((uint32_t)'e' << 24);
 
-struct SeriesArgs {
+struct FindArgs {
     const char* bodies;
-    const int64_t* offs;
-    int64_t first, n;
-    int32_t want_ts;
-    int32_t label_len;
-    const char* label;              // device copy of the routing label key
-    double* tmp_v;
-    double* tmp_t;
-    int64_t* recs;                  // [rec_cap][kSeriesRecWords]
-    int64_t rec_cap;
-    unsigned long long* rec_count;  // appended with atomics (order restored by (body, index))
-    int32_t* status;
+    int64_t total;                // bytes (readable up to total + 128)
+    int64_t* cand;                // absolute offsets of the candidates' '{'
+    int64_t cap;
+    unsigned long long* n_cand;
 };
 
-// One body per wave: lane 0 walks the envelope and every series (GroupedWalker), all 64
-// lanes parse each values array (values_array, scratch slot = the array's byte offset / 8),
-// lane 0 appends one record per series.
-__global__ __launch_bounds__(64) void k_json_series(SeriesArgs A) {
+__global__ __launch_bounds__(64) void k_json_find_series(FindArgs F) {
+    const int lane = threadIdx.x;
+    constexpr int kLane = 64;
+    for (int64_t blk = (int64_t)blockIdx.x * kLane * kWave; blk < F.total; blk += (int64_t)gridDim.x * kLane * kWave) {
+        const int64_t r0 = blk + (int64_t)lane * kLane;
+        if (r0 >= F.total) continue;
+        const v4u32* q = reinterpret_cast<const v4u32*>(F.bodies + r0);
+        uint32_t w[20];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const v4u32 x = q[k];
+            w[4 * k] = x[0], w[4 * k + 1] = x[1], w[4 * k + 2] = x[2], w[4 * k + 3] = x[3];
+        }
+#pragma unroll
+        for (int k = 0; k < kLane; ++k) {
+            const int s = 8 * (k & 3);
+            const uint32_t win = s ? ((w[k >> 2] >> s) | (w[(k >> 2) + 1] << (32 - s))) : w[k >> 2];
+            if (win != kMetricHead) continue;
+            const int64_t x = r0 + k;
+            if (x == 0 || x + 10 > F.total) continue;
+            const char* c = F.bodies + x;
+            const char pre = c[-1];
+            if ((pre != '[' && pre != ',') || c[4] != 't' || c[5] != 'r' || c[6] != 'i' || c[7] != 'c' ||
+                c[8] != '"' || c[9] != ':')
+                continue;
+            const unsigned long long slot = atomicAdd(F.n_cand, 1ull);
+            if ((int64_t)slot < F.cap) F.cand[slot] = x;
+        }
+    }
+}
+
+struct SegArgs {
+    const char* bodies;
+    const int64_t* offs;       // body byte offsets
+    const int64_t* start;      // [n] candidate '{' (absolute)
+    const int64_t* body;       // [n] its body
+    int64_t n;
+    int32_t want_ts;
+    int32_t label_len;
+    const char* label;         // device copy of the routing label key
+    double* tmp_v;
+    double* tmp_t;
+    int64_t* seg;              // [n][kSegWords]
+};
+
+__global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
     const int lane = threadIdx.x;
-    for (int64_t i = blockIdx.x; i < A.n; i += gridDim.x) {
-        const int64_t bi = A.first + i;
-        const int64_t ob = A.offs[bi], oe = A.offs[bi + 1];
-        const char* s = A.bodies + ob;
-        const char* e = A.bodies + oe;
+    for (int64_t j = blockIdx.x; j < A.n; j += gridDim.x) {
+        const int64_t x = A.start[j], bi = A.body[j];
+        const char* e = A.bodies + A.offs[bi + 1];
         GroupedWalker W;
-        if (lane == 0) W.init(s, e, A.label, A.label_len);
-        int32_t status = JSON_HOST;
+        if (lane == 0) {
+            W.init(A.bodies + x, e, A.label, A.label_len);
+            W.resume(A.bodies + x, GroupedWalker::SERIES_OPEN);
+        }
+        int ok = 0;
         for (;;) {
             int ev = W_HOST;
             int64_t at = 0;
@@ -287,46 +334,35 @@ __global__ __launch_bounds__(64) void k_json_series(SeriesArgs A) {
             }
             ev = (int)__builtin_amdgcn_readfirstlane(ev);
             at = (int64_t)uni64((uint64_t)at);
-            if (ev == W_HOST) break;
-            if (ev == W_DONE) {
-                status = JSON_OK;
+            if (ev == W_SERIES) {
+                ok = 1;
                 break;
             }
-            if (ev == W_SERIES) {
-                int ok = 1;
-                if (lane == 0) {
-                    const unsigned long long k = atomicAdd(A.rec_count, 1ull);
-                    if ((int64_t)k < A.rec_cap) {
-                        int64_t* r = A.recs + (int64_t)k * kSeriesRecWords;
-                        r[0] = bi;
-                        r[1] = W.index;
-                        r[2] = W.lab ? (int64_t)(W.lab - A.bodies) : -1;
-                        r[3] = W.lab_len;
-                        r[4] = (W.values_at - A.bodies) >> 3;
-                        r[5] = W.count;
-                    } else {
-                        ok = 0;  // more series than the table holds: the host's call
-                    }
-                }
-                if (!__builtin_amdgcn_readfirstlane(ok)) break;
-                continue;
-            }
-            // W_VALUES: the array's first byte is at `at`
+            if (ev != W_VALUES) break;
             const char* vs = A.bodies + at;
             const char* vend = nullptr;
             int64_t count = 0;
-            bool ok = false;
+            bool vok = false;
             if (vs < e && *vs == ']') {
-                ok = true;
+                vok = true;
                 vend = vs + 1;
             } else if (vs < e && *vs == '[') {
-                ok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (at >> 3),
-                                  A.tmp_t ? A.tmp_t + (at >> 3) : nullptr, lane, lds, &count, &vend);
+                vok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (at >> 3),
+                                   A.tmp_t ? A.tmp_t + (at >> 3) : nullptr, lane, lds, &count, &vend);
             }
-            if (!ok) break;
+            if (!vok) break;
             if (lane == 0) W.values_done(vend, count);
         }
-        if (lane == 0) A.status[bi] = status;
+        if (lane == 0) {
+            int64_t* r = A.seg + j * kSegWords;
+            r[0] = x;
+            r[1] = ok ? (int64_t)(W.r.p - A.bodies) : -1;
+            r[2] = (ok && W.lab) ? (int64_t)(W.lab - A.bodies) : -1;
+            r[3] = ok ? W.lab_len : 0;
+            r[4] = ok ? (int64_t)((W.values_at - A.bodies) >> 3) : 0;
+            r[5] = ok ? W.count : 0;
+            r[6] = ok;
+        }
     }
 }
 

@@ -541,7 +541,7 @@ KRR_JHD inline bool envelope_tail(Reader& r, Envelope env) {
 // the next values array starts (W_VALUES: the caller parses it, then values_done()), a
 // series ends (W_SERIES: its label span and values are final), or the body ends
 // (W_DONE) / leaves the device grammar (W_HOST).
-enum : int { W_HOST = 0, W_VALUES = 1, W_SERIES = 2, W_DONE = 3 };
+enum : int { W_HOST = 0, W_VALUES = 1, W_SERIES = 2, W_DONE = 3, W_AT_SERIES = 4 };
 
 struct GroupedWalker {
     enum : int { TOP_OPEN, TOP_KEY, TOP_NEXT, DATA_KEY, DATA_NEXT, SERIES_OPEN, SERIES_KEY, SERIES_NEXT, RESULT_NEXT };
@@ -550,6 +550,7 @@ struct GroupedWalker {
     int64_t label_len;
     int state;
     bool have_status, ok_status, have_result, have_data;
+    bool stop_at_series;  // step() returns W_AT_SERIES before each series object (r.p at its '{')
     // the current series
     int64_t index;        // 0-based position in data.result
     const char* lab;      // its label value (raw bytes, no escapes) or nullptr
@@ -565,7 +566,14 @@ struct GroupedWalker {
         label_len = lbl_len;
         state = TOP_OPEN;
         have_status = ok_status = have_result = have_data = false;
+        stop_at_series = false;
         index = -1;
+    }
+    // Resume inside data.result: at a series object (SERIES_OPEN) or right after one
+    // (RESULT_NEXT), at p.  The envelope flags are the head walk's.
+    KRR_JHD void resume(const char* p, int st) {
+        r.p = p;
+        state = st;
     }
     KRR_JHD bool key_is(const char* kb, int64_t kn, const char* k, int64_t n) const {
         if (kn != n) return false;
@@ -638,6 +646,10 @@ struct GroupedWalker {
                     state = TOP_NEXT;
                     break;
                 case SERIES_OPEN:
+                    if (stop_at_series) {
+                        r.ws();
+                        return W_AT_SERIES;
+                    }
                     if (!r.lit('{') || r.peek('}')) return W_HOST;  // a series without values: the host's error
                     ++index;
                     lab = nullptr;
@@ -710,6 +722,43 @@ struct GroupedWalker {
         }
     }
 };
+
+
+// Chain check of one grouped body (host side of the device packer): the head walk finds
+// data.result's first series; segment records (parsed on the device, one wave per series
+// object, found by the `{"metric":` pattern) must then follow each other exactly — series
+// k ends where series k + 1 starts (a ',' between them) — until the one followed by ']';
+// then the tail walk validates the rest.  seg[j] = {start, end, label_off, label_len,
+// slot, count, ok} (absolute byte offsets, sorted by start); find(pos) returns the index of
+// the segment starting at pos or -1.  Emits each chained series in order through emit(j).
+// Returns false when the body is not canonical (the caller hands it to the host packer).
+template <class Find, class Emit>
+inline bool chain_grouped(const char* buf, int64_t ob, int64_t oe, const char* label, int64_t label_len,
+                          const int64_t* seg, Find find, Emit emit) {
+    GroupedWalker W;
+    W.init(buf + ob, buf + oe, label, label_len);
+    W.stop_at_series = true;
+    int ev = W.step();
+    if (ev == W_DONE) return true;   // no series (empty result)
+    if (ev != W_AT_SERIES) return false;
+    const char* p = W.r.p;
+    for (;;) {
+        const int64_t j = find((int64_t)(p - buf));
+        if (j < 0 || !seg[7 * j + 6]) return false;
+        emit(j);
+        const char* q = buf + seg[7 * j + 1];  // one past the series' '}'
+        if (q >= buf + oe) return false;
+        if (*q == ',') {
+            p = q + 1;
+            if (p >= buf + oe || *p != '{') return false;
+            continue;
+        }
+        if (*q != ']') return false;
+        W.resume(q, GroupedWalker::RESULT_NEXT);
+        W.stop_at_series = false;
+        return W.step() == W_DONE;
+    }
+}
 
 }  // namespace json
 }  // namespace krr

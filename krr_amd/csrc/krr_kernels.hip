@@ -3277,7 +3277,7 @@ struct krr_ctx {
     hipEvent_t fail_ev;
     hipStream_t fail_stream;
     bool fail_ev_valid;
-    char* d_label;                // krr_json_parse_series: the routing label key (device copy)
+    char* d_label;                // krr_json_parse_segments: the routing label key (device copy)
     char err[512];
 };
 
@@ -4078,39 +4078,43 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
     return KRR_OK;
 }
 
-int krr_json_parse_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t first, int64_t n, const char* label,
-                          int32_t want_timestamps, double* scratch_values, double* scratch_ts, int64_t* records,
-                          int64_t rec_cap, uint64_t* n_records, int32_t* status, void* stream) {
+int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t* candidates, int64_t cap,
+                         uint64_t* n_candidates, void* stream) {
     if (!ctx) return KRR_E_INVALID;
-    if (!b || b->n_bodies < 0 || first < 0 || n < 0 || first + n > b->n_bodies || rec_cap < 0)
-        return set_err(ctx, KRR_E_INVALID, "json: bad body range%s", "");
+    if (!b || b->n_bodies < 0 || b->total_bytes < 0 || cap < 0)
+        return set_err(ctx, KRR_E_INVALID, "json: bad bodies%s", "");
+    if (b->total_bytes == 0) return KRR_OK;
+    if (!b->bodies || !candidates || !n_candidates) return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    if (((uintptr_t)b->bodies & 15) != 0) return set_err(ctx, KRR_E_INVALID, "json: bodies not 16-byte aligned%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    json::FindArgs F{b->bodies, b->total_bytes, candidates, cap, (unsigned long long*)n_candidates};
+    const int64_t blocks = (b->total_bytes + 4095) / 4096;
+    hipLaunchKernelGGL(json::k_json_find_series, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(64), 0,
+                       (hipStream_t)stream, F);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
+                            int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
+                            double* scratch_ts, int64_t* segments, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!b || n < 0) return set_err(ctx, KRR_E_INVALID, "json: bad arguments%s", "");
     if (!label) return set_err(ctx, KRR_E_INVALID, "json: null label%s", "");
     const size_t ll = strlen(label);
     if (ll >= (size_t)json::kMaxLabel) return set_err(ctx, KRR_E_INVALID, "json: label longer than 63 bytes%s", "");
     if (n == 0) return KRR_OK;
-    if (!b->bodies || !b->body_offsets || !scratch_values || !records || !n_records || !status ||
+    if (!b->bodies || !b->body_offsets || !starts || !body_of || !scratch_values || !segments ||
         (want_timestamps && !scratch_ts))
         return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
-    if (((uintptr_t)b->bodies & 15) != 0) return set_err(ctx, KRR_E_INVALID, "json: bodies not 16-byte aligned%s", "");
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
-    json::SeriesArgs A{};
-    A.bodies = b->bodies;
-    A.offs = b->body_offsets;
-    A.first = first;
-    A.n = n;
-    A.want_ts = want_timestamps ? 1 : 0;
     if (!ctx->d_label) KRR_HIP(ctx, hipMalloc(&ctx->d_label, json::kMaxLabel));
     KRR_HIP(ctx, hipMemcpyAsync(ctx->d_label, label, ll + 1, hipMemcpyHostToDevice, (hipStream_t)stream));
-    A.label_len = (int32_t)ll;
-    A.label = ctx->d_label;
-    A.tmp_v = scratch_values;
-    A.tmp_t = want_timestamps ? scratch_ts : nullptr;
-    A.recs = records;
-    A.rec_cap = rec_cap;
-    A.rec_count = (unsigned long long*)n_records;
-    A.status = status;
-    hipLaunchKernelGGL(json::k_json_series, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
+    json::SegArgs A{b->bodies, b->body_offsets, starts, body_of, n, want_timestamps ? 1 : 0, (int32_t)ll,
+                    ctx->d_label, scratch_values, want_timestamps ? scratch_ts : nullptr, segments};
+    hipLaunchKernelGGL(json::k_json_segments, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -9,6 +9,7 @@
 // std::from_chars.  Bodies are independent, so a pool of threads parses them in
 // parallel, then the kept samples are copied into one CSR buffer.
 #include "krr_pack.h"
+#include "krr_json_parse.h"
 
 #include <algorithm>
 #include <atomic>
@@ -736,39 +737,46 @@ int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t
     return KRR_PACK_OK;
 }
 
-int krr_pack_match_grouped(const int64_t* records, int64_t n_records, const char* bodies, int64_t n_bodies,
-                           const int64_t* slot_body, const char* slot_names, const int64_t* slot_name_offsets,
-                           int64_t n_slots, int64_t* slot_src, int64_t* slot_count, int32_t threads) {
-    if (n_records < 0 || n_bodies < 0 || n_slots < 0 || (n_records > 0 && (!records || !bodies)) ||
-        (n_slots > 0 && (!slot_body || !slot_name_offsets || !slot_src || !slot_count)))
+int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int64_t n_bodies, const char* label,
+                           const int64_t* segments, int64_t n_segments, const int64_t* slot_body,
+                           const char* slot_names, const int64_t* slot_name_offsets, int64_t n_slots,
+                           int64_t* slot_src, int64_t* slot_count, int32_t* body_ok, int32_t threads) {
+    if (n_bodies < 0 || n_segments < 0 || n_slots < 0 || !label || (n_bodies > 0 && (!bodies || !body_offsets ||
+                                                                                      !body_ok)) ||
+        (n_segments > 0 && !segments) || (n_slots > 0 && (!slot_body || !slot_name_offsets || !slot_src ||
+                                                          !slot_count)))
         return KRR_PACK_E_INVALID;
-    // records of each body, in data.result order
-    std::vector<std::vector<int64_t>> per_body;
-    std::vector<std::unordered_map<std::string_view, int64_t>> index;
-    try {
-        per_body.resize((size_t)n_bodies);
-        index.resize((size_t)n_bodies);
-        for (int64_t r = 0; r < n_records; ++r) {
-            const int64_t* R = records + 6 * r;
-            if (R[0] < 0 || R[0] >= n_bodies) return KRR_PACK_E_INVALID;
-            per_body[(size_t)R[0]].push_back(r);
-        }
-    } catch (...) {
-        return KRR_PACK_E_INVALID;
-    }
-    parallel_for(n_bodies, threads, [&](int64_t b) {
-        auto& v = per_body[(size_t)b];
-        std::sort(v.begin(), v.end(), [&](int64_t x, int64_t y) { return records[6 * x + 1] < records[6 * y + 1]; });
-        auto& ix = index[(size_t)b];
-        ix.reserve(v.size() * 2);
-        for (int64_t r : v) {
-            const int64_t* R = records + 6 * r;
-            if (R[2] >= 0) ix.emplace(std::string_view(bodies + R[2], (size_t)R[3]), r);  // the first one wins
-        }
-    });
+    for (int64_t j = 1; j < n_segments; ++j)
+        if (segments[7 * j] <= segments[7 * (j - 1)]) return KRR_PACK_E_INVALID;  // sorted, distinct starts
     for (int64_t s = 0; s < n_slots; ++s)
         if (slot_body[s] < 0 || slot_body[s] >= n_bodies || slot_name_offsets[s + 1] < slot_name_offsets[s])
             return KRR_PACK_E_INVALID;
+    const int64_t ll = (int64_t)strlen(label);
+    std::vector<std::unordered_map<std::string_view, int64_t>> index;
+    try {
+        index.resize((size_t)n_bodies);
+    } catch (...) {
+        return KRR_PACK_E_INVALID;
+    }
+    auto find = [&](int64_t pos) -> int64_t {
+        int64_t lo = 0, hi = n_segments;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (segments[7 * mid] < pos) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo < n_segments && segments[7 * lo] == pos ? lo : -1;
+    };
+    parallel_for(n_bodies, threads, [&](int64_t b) {
+        auto& ix = index[(size_t)b];
+        const bool ok = krr::json::chain_grouped(bodies, body_offsets[b], body_offsets[b + 1], label, ll, segments,
+                                                 find, [&](int64_t j) {
+                                                     const int64_t* R = segments + 7 * j;
+                                                     if (R[2] >= 0)  // the first series with the label wins
+                                                         ix.emplace(std::string_view(bodies + R[2], (size_t)R[3]), j);
+                                                 });
+        body_ok[b] = ok ? 1 : 0;
+    });
     parallel_for(n_slots, threads, [&](int64_t s) {
         const std::string_view name(slot_names + slot_name_offsets[s],
                                     (size_t)(slot_name_offsets[s + 1] - slot_name_offsets[s]));
@@ -778,8 +786,8 @@ int krr_pack_match_grouped(const int64_t* records, int64_t n_records, const char
             slot_src[s] = -1;
             slot_count[s] = -1;
         } else {
-            slot_src[s] = records[6 * it->second + 4];
-            slot_count[s] = records[6 * it->second + 5];
+            slot_src[s] = segments[7 * it->second + 4];
+            slot_count[s] = segments[7 * it->second + 5];
         }
     });
     return KRR_PACK_OK;
