@@ -31,6 +31,9 @@
  *   krr_json_parse / _compact <- PrometheusLoader.gather_data's per-pod value parse,
  *                                robusta_krr/core/integrations/prometheus.py:147-155,
  *                                on response bodies in HBM (device packer)
+ *   krr_json_find_series / _parse_segments / _gather
+ *                             <- the same for grouped `sum by (pod)` bodies (the fleet
+ *                                batching of prometheus.py:118-143's per-pod queries)
  *
  * Ownership: the caller owns every buffer; no allocation crosses the ABI.
  * Device pointers are HIP device pointers on the ctx's device; `stream` is a

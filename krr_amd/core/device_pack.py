@@ -206,23 +206,42 @@ class DevicePacker:
         return DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
                             ts[:n_vals] if ts is not None else None)
 
+    def pack_many(self, resources: Sequence[Sequence[Sequence[bytes]]], *, want_timestamps: bool = False,
+                  return_pod_counts: bool = False, stream=None) -> list:
+        """Several resources' bodies (e.g. CPU and memory of one fleet) through ONE staging /
+        copy / parse pipeline: one DevicePacked per resource, each as ``pack`` would give it."""
+        with self._lock:
+            return self._pack_multi(resources, want_timestamps, return_pod_counts, stream)
+
     def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:
+        return self._pack_multi([per_object_bodies], want_ts, want_counts, stream)[0]
+
+    def _pack_multi(self, resources, want_ts, want_counts, stream) -> list:
         import torch
 
         flat: list = []
-        obj: list = []
-        for o, bodies in enumerate(per_object_bodies):
-            for b in bodies:
-                flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
-                obj.append(o)
-        n_obj, nb = len(per_object_bodies), len(flat)
+        obj: list = []      # global object index (objects of resource r after those of r - 1)
+        body0, obj0 = [0], [0]
+        for per_object_bodies in resources:
+            base = obj0[-1]
+            for o, bodies in enumerate(per_object_bodies):
+                for b in bodies:
+                    flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
+                    obj.append(base + o)
+            body0.append(len(flat))
+            obj0.append(base + len(per_object_bodies))
+        n_obj, nb = obj0[-1], len(flat)
         dev = self.device
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         if nb == 0:
-            offs = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
-            return DevicePacked(PackedSeries(torch.empty(0, dtype=torch.float64, device=dev), offs, 0), "device", 0,
-                                torch.empty(0, dtype=torch.int64, device=dev) if want_counts else None,
-                                torch.empty(0, dtype=torch.float64, device=dev) if want_ts else None)
+            out = []
+            for per_object_bodies in resources:
+                offs = torch.zeros(len(per_object_bodies) + 1, dtype=torch.int64, device=dev)
+                out.append(DevicePacked(PackedSeries(torch.empty(0, dtype=torch.float64, device=dev), offs, 0),
+                                        "device", 0,
+                                        torch.empty(0, dtype=torch.int64, device=dev) if want_counts else None,
+                                        torch.empty(0, dtype=torch.float64, device=dev) if want_ts else None))
+            return out
         counts = torch.empty(nb, dtype=torch.int64, device=dev)
         status = torch.empty(nb, dtype=torch.int32, device=dev)
 
@@ -230,24 +249,18 @@ class DevicePacker:
             self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
 
         lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
+        R = len(resources)
         with torch.cuda.stream(st):
             obj_t = torch.from_numpy(np.asarray(obj, dtype=np.int64)).to(dev, non_blocking=False)
             seg = torch.zeros(n_obj, dtype=torch.int64, device=dev).index_add_(0, obj_t, counts)
             offsets = torch.zeros(n_obj + 1, dtype=torch.int64, device=dev)
             torch.cumsum(seg, 0, out=offsets[1:])
-            summary = torch.stack([status.max().to(torch.int64), offsets[-1], seg.max()]).cpu()  # the one sync
-        worst, n_vals, max_len = (int(x) for x in summary)
-        if worst == _native.KRR_JSON_HOST:
-            n_host = int((status == _native.KRR_JSON_HOST).sum().item())
-            res = pack_query_range_bodies(per_object_bodies, want_timestamps=want_ts, threads=self.threads,
-                                          return_pod_counts=want_counts)
-            if not isinstance(res, tuple):
-                res = (res,)
-            series = res[0]
-            rest = list(res[1:])
-            ts = rest.pop(0) if want_ts else None
-            pc = rest.pop(0) if want_counts else None
-            return DevicePacked(series, "host", n_host, pc, ts)
+            host_flag = (status == _native.KRR_JSON_HOST).to(torch.int64)
+            per_res = [torch.stack([host_flag[body0[r]:body0[r + 1]].sum(),
+                                    seg[obj0[r]:obj0[r + 1]].max() if obj0[r + 1] > obj0[r] else offsets[0]])
+                       for r in range(R)]
+            summary = torch.stack(per_res + [torch.stack([offsets[-1], offsets[-1]])]).cpu()  # the one sync
+        n_vals = int(summary[R, 0])
         with torch.cuda.stream(st):
             out_pos = torch.cumsum(counts, 0) - counts
             values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
@@ -255,10 +268,29 @@ class DevicePacker:
             self.ctx.json_compact(jb, tmp_v, tmp_t, counts, status, out_pos, values, ts, stream=st)
             pc = torch.where(status == _native.KRR_JSON_DROPPED, torch.full_like(counts, -1), counts) \
                 if want_counts else None
-        # the staging buffer is reused by the next call: its copies must be done (they are:
-        # the parse launches waited for them before the summary synchronised)
-        return DevicePacked(PackedSeries(values[:n_vals], offsets, max_len), "device", 0, pc,
-                            ts[:n_vals] if ts is not None else None)
+        offs_h = None
+        out = []
+        for r in range(R):
+            n_host, max_len = int(summary[r, 0]), int(summary[r, 1])
+            if n_host:  # this resource's batch goes to the host packer: its result or its error
+                res = pack_query_range_bodies(resources[r], want_timestamps=want_ts, threads=self.threads,
+                                              return_pod_counts=want_counts)
+                res = res if isinstance(res, tuple) else (res,)
+                rest = list(res[1:])
+                t_r = rest.pop(0) if want_ts else None
+                c_r = rest.pop(0) if want_counts else None
+                out.append(DevicePacked(res[0], "host", n_host, c_r, t_r))
+                continue
+            if offs_h is None:
+                offs_h = offsets.cpu()
+            lo, hi = int(offs_h[obj0[r]]), int(offs_h[obj0[r + 1]])
+            o_r = offsets[obj0[r]:obj0[r + 1] + 1] - lo
+            out.append(DevicePacked(PackedSeries(values[lo:hi], o_r, max_len if obj0[r + 1] > obj0[r] else 0),
+                                    "device", 0, pc[body0[r]:body0[r + 1]] if want_counts else None,
+                                    ts[lo:hi] if ts is not None else None))
+        # the staging buffer is reused by the next call: its copies are done (the parse
+        # launches waited for them before the summary synchronised)
+        return out
 
 
 _packers: dict = {}

@@ -160,8 +160,7 @@ class BatchedRunner:
         from krr_amd.core.packing import PackedFleet
 
         packer = self._device_packer(threads, device)
-        cpu = packer.pack(cpu_bodies)
-        mem = packer.pack(mem_bodies)
+        cpu, mem = packer.pack_many([cpu_bodies, mem_bodies])  # one staging / copy / parse pipeline
         self.last_pack_via = (cpu.via, mem.via)
         return PackedFleet(cpu.series, mem.series)
 

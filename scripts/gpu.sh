@@ -13,6 +13,7 @@
 #   ab:ARGS      same-process A/B of every krr_amd/lib/variants/lib_*.so (scripts/build_variants.sh)
 #                on the ab_variants.py workload ARGS, e.g. ab:--config,3,--percentile,50
 #   sq:ARGS      SQ issue / wait counters (two rocprofv3 --pmc passes) of the ab_variants.py workload
+#   script:NAME,ARGS  python scripts/NAME.py ARGS -> script_NAME_ARGS.log
 #   diag:ARGS    per-segment phase breakdown with krr_amd/lib/variants/lib_diag.so (-DKRR_DIAG)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -u
@@ -75,6 +76,15 @@ EOF
       timeout -k 10 300 python -u scripts/ab_variants.py $libs $args > "$OUT/ab${n:+_$n}.log" 2>&1 \
         || { echo "ab $args failed"; tail -20 "$OUT/ab${n:+_$n}.log"; exit 1; }
       echo "== ab $args"; grep fused "$OUT/ab${n:+_$n}.log"
+      ;;
+    script)
+      # script:NAME,ARGS  python -u scripts/NAME.py ARGS (under its own 300-s limit)
+      sname=${args%% *}
+      sargs=""
+      [[ "$args" == *" "* ]] && sargs=${args#* }
+      timeout -k 10 300 python -u "scripts/$sname.py" $sargs > "$OUT/script_${n}.log" 2>&1 \
+        || { echo "script $args failed"; tail -20 "$OUT/script_${n}.log"; exit 1; }
+      echo "== script $args"; tail -5 "$OUT/script_${n}.log"
       ;;
     diag)
       timeout -k 10 120 python -u scripts/diag_select.py krr_amd/lib/variants/lib_diag.so $args \

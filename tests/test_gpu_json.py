@@ -243,3 +243,21 @@ def test_grouped_large_bodies(packer):
     assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
     assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
     assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+def test_pack_many_equals_separate(packer):
+    """CPU and memory bodies through one pipeline (pack_many) equal each packed alone; a
+    resource with a non-canonical body goes to the host alone."""
+    cpu = _fleet(21, n_obj=30)
+    mem = _fleet(22, n_obj=30)
+    a, b = packer.pack_many([cpu, mem], want_timestamps=True, return_pod_counts=True)
+    assert a.via == b.via == "device"
+    _same(a, cpu)
+    _same(b, mem)
+    mem_bad = [list(x) for x in mem]
+    mem_bad[3] = mem_bad[3] + [json.dumps({"status": "success", "data": {"result": [  # spaces in the values
+        {"metric": {}, "values": [[1, "2"], [2, "3"]]}]}}).encode()]
+    a, b = packer.pack_many([cpu, mem_bad], want_timestamps=True, return_pod_counts=True)
+    assert a.via == "device" and b.via == "host"
+    _same(a, cpu)
+    _same(b, mem_bad)
