@@ -137,7 +137,7 @@ class DevicePacker:
 
         if len(bodies) != len(plan.groups):
             raise ValueError(f"expected {len(plan.groups)} bodies (one per group query), got {len(bodies)}")
-        flat = [b if isinstance(b, (bytes, bytearray)) else bytes(b) for b in bodies]
+        flat = [b if isinstance(b, bytes) else bytes(b) for b in bodies]  # c_char_p takes bytes only
         dev = self.device
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         n_obj, nb, ns = plan.n_objects, len(flat), plan.n_slots
@@ -226,7 +226,7 @@ class DevicePacker:
             base = obj0[-1]
             for o, bodies in enumerate(per_object_bodies):
                 for b in bodies:
-                    flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
+                    flat.append(b if isinstance(b, bytes) else bytes(b))  # c_char_p takes bytes only
                     obj.append(base + o)
             body0.append(len(flat))
             obj0.append(base + len(per_object_bodies))

@@ -202,7 +202,7 @@ class FleetQueryPlan:
         if len(bodies) != len(self.groups):
             raise ValueError(f"expected {len(self.groups)} bodies (one per group query), got {len(bodies)}")
         lib = load_library()
-        flat = [b if isinstance(b, (bytes, bytearray)) else bytes(b) for b in bodies]
+        flat = [b if isinstance(b, bytes) else bytes(b) for b in bodies]  # c_char_p takes bytes only
         nb, ns, no = len(flat), self.n_slots, self.n_objects
         ptrs = (ctypes.c_char_p * max(nb, 1))(*flat)
         lens = np.array([len(b) for b in flat] or [0], dtype=np.int64)

@@ -159,7 +159,7 @@ def pack_query_range_bodies(per_object_bodies: Sequence[Sequence[bytes]], *, wan
     obj: list[int] = []
     for o, bodies in enumerate(per_object_bodies):
         for b in bodies:
-            flat.append(b if isinstance(b, (bytes, bytearray)) else bytes(b))
+            flat.append(b if isinstance(b, bytes) else bytes(b))  # c_char_p takes bytes only
             obj.append(o)
     n_obj = len(per_object_bodies)
     nb = len(flat)
