@@ -402,8 +402,11 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
 
 /* Grouped bodies (`sum by (pod) (...)`, one series per pod: the host packer's
  * krr_pack_parse_grouped, include/krr_pack.h), one wave per SERIES:
- *   krr_json_find_series    every `[{"metric":` / `,{"metric":` in the bodies: the absolute
- *                           offset of its '{' appended at candidates[*n_candidates ..]
+ *   krr_json_find_series    every `[{"metric":` / `,{"metric":` starting in [begin, end) whose
+ *                           11 bytes lie below `limit` (the bytes already copied: a caller
+ *                           searches each chunk as it lands, the chunk's last 16 bytes
+ *                           with the next one): the absolute offset of its '{' appended at
+ *                           candidates[*n_candidates ..]
  *                           (device counter, zeroed by the caller; any order; the count
  *                           may exceed cap, then only cap are stored);
  *   krr_json_parse_segments one series object per candidate (sorted starts, body_of[j] its
@@ -414,8 +417,8 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
  * The host then chains the segments from each body's envelope (krr_pack_route_grouped,
  * include/krr_pack.h); a body whose series do not chain goes to the host packer.
  * Bodies need 128 readable bytes past the last one. */
-int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t* candidates, int64_t cap,
-                         uint64_t* n_candidates, void* stream);
+int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t begin, int64_t end, int64_t limit,
+                         int64_t* candidates, int64_t cap, uint64_t* n_candidates, void* stream);
 int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
                             int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
                             double* scratch_ts, int64_t* segments, void* stream);

@@ -273,7 +273,7 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse.restype = ctypes.c_int
         lib.krr_json_compact.argtypes = [vp, jb, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_compact.restype = ctypes.c_int
-        lib.krr_json_find_series.argtypes = [vp, jb, vp, i64, vp, vp]
+        lib.krr_json_find_series.argtypes = [vp, jb, i64, i64, i64, vp, i64, vp, vp]
         lib.krr_json_find_series.restype = ctypes.c_int
         lib.krr_json_parse_segments.argtypes = [vp, jb, vp, vp, i64, ctypes.c_char_p, i32, vp, vp, vp, vp]
         lib.krr_json_parse_segments.restype = ctypes.c_int
@@ -598,12 +598,17 @@ class Context:
             out_pos.data_ptr(), values.data_ptr(), timestamps.data_ptr() if timestamps is not None else None,
             self._stream(stream)))
 
-    def json_find_series(self, jb: KrrJsonBodies, candidates, n_candidates, stream=None) -> None:
-        """candidates: int64 [cap]; n_candidates: int64 [1] device counter (zeroed by the caller)."""
+    def json_find_series(self, jb: KrrJsonBodies, candidates, n_candidates, begin: int = 0, end: Optional[int] = None,
+                         limit: Optional[int] = None, stream=None) -> None:
+        """candidates: int64 [cap]; n_candidates: int64 [1] device counter (zeroed by the caller);
+        positions [begin, end) with the bytes below ``limit`` in place (default: all)."""
         _check_tensor(candidates, "int64")
         _check_tensor(n_candidates, "int64", 1)
-        self._check(self._lib.krr_json_find_series(self._h, ctypes.byref(jb), candidates.data_ptr(),
-                                                   candidates.numel(), n_candidates.data_ptr(), self._stream(stream)))
+        end = jb.total_bytes if end is None else int(end)
+        limit = jb.total_bytes if limit is None else int(limit)
+        self._check(self._lib.krr_json_find_series(self._h, ctypes.byref(jb), int(begin), end, limit,
+                                                   candidates.data_ptr(), candidates.numel(), n_candidates.data_ptr(),
+                                                   self._stream(stream)))
 
     def json_parse_segments(self, jb: KrrJsonBodies, starts, body_of, label: str, want_timestamps: bool,
                             scratch_values, scratch_ts, segments, stream=None) -> None:

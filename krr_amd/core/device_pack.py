@@ -79,8 +79,8 @@ class DevicePacker:
 
     def _upload(self, flat, want_ts, st, launch):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
-        copy stream and call ``launch(jb, a, b, tmp_v, tmp_t)`` on ``st`` for bodies [a, b)
-        once the chunk is there."""
+        copy stream and call ``launch(jb, a, b, tmp_v, tmp_t, lo, hi)`` on ``st`` for bodies
+        [a, b) = bytes [lo, hi) once the chunk is there."""
         import torch
 
         dev = self.device
@@ -117,7 +117,7 @@ class DevicePacker:
                 ev = torch.cuda.Event()
                 ev.record(cs)
             st.wait_event(ev)
-            launch(jb, a, b, tmp_v, tmp_t)
+            launch(jb, a, b, tmp_v, tmp_t, lo, hi)
             a = b
         self._last = (d_bodies, stage)
         return lens, boffs, total, jb, tmp_v, tmp_t
@@ -129,20 +129,31 @@ class DevicePacker:
         bit for bit, with the bodies parsed on the device one wave per series
         (krr_json_find_series + krr_json_parse_segments) and chained and routed by pod label
         on the host (krr_pack_route_grouped)."""
-        with self._lock:
-            return self._pack_grouped(plan, bodies, want_timestamps, return_pod_counts, stream, label)
+        return self.pack_grouped_many([(plan, bodies)], want_timestamps=want_timestamps,
+                                      return_pod_counts=return_pod_counts, stream=stream, label=label)[0]
 
-    def _pack_grouped(self, plan, bodies, want_ts, want_counts, stream, label) -> DevicePacked:
+    def pack_grouped_many(self, items, *, want_timestamps: bool = False, return_pod_counts: bool = False,
+                          stream=None, label: str = "pod") -> list:
+        """Several (plan, bodies) pairs (e.g. CPU and memory) through ONE staging / copy /
+        candidate-search pipeline; one DevicePacked per pair."""
+        with self._lock:
+            return self._pack_grouped_multi(items, want_timestamps, return_pod_counts, stream, label)
+
+    def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label) -> list:
         import torch
 
-        if len(bodies) != len(plan.groups):
-            raise ValueError(f"expected {len(plan.groups)} bodies (one per group query), got {len(bodies)}")
-        flat = [b if isinstance(b, bytes) else bytes(b) for b in bodies]  # c_char_p takes bytes only
+        flat: list = []
+        body0 = [0]
+        for plan, bodies in items:
+            if len(bodies) != len(plan.groups):
+                raise ValueError(f"expected {len(plan.groups)} bodies (one per group query), got {len(bodies)}")
+            flat.extend(b if isinstance(b, bytes) else bytes(b) for b in bodies)  # c_char_p takes bytes only
+            body0.append(len(flat))
         dev = self.device
         st = stream if stream is not None else torch.cuda.current_stream(dev)
-        n_obj, nb, ns = plan.n_objects, len(flat), plan.n_slots
 
-        def host_fallback(n_host):
+        def host_fallback(r, n_host):
+            plan, bodies = items[r]
             res = plan.pack(bodies, want_timestamps=want_ts, threads=self.threads, return_pod_counts=want_counts)
             res = res if isinstance(res, tuple) else (res,)
             rest = list(res[1:])
@@ -150,22 +161,25 @@ class DevicePacker:
             pc = rest.pop(0) if want_counts else None
             return DevicePacked(res[0], "host", n_host, pc, ts)
 
-        if nb == 0 or ns == 0:
-            return host_fallback(0)
-        status = None
-
-        def launch(jb, a, b, tmp_v, tmp_t):  # the bodies are parsed once all are in HBM
-            pass
-
-        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
-        cap = max(1024, total // 4096)
+        if not flat or all(plan.n_slots == 0 for plan, _ in items):
+            return [host_fallback(r, 0) for r in range(len(items))]
+        total_bytes = sum(len(b) for b in flat)
+        cap = max(1024, total_bytes // 4096)
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ctx.json_find_series(jb, cand, n_cand, stream=st)
+        seen = [0]  # positions below this were searched
+
+        def launch(jb, a, b, tmp_v, tmp_t, lo, hi):  # search each chunk as it lands
+            last = b == len(flat)
+            end = hi if last else max(hi - 16, seen[0])
+            self.ctx.json_find_series(jb, cand, n_cand, begin=seen[0], end=end, limit=hi, stream=st)
+            seen[0] = end
+
+        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
         with torch.cuda.stream(st):
             nc = int(n_cand.item())  # sync
         if nc > cap:
-            return host_fallback(nb)
+            return [host_fallback(r, body0[r + 1] - body0[r]) for r in range(len(items))]
         starts = torch.sort(cand[:nc]).values
         starts_h = starts.cpu().numpy()
         body_of = np.searchsorted(boffs, starts_h, side="right") - 1
@@ -173,38 +187,46 @@ class DevicePacker:
         with torch.cuda.stream(st):
             self.ctx.json_parse_segments(jb, starts, torch.from_numpy(body_of).to(dev), label, want_ts, tmp_v, tmp_t,
                                          segs, stream=st)
-            segs_h = segs[:nc].cpu().numpy()  # sync
-        slot_src = np.empty(ns, dtype=np.int64)
-        slot_cnt = np.empty(ns, dtype=np.int64)
-        body_ok = np.empty(nb, dtype=np.int32)
+            segs_h = np.ascontiguousarray(segs[:nc].cpu().numpy())  # sync
         host = load_library()
         stage = self._last[1]
-        rc = host.krr_pack_route_grouped(stage.data_ptr(), boffs.ctypes.data, nb, label.encode(),
-                                         np.ascontiguousarray(segs_h).ctypes.data, nc, plan.slot_group.ctypes.data,
-                                         plan._names or b"\0", plan._name_offsets.ctypes.data, ns,
-                                         slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data, self.threads)
-        if rc != KRR_PACK_OK:
-            raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
-        if not body_ok.all():
-            return host_fallback(int((body_ok == 0).sum()))
-        kept = np.maximum(slot_cnt, 0)
-        dst = np.zeros(ns, dtype=np.int64)
-        if ns > 1:
-            np.cumsum(kept[:-1], out=dst[1:])
-        seg = np.zeros(n_obj, dtype=np.int64)
-        np.add.at(seg, plan.slot_obj, kept)
-        offsets = np.zeros(n_obj + 1, dtype=np.int64)
-        np.cumsum(seg, out=offsets[1:])
-        n_vals = int(offsets[-1])
-        with torch.cuda.stream(st):
-            values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
-            ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
-            d = [torch.from_numpy(x).to(dev) for x in (np.maximum(slot_src, 0), kept, dst)]
-            self.ctx.json_gather(d[0], d[1], d[2], tmp_v, tmp_t, values, ts, stream=st)
-            offs_d = torch.from_numpy(offsets).to(dev)
-        series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
-        return DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
-                            ts[:n_vals] if ts is not None else None)
+        out = []
+        for r, (plan, bodies) in enumerate(items):
+            ns, n_obj, nb = plan.n_slots, plan.n_objects, body0[r + 1] - body0[r]
+            slot_src = np.empty(ns, dtype=np.int64)
+            slot_cnt = np.empty(ns, dtype=np.int64)
+            body_ok = np.empty(max(nb, 1), dtype=np.int32)
+            b_offs = np.ascontiguousarray(boffs[body0[r]:body0[r + 1] + 1])
+            rc = host.krr_pack_route_grouped(stage.data_ptr(), b_offs.ctypes.data, nb, label.encode(),
+                                             segs_h.ctypes.data, nc, plan.slot_group.ctypes.data,
+                                             plan._names or b"\0", plan._name_offsets.ctypes.data, ns,
+                                             slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data,
+                                             self.threads)
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
+            if not body_ok[:nb].all():
+                out.append(host_fallback(r, int((body_ok[:nb] == 0).sum())))
+                continue
+            kept = np.maximum(slot_cnt, 0)
+            dst = np.zeros(ns, dtype=np.int64)
+            if ns > 1:
+                np.cumsum(kept[:-1], out=dst[1:])
+            seg = np.zeros(n_obj, dtype=np.int64)
+            np.add.at(seg, plan.slot_obj, kept)
+            offsets = np.zeros(n_obj + 1, dtype=np.int64)
+            np.cumsum(seg, out=offsets[1:])
+            n_vals = int(offsets[-1])
+            with torch.cuda.stream(st):
+                values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
+                ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
+                if ns:
+                    d = [torch.from_numpy(x).to(dev) for x in (np.maximum(slot_src, 0), kept, dst)]
+                    self.ctx.json_gather(d[0], d[1], d[2], tmp_v, tmp_t, values, ts, stream=st)
+                offs_d = torch.from_numpy(offsets).to(dev)
+            series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
+            out.append(DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
+                                    ts[:n_vals] if ts is not None else None))
+        return out
 
     def pack_many(self, resources: Sequence[Sequence[Sequence[bytes]]], *, want_timestamps: bool = False,
                   return_pod_counts: bool = False, stream=None) -> list:
@@ -245,7 +267,7 @@ class DevicePacker:
         counts = torch.empty(nb, dtype=torch.int64, device=dev)
         status = torch.empty(nb, dtype=torch.int32, device=dev)
 
-        def launch(jb, a, b, tmp_v, tmp_t):
+        def launch(jb, a, b, tmp_v, tmp_t, lo, hi):
             self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
 
         lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)

@@ -181,8 +181,7 @@ class BatchedRunner:
         if parser == "host":
             return plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads, alloc=_pinned_alloc_or_none())
         packer = self._device_packer(threads)
-        cpu = packer.pack_grouped(plan, cpu_bodies)
-        mem = packer.pack_grouped(plan, mem_bodies)
+        cpu, mem = packer.pack_grouped_many([(plan, cpu_bodies), (plan, mem_bodies)])
         self.last_pack_via = (cpu.via, mem.via)
         return PackedFleet(cpu.series, mem.series)
 

@@ -262,7 +262,8 @@ constexpr uint32_t kMetricHead = (uint32_t)'{' | ((uint32_t)'"' << 8) | ((uint32
 
 struct FindArgs {
     const char* bodies;
-    int64_t total;                // bytes (readable up to total + 128)
+    int64_t begin, end;           // candidate positions searched: [begin, end)
+    int64_t limit;                // bytes [0, limit) are in place (a pattern must end below it)
     int64_t* cand;                // absolute offsets of the candidates' '{'
     int64_t cap;
     unsigned long long* n_cand;
@@ -271,9 +272,11 @@ struct FindArgs {
 __global__ __launch_bounds__(64) void k_json_find_series(FindArgs F) {
     const int lane = threadIdx.x;
     constexpr int kLane = 64;
-    for (int64_t blk = (int64_t)blockIdx.x * kLane * kWave; blk < F.total; blk += (int64_t)gridDim.x * kLane * kWave) {
+    const int64_t base = F.begin & ~(int64_t)15;  // 16-B aligned loads
+    for (int64_t blk = base + (int64_t)blockIdx.x * kLane * kWave; blk < F.end;
+         blk += (int64_t)gridDim.x * kLane * kWave) {
         const int64_t r0 = blk + (int64_t)lane * kLane;
-        if (r0 >= F.total) continue;
+        if (r0 >= F.end) continue;
         const v4u32* q = reinterpret_cast<const v4u32*>(F.bodies + r0);
         uint32_t w[20];
 #pragma unroll
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(64) void k_json_find_series(FindArgs F) {
             const uint32_t win = s ? ((w[k >> 2] >> s) | (w[(k >> 2) + 1] << (32 - s))) : w[k >> 2];
             if (win != kMetricHead) continue;
             const int64_t x = r0 + k;
-            if (x == 0 || x + 10 > F.total) continue;
+            if (x < F.begin || x >= F.end || x == 0 || x + 10 > F.limit) continue;
             const char* c = F.bodies + x;
             const char pre = c[-1];
             if ((pre != '[' && pre != ',') || c[4] != 't' || c[5] != 'r' || c[6] != 'i' || c[7] != 'c' ||

@@ -4078,18 +4078,19 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
     return KRR_OK;
 }
 
-int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t* candidates, int64_t cap,
-                         uint64_t* n_candidates, void* stream) {
+int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t begin, int64_t end, int64_t limit,
+                         int64_t* candidates, int64_t cap, uint64_t* n_candidates, void* stream) {
     if (!ctx) return KRR_E_INVALID;
-    if (!b || b->n_bodies < 0 || b->total_bytes < 0 || cap < 0)
-        return set_err(ctx, KRR_E_INVALID, "json: bad bodies%s", "");
-    if (b->total_bytes == 0) return KRR_OK;
+    if (!b || b->n_bodies < 0 || b->total_bytes < 0 || cap < 0 || begin < 0 || end > b->total_bytes ||
+        limit > b->total_bytes || end > limit)
+        return set_err(ctx, KRR_E_INVALID, "json: bad bodies or byte range%s", "");
+    if (end <= begin) return KRR_OK;
     if (!b->bodies || !candidates || !n_candidates) return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
     if (((uintptr_t)b->bodies & 15) != 0) return set_err(ctx, KRR_E_INVALID, "json: bodies not 16-byte aligned%s", "");
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
-    json::FindArgs F{b->bodies, b->total_bytes, candidates, cap, (unsigned long long*)n_candidates};
-    const int64_t blocks = (b->total_bytes + 4095) / 4096;
+    json::FindArgs F{b->bodies, begin, end, limit, candidates, cap, (unsigned long long*)n_candidates};
+    const int64_t blocks = (end - (begin & ~(int64_t)15) + 4095) / 4096;
     hipLaunchKernelGGL(json::k_json_find_series, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(64), 0,
                        (hipStream_t)stream, F);
     KRR_HIP(ctx, hipGetLastError());

@@ -63,7 +63,7 @@ def test_abi_version_and_null_handling(lib):
     assert lib.krr_destroy(None) == 0
     assert lib.krr_json_parse(None, None, 0, 0, 0, None, None, None, None, None) == -1
     assert lib.krr_json_compact(None, None, None, None, None, None, None, None, None, None) == -1
-    assert lib.krr_json_find_series(None, None, None, 0, None, None) == -1
+    assert lib.krr_json_find_series(None, None, 0, 0, 0, None, 0, None, None) == -1
     assert lib.krr_json_parse_segments(None, None, None, None, 0, None, 0, None, None, None, None) == -1
     assert lib.krr_json_gather(None, 0, None, None, None, None, None, None, None, None) == -1
     h = ctypes.c_void_p()

@@ -261,3 +261,28 @@ def test_pack_many_equals_separate(packer):
     assert a.via == "device" and b.via == "host"
     _same(a, cpu)
     _same(b, mem_bad)
+
+
+def test_grouped_many_and_small_chunks(packer):
+    """CPU and memory grouped bodies through one pipeline, with 1-MiB chunks: candidates
+    near chunk ends are searched with the next chunk (the 16-byte carry)."""
+    from test_fleet_query import make_fleet
+
+    from krr_amd.core.device_pack import DevicePacker
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.core.models.allocations import ResourceType
+
+    objects, prom = make_fleet(seed=3, n_obj=40)
+    plan = FleetQueryPlan(objects, max_query_chars=60)
+    bc = [_recompact(prom.query_range(q)) for q in plan.queries(ResourceType.CPU)]
+    bm = [_recompact(prom.query_range(q)) for q in plan.queries(ResourceType.Memory)]
+    small = DevicePacker(packer.ctx, chunk_bytes=4096)
+    for p in (packer, small):
+        a, b = p.pack_grouped_many([(plan, bc), (plan, bm)], want_timestamps=True, return_pod_counts=True)
+        for dp, bodies in ((a, bc), (b, bm)):
+            want, want_ts, want_counts = plan.pack(bodies, want_timestamps=True, return_pod_counts=True)
+            assert dp.via == "device"
+            assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+            assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+            assert np.array_equal(dp.timestamps.cpu().numpy().view(np.uint64), want_ts.view(np.uint64))
+            assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
