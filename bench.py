@@ -862,6 +862,9 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         torch.cuda.synchronize()
         best_d = min(best_d, time.perf_counter() - t0)
     out["device_pack_samples_per_s"] = samples / best_d
+    # the reference's own loader (json + Decimal(value) per sample, prometheus.py:150-155),
+    # measured in the build container only (it cannot travel): SURVEY.md §8(a) A1
+    out["reference_loader_samples_per_s_build_container"] = 4.57e6
     # --- the same fleet through fleet-batched queries: one `sum by (pod)` body per
     # (namespace, container) group (krr_amd.core.fleet_query), 20 namespaces
     from krr_amd.core.fleet_query import FleetQueryPlan
