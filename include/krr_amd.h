@@ -367,7 +367,7 @@ int krr_synth_fill_global(krr_ctx* ctx, double* values, const int64_t* offsets, 
  *   [Decimal(value) for _, value in pod_result[0]["values"]] + the empty-pod drop
  * of PrometheusLoader.gather_data, robusta_krr/core/integrations/prometheus.py:147-155.
  * One wave per body.  A body whose bytes lie outside the canonical query_range form
- * Prometheus writes (whitespace inside the values array, escapes in keys or values,
+ * Prometheus writes (escapes in keys or values, whitespace inside a value string,
  * spellings of NaN/Inf other than "NaN"/"Inf", more than 19 significant digits,
  * status != "success", malformed JSON) is NOT an error here: its status is
  * KRR_JSON_HOST and the caller parses that batch with krr_pack_parse, which returns

@@ -15,9 +15,9 @@ Here the raw bodies cross PCIe instead and the MI355X parses them (include/krr_a
      sums (bodies are in fleet order) give the segment offsets and each body's place, and
      ``krr_json_compact`` writes the CSR.
 
-A body outside the canonical form Prometheus writes (KRR_JSON_HOST: whitespace in the
-values array, escapes, other NaN/Inf spellings, > 19 significant digits, an error status,
-malformed JSON) is not decided here: the whole batch is then parsed by the host packer,
+A body outside the form the device decides (KRR_JSON_HOST: escapes in keys or values,
+whitespace inside a value string, other NaN/Inf spellings, > 19 significant digits, an error
+status, malformed JSON; JSON whitespace between tokens is fine) is not decided here: the whole batch is then parsed by the host packer,
 which returns the host's result or raises its error — the outcome is the host packer's
 either way (``DevicePacked.via`` says which ran).
 """

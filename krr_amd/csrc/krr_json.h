@@ -247,15 +247,16 @@ __global__ __launch_bounds__(256) void k_json_compact(CompactArgs C) {
 // ---- grouped bodies ("sum by (pod) (...)"): one wave per SERIES ----
 // A grouped body holds one series per pod (megabytes per body, a few bodies per fleet), so
 // a wave per body would leave the GPU idle.  Instead:
-//   k_json_find_series  every `[{"metric":` / `,{"metric":` in the bodies (a 32-bit window
-//                       compare at each byte, 64 bytes per lane): the candidate series starts;
+//   k_json_find_series  every `{"metric":` after '[', ',' or whitespace in the bodies (a 32-bit
+//                       window compare at each byte, 64 bytes per lane): the candidate series
+//                       starts;
 //   k_json_segments     one wave per candidate: the series object (GroupedWalker from
 //                       SERIES_OPEN) — label span, values by the whole wave into scratch slot
 //                       (array offset / 8), and where the object ends;
 // and the host chains the segments body by body from the envelope head to its tail
 // (krr_json_parse.h chain_grouped, in krr_pack_route_grouped): a candidate that is not a
 // real series start is never reached by the chain, and a real series that is not a
-// candidate (another key order, whitespace) breaks it — that body goes to the host packer.
+// candidate (another key order) breaks it — that body goes to the host packer.
 constexpr int kSegWords = 7;  // start, end (one past '}'), label offset (-1), label length, slot, count, ok
 constexpr int kMaxLabel = 64;
 constexpr uint32_t kMetricHead = (uint32_t)'{' | ((uint32_t)'"' << 8) | ((uint32_t)'m' << 16) | ((uint32_t)'e' << 24);
@@ -293,7 +294,8 @@ __global__ __launch_bounds__(64) void k_json_find_series(FindArgs F) {
             if (x < F.begin || x >= F.end || x == 0 || x + 10 > F.limit) continue;
             const char* c = F.bodies + x;
             const char pre = c[-1];
-            if ((pre != '[' && pre != ',') || c[4] != 't' || c[5] != 'r' || c[6] != 'i' || c[7] != 'c' ||
+            const bool pre_ok = pre == '[' || pre == ',' || pre == ' ' || pre == '\n' || pre == '\r' || pre == '\t';
+            if (!pre_ok || c[4] != 't' || c[5] != 'r' || c[6] != 'i' || c[7] != 'c' ||
                 c[8] != '"' || c[9] != ':')
                 continue;
             const unsigned long long slot = atomicAdd(F.n_cand, 1ull);

@@ -12,11 +12,11 @@
 //     (N. Mushtak and D. Lemire, "Fast number parsing without fallback", Software:
 //     Practice and Experience 53(6), 2023), so no big-integer path exists here; a
 //     string with more significant digits is handed back to the host packer.
-//   * one sample element `[<time>,"<value>"]` of the canonical (whitespace-free)
-//     values array Prometheus writes;
+//   * one sample element `[<time>,"<value>"]` of a values array (JSON whitespace between
+//     tokens as the host reader allows it);
 //   * a small JSON reader for the envelope around that array.
 // Contract with the host packer: whatever this code ACCEPTS it parses to exactly the
-// bits krr_pack.cpp produces; anything else (whitespace inside the values array,
+// bits krr_pack.cpp produces; anything else (whitespace inside a value string,
 // escapes, "nan"/"infinity" spellings, > 19 digits, status != "success", a malformed
 // body ...) is reported as JSON_HOST and the caller re-parses the batch on the host,
 // which yields the host's own result or error.  So the device never invents an error.
@@ -251,29 +251,51 @@ KRR_JHD inline int value_bits(const char* b, const char* e, double* out) {
     return NUM_OK;
 }
 
-// One element of a canonical values array at p (which must be '['):
-// `[<json number>,"<value>"]` followed by ',' + '[' (more follow) or ']' (the last one).
-// On success: *next = the following element's '[' or one past the array's ']', *last set.
-// Returns false for anything else (the caller hands the body to the host).  One pass:
-// every byte is read once through ld.
+template <class Load>
+KRR_JHD inline void skip_ws(const char*& p, const char* e, Load ld) {
+    while (p < e) {
+        const char c = ld(p);
+        if (c != ' ' && c != '\n' && c != '\r' && c != '\t') break;
+        ++p;
+    }
+}
+
+// One element of a values array at p (which must be '['): `[<json number>,"<value>"]`
+// followed by ',' + '[' (more follow) or ']' (the last one); JSON whitespace between the
+// tokens as the host reader allows it (none inside the value string).  On success: *next =
+// the following element's '[' or one past the array's ']', *last set.  Returns false for
+// anything else (the caller hands the body to the host).  One pass: every byte is read
+// once through ld.
 template <class Load>
 KRR_JHD inline bool sample_element(const char* p, const char* e, bool want_ts, double* value, double* ts,
                                    const char** next, bool* last, Load ld) {
     if (p >= e || ld(p) != '[') return false;
     ++p;
+    skip_ws(p, e, ld);
     uint64_t tb;
     if (!scan_number(p, e, ld, false, &tb)) return false;
-    if (p + 1 >= e || ld(p) != ',' || ld(p + 1) != '"') return false;
-    p += 2;
+    skip_ws(p, e, ld);
+    if (p >= e || ld(p) != ',') return false;
+    ++p;
+    skip_ws(p, e, ld);
+    if (p >= e || ld(p) != '"') return false;
+    ++p;
     uint64_t vb;
     if (!scan_number(p, e, ld, true, &vb)) return false;
-    if (p + 2 >= e || ld(p) != '"' || ld(p + 1) != ']') return false;
-    p += 2;
+    if (p >= e || ld(p) != '"') return false;
+    ++p;
+    skip_ws(p, e, ld);
+    if (p >= e || ld(p) != ']') return false;
+    ++p;
+    skip_ws(p, e, ld);
+    if (p >= e) return false;
     const char d = ld(p);
     if (d == ',') {
-        if (p + 1 >= e || ld(p + 1) != '[') return false;
+        ++p;
+        skip_ws(p, e, ld);
+        if (p >= e || ld(p) != '[') return false;
         *last = false;
-        *next = p + 1;
+        *next = p;
     } else if (d == ']') {
         *last = true;
         *next = p + 1;
@@ -464,6 +486,7 @@ KRR_JHD inline int envelope_head(Reader& r, Envelope& env, const char** at) {
                                 if (sk < 0) return 0;
                                 if (sk == 1) {
                                     if (!r.lit('[')) return 0;
+                                    r.ws();
                                     *at = r.p;
                                     return 1;
                                 }
@@ -692,6 +715,7 @@ struct GroupedWalker {
                     } else if (key_is(kb, kn, "values", 6)) {
                         if (have_values || !r.lit('[')) return W_HOST;
                         have_values = true;
+                        r.ws();
                         values_at = r.p;
                         return W_VALUES;  // the caller parses the array, then values_done()
                     } else {
@@ -727,7 +751,8 @@ struct GroupedWalker {
 // Chain check of one grouped body (host side of the device packer): the head walk finds
 // data.result's first series; segment records (parsed on the device, one wave per series
 // object, found by the `{"metric":` pattern) must then follow each other exactly — series
-// k ends where series k + 1 starts (a ',' between them) — until the one followed by ']';
+// k ends where series k + 1 starts (a ',' and whitespace between them) — until the one
+// followed by ']';
 // then the tail walk validates the rest.  seg[j] = {start, end, label_off, label_len,
 // slot, count, ok} (absolute byte offsets, sorted by start); find(pos) returns the index of
 // the segment starting at pos or -1.  Emits each chained series in order through emit(j).
@@ -747,9 +772,11 @@ inline bool chain_grouped(const char* buf, int64_t ob, int64_t oe, const char* l
         if (j < 0 || !seg[7 * j + 6]) return false;
         emit(j);
         const char* q = buf + seg[7 * j + 1];  // one past the series' '}'
+        skip_ws(q, buf + oe, PlainLoad{});
         if (q >= buf + oe) return false;
         if (*q == ',') {
             p = q + 1;
+            skip_ws(p, buf + oe, PlainLoad{});
             if (p >= buf + oe || *p != '{') return false;
             continue;
         }

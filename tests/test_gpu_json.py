@@ -101,14 +101,24 @@ def test_prom_native_vectors_compacted(packer):
     _same(dp, per_obj)
 
 
-def test_prom_native_vectors_as_is_go_to_the_host(packer):
-    """The same vectors as json.dumps writes them (spaces inside the values array): the
-    device hands the batch to the host packer, and the result is the host's."""
+def test_prom_native_vectors_as_is(packer):
+    """The same vectors as json.dumps writes them (', ' and ': ' between every token): parsed
+    on the device too, with the host's bits."""
     from test_prom_native import _fleet as pn_fleet
 
     per_obj = pn_fleet(1)
     dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
-    assert dp.via == "host" and dp.host_bodies > 0
+    assert dp.via == "device"
+    _same(dp, per_obj)
+
+
+def test_non_canonical_batch_goes_to_the_host(packer):
+    """A body the device does not decide (an escaped key): the batch is the host packer's."""
+    per_obj = _fleet(4, n_obj=12)
+    per_obj[5] = per_obj[5] + [_compact({"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {}, "values": [[1, "2"]]}]}}).replace(b'"status"', b'"st\\u0061tus"')]
+    dp = packer.pack(per_obj, want_timestamps=True, return_pod_counts=True)
+    assert dp.via == "host" and dp.host_bodies == 1
     _same(dp, per_obj)
 
 
@@ -210,10 +220,18 @@ def test_grouped_bodies_on_device_equal_host_plan(packer, resource, max_chars):
     assert np.array_equal(dp.timestamps.cpu().numpy().view(np.uint64), want_ts.view(np.uint64))
     assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
     assert dp.series.max_len == want.max_len
-    # as json.dumps wrote them (spaces): the host decides, same result
+    # as json.dumps wrote them (', ' / ': ' between tokens): on the device too, same bits
     raw = [prom.query_range(q) for q in plan.queries(rt)]
     dh = packer.pack_grouped(plan, raw, want_timestamps=True, return_pod_counts=True)
-    assert dh.via == "host" and np.array_equal(dh.series.values.view(np.uint64), want.values.view(np.uint64))
+    assert dh.via == "device"
+    assert np.array_equal(dh.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+    assert np.array_equal(dh.series.offsets.cpu().numpy(), want.offsets)
+    # a body with an escaped series key: that batch is the host's
+    bad = list(bodies)
+    bad[0] = bad[0].replace(b'"values"', b'"v\\u0061lues"', 1)
+    dh = packer.pack_grouped(plan, bad, want_timestamps=True, return_pod_counts=True)
+    hv = plan.pack(bad, want_timestamps=True, return_pod_counts=True)[0]
+    assert dh.via == "host" and np.array_equal(dh.series.values.view(np.uint64), hv.values.view(np.uint64))
 
 
 def test_grouped_large_bodies(packer):
@@ -255,8 +273,8 @@ def test_pack_many_equals_separate(packer):
     _same(a, cpu)
     _same(b, mem)
     mem_bad = [list(x) for x in mem]
-    mem_bad[3] = mem_bad[3] + [json.dumps({"status": "success", "data": {"result": [  # spaces in the values
-        {"metric": {}, "values": [[1, "2"], [2, "3"]]}]}}).encode()]
+    mem_bad[3] = mem_bad[3] + [_compact({"status": "success", "data": {"result": [  # an escaped key
+        {"metric": {}, "values": [[1, "2"], [2, "3"]]}]}}).replace(b'"status"', b'"st\\u0061tus"')]
     a, b = packer.pack_many([cpu, mem_bad], want_timestamps=True, return_pod_counts=True)
     assert a.via == "device" and b.via == "host"
     _same(a, cpu)

@@ -182,14 +182,32 @@ def test_canonical_bodies_parse_like_the_host_packer(lib):
         assert np.array_equal(t.view(np.uint64), ts[offs[i]:offs[i + 1]].view(np.uint64))
 
 
-@pytest.mark.parametrize("kind", ["spaces", "escaped_key", "escaped_value", "status_error", "no_status",
+def test_whitespace_between_tokens_is_parsed_like_the_host(lib):
+    """json.dumps' default separators (', ' and ': ') and newlines / tabs between the tokens of
+    the values array and the envelope: the device logic accepts them, with the host's bits."""
+    from krr_amd.core.prom_native import pack_query_range_bodies
+
+    rng = np.random.default_rng(17)
+    xs = rng.gamma(2.0, 0.05, 40)
+    vals = [[1.7e9 + 15 * k, go_format(float(x))] for k, x in enumerate(xs)]
+    doc = {"status": "success", "data": {"resultType": "matrix", "result": [{"metric": {"pod": "a"}, "values": vals}]}}
+    for b in (json.dumps(doc).encode(), json.dumps(doc, indent=2).encode(),
+              json.dumps(doc, indent="\t").encode().replace(b"],", b"] \r\n,")):
+        rc, v, t = _check_body(lib, b, want_ts=1)
+        assert rc == JSON_OK, b[:120]
+        ps, ts = pack_query_range_bodies([[b]], want_timestamps=True)
+        assert np.array_equal(v.view(np.uint64), ps.values.view(np.uint64))
+        assert np.array_equal(t.view(np.uint64), ts.view(np.uint64))
+
+
+@pytest.mark.parametrize("kind", ["space_in_value", "escaped_key", "escaped_value", "status_error", "no_status",
                                   "two_values", "bad_json", "trailing", "nan_lower", "no_result", "truncated",
                                   "dup_result"])
 def test_non_canonical_bodies_go_to_the_host(lib, kind):
     base = {"status": "success", "data": {"resultType": "matrix",
                                           "result": [{"metric": {}, "values": [[1, "0.5"], [2, "1"]]}]}}
     b = {
-        "spaces": json.dumps(base).encode(),
+        "space_in_value": _compact(base).replace(b'"0.5"', b'" 0.5"'),
         "escaped_key": _compact(base).replace(b'"status"', b'"st\\u0061tus"'),
         "escaped_value": _compact(base).replace(b'"0.5"', b'"0\\u002e5"'),
         "status_error": _compact(dict(base, status="error")),
@@ -260,7 +278,7 @@ def test_grouped_bodies_walk_like_the_host_packer(lib):
         assert np.array_equal(t[:k].view(np.uint64), flat_t.view(np.uint64))
 
 
-@pytest.mark.parametrize("kind", ["escaped_label", "dup_metric", "dup_values", "no_values", "spaces", "status",
+@pytest.mark.parametrize("kind", ["escaped_label", "dup_metric", "dup_values", "no_values", "value_space", "status",
                                   "escaped_label_key", "empty_series"])
 def test_grouped_non_canonical_go_to_the_host(lib, kind):
     base = {"status": "success", "data": {"resultType": "matrix", "result": [
@@ -271,7 +289,7 @@ def test_grouped_non_canonical_go_to_the_host(lib, kind):
         "dup_metric": b.replace(b'{"metric":{"pod":"a"},', b'{"metric":{"pod":"a"},"metric":{},'),
         "dup_values": b.replace(b'"values":[[1,"1"]]}', b'"values":[[1,"1"]],"values":[]}'),
         "no_values": b.replace(b',"values":[[1,"1"]]', b''),
-        "spaces": json.dumps(base).encode(),
+        "value_space": b.replace(b'"2"', b'"2 "'),
         "status": b.replace(b'"success"', b'"error"'),
         "escaped_label_key": b.replace(b'{"pod":"a"}', b'{"p\\u006fd":"a"}'),
         "empty_series": b.replace(b'{"metric":{"pod":"a"},"values":[[1,"1"]]}', b'{}'),
