@@ -102,6 +102,26 @@ class BatchedRunner:
             return None
         return self.strategy.format_raw(raw_from_records(full), self.cpu_min_value, self.memory_min_value)
 
+    def recommend_bodies_shard(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
+                               group=None, dst: int = 0, device: Optional[int] = None, parser: str = "device",
+                               threads: int = 0):
+        """This rank's objects' raw query_range bodies (its contiguous object range; rank order
+        = fleet order, e.g. ``body_shard_bounds``) -> packed on this rank's GPU (the device
+        packer by default: each GPU's own PCIe link carries its shard's JSON) -> one kernel
+        pass -> the records gathered to ``dst``, which returns every rank's rounded RunResults
+        in fleet order (None elsewhere).  Collective: every rank calls it."""
+        from krr_amd.core.packing import PackedFleet
+        from krr_amd.core.prom_native import pack_query_range_bodies
+
+        if parser not in ("device", "host"):
+            raise ValueError("parser must be 'device' or 'host'")
+        if parser == "device":
+            fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)
+        else:
+            fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads),
+                                pack_query_range_bodies(mem_bodies, threads=threads))
+        return self.recommend_shard(fleet, group=group, dst=dst, device=device)
+
     def recommend_packed_sharded(self, fleet, group=None, dst: int = 0, device: Optional[int] = None):
         """Every rank holds the same packed fleet: each runs its sample-balanced contiguous
         shard (``fleet_shard_bounds``) and ``dst`` receives the whole fleet's results."""
@@ -154,6 +174,14 @@ class BatchedRunner:
             fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
                                 pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
         return self.recommend_packed(fleet)
+
+    @staticmethod
+    def body_shard_bounds(objects: Sequence[K8sObjectData], world: int) -> list:
+        """Contiguous object ranges per rank, cut by pod count (one query_range body per pod
+        and resource): rank r fetches and packs objects[lo:hi] of its (lo, hi)."""
+        from krr_amd.core.distributed import shard_bounds
+
+        return shard_bounds([max(len(o.pods), 1) for o in objects], world)
 
     def pack_bodies_device(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None):
         """PackedFleet in HBM from raw bodies, parsed on the device (krr_amd.core.device_pack)."""

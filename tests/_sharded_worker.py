@@ -43,7 +43,7 @@ def _oracle_records(settings, fleet):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--compute", choices=("oracle", "gpu"), required=True)
-    ap.add_argument("--entry", choices=("packed", "loader"), default="packed")
+    ap.add_argument("--entry", choices=("packed", "loader", "bodies"), default="packed")
     ap.add_argument("--path", default="cli_99_5")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
@@ -76,6 +76,26 @@ def main():
         fleet = PackedFleet(PackedSeries(cpu.reshape(-1).copy(), offs, P * T),
                             PackedSeries(mem.reshape(-1).copy(), offs.copy(), P * T))
         res = runner.recommend_packed_sharded(fleet)
+        rows = None if res is None else [
+            [str(r[ResourceType.CPU].request), str(r[ResourceType.Memory].request), str(r[ResourceType.Memory].limit)]
+            for r in res]
+    elif args.entry == "bodies":
+        # every rank builds (as it would fetch) ONLY its shard's query_range bodies; the device
+        # packer parses them on its GPU (--compute gpu), the host packer stands in otherwise
+        class _O:
+            def __init__(self, o):
+                self.pods = config1.pod_names(o)
+
+        lo, hi = BatchedRunner.body_shard_bounds([_O(o) for o in range(O)], dist.get_world_size())[rank]
+
+        def body(xs):
+            vals = ",".join(f'[{1700000000 + 60 * i},"{prom_format(float(x))}"]' for i, x in enumerate(xs))
+            return ('{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},"values":[' + vals +
+                    ']}]}}').encode()
+
+        cb = [[body(cpu[o, p]) for p in range(P)] for o in range(lo, hi)]
+        mb = [[body(mem[o, p]) for p in range(P)] for o in range(lo, hi)]
+        res = runner.recommend_bodies_shard(cb, mb, parser="device" if args.compute == "gpu" else "host")
         rows = None if res is None else [
             [str(r[ResourceType.CPU].request), str(r[ResourceType.Memory].request), str(r[ResourceType.Memory].limit)]
             for r in res]

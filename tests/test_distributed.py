@@ -171,7 +171,8 @@ def expected_rows(path):
             for w in CONFIG1["results"][path]]
 
 
-@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "cli_99_5"), ("packed", "default_int")])
+@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "cli_99_5"), ("packed", "default_int"),
+                                        ("bodies", "cli_99_5")])
 def test_sharded_runner_matches_reference_fixture(entry, path, tmp_path):
     """recommend_packed_sharded / gather_objects_recommendations_sharded on 2 ranks give the
     reference's own config-1 strings (tests/golden/config1_reference.json) for every object."""

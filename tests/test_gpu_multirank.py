@@ -28,7 +28,7 @@ sys.path.insert(0, HERE)
 from test_distributed import expected_rows, run_sharded_workers  # noqa: E402
 
 
-@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "default_int")])
+@pytest.mark.parametrize("entry,path", [("packed", "cli_99_5"), ("loader", "default_int"), ("bodies", "cli_99_5")])
 def test_sharded_runner_two_ranks_on_gpu(entry, path, tmp_path):
     assert run_sharded_workers(2, "gpu", entry, path, tmp_path, timeout=240) == expected_rows(path)
 
