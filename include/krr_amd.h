@@ -59,7 +59,8 @@ typedef enum {
     KRR_E_INVALID = -1,     /* bad argument (null pointer, bad mode, p out of (0,100]) */
     KRR_E_HIP = -2,         /* HIP runtime error (message in krr_last_error) */
     KRR_E_CAPACITY = -3,    /* a segment needs more selection scratch than was provisioned */
-    KRR_E_UNSUPPORTED = -4  /* option combination not implemented */
+    KRR_E_UNSUPPORTED = -4, /* option combination not implemented */
+    KRR_E_TIMEOUT = -5      /* a bounded wait ran out (krr_comm_init_timeout) */
 } krr_status;
 
 /* Percentile rule for the CPU recommendation.  All rules share n = number of
@@ -188,6 +189,13 @@ int krr_pack_records(krr_ctx* ctx, int64_t n_objects, const double* cpu_value,
 int krr_comm_unique_id(krr_ctx* ctx, void* unique_id);
 /* ncclCommInitRank on the ctx's device. */
 int krr_comm_init(krr_ctx* ctx, int nranks, const void* unique_id, int rank, void** out_comm);
+/* The same, bounded: a nonblocking communicator (ncclCommInitRankConfig, blocking = 0) whose
+ * state is polled for up to timeout_s seconds; when a peer never arrives the communicator is
+ * aborted (ncclCommAbort) and KRR_E_TIMEOUT is returned instead of hanging.  Calls on the
+ * communicator then wait for its state themselves (krr_gather_results does).  timeout_s <= 0:
+ * krr_comm_init. */
+int krr_comm_init_timeout(krr_ctx* ctx, int nranks, const void* unique_id, int rank, double timeout_s,
+                          void** out_comm);
 int krr_comm_destroy(krr_ctx* ctx, void* comm);
 
 /* Gather every rank's n_local records (device int64[4 * n_local]) to `root`,

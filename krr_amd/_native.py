@@ -23,6 +23,7 @@ KRR_E_INVALID = -1
 KRR_E_HIP = -2
 KRR_E_CAPACITY = -3
 KRR_E_UNSUPPORTED = -4
+KRR_E_TIMEOUT = -5
 
 KRR_PCT_REF_INDEX = 0
 KRR_PCT_SORTED_LOWER = 1
@@ -74,6 +75,7 @@ EXPORTED_SYMBOLS = (
     "krr_get_stats",
     "krr_comm_unique_id",
     "krr_comm_init",
+    "krr_comm_init_timeout",
     "krr_comm_destroy",
     "krr_gather_results",
 )
@@ -239,6 +241,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_comm_unique_id.restype = ctypes.c_int
         lib.krr_comm_init.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
         lib.krr_comm_init.restype = ctypes.c_int
+        lib.krr_comm_init_timeout.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_double, ctypes.POINTER(vp)]
+        lib.krr_comm_init_timeout.restype = ctypes.c_int
         lib.krr_comm_destroy.argtypes = [vp, vp]
         lib.krr_comm_destroy.restype = ctypes.c_int
         lib.krr_gather_results.argtypes = [vp, vp, ctypes.c_int, vp, i64, vp, vp, vp]
@@ -412,13 +416,19 @@ class Context:
         self._check(self._lib.krr_comm_unique_id(self._h, buf))
         return buf.raw
 
-    def comm_init(self, nranks: int, unique_id: bytes, rank: int) -> int:
-        """ncclCommInitRank on this ctx's device; returns the ncclComm_t as an int."""
+    def comm_init(self, nranks: int, unique_id: bytes, rank: int, timeout_s: float = 0.0) -> int:
+        """ncclCommInitRank on this ctx's device; returns the ncclComm_t as an int.
+        timeout_s > 0: bounded (krr_comm_init_timeout; NativeError KRR_E_TIMEOUT when a peer
+        never arrives)."""
         if len(unique_id) != NCCL_UNIQUE_ID_BYTES:
             raise ValueError("unique_id must be 128 bytes")
         comm = ctypes.c_void_p()
-        self._check(self._lib.krr_comm_init(self._h, int(nranks), ctypes.c_char_p(unique_id), int(rank),
-                                            ctypes.byref(comm)))
+        if timeout_s > 0:
+            self._check(self._lib.krr_comm_init_timeout(self._h, int(nranks), ctypes.c_char_p(unique_id), int(rank),
+                                                        float(timeout_s), ctypes.byref(comm)))
+        else:
+            self._check(self._lib.krr_comm_init(self._h, int(nranks), ctypes.c_char_p(unique_id), int(rank),
+                                                ctypes.byref(comm)))
         return int(comm.value or 0)
 
     def comm_destroy(self, comm: int) -> None:

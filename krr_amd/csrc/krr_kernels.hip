@@ -21,6 +21,8 @@
 
 #include <dlfcn.h>
 #include <sched.h>
+#include <time.h>
+#include <unistd.h>
 #include <rccl/rccl.h>  // types only: RCCL is resolved with dlopen/dlsym (krr_comm_*)
 
 #include <new>
@@ -4180,6 +4182,8 @@ struct RcclApi {
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
     decltype(&ncclCommGetAsyncError) async_error = nullptr;  // optional: nonblocking communicators
+    decltype(&ncclCommInitRankConfig) init_config = nullptr;  // optional: bounded init
+    decltype(&ncclCommAbort) abort = nullptr;
 };
 
 const RcclApi& rccl() {
@@ -4206,6 +4210,8 @@ const RcclApi& rccl() {
         sym(a.error_string, "ncclGetErrorString");
         a.ok = all;
         a.async_error = reinterpret_cast<decltype(a.async_error)>(dlsym(h, "ncclCommGetAsyncError"));
+        a.init_config = reinterpret_cast<decltype(a.init_config)>(dlsym(h, "ncclCommInitRankConfig"));
+        a.abort = reinterpret_cast<decltype(a.abort)>(dlsym(h, "ncclCommAbort"));
         return a;
     }();
     return api;
@@ -4244,6 +4250,50 @@ int krr_comm_init(krr_ctx* ctx, int nranks, const void* unique_id, int rank, voi
     ncclComm_t comm = nullptr;
     const ncclResult_t r = R.comm_init_rank(&comm, nranks, id, rank);
     if (r != ncclSuccess) return nccl_err(ctx, "ncclCommInitRank", r);
+    *out_comm = comm;
+    return KRR_OK;
+}
+
+int krr_comm_init_timeout(krr_ctx* ctx, int nranks, const void* unique_id, int rank, double timeout_s,
+                          void** out_comm) {
+    if (timeout_s <= 0) return krr_comm_init(ctx, nranks, unique_id, rank, out_comm);
+    if (!ctx) return KRR_E_INVALID;
+    if (!unique_id || !out_comm || nranks < 1 || rank < 0 || rank >= nranks)
+        return set_err(ctx, KRR_E_INVALID, "bad comm arguments%s", "");
+    *out_comm = nullptr;
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    if (!R.init_config || !R.abort || !R.async_error)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "this RCCL has no nonblocking init%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = R.init_config(&comm, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) return nccl_err(ctx, "ncclCommInitRankConfig", r);
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        r = R.async_error(comm, &st);
+        if (r != ncclSuccess) st = r;
+        if (st == ncclSuccess) break;
+        if (st != ncclInProgress) {
+            (void)R.abort(comm);
+            return nccl_err(ctx, "ncclCommInitRankConfig", st);
+        }
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        if ((double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec) > timeout_s) {
+            (void)R.abort(comm);
+            return set_err(ctx, KRR_E_TIMEOUT, "ncclCommInitRankConfig: not every rank arrived within the timeout%s",
+                           "");
+        }
+        usleep(1000);
+    }
     *out_comm = comm;
     return KRR_OK;
 }

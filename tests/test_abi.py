@@ -113,6 +113,7 @@ def test_select_plan_layout_and_null_handling(lib):
     assert lib.krr_gather_results(None, None, 0, None, 0, None, None, None) == -1
     assert lib.krr_comm_unique_id(None, None) == -1
     assert lib.krr_comm_init(None, 1, None, 0, None) == -1
+    assert lib.krr_comm_init_timeout(None, 1, None, 0, 1.0, None) == -1
     assert lib.krr_comm_destroy(None, None) == -1
     assert lib.krr_synth_fill_global(None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, None) == -1
     info = _native.KrrSelectPlanInfo()

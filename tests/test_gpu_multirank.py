@@ -181,6 +181,53 @@ def test_c_abi_gather_one_rank_rccl():
         ctx.close()
 
 
+def test_c_abi_comm_init_timeout_one_rank():
+    """krr_comm_init_timeout: a bounded (nonblocking) 1-rank communicator works for the
+    gather like the blocking one."""
+    import torch
+
+    from krr_amd import _native
+
+    ctx = _native.Context(0)
+    dev = torch.device("cuda:0")
+    comm = ctx.comm_init(1, ctx.comm_unique_id(), 0, timeout_s=60.0)
+    try:
+        rec = _records(500, 3, dev)
+        out = torch.zeros((500, 4), dtype=torch.int64, device=dev)
+        ctx.gather_results(comm, 0, rec, counts=[500], out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, rec)
+    finally:
+        ctx.comm_destroy(comm)
+        ctx.close()
+
+
+_MISSING_PEER = """
+import sys, time
+sys.path.insert(0, {root!r})
+import torch
+from krr_amd import _native
+ctx = _native.Context(0)
+t0 = time.time()
+try:
+    ctx.comm_init(2, ctx.comm_unique_id(), 0, timeout_s=3.0)   # rank 1 never comes
+    print("NO-TIMEOUT")
+except _native.NativeError as e:
+    print("TIMEOUT" if "error -5" in str(e) else "OTHER " + str(e), round(time.time() - t0, 1))
+"""
+
+
+def test_c_abi_comm_init_timeout_missing_peer():
+    """A 2-rank init whose second rank never arrives returns KRR_E_TIMEOUT after the bound
+    instead of hanging (run in a child process under its own time limit)."""
+    p = subprocess.run(["timeout", "-k", "5", "90", sys.executable, "-c", _MISSING_PEER.format(root=ROOT)],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = p.stdout.strip().splitlines()[-1]
+    assert out.startswith("TIMEOUT"), out
+    assert float(out.split()[-1]) < 30
+
+
 def test_c_abi_gather_with_torch_process_group_comm():
     """The communicator of a torch.distributed "nccl" group (PyTorch's own librccl.so.1) goes
     straight into krr_gather_results: the ABI binds the RCCL already in the process."""
