@@ -62,6 +62,12 @@ class DevicePacker:
         self._copy_stream = torch.cuda.Stream(device=self.device)
         self._lock = threading.Lock()
 
+    def release(self) -> None:
+        """Drop the page-locked staging buffer (it keeps the largest batch's size otherwise)."""
+        with self._lock:
+            self._stage = None
+            self._last = None
+
     def _staging(self, nbytes: int):
         import torch
 
@@ -164,7 +170,7 @@ class DevicePacker:
         if not flat or all(plan.n_slots == 0 for plan, _ in items):
             return [host_fallback(r, 0) for r in range(len(items))]
         total_bytes = sum(len(b) for b in flat)
-        cap = max(1024, total_bytes // 4096)
+        cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
         seen = [0]  # positions below this were searched
