@@ -59,6 +59,7 @@ class DevicePacker:
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
         self._stage = None
+        self._last = None  # (device bodies, staging buffer) of the last batch
         self._copy_stream = torch.cuda.Stream(device=self.device)
         self._lock = threading.Lock()
 
