@@ -850,9 +850,8 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     out["e2e_device_equals_host"] = e2e["device"][1] == e2e["host"][1]
     # the device packer alone: staging copy -> H2D -> parse -> CSR in HBM, both resources
     from krr_amd.core.device_pack import default_packer
-    from krr_amd.core.engine import default_engine
 
-    packer = default_packer(default_engine(dev.index or 0).context())
+    packer = default_packer(dev.index or 0)
     best_d = float("inf")
     for _ in range(3):
         torch.cuda.synchronize()

@@ -326,12 +326,15 @@ _packers: dict = {}
 _packers_lock = threading.Lock()
 
 
-def default_packer(ctx: _native.Context) -> DevicePacker:
-    key = (threading.get_ident(), id(ctx))
+def default_packer(device: int = 0) -> DevicePacker:
+    """The process's packer for ``device``: one page-locked staging buffer and one krr_ctx of
+    its own per device, whichever thread calls (calls are serialised by the packer's lock, so
+    the ctx is never used by two threads at once)."""
+    device = int(device.device if isinstance(device, _native.Context) else device)
     with _packers_lock:
-        p = _packers.get(key)
+        p = _packers.get(device)
         if p is None:
-            p = _packers[key] = DevicePacker(ctx)
+            p = _packers[device] = DevicePacker(_native.Context(device))
         return p
 
 

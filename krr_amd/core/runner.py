@@ -215,10 +215,9 @@ class BatchedRunner:
 
     def _device_packer(self, threads: int = 0, device: Optional[int] = None):
         from krr_amd.core.device_pack import default_packer
-        from krr_amd.core.engine import default_engine
 
         dev = getattr(self.strategy.settings, "device", 0) if device is None else int(device)
-        packer = default_packer(default_engine(dev).context())  # NativeUnavailable without a GPU
+        packer = default_packer(dev)  # NativeUnavailable without a GPU
         if threads:
             packer.threads = int(threads)
         return packer
