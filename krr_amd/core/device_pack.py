@@ -81,8 +81,16 @@ class DevicePacker:
         """per_object_bodies[o][i] = the raw query_range body of pod i of object o, for ONE
         resource (as ``pack_query_range_bodies``).  Returns a DevicePacked whose series is
         the host packer's CSR, bit for bit, in HBM."""
-        with self._lock:
-            return self._pack(per_object_bodies, want_timestamps, return_pod_counts, stream)
+        with self._lock, self._on(stream):
+            return self._pack(per_object_bodies, want_timestamps, return_pod_counts, None)
+
+    def _on(self, stream):
+        """Every buffer of a call is allocated, and every launch enqueued, on ONE stream (the
+        caller's ``stream`` or the device's current one): the caching allocator then never
+        hands a block that is still read by an enqueued launch to another stream."""
+        import torch
+
+        return torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
 
     def _upload(self, flat, want_ts, st, launch):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
@@ -143,8 +151,8 @@ class DevicePacker:
                           stream=None, label: str = "pod") -> list:
         """Several (plan, bodies) pairs (e.g. CPU and memory) through ONE staging / copy /
         candidate-search pipeline; one DevicePacked per pair."""
-        with self._lock:
-            return self._pack_grouped_multi(items, want_timestamps, return_pod_counts, stream, label)
+        with self._lock, self._on(stream):
+            return self._pack_grouped_multi(items, want_timestamps, return_pod_counts, None, label)
 
     def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label) -> list:
         import torch
@@ -239,8 +247,8 @@ class DevicePacker:
                   return_pod_counts: bool = False, stream=None) -> list:
         """Several resources' bodies (e.g. CPU and memory of one fleet) through ONE staging /
         copy / parse pipeline: one DevicePacked per resource, each as ``pack`` would give it."""
-        with self._lock:
-            return self._pack_multi(resources, want_timestamps, return_pod_counts, stream)
+        with self._lock, self._on(stream):
+            return self._pack_multi(resources, want_timestamps, return_pod_counts, None)
 
     def _pack(self, per_object_bodies, want_ts, want_counts, stream) -> DevicePacked:
         return self._pack_multi([per_object_bodies], want_ts, want_counts, stream)[0]
