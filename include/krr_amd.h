@@ -257,6 +257,44 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
                      const double* vmax, const krr_sketch_params* sp, const krr_percentile_params* params,
                      double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);
 
+/* ---- KLL-style compactor sketch: a data-independent RANK-error bound ----
+ * (north_star: "an optional mergeable t-digest/KLL sketch mode"; the log-linear sketch
+ * above bounds the value error only.)  One HBM pass per series slice: blocks of 512
+ * slots sorted on the wave and compacted (every other key from a coin-chosen offset,
+ * weight x2), runs of <= 256 keys merged and compacted level by level, the lowest runs
+ * compacted until at most `budget` keys remain; exported as one row of
+ * krr_kll_row_words() uint64 words per series (layout in krr_amd/csrc/krr_kll.h).
+ * A slice that fits one 1,024-slot chunk with <= budget present samples is kept whole
+ * (exact).  Rows of one series' time slices merge by concatenation.  Row word 8 holds
+ * sum(w^2) over the slice's compactions: with probability >= 1 - delta the weighted rank
+ * of any value is off by at most sqrt(2 ln(2/delta) * sum(w^2)) (Hoeffding) — a bound in
+ * n and the schedule only, whatever the values. */
+typedef struct {
+    int32_t budget;   /* keys kept per series slice, in [256, 4096] */
+    int32_t slice;    /* this slice's index (time shard): part of the compaction coin */
+    uint64_t seed;    /* compaction coins: splitmix64 of (seed, seg_base + s, slice, level, count) */
+} krr_kll_params;
+
+/* uint64 words per exported row (10 + budget), or < 0 if invalid. */
+int64_t krr_kll_row_words(const krr_kll_params* kp);
+
+/* rows[S * row_words] (device): one row per segment of `series` (gaps_are_nan respected:
+ * NaN gaps are absent; a NaN sample in the compact layout is counted in row word 1).
+ * seg_base: global index of segment 0 (coins depend on it).  KRR_E_UNSUPPORTED for
+ * segments longer than ~4.2 M slots. */
+int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
+                  uint64_t* rows, void* stream);
+
+/* Percentile of every series from its rows_per_series rows (rows[(s * W + w) * row_words],
+ * e.g. W time slices after an all-to-all): SORTED_LOWER or LINEAR over n = sum(present);
+ * rank r is answered by the smallest kept key whose weighted count c satisfies
+ * c * n > r * total_weight (r = 0 and n - 1: the exact min / max).  out_flags:
+ * KRR_FLAG_EMPTY, KRR_FLAG_NAN (value NaN), KRR_FLAG_CAPACITY (a row overflowed; never
+ * expected).  REF_INDEX -> KRR_E_UNSUPPORTED. */
+int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
+                  const krr_kll_params* kp, const krr_percentile_params* params, double* out_value,
+                  int64_t* out_count, uint32_t* out_flags, void* stream);
+
 /* ---- Exact refinement of merged sketches (config 5, exact percentiles) ----
  * The merged counts are exact, so they locate each needed rank's bin exactly:
  *   1. krr_sketch_locate on the owner's merged sketches -> krr_sketch_loc per series;

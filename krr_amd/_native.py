@@ -62,6 +62,9 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_width",
     "krr_sketch_build",
     "krr_sketch_query",
+    "krr_kll_row_words",
+    "krr_kll_build",
+    "krr_kll_query",
     "krr_sketch_locate",
     "krr_sketch_range_count",
     "krr_sketch_collect",
@@ -119,6 +122,15 @@ class KrrSketchParams(ctypes.Structure):
         ("min_exponent", ctypes.c_int32),
         ("octaves", ctypes.c_int32),
         ("reserved", ctypes.c_int32),
+    ]
+
+
+class KrrKllParams(ctypes.Structure):
+    """include/krr_amd.h krr_kll_params: the KLL-style compactor sketch."""
+    _fields_ = [
+        ("budget", ctypes.c_int32),
+        ("slice", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
     ]
 
 
@@ -254,6 +266,13 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_sketch_build.restype = ctypes.c_int
         lib.krr_sketch_query.argtypes = [vp, i64, vp, vp, vp, skp, pp, vp, vp, vp, vp]
         lib.krr_sketch_query.restype = ctypes.c_int
+        kkp = ctypes.POINTER(KrrKllParams)
+        lib.krr_kll_row_words.argtypes = [kkp]
+        lib.krr_kll_row_words.restype = i64
+        lib.krr_kll_build.argtypes = [vp, sp, kkp, i64, vp, vp]
+        lib.krr_kll_build.restype = ctypes.c_int
+        lib.krr_kll_query.argtypes = [vp, i64, i32, vp, kkp, pp, vp, vp, vp, vp]
+        lib.krr_kll_query.restype = ctypes.c_int
         lib.krr_rank_of.argtypes = [vp, sp, vp, vp, vp, vp]
         lib.krr_rank_of.restype = ctypes.c_int
         lib.krr_sketch_locate.argtypes = [vp, i64, vp, skp, pp, vp, vp]
@@ -515,6 +534,30 @@ class Context:
         self._check(self._lib.krr_sketch_refine(self._h, ctypes.byref(collected), loc.data_ptr(),
                                                 out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(),
                                                 self._stream(stream)))
+
+    def kll_row_words(self, kp: KrrKllParams) -> int:
+        w = int(self._lib.krr_kll_row_words(ctypes.byref(kp)))
+        if w < 0:
+            raise ValueError("invalid kll parameters (budget must be in [256, 4096])")
+        return w
+
+    def kll_build(self, series: KrrSeries, kp: KrrKllParams, rows, seg_base: int = 0, stream=None) -> None:
+        """rows: int64 [S, kll_row_words] (uint64 words)."""
+        S = series.n_segments
+        _check_tensor(rows, "int64", S * self.kll_row_words(kp))
+        self._check(self._lib.krr_kll_build(self._h, ctypes.byref(series), ctypes.byref(kp), int(seg_base),
+                                            rows.data_ptr(), self._stream(stream)))
+
+    def kll_query(self, rows, rows_per_series: int, kp: KrrKllParams, params: KrrPercentileParams, out_value,
+                  out_count, out_flags, stream=None) -> None:
+        """rows: int64 [S * rows_per_series, kll_row_words], series-major."""
+        S = out_value.numel()
+        _check_tensor(rows, "int64", S * int(rows_per_series) * self.kll_row_words(kp))
+        for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
+            _check_tensor(t, dt, S)
+        self._check(self._lib.krr_kll_query(self._h, S, int(rows_per_series), rows.data_ptr(), ctypes.byref(kp),
+                                            ctypes.byref(params), out_value.data_ptr(), out_count.data_ptr(),
+                                            out_flags.data_ptr(), self._stream(stream)))
 
     def rank_of(self, series: KrrSeries, values, out_lt, out_le, stream=None) -> None:
         S = series.n_segments

@@ -30,6 +30,12 @@ r-th contiguous time slice of every series.
   all-to-all hands them to the owner in time order, and ``krr_sketch_refine``
   selects the ranks inside the short lists: bit-identical to selecting over the
   whole series on one GPU.
+* KLL-style compactor sketch (``kll_time_sharded``, ``bench.py --sketch-only --sketch-kind
+  kll``): per slice one HBM pass sorts 512-slot blocks on the wave and compacts them
+  level by level into at most ``budget`` weighted keys (``krr_kll_build``); the W rows of
+  a series reach its owner in one all-to-all and are queried together
+  (``krr_kll_query``).  Unlike the histogram its RANK error has a data-independent bound:
+  ``kll_rank_bound`` (Hoeffding over the compactions' coins, from the rows' sum of w^2).
 * REF_INDEX (the reference's rule, ``simple.py:36``) stays exact: all-gather the
   per-slice present counts, the rank whose slice holds global index k selects it
   (``krr_select_present``), one all-gather collects the answers.
@@ -623,3 +629,123 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
     ctx.segmented_percentile(sub, params, v, n, f, stream)
     loc = per_owner[rank] - blocks[rank][0]
     out["value"][loc], out["count"][loc], out["flags"][loc] = v, n, f
+
+
+# ------------------------- KLL-style compactor sketch -------------------------
+
+@dataclass(frozen=True)
+class KllConfig:
+    """``budget`` weighted keys kept per series slice (krr_kll_params); ``seed`` drives the
+    compaction coins, so a run is reproducible (and checkable against a CPU restatement)."""
+    budget: int = 512
+    seed: int = 0x4B4C4C5345454431
+
+    def params(self, slice_id: int = 0) -> _native.KrrKllParams:
+        return _native.KrrKllParams(self.budget, int(slice_id), self.seed & (2 ** 64 - 1))
+
+    @property
+    def row_words(self) -> int:
+        return 10 + self.budget
+
+
+def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, seg_base: int = 0,
+              stream=None):
+    """One HBM pass: int64 [S, row_words] rows of this rank's slice of every series.
+    ``series``: a KrrSeries, or (lo, hi, KrrSeries) parts in buffers of their own."""
+    import torch
+
+    parts = _parts(series)
+    S = parts[-1][1] if parts else 0
+    dev = parts[0][2]._keep[0].device
+    rows = torch.empty((max(S, 1), cfg.row_words), dtype=torch.int64, device=dev)
+    for lo, hi, ser in parts:
+        if hi > lo:
+            ctx.kll_build(ser, cfg.params(slice_id), rows[lo:hi], seg_base=seg_base + lo, stream=stream)
+    return rows[:S]
+
+
+def kll_exchange(rows, group=None):
+    """The W slice rows of each series of this rank's owner block (``owner_blocks``), as
+    int64 [n_block * W, row_words] series-major (one all-to-all).  World size 1: ``rows``."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return rows, 1
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S, RW = rows.shape
+    per = -(-S // world) if S else 0
+    dev = rows.device
+    coll = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    send = torch.zeros((per * world, RW), dtype=torch.int64, device=dev)
+    send[:S] = rows
+    recv = torch.empty((per * world, RW), dtype=torch.int64, device=coll)
+    if per:
+        dist.all_to_all_single(recv, send.to(coll), group=group)
+    lo, hi = owner_blocks(S, world)[rank]
+    # recv[v * per + i] = rank v's slice of series lo + i: to series-major [i][v]
+    merged = recv.to(dev).view(world, per, RW)[:, : hi - lo].transpose(0, 1).contiguous()
+    return merged.view((hi - lo) * world, RW), world
+
+
+def kll_query(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig,
+              params: _native.KrrPercentileParams, stream=None) -> dict:
+    import torch
+
+    n = rows.shape[0] // max(rows_per_series, 1)
+    dev = rows.device
+    out = {"value": torch.empty(max(n, 1), dtype=torch.float64, device=dev)[:n],
+           "count": torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n],
+           "flags": torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]}
+    if n:
+        ctx.kll_query(rows, rows_per_series, cfg.params(), params, out["value"], out["count"], out["flags"], stream)
+    return out
+
+
+def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _native.KrrPercentileParams,
+                     group=None, stream=None, events=None) -> dict:
+    """Sketch-only percentile of every time-sharded series: build (one pass over this
+    rank's slices; slice id = rank) -> all-to-all of the rows -> query on the owner.
+    value/count/flags of this rank's owner block, plus 'block' and 'rows' (the owner's
+    merged rows, series-major, for ``kll_rank_bound``)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    st = stream
+    if events is not None:
+        events[0].record(st) if st is not None else events[0].record()
+    rows = kll_build(ctx, series, cfg, slice_id=rank, stream=stream)
+    if events is not None:
+        events[1].record(st) if st is not None else events[1].record()
+    merged, W = kll_exchange(rows, group)
+    out = kll_query(ctx, merged, W, cfg, params, stream)
+    S = rows.shape[0]
+    out.update(block=owner_blocks(S, world)[rank] if world > 1 else (0, S), rows=merged, rows_per_series=W)
+    return out
+
+
+def kll_rank_bound(rows, rows_per_series: int, delta: float = 0.01) -> np.ndarray:
+    """Per series, the normalised rank-error bound that holds with probability >= 1 - delta:
+    (2 sqrt(2 ln(6/delta) sum w^2) + w_max) / n, from the rows' headers (word 8: sum w^2
+    of the slice's compactions; run lengths: the heaviest kept key).
+
+    Why: a compaction of weight-w keys changes the weighted count of keys <= x, for a
+    FIXED x, by 0 or +-w, zero-mean over its coin and independent of the others, so by
+    Hoeffding |E(x)| <= t = sqrt(2 ln(6/delta) sum w^2) except with probability delta/3.
+    Take x- and x+ = the true order statistics at ranks r -+ (2t + w_max) and the total
+    weight (x = +inf): on the three events, the query's threshold r * W / n is within t
+    of r, the answer's weighted count jumps by at most w_max, so its true rank lies
+    between those of x- and x+.  Data-independent: n and the compaction schedule only.
+    NaN for empty series."""
+    h = rows[:, :10].cpu().numpy().astype(np.uint64).reshape(-1, rows_per_series, 10)
+    n = h[:, :, 0].sum(axis=1).astype(np.float64)
+    w2 = h[:, :, 8].astype(np.float64).sum(axis=1)
+    lens = np.stack([(h[:, :, 4 + (lv >> 2)] >> np.uint64(16 * (lv & 3))) & np.uint64(0xFFFF) for lv in range(16)],
+                    axis=-1)  # [S, W, 16]
+    present = (lens > 0).any(axis=1)  # [S, 16]
+    top = np.where(present.any(axis=1), 15 - np.argmax(present[:, ::-1], axis=1), 0)
+    wmax = np.where(present.any(axis=1), 2.0 ** top, 0.0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return (2.0 * np.sqrt(2.0 * np.log(6.0 / delta) * w2) + wmax) / n

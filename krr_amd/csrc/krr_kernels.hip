@@ -2927,6 +2927,10 @@ __global__ __launch_bounds__(64) void k_rank_of(const double* __restrict__ vals,
     }
 }
 
+}  // namespace krr
+#include "krr_kll.h"
+namespace krr {
+
 // The k[s]-th present sample (0-based, position order; NaN slots absent when
 // gaps) of each segment, k[s] < 0 -> skipped.  The time-sharded REF_INDEX: the
 // rank whose slice holds global index k selects it locally.
@@ -3481,7 +3485,8 @@ int krr_create(int device, krr_ctx** out_ctx) {
     (void)hipFuncSetAttribute((const void*)k_sketch_build, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)c->max_lds);
     for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
-                          (const void*)k_window_export<false>, (const void*)k_window_merge})
+                          (const void*)k_window_export<false>, (const void*)k_window_merge,
+                          (const void*)k_kll_build, (const void*)k_kll_query})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -3827,6 +3832,67 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
     SketchQueryArgs A{n_segments, sketch_geom(*sp), counts, vmin, vmax, params->mode, params->p_num,
                       params->p_den, params->q, out_value, out_count, out_flags};
     hipLaunchKernelGGL(k_sketch_query, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int64_t krr_kll_row_words(const krr_kll_params* kp) {
+    if (!kp || kp->budget < kKllRun || kp->budget > 4096) return -1;
+    return (int64_t)kKllHdr + kp->budget;
+}
+
+static size_t kll_build_lds(int levels) {
+    return (size_t)(2 + levels) * kKllRun * 8 + 2 * kKllLevels * 4;
+}
+
+int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
+                  uint64_t* rows, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    if (krr_kll_row_words(kp) < 0) return set_err(ctx, KRR_E_INVALID, "kll budget must be in [256, 4096]%s", "");
+    if (seg_base < 0) return set_err(ctx, KRR_E_INVALID, "negative seg_base%s", "");
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!rows) return set_err(ctx, KRR_E_INVALID, "null rows%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    int64_t maxlen = 0;
+    rc = resolve_maxlen(ctx, series, (hipStream_t)stream, &maxlen);
+    if (rc) return rc;
+    const int levels = kll_levels(maxlen);
+    if (levels > kKllLevels - 1)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "kll: segments of %s%lld slots need more run levels", "",
+                       (long long)maxlen);
+    const size_t lds = kll_build_lds(levels);
+    if (lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "kll needs %s%lld B of LDS", "", (long long)lds);
+    KllBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, kp->budget, levels,
+                   (uint32_t)kp->slice, kp->seed, seg_base, rows};
+    hipLaunchKernelGGL(k_kll_build, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
+                  const krr_kll_params* kp, const krr_percentile_params* params, double* out_value,
+                  int64_t* out_count, uint32_t* out_flags, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_params(ctx, params);
+    if (rc) return rc;
+    if (params->mode == KRR_PCT_REF_INDEX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no sketch form: use krr_select_present%s", "");
+    if (krr_kll_row_words(kp) < 0) return set_err(ctx, KRR_E_INVALID, "kll budget must be in [256, 4096]%s", "");
+    if (n_series < 0 || rows_per_series < 1) return set_err(ctx, KRR_E_INVALID, "bad n_series / rows_per_series%s", "");
+    if (n_series == 0) return KRR_OK;
+    if (!rows || !out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    const size_t lds = (size_t)rows_per_series * kp->budget * 9;
+    if (lds > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll query of %s%lld rows needs more LDS", "", (long long)rows_per_series);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    KllQueryArgs A{n_series, rows_per_series, kp->budget, rows, params->mode, params->p_num, params->p_den,
+                   params->q, out_value, out_count, out_flags};
+    hipLaunchKernelGGL(k_kll_query, dim3(grid_for(n_series)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -1,0 +1,511 @@
+// krr_kll.h — KLL-style compactor sketch with a data-independent rank-error bound
+// (config 5, sketch-only mode; included by krr_kernels.hip after the streaming skeleton).
+//
+// north_star names "an optional mergeable t-digest/KLL sketch mode" whose rank error is
+// reported.  The log-linear histogram (k_sketch_build) bounds the VALUE error only; this
+// one bounds the RANK error whatever the data (low dispersion, heavy quantisation, ties).
+//
+// One wave per series slice streams it once (stream_segment, 1,024 slots per chunk):
+//   * each chunk is split in two level-0 blocks of 512 slots (block b = lanes 32b..32b+31,
+//     16 slots per lane), sorted by an in-register bitonic network (in-lane stages on the
+//     lane's 16 keys, cross-lane stages by shuffles); NaN slots sort last and are dropped;
+//   * a block is COMPACTED: the keys at sorted positions off, off+2, ... (off a coin from a
+//     counter hash of (seed, series, slice, level, count)) become a run of <= 256 keys of
+//     weight 2, pushed to level 1;
+//   * level h >= 1 holds at most one sorted run (LDS).  Pushing a run onto a full level
+//     merges the two runs (merge-path positions by binary search) and compacts the merge
+//     (same coin rule): <= 256 keys of weight 2^(h+1) go up — a binary counter of runs;
+//   * at the end, while more than `budget` keys remain, the lowest run is compacted alone
+//     and pushed up; the runs are exported as one fixed-size row.
+// A slice of <= budget present samples that fits one chunk is exported whole (weight 1):
+// short series are exact.
+//
+// Rank error: a compaction of weight-w keys moves the weighted rank of any fixed value by
+// 0 or +-w, zero-mean over its coin, independently; so |error| <= sqrt(2 ln(2/delta) sum w^2)
+// with probability >= 1 - delta (Hoeffding), plus one key's weight for the answer's own
+// granularity.  sum w^2 is exported per row and merged by addition: the bound depends on
+// n and the compaction schedule only, never on the values.
+//
+// Rows merge across time slices by concatenation (all-to-all to the series' owner, as the
+// window export); k_kll_query stages a series' W rows in LDS and bisects the 64-bit key
+// space for the smallest key whose weighted count passes rank r * total_weight / n.
+#pragma once
+
+namespace krr {
+
+constexpr int kKllBlock = 512;   // level-0 block (half a streaming chunk)
+constexpr int kKllRun = 256;     // keys per run at levels >= 1
+constexpr int kKllLevels = 16;   // run slots: level 0 (whole short slices) .. 15
+constexpr int kKllHdr = 10;      // header words of an exported row
+constexpr uint64_t kKllNanKey = ~0ull;  // sorts after every okey() of a non-NaN value
+
+// Row layout (uint64 words): [0] present samples  [1] NaN samples (compact layout; 0 with
+// gaps)  [2] min  [3] max (f64 bits, NaN when empty)  [4..7] run lengths, u16 x 16, level
+// h at bits 16(h & 3) of word 4 + h/4  [8] sum over compactions of w^2  [9] total weight
+// (sum of len_h 2^h)  [10 ..] keys (okey order), level 0 first, then level 1, 2, ...
+// Within a run the keys ascend, except level 0 = block 0's keys then block 1's.
+
+__host__ __device__ inline uint64_t kll_mix(uint64_t z) {  // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// Compaction offset (0 or 1) of the `cnt`-th compaction at `level` of a series' slice.
+__host__ __device__ inline uint32_t kll_coin(uint64_t seed, uint64_t series, uint32_t slice, uint32_t level,
+                                             uint32_t cnt) {
+    const uint64_t x = seed + 0x9E3779B97F4A7C15ull * (series + 1) + 0xD1B54A32D192ED03ull * ((uint64_t)slice + 1) +
+                       0x8CB92BA72F3D8DD7ull * (((uint64_t)level << 32) | cnt);
+    return (uint32_t)(kll_mix(x) >> 63);
+}
+
+// Chunks stream_segment delivers for [beg, end) (the same arithmetic).
+__host__ __device__ inline int64_t kll_nchunks(int64_t beg, int64_t end) {
+    int64_t a0 = (beg + 1) & ~(int64_t)1;
+    if (a0 > end) a0 = end;
+    int64_t a1 = end & ~(int64_t)1;
+    if (a1 < a0) a1 = a0;
+    const int64_t nunits = (a1 - a0) >> 1, CH = (int64_t)kUnroll * kWave;
+    const int64_t nfull = nunits / CH, rem = nunits - nfull * CH;
+    return nfull + ((rem > 0 || a0 > beg || a1 < end) ? 1 : 0);
+}
+
+// Highest run level a segment of `len` slots can reach (runs pushed by the blocks form a
+// binary counter; the final compression may carry one level further).
+__host__ __device__ inline int kll_levels(int64_t len) {
+    const int64_t blocks = 2 * kll_nchunks(0, len) + 2;
+    int lg = 0;
+    while ((int64_t(1) << (lg + 1)) <= blocks) ++lg;
+    return lg + 2;
+}
+
+struct KllBuildArgs {
+    const double* vals;
+    const int64_t* offs;
+    int64_t S;
+    int32_t gaps;
+    int32_t budget;
+    int32_t levels;   // LDS run slots for levels 1..levels
+    uint32_t slice;
+    uint64_t seed;
+    int64_t seg_base;
+    uint64_t* rows;   // [S][kKllHdr + budget]
+};
+
+// u64 compare-exchange: after it, a holds the min if asc, else the max.
+__device__ __forceinline__ void kll_cx(uint64_t& a, uint64_t& b, bool asc) {
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = asc ? lo : hi;
+    b = asc ? hi : lo;
+}
+
+__device__ __forceinline__ uint64_t kll_shfl_xor(uint64_t x, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, m, kWave);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), m, kWave);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// In-lane substeps j = J, J/2, .., 1 of bitonic stage k on the lane's 16 keys
+// (position = lane * 16 + i; direction from bit k of the position, all ascending at k = 512).
+template <int J>
+__device__ __forceinline__ void kll_inlane(uint64_t (&x)[16], uint32_t k, int lane) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i & J) continue;
+        const uint32_t pos = (uint32_t)lane * 16u + (uint32_t)i;
+        const bool asc = k >= (uint32_t)kKllBlock || (pos & k) == 0;
+        kll_cx(x[i], x[i + J], asc);
+    }
+    if constexpr (J > 1) kll_inlane<J / 2>(x, k, lane);
+}
+
+// Sort each 512-key block (lanes 0-31: block 0, lanes 32-63: block 1) ascending.
+__device__ __forceinline__ void kll_sort_blocks(uint64_t (&x)[16], int lane) {
+    kll_inlane<1>(x, 2, lane);
+    kll_inlane<2>(x, 4, lane);
+    kll_inlane<4>(x, 8, lane);
+    kll_inlane<8>(x, 16, lane);
+#pragma unroll 1
+    for (uint32_t k = 32; k <= (uint32_t)kKllBlock; k <<= 1) {
+        const bool asc = k >= (uint32_t)kKllBlock || (((uint32_t)lane * 16u) & k) == 0;
+#pragma unroll 1
+        for (uint32_t j = k >> 1; j >= 16; j >>= 1) {
+            const int m = (int)(j >> 4);
+            const bool lower = (lane & m) == 0;
+            const bool take_min = lower == asc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint64_t o = kll_shfl_xor(x[i], m);
+                const uint64_t lo = x[i] < o ? x[i] : o, hi = x[i] < o ? o : x[i];
+                x[i] = take_min ? lo : hi;
+            }
+        }
+        kll_inlane<8>(x, k, lane);
+    }
+}
+
+// #keys < v (STRICT) or <= v in the sorted run r[0, n).
+template <bool STRICT>
+__device__ __forceinline__ uint32_t kll_rank_in(const uint64_t* r, uint32_t n, uint64_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const bool go = STRICT ? r[mid] < v : r[mid] <= v;
+        lo = go ? mid + 1 : lo;
+        hi = go ? hi : mid;
+    }
+    return lo;
+}
+
+struct KllState {
+    uint64_t* tmp[2];   // two LDS runs of kKllRun keys
+    uint64_t* lv;       // LDS runs, level h at lv + (h - 1) * kKllRun
+    uint32_t* lens;     // LDS [kKllLevels]
+    uint32_t* cnt;      // LDS [kKllLevels] compactions done per level
+    uint64_t seed, series;
+    uint32_t slice;
+    uint64_t sum_w2;    // wave-uniform
+    uint32_t overflow;  // a run above the provisioned levels (never expected)
+    int lane;
+
+    __device__ __forceinline__ uint64_t* run(uint32_t h) const { return lv + (size_t)(h - 1) * kKllRun; }
+
+    // Push the run tmp[t_sel][0, t) at level h (>= 1): store it, or merge-compact and carry.
+    __device__ void push(uint32_t t_sel, uint32_t t, uint32_t h, int levels) {
+        while (t) {  // an empty run changes nothing
+            if ((int)h > levels) {
+                overflow = 1;
+                return;
+            }
+            const uint32_t a = uni32(lens[h]);
+            const uint64_t* T = tmp[t_sel];
+            if (a == 0) {
+                uint64_t* L = run(h);
+                for (uint32_t i = lane; i < t; i += kWave) L[i] = T[i];
+                __syncthreads();
+                if (lane == 0) lens[h] = t;
+                __syncthreads();
+                return;
+            }
+            const uint32_t c = uni32(cnt[h]);
+            const uint32_t off = kll_coin(seed, series, slice, h, c);
+            const uint64_t* A = run(h);
+            uint64_t* O = tmp[t_sel ^ 1];
+            for (uint32_t i = lane; i < a; i += kWave) {  // A's keys before T's equal keys
+                const uint64_t v = A[i];
+                const uint32_t p = i + kll_rank_in<true>(T, t, v);
+                if (p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v;
+            }
+            for (uint32_t j = lane; j < t; j += kWave) {
+                const uint64_t v = T[j];
+                const uint32_t p = j + kll_rank_in<false>(A, a, v);
+                if (p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v;
+            }
+            sum_w2 += (uint64_t)1 << (2 * h);
+            __syncthreads();
+            if (lane == 0) {
+                lens[h] = 0;
+                cnt[h] = c + 1;
+            }
+            __syncthreads();
+            t = (a + t > off) ? (a + t - off + 1) >> 1 : 0;
+            t_sel ^= 1;
+            ++h;
+        }
+    }
+};
+
+__global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    KllState K;
+    K.tmp[0] = reinterpret_cast<uint64_t*>(smem);
+    K.tmp[1] = K.tmp[0] + kKllRun;
+    K.lv = K.tmp[1] + kKllRun;
+    K.lens = reinterpret_cast<uint32_t*>(K.lv + (size_t)A.levels * kKllRun);
+    K.cnt = K.lens + kKllLevels;
+    K.seed = A.seed;
+    K.slice = A.slice;
+    K.lane = lane;
+    const uint32_t RW = (uint32_t)(kKllHdr + A.budget);
+    const int blk = lane >> 5;                 // this lane's level-0 block
+    const uint32_t bpos = (uint32_t)(lane & 31) * 16u;  // its first position in the block
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        if (lane < kKllLevels) {
+            K.lens[lane] = 0;
+            K.cnt[lane] = 0;
+        }
+        __syncthreads();
+        K.series = (uint64_t)(A.seg_base + s);
+        K.sum_w2 = 0;
+        K.overflow = 0;
+        const bool whole = kll_nchunks(beg, end) <= 1;  // one chunk: kept exactly if it fits the budget
+        uint64_t* row = A.rows + (size_t)s * RW;
+        uint32_t nan_l = 0, pres_l = 0, c_whole[2] = {0, 0};
+        uint64_t kmin = kKllNanKey, kmax = 0;
+        bool any = false;
+        uint32_t blocks = 0;
+
+        struct Proc {
+            KllState& K;
+            const KllBuildArgs& A;
+            uint64_t* row;
+            int lane, blk;
+            uint32_t bpos;
+            bool whole;
+            uint32_t& nan_l;
+            uint32_t& pres_l;
+            uint32_t (&c_whole)[2];
+            uint64_t& kmin;
+            uint64_t& kmax;
+            bool& any;
+            uint32_t& blocks;
+            __device__ void chunk(const double2 (&c)[kUnroll]) {
+                uint64_t x[16];
+                uint32_t valid = 0;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t b = dbits(slot_val(c, j));
+                    const bool nan = is_nan_bits(b);
+                    const uint64_t key = nan ? kKllNanKey : okey(b);
+                    x[j] = key;
+                    valid += nan ? 0u : 1u;
+                    kmin = (!nan && key < kmin) ? key : kmin;
+                    kmax = (!nan && key > kmax) ? key : kmax;
+                    any = any || !nan;
+                }
+                nan_l += 16u - valid;
+                pres_l += valid;
+                // present keys per block (lanes 0-31 / 32-63)
+                const uint32_t incl = wave_scan32(valid, 0u, OpAdd32{});
+                const uint32_t c0 = lane_bcast32(incl, 31), c1 = lane_bcast32(incl, kWave - 1) - c0;
+                kll_sort_blocks(x, lane);
+                if (whole) {  // held in registers until the end (the only chunk)
+                    c_whole[0] = c0;
+                    c_whole[1] = c1;
+                    // exported now if it fits: level 0, block 0's keys then block 1's
+                    if (c0 + c1 <= (uint32_t)A.budget) {
+                        const uint32_t base = blk ? c0 : 0u, cb = blk ? c1 : c0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            if (bpos + (uint32_t)i < cb) row[kKllHdr + base + bpos + i] = x[i];
+                        return;
+                    }
+                }
+#pragma unroll 1
+                for (int b = 0; b < 2; ++b) {
+                    const uint32_t cb = b ? c1 : c0;
+                    if (cb == 0) continue;  // an all-NaN block: nothing to compact
+                    const uint32_t c0n = uni32(K.cnt[0]);
+                    const uint32_t off = kll_coin(K.seed, K.series, K.slice, 0, c0n);
+                    if (blk == b) {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const uint32_t p = bpos + (uint32_t)i;
+                            if (p < cb && p >= off && ((p - off) & 1u) == 0) K.tmp[0][(p - off) >> 1] = x[i];
+                        }
+                    }
+                    K.sum_w2 += 1;
+                    __syncthreads();
+                    if (lane == 0) K.cnt[0] = c0n + 1;
+                    __syncthreads();
+                    const uint32_t t = cb > off ? (cb - off + 1) >> 1 : 0u;
+                    K.push(0, t, 1, A.levels);
+                    ++blocks;
+                }
+            }
+        } P{K, A, row, lane, blk, bpos, whole, nan_l, pres_l, c_whole, kmin, kmax, any, blocks};
+
+        const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
+        const uint64_t n_nan = (uint64_t)wave_sum_u32(nan_l) - pad;
+        const uint64_t n_pres = wave_sum_u32(pres_l);
+        const uint64_t gmin = wave_min_u64(kmin), gmax = wave_max_u64(any ? kmax : 0ull);
+        const bool exact0 = whole && c_whole[0] + c_whole[1] <= (uint32_t)A.budget;
+        // final compression: the lowest run alone, until the budget holds
+        if (!exact0) {
+#pragma unroll 1
+            while (true) {
+                uint32_t total = 0, low = 0;
+#pragma unroll 1
+                for (int h = A.levels; h >= 1; --h) {
+                    const uint32_t l = uni32(K.lens[h]);
+                    total += l;
+                    low = l ? (uint32_t)h : low;
+                }
+                if (total <= (uint32_t)A.budget || low == 0 || K.overflow) break;
+                const uint32_t a = uni32(K.lens[low]);
+                const uint32_t c = uni32(K.cnt[low]);
+                const uint32_t off = kll_coin(K.seed, K.series, K.slice, low, c);
+                const uint64_t* L = K.run(low);
+                uint64_t keep[kKllRun / kWave / 2];
+#pragma unroll
+                for (int q = 0; q < kKllRun / kWave / 2; ++q) {
+                    const uint32_t p = off + 2u * ((uint32_t)lane + (uint32_t)q * kWave);  // output index -> position
+                    keep[q] = p < a ? L[p] : 0ull;
+                }
+                K.sum_w2 += (uint64_t)1 << (2 * low);
+                __syncthreads();
+                const uint32_t t = a > off ? (a - off + 1) >> 1 : 0u;
+#pragma unroll
+                for (int q = 0; q < kKllRun / kWave / 2; ++q) {
+                    const uint32_t m = (uint32_t)lane + (uint32_t)q * kWave;
+                    if (m < t) K.tmp[0][m] = keep[q];
+                }
+                if (lane == 0) {
+                    K.lens[low] = 0;
+                    K.cnt[low] = c + 1;
+                }
+                __syncthreads();
+                K.push(0, t, low + 1, A.levels);
+            }
+        }
+        // export: header, then the runs in level order
+        uint64_t wtot = 0, lw[4] = {0, 0, 0, 0};
+        uint32_t pos = 0;
+        if (exact0) {
+            wtot = c_whole[0] + c_whole[1];
+            lw[0] = wtot;
+            pos = (uint32_t)wtot;
+        } else {
+#pragma unroll 1
+            for (int h = 1; h <= A.levels && h < kKllLevels; ++h) {
+                const uint32_t l = uni32(K.lens[h]);
+                if (!l) continue;
+                if (pos + l > (uint32_t)A.budget) {  // only after an overflow
+                    K.overflow = 1;
+                    break;
+                }
+                const uint64_t* L = K.run((uint32_t)h);
+                for (uint32_t i = lane; i < l; i += kWave) row[kKllHdr + pos + i] = L[i];
+                pos += l;
+                wtot += (uint64_t)l << h;
+                lw[h >> 2] |= (uint64_t)l << (16 * (h & 3));
+            }
+        }
+        if (lane == 0) {
+            row[0] = n_pres;
+            row[1] = A.gaps ? 0ull : n_nan;
+            row[2] = n_pres ? okey_inv(gmin) : kQuietNaN;
+            row[3] = n_pres ? okey_inv(gmax) : kQuietNaN;
+            row[4] = lw[0];
+            row[5] = lw[1];
+            row[6] = lw[2];
+            row[7] = lw[3];
+            row[8] = K.overflow ? ~0ull : K.sum_w2;
+            row[9] = wtot;
+        }
+        __syncthreads();
+    }
+}
+
+struct KllQueryArgs {
+    int64_t S;
+    int32_t W;        // rows per series (time slices)
+    int32_t budget;
+    const uint64_t* rows;  // [S][W][kKllHdr + budget]
+    int32_t mode;
+    int64_t p_num, p_den;
+    double q;
+    double* out_v;
+    int64_t* out_n;
+    uint32_t* out_f;
+};
+
+// Smallest key K with (weighted count of keys <= K) * n > r * wtot (an item's key).
+__device__ uint64_t kll_select(const uint64_t* key, const uint8_t* lvl, uint32_t m, uint64_t r, uint64_t n,
+                               uint64_t wtot, int lane) {
+    uint64_t lo = 0, hi = kKllNanKey;
+#pragma unroll 1
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        uint64_t c = 0;
+        for (uint32_t i = lane; i < m; i += kWave) c += key[i] <= mid ? (uint64_t)1 << lvl[i] : 0ull;
+        c = lane_bcast64(wave_scan64(c, 0ull, OpAdd64{}), kWave - 1);
+        const bool ok = (unsigned __int128)c * n > (unsigned __int128)r * wtot;
+        lo = ok ? lo : mid + 1;
+        hi = ok ? mid : hi;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const uint32_t RW = (uint32_t)(kKllHdr + A.budget);
+    uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+    uint8_t* lvl = reinterpret_cast<uint8_t*>(key + (size_t)A.W * A.budget);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const uint64_t* rows = A.rows + (size_t)s * A.W * RW;
+        uint64_t n = 0, nan = 0, wtot = 0;
+        double mn = bitsd(kQuietNaN), mx = bitsd(kQuietNaN);
+        bool bad = false;
+        uint32_t m = 0;
+#pragma unroll 1
+        for (int w = 0; w < A.W; ++w) {
+            const uint64_t* row = rows + (size_t)w * RW;
+            n += row[0];
+            nan += row[1];
+            mn = fmin(mn, bitsd(row[2]));
+            mx = fmax(mx, bitsd(row[3]));
+            bad = bad || row[8] == ~0ull;
+            wtot += row[9];
+            uint32_t pos = 0;
+#pragma unroll 1
+            for (int h = 0; h < kKllLevels; ++h) {
+                const uint32_t l = (uint32_t)(row[4 + (h >> 2)] >> (16 * (h & 3))) & 0xFFFFu;
+                for (uint32_t i = lane; i < l; i += kWave) {
+                    key[m + i] = row[kKllHdr + pos + i];
+                    lvl[m + i] = (uint8_t)h;
+                }
+                pos += l;
+                m += l;
+            }
+        }
+        __syncthreads();
+        uint32_t flags = 0;
+        double result = bitsd(kQuietNaN);
+        if (bad) {
+            flags = KRR_FLAG_CAPACITY;
+        } else if (nan) {
+            flags = KRR_FLAG_NAN;
+        } else if (n == 0) {
+            flags = KRR_FLAG_EMPTY;
+        } else {
+            int64_t r0, r1;
+            double gamma = 0.0;
+            if (A.mode == KRR_PCT_SORTED_LOWER) {
+                r0 = r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+            } else {
+                const double vidx = __dmul_rn((double)(n - 1), A.q);
+                if (vidx >= (double)(n - 1)) {
+                    r0 = r1 = (int64_t)n - 1;
+                    gamma = __dsub_rn(vidx, -1.0);
+                } else {
+                    const double fl = floor(vidx);
+                    r0 = (int64_t)fl;
+                    r1 = r0 + 1;
+                    gamma = __dsub_rn(vidx, fl);
+                }
+            }
+            double v[2];
+#pragma unroll 1
+            for (int qi = 0; qi < 2; ++qi) {
+                const uint64_t r = (uint64_t)(qi ? r1 : r0);
+                if (qi && r1 == r0) {
+                    v[1] = v[0];
+                    continue;
+                }
+                v[qi] = r == 0 ? mn : (r == n - 1 ? mx : bitsd(okey_inv(kll_select(key, lvl, m, r, n, wtot, lane))));
+            }
+            result = A.mode == KRR_PCT_SORTED_LOWER ? v[0] : np_lerp(v[0], v[1], gamma);
+        }
+        if (lane == 0) {
+            A.out_v[s] = result;
+            A.out_n[s] = (int64_t)n;
+            A.out_f[s] = flags;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace krr
