@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--sketch-bits", type=int, default=5, help="config 5: log-linear bins per octave = 2^bits")
     ap.add_argument("--sketch-only", action="store_true",
                     help="config 5: stop at the sketch answer (approximate) instead of the exact refinement")
+    ap.add_argument("--sketch-kind", choices=("kll", "loglinear"), default="kll",
+                    help="config 5 --sketch-only: kll = KLL-style compactor sketch (rank error bounded whatever the "
+                         "data, reported as sketch_error.rank_error_bound); loglinear = the log-linear histogram "
+                         "(value error <= 2^-bits, rank error measured only)")
+    ap.add_argument("--kll-budget", type=int, default=512, help="config 5 kll: weighted keys kept per series slice")
     ap.add_argument("--c5-refine", action="store_true",
                     help="config 5 at N=1: run the time-sharded exact path (--c5-method) instead of the direct "
                          "single-window select (N>1 always uses it)")
@@ -1031,7 +1036,9 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     params = percentile_params(Decimal(args.percentile), params_mode(args))
     exact = not args.sketch_only
     direct = exact and world == 1 and not args.c5_refine
-    method = "direct" if direct else (args.c5_method if exact else "sketch-only")
+    method = "direct" if direct else (args.c5_method if exact else ("kll" if args.sketch_kind == "kll" else
+                                                                     "sketch-only"))
+    kcfg = sketch.KllConfig(budget=args.kll_budget)
     # the direct pass and the window export run per chunk of series in buffers of their own
     # (as configs 2-4, fleet_chunks); the sketch paths keep one buffer per rank
     chunked = direct or method == "window"
@@ -1090,7 +1097,11 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                                torch.zeros_like(dres["count"]), torch.zeros_like(dres["count"])], dim=1)
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
             return
-        if method == "window":
+        if method == "kll":
+            res = sketch.kll_time_sharded(ctx, ser_parts, kcfg, params, stream=stream,
+                                          events=None if ev is None else ev[0:2])
+            state["rows"], state["rows_per_series"] = res["rows"], res["rows_per_series"]
+        elif method == "window":
             res = sketch.window_exact_time_sharded(ctx, ser_parts, params, ext_slots=T - Lr, stream=stream,
                                                    events=None if ev is None else ev[0:2])
             state["misses"] += res["misses"]
@@ -1147,6 +1158,11 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     if method == "direct":
         kname = "k_select"
         kbytes = 8 * N + 8 * (S + 1) + 20 * S
+    elif method == "kll":
+        kname = "k_kll_build"
+        # every slot once + offsets + the exported rows
+        kbytes = 8 * N + 8 * (S + 1) + 8 * kcfg.row_words * S
+        kernels_ms["merge_exchange_query_ms"] = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     elif method == "window":
         kname = "k_window_export"
         hdr = state["hdr"]
@@ -1176,11 +1192,15 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                        f"refinement (collect + select in the located bins; two HBM passes)"),
             "sketch-only": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks "
                             f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave, "
-                            f"approximate")}[method]
+                            f"approximate"),
+            "kll": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
+                    f"samples/series/rank), KLL-style compactor sketch ({kcfg.budget} keys per slice, "
+                    f"one build launch per rank), approximate")}[method]
     par = {"direct": "single GPU, whole series",
            "window": f"time-shard{world} (all-to-all of per-slice windows to the series' owners, RCCL)",
            "sketch": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
-           "sketch-only": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)"}[method]
+           "sketch-only": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
+           "kll": f"time-shard{world} (all-to-all of {kcfg.row_words}-word rows to the series' owners, RCCL)"}[method]
     result = {
         "metric": METRIC,
         "value": S / step_s,
@@ -1294,6 +1314,22 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                                            + ", first sample series")
             if method == "sketch":
                 result["collected_samples_per_rank"] = int(state.get("collected", 0))
+        elif method == "kll":
+            rel = np.abs(got - exact_v) / np.abs(exact_v)
+            rows_m = state["rows"][: m * state["rows_per_series"]]
+            bound = sketch.kll_rank_bound(rows_m, state["rows_per_series"], delta=0.01)
+            result["sketch_error"] = {
+                "kind": "kll", "sample_series": m, "rank_error_max": float(err.max()),
+                "rank_error_mean": float(err.mean()), "rank_error_bound_max": float(np.nanmax(bound)),
+                "rank_error_bound_mean": float(np.nanmean(bound)), "bound_confidence": 0.99,
+                "within_bound": bool(np.all(err <= bound)),
+                "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
+                "budget_keys_per_slice": kcfg.budget,
+                "guarantee": ("rank: |rank(answer) - (n-1)p/100| / n <= (2 sqrt(2 ln(6/delta) sum w^2) + w_max) / n "
+                              "with probability >= 1 - delta, from each series' compaction schedule only "
+                              "(krr_amd.core.sketch.kll_rank_bound); value: none"),
+                "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
+                              "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
         else:
             rel = np.abs(got - exact_v) / np.abs(exact_v)
             result["sketch_error"] = {

@@ -98,10 +98,29 @@ __device__ __forceinline__ void kll_cx(uint64_t& a, uint64_t& b, bool asc) {
     b = asc ? hi : lo;
 }
 
-__device__ __forceinline__ uint64_t kll_shfl_xor(uint64_t x, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, m, kWave);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), m, kWave);
-    return ((uint64_t)hi << 32) | lo;
+// x of lane ^ M (M in {1, 2, 4, 8, 16}: never across the 32-lane halves): DPP quad_perm for
+// 1 and 2, DPP row_ror:8 for 8 (a rotation by 8 in a 16-lane row is lane ^ 8), ds_swizzle
+// (bit mode, xor mask) for 4 and 16 — no address registers, no bpermute.
+template <int M>
+__device__ __forceinline__ uint32_t kll_xor32(uint32_t v) {
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false);
+    else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));
+}
+template <int M>
+__device__ __forceinline__ uint64_t kll_xor64(uint64_t x) {
+    return ((uint64_t)kll_xor32<M>((uint32_t)(x >> 32)) << 32) | kll_xor32<M>((uint32_t)x);
+}
+
+template <int M>
+__device__ __forceinline__ void kll_cross(uint64_t (&x)[16], bool take_min) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint64_t o = kll_xor64<M>(x[i]);
+        const uint64_t lo = x[i] < o ? x[i] : o, hi = x[i] < o ? o : x[i];
+        x[i] = take_min ? lo : hi;
+    }
 }
 
 // In-lane substeps j = J, J/2, .., 1 of bitonic stage k on the lane's 16 keys
@@ -130,34 +149,62 @@ __device__ __forceinline__ void kll_sort_blocks(uint64_t (&x)[16], int lane) {
 #pragma unroll 1
         for (uint32_t j = k >> 1; j >= 16; j >>= 1) {
             const int m = (int)(j >> 4);
-            const bool lower = (lane & m) == 0;
-            const bool take_min = lower == asc;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint64_t o = kll_shfl_xor(x[i], m);
-                const uint64_t lo = x[i] < o ? x[i] : o, hi = x[i] < o ? o : x[i];
-                x[i] = take_min ? lo : hi;
+            const bool take_min = ((lane & m) == 0) == asc;  // the lower lane of the pair keeps the min if ascending
+            switch (m) {  // wave-uniform
+                case 1: kll_cross<1>(x, take_min); break;
+                case 2: kll_cross<2>(x, take_min); break;
+                case 4: kll_cross<4>(x, take_min); break;
+                case 8: kll_cross<8>(x, take_min); break;
+                default: kll_cross<16>(x, take_min); break;
             }
         }
         kll_inlane<8>(x, k, lane);
     }
 }
 
-// #keys < v (STRICT) or <= v in the sorted run r[0, n).
+// Merge-path step of a merge-compaction: every key X[i] (i = lane + 64 q, i < nx <= 256)
+// lands at merged position p = i + #(Y < X[i]) (STRICT: X's keys go before Y's equal keys)
+// or i + #(Y <= X[i]); positions off, off + 2, ... are kept, at O[(p - off) / 2].  The four
+// binary searches of a lane advance together (their LDS reads overlap), 9 halvings each
+// (ny <= 256).
 template <bool STRICT>
-__device__ __forceinline__ uint32_t kll_rank_in(const uint64_t* r, uint32_t n, uint64_t v) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const bool go = STRICT ? r[mid] < v : r[mid] <= v;
-        lo = go ? mid + 1 : lo;
-        hi = go ? hi : mid;
+__device__ __forceinline__ void kll_merge_half(const uint64_t* X, uint32_t nx, const uint64_t* Y, uint32_t ny,
+                                               uint32_t off, uint64_t* O, int lane) {
+    constexpr int Q = kKllRun / kWave;
+    uint64_t v[Q];
+    uint32_t lo[Q], hi[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t i = (uint32_t)lane + (uint32_t)q * kWave;
+        v[q] = i < nx ? X[i] : 0ull;
+        lo[q] = 0;
+        hi[q] = i < nx ? ny : 0u;
     }
-    return lo;
+    if (ny) {
+        const uint32_t last = ny - 1;
+#pragma unroll
+        for (int step = 0; step < 9; ++step) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const uint32_t mid = (lo[q] + hi[q]) >> 1;
+                const uint64_t y = Y[mid < last ? mid : last];
+                const bool active = lo[q] < hi[q];
+                const bool go = STRICT ? y < v[q] : y <= v[q];
+                lo[q] = (active && go) ? mid + 1 : lo[q];
+                hi[q] = (active && !go) ? mid : hi[q];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t i = (uint32_t)lane + (uint32_t)q * kWave;
+        const uint32_t p = i + lo[q];
+        if (i < nx && p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v[q];
+    }
 }
 
 struct KllState {
-    uint64_t* tmp[2];   // two LDS runs of kKllRun keys
+    uint64_t* tmp;      // two LDS runs of kKllRun keys (tb(0), tb(1))
     uint64_t* lv;       // LDS runs, level h at lv + (h - 1) * kKllRun
     uint32_t* lens;     // LDS [kKllLevels]
     uint32_t* cnt;      // LDS [kKllLevels] compactions done per level
@@ -168,6 +215,7 @@ struct KllState {
     int lane;
 
     __device__ __forceinline__ uint64_t* run(uint32_t h) const { return lv + (size_t)(h - 1) * kKllRun; }
+    __device__ __forceinline__ uint64_t* tb(uint32_t sel) const { return tmp + (size_t)sel * kKllRun; }
 
     // Push the run tmp[t_sel][0, t) at level h (>= 1): store it, or merge-compact and carry.
     __device__ void push(uint32_t t_sel, uint32_t t, uint32_t h, int levels) {
@@ -177,7 +225,7 @@ struct KllState {
                 return;
             }
             const uint32_t a = uni32(lens[h]);
-            const uint64_t* T = tmp[t_sel];
+            const uint64_t* T = tb(t_sel);
             if (a == 0) {
                 uint64_t* L = run(h);
                 for (uint32_t i = lane; i < t; i += kWave) L[i] = T[i];
@@ -189,17 +237,9 @@ struct KllState {
             const uint32_t c = uni32(cnt[h]);
             const uint32_t off = kll_coin(seed, series, slice, h, c);
             const uint64_t* A = run(h);
-            uint64_t* O = tmp[t_sel ^ 1];
-            for (uint32_t i = lane; i < a; i += kWave) {  // A's keys before T's equal keys
-                const uint64_t v = A[i];
-                const uint32_t p = i + kll_rank_in<true>(T, t, v);
-                if (p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v;
-            }
-            for (uint32_t j = lane; j < t; j += kWave) {
-                const uint64_t v = T[j];
-                const uint32_t p = j + kll_rank_in<false>(A, a, v);
-                if (p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v;
-            }
+            uint64_t* O = tb(t_sel ^ 1);
+            kll_merge_half<true>(A, a, T, t, off, O, lane);  // A's keys before T's equal keys
+            kll_merge_half<false>(T, t, A, a, off, O, lane);
             sum_w2 += (uint64_t)1 << (2 * h);
             __syncthreads();
             if (lane == 0) {
@@ -218,9 +258,8 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     KllState K;
-    K.tmp[0] = reinterpret_cast<uint64_t*>(smem);
-    K.tmp[1] = K.tmp[0] + kKllRun;
-    K.lv = K.tmp[1] + kKllRun;
+    K.tmp = reinterpret_cast<uint64_t*>(smem);
+    K.lv = K.tmp + 2 * kKllRun;
     K.lens = reinterpret_cast<uint32_t*>(K.lv + (size_t)A.levels * kKllRun);
     K.cnt = K.lens + kKllLevels;
     K.seed = A.seed;
@@ -241,25 +280,18 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
         K.overflow = 0;
         const bool whole = kll_nchunks(beg, end) <= 1;  // one chunk: kept exactly if it fits the budget
         uint64_t* row = A.rows + (size_t)s * RW;
-        uint32_t nan_l = 0, pres_l = 0, c_whole[2] = {0, 0};
-        uint64_t kmin = kKllNanKey, kmax = 0;
-        bool any = false;
-        uint32_t blocks = 0;
 
-        struct Proc {
-            KllState& K;
-            const KllBuildArgs& A;
+        struct Proc {  // by value: nothing here is address-taken (no scratch)
+            KllState K;
+            int budget, levels;
             uint64_t* row;
             int lane, blk;
             uint32_t bpos;
             bool whole;
-            uint32_t& nan_l;
-            uint32_t& pres_l;
-            uint32_t (&c_whole)[2];
-            uint64_t& kmin;
-            uint64_t& kmax;
-            bool& any;
-            uint32_t& blocks;
+            uint32_t nan_l, pres_l;
+            uint32_t c_whole[2];
+            uint64_t kmin, kmax;
+            bool any;
             __device__ void chunk(const double2 (&c)[kUnroll]) {
                 uint64_t x[16];
                 uint32_t valid = 0;
@@ -284,7 +316,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                     c_whole[0] = c0;
                     c_whole[1] = c1;
                     // exported now if it fits: level 0, block 0's keys then block 1's
-                    if (c0 + c1 <= (uint32_t)A.budget) {
+                    if (c0 + c1 <= (uint32_t)budget) {
                         const uint32_t base = blk ? c0 : 0u, cb = blk ? c1 : c0;
 #pragma unroll
                         for (int i = 0; i < 16; ++i)
@@ -302,7 +334,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             const uint32_t p = bpos + (uint32_t)i;
-                            if (p < cb && p >= off && ((p - off) & 1u) == 0) K.tmp[0][(p - off) >> 1] = x[i];
+                            if (p < cb && p >= off && ((p - off) & 1u) == 0) K.tb(0)[(p - off) >> 1] = x[i];
                         }
                     }
                     K.sum_w2 += 1;
@@ -310,13 +342,16 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                     if (lane == 0) K.cnt[0] = c0n + 1;
                     __syncthreads();
                     const uint32_t t = cb > off ? (cb - off + 1) >> 1 : 0u;
-                    K.push(0, t, 1, A.levels);
-                    ++blocks;
+                    K.push(0, t, 1, levels);
                 }
             }
-        } P{K, A, row, lane, blk, bpos, whole, nan_l, pres_l, c_whole, kmin, kmax, any, blocks};
+        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, kKllNanKey, 0ull, false};
 
         const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
+        K = P.K;
+        const uint32_t nan_l = P.nan_l, pres_l = P.pres_l, c_whole[2] = {P.c_whole[0], P.c_whole[1]};
+        const uint64_t kmin = P.kmin, kmax = P.kmax;
+        const bool any = P.any;
         const uint64_t n_nan = (uint64_t)wave_sum_u32(nan_l) - pad;
         const uint64_t n_pres = wave_sum_u32(pres_l);
         const uint64_t gmin = wave_min_u64(kmin), gmax = wave_max_u64(any ? kmax : 0ull);
@@ -349,7 +384,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
 #pragma unroll
                 for (int q = 0; q < kKllRun / kWave / 2; ++q) {
                     const uint32_t m = (uint32_t)lane + (uint32_t)q * kWave;
-                    if (m < t) K.tmp[0][m] = keep[q];
+                    if (m < t) K.tb(0)[m] = keep[q];
                 }
                 if (lane == 0) {
                     K.lens[low] = 0;
@@ -360,11 +395,11 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             }
         }
         // export: header, then the runs in level order
-        uint64_t wtot = 0, lw[4] = {0, 0, 0, 0};
+        uint64_t wtot = 0, lw0 = 0, lw1 = 0, lw2 = 0, lw3 = 0;  // run lengths, u16 x 4 per word
         uint32_t pos = 0;
         if (exact0) {
             wtot = c_whole[0] + c_whole[1];
-            lw[0] = wtot;
+            lw0 = wtot;
             pos = (uint32_t)wtot;
         } else {
 #pragma unroll 1
@@ -379,7 +414,11 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                 for (uint32_t i = lane; i < l; i += kWave) row[kKllHdr + pos + i] = L[i];
                 pos += l;
                 wtot += (uint64_t)l << h;
-                lw[h >> 2] |= (uint64_t)l << (16 * (h & 3));
+                const uint64_t f = (uint64_t)l << (16 * (h & 3));
+                lw0 |= (h >> 2) == 0 ? f : 0ull;
+                lw1 |= (h >> 2) == 1 ? f : 0ull;
+                lw2 |= (h >> 2) == 2 ? f : 0ull;
+                lw3 |= (h >> 2) == 3 ? f : 0ull;
             }
         }
         if (lane == 0) {
@@ -387,10 +426,10 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             row[1] = A.gaps ? 0ull : n_nan;
             row[2] = n_pres ? okey_inv(gmin) : kQuietNaN;
             row[3] = n_pres ? okey_inv(gmax) : kQuietNaN;
-            row[4] = lw[0];
-            row[5] = lw[1];
-            row[6] = lw[2];
-            row[7] = lw[3];
+            row[4] = lw0;
+            row[5] = lw1;
+            row[6] = lw2;
+            row[7] = lw3;
             row[8] = K.overflow ? ~0ull : K.sum_w2;
             row[9] = wtot;
         }
