@@ -117,9 +117,21 @@ def test_bench_config5_sketch_only_two_ranks():
     the log-linear sketch's bin mass (2^5 bins per octave; the same bound the N = 1 sketch
     test holds) and is reported beside the value."""
     r = _bench(["--gpus", "2", "--config", "5", "--containers", "600", "--steps", "2", "--warmup", "1",
-                "--sketch-only", "--error-sample", "600"], timeout=300)
+                "--sketch-only", "--sketch-kind", "loglinear", "--error-sample", "600"], timeout=300)
     e = r["sketch_error"]
     assert e["sample_series"] == 600 and 0.0 <= e["rank_error_max"] < 1e-3 and e["value_rel_error_max"] < 0.01, e
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_config5_kll_time_sharded_ranks(world):
+    """KLL sketch-only over 2 and 3 time-sharded ranks: every rank builds its slices' rows,
+    one all-to-all hands each series' rows to its owner, the answers gathered to rank 0
+    carry a rank error within the rows' data-independent bound."""
+    r = _bench(["--gpus", str(world), "--config", "5", "--containers", "600", "--steps", "2", "--warmup", "1",
+                "--sketch-only", "--sketch-kind", "kll", "--error-sample", "300"], timeout=300)
+    e = r["sketch_error"]
+    assert r["config"]["method"] == "kll" and e["kind"] == "kll" and e["sample_series"] == 300, e
+    assert e["within_bound"] is True and e["rank_error_max"] <= e["rank_error_bound_max"] < 0.02, e
 
 
 def test_synth_global_index_shards_equal_whole_fleet():

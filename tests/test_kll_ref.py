@@ -99,3 +99,60 @@ def test_rank_bound_helper_matches_restatement():
     assert np.isnan(got[0])
     for s in range(1, 4):
         assert got[s] == pytest.approx(M.rank_bound(rows[s]), rel=1e-12)
+
+
+def _exchange_worker(rank, world, port, q, n_series, T, budget):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from krr_amd.core import sketch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(0)
+        x = rng.gamma(2.0, 0.05, (n_series, T))
+        t0, t1 = T * rank // world, T * (rank + 1) // world
+        rows = np.stack([M.build_row(x[s], t0, t1, budget=budget, seed=9, series=s, slc=rank)
+                         for s in range(n_series)])
+        merged, W = sketch.kll_exchange(torch.from_numpy(rows.view(np.int64)))
+        lo, hi = sketch.owner_blocks(n_series, world)[rank]
+        q.put((rank, lo, hi, W, merged.numpy().view(np.uint64)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_hands_each_owner_its_series_rows(world):
+    """gloo: kll_exchange gives each rank the W slice rows of its owner block, series-major
+    in slice (= time) order: the rows a single process builds for the same slices."""
+    import multiprocessing as mp
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    n_series, T, budget = 7, 5000, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, n_series, T, budget))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x = np.random.default_rng(0).gamma(2.0, 0.05, (n_series, T))
+    prm = percentile_params(Decimal("99"), "linear")
+    for rank, lo, hi, W, merged in got:
+        assert W == world and merged.shape[0] == (hi - lo) * world
+        for s in range(lo, hi):
+            want = np.stack([M.build_row(x[s], T * w // world, T * (w + 1) // world, budget=budget, seed=9, series=s,
+                                         slc=w) for w in range(world)])
+            have = merged[(s - lo) * world:(s - lo + 1) * world]
+            assert np.array_equal(have, want)
+            v, n, f = M.query(have, prm.mode, prm.p_num, prm.p_den, prm.q)
+            assert n == T and f == 0 and np.isfinite(v)
