@@ -3841,8 +3841,8 @@ int64_t krr_kll_row_words(const krr_kll_params* kp) {
     return (int64_t)kKllHdr + kp->budget;
 }
 
-static size_t kll_build_lds(int levels) {
-    return (size_t)(2 + levels) * kKllRun * 8 + 2 * kKllLevels * 4;
+static size_t kll_build_lds(int levels) {  // two work runs + levels kKllFirst..levels + lens/counters
+    return (size_t)(2 + levels - (int)kKllFirst + 1) * kKllRun * 8 + 2 * kKllLevels * 4;
 }
 
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,

@@ -5,16 +5,19 @@
 // reported.  The log-linear histogram (k_sketch_build) bounds the VALUE error only; this
 // one bounds the RANK error whatever the data (low dispersion, heavy quantisation, ties).
 //
-// One wave per series slice streams it once (stream_segment, 1,024 slots per chunk):
-//   * each chunk is split in two level-0 blocks of 512 slots (block b = lanes 32b..32b+31,
-//     16 slots per lane), sorted by an in-register bitonic network (in-lane stages on the
-//     lane's 16 keys, cross-lane stages by shuffles); NaN slots sort last and are dropped;
-//   * a block is COMPACTED: the keys at sorted positions off, off+2, ... (off a coin from a
-//     counter hash of (seed, series, slice, level, count)) become a run of <= 256 keys of
-//     weight 2, pushed to level 1;
-//   * level h >= 1 holds at most one sorted run (LDS).  Pushing a run onto a full level
-//     merges the two runs (merge-path positions by binary search) and compacts the merge
-//     (same coin rule): <= 256 keys of weight 2^(h+1) go up — a binary counter of runs;
+// One wave per series slice streams it once (stream_segment, 1,024 slots per chunk).  A
+// COMPACTION keeps the keys at sorted positions off, off+2, ... (off a coin from a counter
+// hash of (seed, series, slice, level, count)) and doubles their weight:
+//   * level 0, per lane: the lane's 16 slots of a chunk are sorted in registers (NaN slots
+//     sort last and are dropped) and compacted to <= 8 keys of weight 2;
+//   * level 1, per lane: the runs of two consecutive chunks are merged in registers and
+//     compacted to <= 8 keys of weight 4;
+//   * level 2, per wave (every other chunk): the 64 lanes' weight-4 keys are sorted across
+//     the wave (bitonic network: DPP / ds_swizzle exchanges) and compacted to a run of
+//     <= 256 keys of weight 8, pushed to level 3;
+//   * level h >= 3 holds at most one sorted run (LDS).  Pushing a run onto a full level
+//     merges the two runs (merge-path positions by binary search) and compacts the merge:
+//     <= 256 keys of weight 2^(h+1) go up — a binary counter of runs;
 //   * at the end, while more than `budget` keys remain, the lowest run is compacted alone
 //     and pushed up; the runs are exported as one fixed-size row.
 // A slice of <= budget present samples that fits one chunk is exported whole (weight 1):
@@ -38,6 +41,8 @@ constexpr int kKllRun = 256;     // keys per run at levels >= 1
 constexpr int kKllLevels = 16;   // run slots: level 0 (whole short slices) .. 15
 constexpr int kKllHdr = 10;      // header words of an exported row
 constexpr uint64_t kKllNanKey = ~0ull;  // sorts after every okey() of a non-NaN value
+constexpr uint32_t kKllFirst = 3;  // first LDS run level (levels 0-2 are the lane and wave stages)
+constexpr uint32_t kKllLane0 = 32, kKllLane1 = 96;  // coin "levels" of lane l's compactions: 32 + l, 96 + l
 
 // Row layout (uint64 words): [0] present samples  [1] NaN samples (compact layout; 0 with
 // gaps)  [2] min  [3] max (f64 bits, NaN when empty)  [4..7] run lengths, u16 x 16, level
@@ -69,13 +74,13 @@ __host__ __device__ inline int64_t kll_nchunks(int64_t beg, int64_t end) {
     return nfull + ((rem > 0 || a0 > beg || a1 < end) ? 1 : 0);
 }
 
-// Highest run level a segment of `len` slots can reach (runs pushed by the blocks form a
-// binary counter; the final compression may carry one level further).
+// Highest run level a segment of `len` slots can reach: level 3 receives one run per two
+// chunks, the runs form a binary counter, the final compression may carry one level more.
 __host__ __device__ inline int kll_levels(int64_t len) {
-    const int64_t blocks = 2 * kll_nchunks(0, len) + 2;
+    const int64_t pushes = (kll_nchunks(0, len) + 2) / 2 + 1;
     int lg = 0;
-    while ((int64_t(1) << (lg + 1)) <= blocks) ++lg;
-    return lg + 2;
+    while ((int64_t(1) << (lg + 1)) <= pushes) ++lg;
+    return (int)kKllFirst + lg + 1;
 }
 
 struct KllBuildArgs {
@@ -84,7 +89,7 @@ struct KllBuildArgs {
     int64_t S;
     int32_t gaps;
     int32_t budget;
-    int32_t levels;   // LDS run slots for levels 1..levels
+    int32_t levels;   // highest run level (LDS slots for levels kKllFirst..levels)
     uint32_t slice;
     uint64_t seed;
     int64_t seg_base;
@@ -110,13 +115,18 @@ __device__ __forceinline__ uint32_t kll_xor32(uint32_t v) {
 }
 template <int M>
 __device__ __forceinline__ uint64_t kll_xor64(uint64_t x) {
+    if constexpr (M == 32) {  // across the 32-lane halves
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, 32, kWave);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), 32, kWave);
+        return ((uint64_t)hi << 32) | lo;
+    }
     return ((uint64_t)kll_xor32<M>((uint32_t)(x >> 32)) << 32) | kll_xor32<M>((uint32_t)x);
 }
 
-template <int M>
-__device__ __forceinline__ void kll_cross(uint64_t (&x)[16], bool take_min) {
+template <int M, int N>
+__device__ __forceinline__ void kll_cross(uint64_t (&x)[N], bool take_min) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < N; ++i) {
         const uint64_t o = kll_xor64<M>(x[i]);
         const uint64_t lo = x[i] < o ? x[i] : o, hi = x[i] < o ? o : x[i];
         x[i] = take_min ? lo : hi;
@@ -151,14 +161,79 @@ __device__ __forceinline__ void kll_sort_blocks(uint64_t (&x)[16], int lane) {
             const int m = (int)(j >> 4);
             const bool take_min = ((lane & m) == 0) == asc;  // the lower lane of the pair keeps the min if ascending
             switch (m) {  // wave-uniform
-                case 1: kll_cross<1>(x, take_min); break;
-                case 2: kll_cross<2>(x, take_min); break;
-                case 4: kll_cross<4>(x, take_min); break;
-                case 8: kll_cross<8>(x, take_min); break;
-                default: kll_cross<16>(x, take_min); break;
+                case 1: kll_cross<1, 16>(x, take_min); break;
+                case 2: kll_cross<2, 16>(x, take_min); break;
+                case 4: kll_cross<4, 16>(x, take_min); break;
+                case 8: kll_cross<8, 16>(x, take_min); break;
+                default: kll_cross<16, 16>(x, take_min); break;
             }
         }
         kll_inlane<8>(x, k, lane);
+    }
+}
+
+// The lane's 16 keys ascending (a full bitonic sort in registers).
+__device__ __forceinline__ void kll_sort16(uint64_t (&x)[16]) {
+#pragma unroll
+    for (int k = 2; k <= 16; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (!(i & j)) kll_cx(x[i], x[i + j], k == 16 || (i & k) == 0);
+        }
+    }
+}
+
+// z[0, 8) and z[8, 16) ascending -> z ascending (reverse the second half: bitonic; clean).
+__device__ __forceinline__ void kll_merge16(uint64_t (&z)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t t = z[8 + i];
+        z[8 + i] = z[15 - i];
+        z[15 - i] = t;
+    }
+#pragma unroll
+    for (int j = 8; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (!(i & j)) kll_cx(z[i], z[i + j], true);
+    }
+}
+
+// 512 keys ascending across the wave: lane l holds positions 8l .. 8l+7, each lane's 8
+// already ascending (odd lanes' runs are reversed first, so stage 16 starts bitonic).
+__device__ __forceinline__ void kll_sort512(uint64_t (&y)[8], int lane) {
+    if (lane & 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t t = y[i];
+            y[i] = y[7 - i];
+            y[7 - i] = t;
+        }
+    }
+#pragma unroll 1
+    for (uint32_t k = 16; k <= 512; k <<= 1) {
+        const bool asc = k >= 512 || (((uint32_t)lane * 8u) & k) == 0;
+#pragma unroll 1
+        for (uint32_t j = k >> 1; j >= 8; j >>= 1) {
+            const int m = (int)(j >> 3);
+            const bool take_min = ((lane & m) == 0) == asc;
+            switch (m) {  // wave-uniform
+                case 1: kll_cross<1, 8>(y, take_min); break;
+                case 2: kll_cross<2, 8>(y, take_min); break;
+                case 4: kll_cross<4, 8>(y, take_min); break;
+                case 8: kll_cross<8, 8>(y, take_min); break;
+                case 16: kll_cross<16, 8>(y, take_min); break;
+                default: kll_cross<32, 8>(y, take_min); break;
+            }
+        }
+#pragma unroll
+        for (int j = 4; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (!(i & j)) kll_cx(y[i], y[i + j], asc);
+        }
     }
 }
 
@@ -214,10 +289,30 @@ struct KllState {
     uint32_t overflow;  // a run above the provisioned levels (never expected)
     int lane;
 
-    __device__ __forceinline__ uint64_t* run(uint32_t h) const { return lv + (size_t)(h - 1) * kKllRun; }
+    __device__ __forceinline__ uint64_t* run(uint32_t h) const { return lv + (size_t)(h - kKllFirst) * kKllRun; }
     __device__ __forceinline__ uint64_t* tb(uint32_t sel) const { return tmp + (size_t)sel * kKllRun; }
 
-    // Push the run tmp[t_sel][0, t) at level h (>= 1): store it, or merge-compact and carry.
+    // Level 2: the lanes' weight-4 keys (y ascending per lane, NaN keys past cy) sorted
+    // across the wave, compacted to <= 256 keys of weight 8, pushed to level 3.
+    __device__ void wave_stage(uint64_t (&y)[8], uint32_t cy, int levels) {
+        const uint32_t C = wave_sum_u32(cy);
+        if (C == 0) return;
+        kll_sort512(y, lane);
+        const uint32_t c = uni32(cnt[2]);
+        const uint32_t off = kll_coin(seed, series, slice, 2, c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t p = (uint32_t)lane * 8u + (uint32_t)i;
+            if (p < C && p >= off && ((p - off) & 1u) == 0) tb(0)[(p - off) >> 1] = y[i];
+        }
+        sum_w2 += 16;
+        __syncthreads();
+        if (lane == 0) cnt[2] = c + 1;
+        __syncthreads();
+        push(0, C > off ? (C - off + 1) >> 1 : 0u, kKllFirst, levels);
+    }
+
+    // Push the run tmp[t_sel][0, t) at level h (>= kKllFirst): store it, or merge-compact and carry.
     __device__ void push(uint32_t t_sel, uint32_t t, uint32_t h, int levels) {
         while (t) {  // an empty run changes nothing
             if ((int)h > levels) {
@@ -260,7 +355,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
     KllState K;
     K.tmp = reinterpret_cast<uint64_t*>(smem);
     K.lv = K.tmp + 2 * kKllRun;
-    K.lens = reinterpret_cast<uint32_t*>(K.lv + (size_t)A.levels * kKllRun);
+    K.lens = reinterpret_cast<uint32_t*>(K.lv + (size_t)(A.levels - (int)kKllFirst + 1) * kKllRun);
     K.cnt = K.lens + kKllLevels;
     K.seed = A.seed;
     K.slice = A.slice;
@@ -292,6 +387,10 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             uint32_t c_whole[2];
             uint64_t kmin, kmax;
             bool any;
+            bool have;           // a level-1 run is pending in pend (wave-uniform)
+            uint32_t cpend;      // its present keys
+            uint32_t ci;         // chunks seen
+            uint64_t pend[8];
             __device__ void chunk(const double2 (&c)[kUnroll]) {
                 uint64_t x[16];
                 uint32_t valid = 0;
@@ -308,15 +407,14 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                 }
                 nan_l += 16u - valid;
                 pres_l += valid;
-                // present keys per block (lanes 0-31 / 32-63)
-                const uint32_t incl = wave_scan32(valid, 0u, OpAdd32{});
-                const uint32_t c0 = lane_bcast32(incl, 31), c1 = lane_bcast32(incl, kWave - 1) - c0;
-                kll_sort_blocks(x, lane);
-                if (whole) {  // held in registers until the end (the only chunk)
+                if (whole) {  // the only chunk: kept whole if it fits the budget
+                    // present keys per block (lanes 0-31 / 32-63)
+                    const uint32_t incl = wave_scan32(valid, 0u, OpAdd32{});
+                    const uint32_t c0 = lane_bcast32(incl, 31), c1 = lane_bcast32(incl, kWave - 1) - c0;
                     c_whole[0] = c0;
                     c_whole[1] = c1;
-                    // exported now if it fits: level 0, block 0's keys then block 1's
-                    if (c0 + c1 <= (uint32_t)budget) {
+                    if (c0 + c1 <= (uint32_t)budget) {  // level 0, block 0's keys then block 1's, sorted
+                        kll_sort_blocks(x, lane);
                         const uint32_t base = blk ? c0 : 0u, cb = blk ? c1 : c0;
 #pragma unroll
                         for (int i = 0; i < 16; ++i)
@@ -324,30 +422,50 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                         return;
                     }
                 }
-#pragma unroll 1
-                for (int b = 0; b < 2; ++b) {
-                    const uint32_t cb = b ? c1 : c0;
-                    if (cb == 0) continue;  // an all-NaN block: nothing to compact
-                    const uint32_t c0n = uni32(K.cnt[0]);
-                    const uint32_t off = kll_coin(K.seed, K.series, K.slice, 0, c0n);
-                    if (blk == b) {
+                // level 0 (per lane): sort the lane's 16 slots, keep every other from a coin
+                kll_sort16(x);
+                const uint32_t off = kll_coin(K.seed, K.series, K.slice, kKllLane0 + lane, ci);
+                uint64_t y[8];
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const uint32_t p = bpos + (uint32_t)i;
-                            if (p < cb && p >= off && ((p - off) & 1u) == 0) K.tb(0)[(p - off) >> 1] = x[i];
-                        }
+                for (int m = 0; m < 8; ++m) y[m] = off ? x[2 * m + 1] : x[2 * m];  // NaN keys stay past cy
+                const uint32_t cy = valid > off ? (valid - off + 1) >> 1 : 0u;
+                K.sum_w2 += popc64(ballot(valid > 0));
+                if (!have) {
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) pend[m] = y[m];
+                    cpend = cy;
+                    have = true;
+                } else {  // level 1 (per lane): merge with the pending run, compact
+                    uint64_t z[16];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) {
+                        z[m] = pend[m];
+                        z[8 + m] = y[m];
                     }
-                    K.sum_w2 += 1;
-                    __syncthreads();
-                    if (lane == 0) K.cnt[0] = c0n + 1;
-                    __syncthreads();
-                    const uint32_t t = cb > off ? (cb - off + 1) >> 1 : 0u;
-                    K.push(0, t, 1, levels);
+                    kll_merge16(z);
+                    const uint32_t cz = cpend + cy;
+                    const uint32_t off1 = kll_coin(K.seed, K.series, K.slice, kKllLane1 + lane, ci >> 1);
+                    uint64_t y2[8];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) y2[m] = off1 ? z[2 * m + 1] : z[2 * m];
+                    K.sum_w2 += 4ull * popc64(ballot(cz > 0));
+                    have = false;
+                    K.wave_stage(y2, cz > off1 ? (cz - off1 + 1) >> 1 : 0u, levels);
                 }
+                ++ci;
             }
-        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, kKllNanKey, 0ull, false};
+        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, kKllNanKey, 0ull, false,
+            false, 0u, 0u, {}};
 
         const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
+        if (P.have) {  // an odd last chunk: its level-1 run is compacted alone
+            const uint32_t off1 = kll_coin(P.K.seed, P.K.series, P.K.slice, kKllLane1 + lane, P.ci >> 1);
+            uint64_t y2[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) y2[m] = (m < 4) ? (off1 ? P.pend[2 * m + 1] : P.pend[2 * m]) : kKllNanKey;
+            P.K.sum_w2 += 4ull * popc64(ballot(P.cpend > 0));
+            P.K.wave_stage(y2, P.cpend > off1 ? (P.cpend - off1 + 1) >> 1 : 0u, A.levels);
+        }
         K = P.K;
         const uint32_t nan_l = P.nan_l, pres_l = P.pres_l, c_whole[2] = {P.c_whole[0], P.c_whole[1]};
         const uint64_t kmin = P.kmin, kmax = P.kmax;
@@ -362,7 +480,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             while (true) {
                 uint32_t total = 0, low = 0;
 #pragma unroll 1
-                for (int h = A.levels; h >= 1; --h) {
+                for (int h = A.levels; h >= (int)kKllFirst; --h) {
                     const uint32_t l = uni32(K.lens[h]);
                     total += l;
                     low = l ? (uint32_t)h : low;
@@ -403,7 +521,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             pos = (uint32_t)wtot;
         } else {
 #pragma unroll 1
-            for (int h = 1; h <= A.levels && h < kKllLevels; ++h) {
+            for (int h = (int)kKllFirst; h <= A.levels && h < kKllLevels; ++h) {
                 const uint32_t l = uni32(K.lens[h]);
                 if (!l) continue;
                 if (pos + l > (uint32_t)A.budget) {  // only after an overflow

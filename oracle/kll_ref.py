@@ -69,6 +69,9 @@ def chunks(vals: np.ndarray, beg: int, end: int):
 
 _POS = np.arange(1024)
 _BLOCK1 = (_POS % 128) >= 64  # slot u*128 + 2*lane + h belongs to block lane >> 5
+_LANE_SLOTS = [np.array([u * 128 + 2 * lane + h for u in range(8) for h in range(2)]) for lane in range(64)]
+FIRST = 3  # first wave-level run level (kKllFirst)
+LANE0, LANE1 = 32, 96  # coin "levels" of lane l's compactions (kKllLane0 / kKllLane1)
 
 
 def build_row(vals: np.ndarray, beg: int, end: int, *, budget: int = 512, seed: int = 0, series: int = 0,
@@ -97,25 +100,53 @@ def build_row(vals: np.ndarray, beg: int, end: int, *, budget: int = 512, seed: 
             sum_w2 += 4 ** h
             h += 1
 
+    def wave_stage(lane_runs):
+        """Level 2: every lane's weight-4 keys sorted together, compacted, pushed to level 3."""
+        nonlocal sum_w2
+        allk = np.sort(np.concatenate(lane_runs))
+        if not allk.size:
+            return
+        off = coin(seed, series, slc, 2, cnt[2])
+        cnt[2] += 1
+        sum_w2 += 16
+        push(allk[off::2], FIRST)
+
     exact0 = None
-    for s in chs:
+    pend = None
+    for ci, s in enumerate(chs):
         nan = np.isnan(s)
         k = okey(s[~nan])
         n_pres += k.size
         if k.size:
             kmin = k.min() if kmin is None else min(kmin, k.min())
             kmax = k.max() if kmax is None else max(kmax, k.max())
-        blocks = [np.sort(okey(s[(~_BLOCK1) & ~nan])), np.sort(okey(s[_BLOCK1 & ~nan]))]
-        if whole and blocks[0].size + blocks[1].size <= budget:
-            exact0 = np.concatenate(blocks)
+        if whole and k.size <= budget:
+            exact0 = np.concatenate([np.sort(okey(s[(~_BLOCK1) & ~nan])), np.sort(okey(s[_BLOCK1 & ~nan]))])
             continue
-        for b in blocks:
-            if not b.size:  # an all-NaN block: nothing to compact
-                continue
-            off = coin(seed, series, slc, 0, cnt[0])
-            cnt[0] += 1
-            sum_w2 += 1
-            push(b[off::2], 1)
+        runs0 = []
+        for lane in range(64):  # level 0, per lane: its 16 slots sorted, every other kept
+            kl = np.sort(okey(s[_LANE_SLOTS[lane]][~np.isnan(s[_LANE_SLOTS[lane]])]))
+            off = coin(seed, series, slc, LANE0 + lane, ci)
+            sum_w2 += 1 if kl.size else 0
+            runs0.append(kl[off::2])
+        if pend is None:
+            pend = runs0
+            continue
+        runs1 = []
+        for lane in range(64):  # level 1, per lane: merged with the pending run, compacted
+            z = np.sort(np.concatenate([pend[lane], runs0[lane]]))
+            off = coin(seed, series, slc, LANE1 + lane, ci >> 1)
+            sum_w2 += 4 if z.size else 0
+            runs1.append(z[off::2])
+        pend = None
+        wave_stage(runs1)
+    if pend is not None:  # an odd last chunk: its level-1 run compacted alone
+        runs1 = []
+        for lane in range(64):
+            off = coin(seed, series, slc, LANE1 + lane, len(chs) >> 1)
+            sum_w2 += 4 if pend[lane].size else 0
+            runs1.append(pend[lane][off::2])
+        wave_stage(runs1)
     n_nan = int(np.isnan(vals[beg:end]).sum())  # real NaN samples (the chunks' padding excluded)
     if exact0 is None:
         while True:

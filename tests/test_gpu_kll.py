@@ -168,7 +168,7 @@ def test_full_length_rank_error_within_bound(ctx, shape):
             parts.append(sketch.kll_build(ctx, ser, cfg, slice_id=w))
         merged = torch.stack(parts, dim=1).reshape(S * W, -1)
         bound = sketch.kll_rank_bound(merged, W)
-        assert np.all(bound < (0.03 if W == 1 else 0.01))
+        assert np.all(bound < (0.03 if W == 1 else 0.015))
         for p in ("50", "90", "99"):
             prm = percentile_params(Decimal(p), "sorted_lower")
             out = sketch.kll_query(ctx, merged, W, cfg, prm)
