@@ -652,7 +652,11 @@ __global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
                     v[1] = v[0];
                     continue;
                 }
-                v[qi] = r == 0 ? mn : (r == n - 1 ? mx : bitsd(okey_inv(kll_select(key, lvl, m, r, n, wtot, lane))));
+                // every kept key compacted away (a few samples spread over several chunks):
+                // only the exact min / max remain
+                v[qi] = r == 0 ? mn : (r == n - 1 ? mx : (wtot == 0 ? (2 * r < n ? mn : mx)
+                                                                     : bitsd(okey_inv(kll_select(key, lvl, m, r, n,
+                                                                                                 wtot, lane)))));
             }
             result = A.mode == KRR_PCT_SORTED_LOWER ? v[0] : np_lerp(v[0], v[1], gamma);
         }

@@ -221,6 +221,8 @@ def query(rows: np.ndarray, mode: int, p_num: int, p_den: int, q: float):
             return mn
         if r == n - 1:
             return mx
+        if wtot == 0:  # every kept key compacted away: only the exact min / max remain
+            return mn if 2 * r < n else mx
         i = next(i for i, c in enumerate(cum) if c * n > r * wtot)
         return float(okey_inv(keys[i]))
 

@@ -199,3 +199,21 @@ def test_time_sharded_helper_world1(ctx):
         v, n, f = R.query(rows[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q)
         got = out["value"][s].item()
         assert out["count"][s].item() == n and (got == v or (np.isnan(got) and np.isnan(v)))
+
+
+def test_sparse_gapped_series_match_restatement(ctx):
+    """A few present samples spread over several chunks (NaN gaps), for many series: kept
+    keys may all be compacted away, and the answer then comes from the exact min / max."""
+    rng = np.random.default_rng(21)
+    S, L = 64, 5000
+    x = np.full(S * L, np.nan)
+    for s in range(S):
+        idx = rng.choice(L, size=int(rng.integers(1, 6)), replace=False)
+        x[s * L + idx] = rng.gamma(2.0, 0.05, idx.size)
+    offs = (np.arange(S + 1) * L).astype(np.int64)
+    cfg, rows = _rows(ctx, x, offs, True, budget=256)
+    _check_rows(rows, x, offs, True, 256)
+    prm, out = _query(ctx, rows, 1, cfg, "sorted_lower", "50")
+    for s in range(S):
+        v, n, f = R.query(rows[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q)
+        assert out["count"][s] == n and out["flags"][s] == f == 0 and out["value"][s] == v and np.isfinite(v)

@@ -156,3 +156,15 @@ def test_exchange_hands_each_owner_its_series_rows(world):
             assert np.array_equal(have, want)
             v, n, f = M.query(have, prm.mode, prm.p_num, prm.p_den, prm.q)
             assert n == T and f == 0 and np.isfinite(v)
+
+
+def test_sparse_series_whose_keys_all_vanish():
+    """Three present samples spread over many chunks (NaN gaps): every kept key can be
+    compacted away; the answer then comes from the exact min / max, never a NaN."""
+    x = np.full(5000, np.nan)
+    x[[10, 2500, 4990]] = [0.3, 0.1, 0.2]
+    prm = percentile_params(Decimal("50"), "sorted_lower")
+    for seed in range(16):
+        row = M.build_row(x, 0, x.size, budget=256, seed=seed, gaps=True)
+        v, n, f = M.query(row[None], prm.mode, prm.p_num, prm.p_den, prm.q)
+        assert n == 3 and f == 0 and v in (0.1, 0.2, 0.3)
