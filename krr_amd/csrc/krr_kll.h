@@ -40,14 +40,17 @@ constexpr int kKllBlock = 512;   // level-0 block (half a streaming chunk)
 constexpr int kKllRun = 256;     // keys per run at levels >= 1
 constexpr int kKllLevels = 16;   // run slots: level 0 (whole short slices) .. 15
 constexpr int kKllHdr = 10;      // header words of an exported row
-constexpr uint64_t kKllNanKey = ~0ull;  // sorts after every okey() of a non-NaN value
+constexpr uint64_t kKllNanKey = ~0ull;  // okey space: above every key (query bisection bound)
+constexpr uint64_t kKllAbsent = 0x7FF0000000000000ull;  // +inf: an absent (NaN) slot sorts last
 constexpr uint32_t kKllFirst = 3;  // first LDS run level (levels 0-2 are the lane and wave stages)
 constexpr uint32_t kKllLane0 = 32, kKllLane1 = 96;  // coin "levels" of lane l's compactions: 32 + l, 96 + l
 
 // Row layout (uint64 words): [0] present samples  [1] NaN samples (compact layout; 0 with
 // gaps)  [2] min  [3] max (f64 bits, NaN when empty)  [4..7] run lengths, u16 x 16, level
 // h at bits 16(h & 3) of word 4 + h/4  [8] sum over compactions of w^2  [9] total weight
-// (sum of len_h 2^h)  [10 ..] keys (okey order), level 0 first, then level 1, 2, ...
+// (sum of len_h 2^h)  [10 ..] keys (f64 bits), level 0 first, then level 1, 2, ...
+// Keys are the sample values with -0 folded into +0 (the sketch keeps no zero sign), so
+// f64 min / max and compares order them totally (NaN slots are absent and never kept).
 // Within a run the keys ascend, except level 0 = block 0's keys then block 1's.
 
 __host__ __device__ inline uint64_t kll_mix(uint64_t z) {  // splitmix64 finaliser
@@ -96,11 +99,13 @@ struct KllBuildArgs {
     uint64_t* rows;   // [S][kKllHdr + budget]
 };
 
-// u64 compare-exchange: after it, a holds the min if asc, else the max.
+// Compare-exchange of two keys (f64 bits; no NaN, no -0): after it, a holds the min if asc,
+// else the max — v_min_f64 / v_max_f64, two instructions when asc is known at compile time.
 __device__ __forceinline__ void kll_cx(uint64_t& a, uint64_t& b, bool asc) {
-    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
-    a = asc ? lo : hi;
-    b = asc ? hi : lo;
+    const double x = bitsd(a), y = bitsd(b);
+    const double lo = fmin(x, y), hi = fmax(x, y);
+    a = dbits(asc ? lo : hi);
+    b = dbits(asc ? hi : lo);
 }
 
 // x of lane ^ M (M in {1, 2, 4, 8, 16}: never across the 32-lane halves): DPP quad_perm for
@@ -127,9 +132,8 @@ template <int M, int N>
 __device__ __forceinline__ void kll_cross(uint64_t (&x)[N], bool take_min) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const uint64_t o = kll_xor64<M>(x[i]);
-        const uint64_t lo = x[i] < o ? x[i] : o, hi = x[i] < o ? o : x[i];
-        x[i] = take_min ? lo : hi;
+        const double o = bitsd(kll_xor64<M>(x[i])), v = bitsd(x[i]);
+        x[i] = dbits(take_min ? fmin(v, o) : fmax(v, o));
     }
 }
 
@@ -262,9 +266,9 @@ __device__ __forceinline__ void kll_merge_half(const uint64_t* X, uint32_t nx, c
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const uint32_t mid = (lo[q] + hi[q]) >> 1;
-                const uint64_t y = Y[mid < last ? mid : last];
+                const double y = bitsd(Y[mid < last ? mid : last]), vq = bitsd(v[q]);
                 const bool active = lo[q] < hi[q];
-                const bool go = STRICT ? y < v[q] : y <= v[q];
+                const bool go = STRICT ? y < vq : y <= vq;
                 lo[q] = (active && go) ? mid + 1 : lo[q];
                 hi[q] = (active && !go) ? mid : hi[q];
             }
@@ -385,8 +389,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             bool whole;
             uint32_t nan_l, pres_l;
             uint32_t c_whole[2];
-            uint64_t kmin, kmax;
-            bool any;
+            double kmin, kmax;   // NaN until a present sample
             bool have;           // a level-1 run is pending in pend (wave-uniform)
             uint32_t cpend;      // its present keys
             uint32_t ci;         // chunks seen
@@ -396,14 +399,13 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                 uint32_t valid = 0;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const uint64_t b = dbits(slot_val(c, j));
-                    const bool nan = is_nan_bits(b);
-                    const uint64_t key = nan ? kKllNanKey : okey(b);
-                    x[j] = key;
+                    const double d = slot_val(c, j);
+                    const bool nan = __builtin_isnan(d);
+                    const double v = d == 0.0 ? 0.0 : d;  // -0 -> +0
+                    x[j] = nan ? kKllAbsent : dbits(v);
                     valid += nan ? 0u : 1u;
-                    kmin = (!nan && key < kmin) ? key : kmin;
-                    kmax = (!nan && key > kmax) ? key : kmax;
-                    any = any || !nan;
+                    kmin = fmin(kmin, d == 0.0 ? 0.0 : d);  // fmin / fmax skip NaN
+                    kmax = fmax(kmax, d == 0.0 ? 0.0 : d);
                 }
                 nan_l += 16u - valid;
                 pres_l += valid;
@@ -454,7 +456,7 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
                 }
                 ++ci;
             }
-        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, kKllNanKey, 0ull, false,
+        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, bitsd(kQuietNaN), bitsd(kQuietNaN),
             false, 0u, 0u, {}};
 
         const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
@@ -462,17 +464,16 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
             const uint32_t off1 = kll_coin(P.K.seed, P.K.series, P.K.slice, kKllLane1 + lane, P.ci >> 1);
             uint64_t y2[8];
 #pragma unroll
-            for (int m = 0; m < 8; ++m) y2[m] = (m < 4) ? (off1 ? P.pend[2 * m + 1] : P.pend[2 * m]) : kKllNanKey;
+            for (int m = 0; m < 8; ++m) y2[m] = (m < 4) ? (off1 ? P.pend[2 * m + 1] : P.pend[2 * m]) : kKllAbsent;
             P.K.sum_w2 += 4ull * popc64(ballot(P.cpend > 0));
             P.K.wave_stage(y2, P.cpend > off1 ? (P.cpend - off1 + 1) >> 1 : 0u, A.levels);
         }
         K = P.K;
         const uint32_t nan_l = P.nan_l, pres_l = P.pres_l, c_whole[2] = {P.c_whole[0], P.c_whole[1]};
-        const uint64_t kmin = P.kmin, kmax = P.kmax;
-        const bool any = P.any;
         const uint64_t n_nan = (uint64_t)wave_sum_u32(nan_l) - pad;
         const uint64_t n_pres = wave_sum_u32(pres_l);
-        const uint64_t gmin = wave_min_u64(kmin), gmax = wave_max_u64(any ? kmax : 0ull);
+        const uint64_t gmin = lane_bcast64(wave_scan64(dbits(P.kmin), kQuietNaN, OpMinF64Bits{}), kWave - 1);
+        const uint64_t gmax = lane_bcast64(wave_scan64(dbits(P.kmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1);
         const bool exact0 = whole && c_whole[0] + c_whole[1] <= (uint32_t)A.budget;
         // final compression: the lowest run alone, until the budget holds
         if (!exact0) {
@@ -542,8 +543,8 @@ __global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
         if (lane == 0) {
             row[0] = n_pres;
             row[1] = A.gaps ? 0ull : n_nan;
-            row[2] = n_pres ? okey_inv(gmin) : kQuietNaN;
-            row[3] = n_pres ? okey_inv(gmax) : kQuietNaN;
+            row[2] = n_pres ? gmin : kQuietNaN;
+            row[3] = n_pres ? gmax : kQuietNaN;
             row[4] = lw0;
             row[5] = lw1;
             row[6] = lw2;
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
             for (int h = 0; h < kKllLevels; ++h) {
                 const uint32_t l = (uint32_t)(row[4 + (h >> 2)] >> (16 * (h & 3))) & 0xFFFFu;
                 for (uint32_t i = lane; i < l; i += kWave) {
-                    key[m + i] = row[kKllHdr + pos + i];
+                    key[m + i] = okey(row[kKllHdr + pos + i]);  // f64 bits -> order-preserving
                     lvl[m + i] = (uint8_t)h;
                 }
                 pos += l;

@@ -76,7 +76,9 @@ LANE0, LANE1 = 32, 96  # coin "levels" of lane l's compactions (kKllLane0 / kKll
 
 def build_row(vals: np.ndarray, beg: int, end: int, *, budget: int = 512, seed: int = 0, series: int = 0,
               slc: int = 0, gaps: bool = False) -> np.ndarray:
-    """The exported row (uint64 [HDR + budget]; unused key words 0) of segment [beg, end)."""
+    """The exported row (uint64 [HDR + budget]; unused key words 0) of segment [beg, end).
+    Keys are ordered by okey() here and stored as f64 bits; -0 is folded into +0."""
+    vals = np.where(vals == 0.0, 0.0, vals)  # -0 -> +0 (the sketch keeps no zero sign)
     chs = list(chunks(vals, beg, end))
     whole = len(chs) <= 1
     runs = {}  # level -> sorted uint64 keys
@@ -165,7 +167,7 @@ def build_row(vals: np.ndarray, beg: int, end: int, *, budget: int = 512, seed: 
     else:
         lens = {0: exact0.size} if exact0.size else {}
         keys = exact0
-    row[HDR: HDR + keys.size] = keys
+    row[HDR: HDR + keys.size] = okey_inv(keys).view(np.uint64) if keys.size else keys
     row[0] = n_pres
     row[1] = 0 if gaps else n_nan
     nanbits = np.uint64(0x7FF8000000000000)
@@ -179,11 +181,11 @@ def build_row(vals: np.ndarray, beg: int, end: int, *, budget: int = 512, seed: 
 
 
 def row_keys(row: np.ndarray):
-    """(keys, level per key) of a row."""
+    """(okeys, level per key) of a row."""
     keys, lvl, pos = [], [], 0
     for h in range(LEVELS):
         ln = int((int(row[4 + (h >> 2)]) >> (16 * (h & 3))) & 0xFFFF)
-        keys.append(row[HDR + pos: HDR + pos + ln])
+        keys.append(okey(row[HDR + pos: HDR + pos + ln].view(np.float64)))
         lvl.append(np.full(ln, h))
         pos += ln
     return np.concatenate(keys), np.concatenate(lvl)
