@@ -53,6 +53,31 @@ def test_bench_self_launches_ranks(cfg, extra):
     assert "cpu_baseline" not in r  # rank 0 at N = 1 only
 
 
+def test_bench_under_torchrun_like_the_driver():
+    """The driver's N > 1 command shape: torch.distributed.run launches the ranks (WORLD_SIZE
+    set by it, bench.py's own per-rank watchdog armed, not fired), rank 0 alone prints the
+    one JSON line; gloo here (two ranks share the one GPU), RCCL on the driver's node."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, KRR_BENCH_BACKEND="gloo")
+    env.pop("KRR_BENCH_LAUNCHED", None)
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--containers", "400", "--steps", "2",
+                        "--warmup", "1", "--parity-block", "64", "--deadline", "200"],
+                       capture_output=True, text=True, env=env, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["backend"] == "gloo" and "status" not in r
+    assert r["parity_vs_oracle_on_sample"] is True and r["parity_gathered_vs_rank0_kernel"] is True, r
+    assert len(r["per_rank_kernel_ms"]) == 2
+
+
 @pytest.mark.parametrize("gather", ["stream", "torch", "blocking"])
 def test_bench_rccl_path_one_rank(gather):
     """The N > 1 step over RCCL at one rank (`--force-dist`): the C-ABI gather on the launch
