@@ -611,6 +611,10 @@ __global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
 #pragma unroll 1
             for (int h = 0; h < kKllLevels; ++h) {
                 const uint32_t l = (uint32_t)(row[4 + (h >> 2)] >> (16 * (h & 3))) & 0xFFFFu;
+                if (pos + l > (uint32_t)A.budget) {  // not a row krr_kll_build wrote: never stage past it
+                    bad = true;
+                    break;
+                }
                 for (uint32_t i = lane; i < l; i += kWave) {
                     key[m + i] = okey(row[kKllHdr + pos + i]);  // f64 bits -> order-preserving
                     lvl[m + i] = (uint8_t)h;
