@@ -281,7 +281,7 @@ int64_t krr_kll_row_words(const krr_kll_params* kp);
 /* rows[S * row_words] (device): one row per segment of `series` (gaps_are_nan respected:
  * NaN gaps are absent; a NaN sample in the compact layout is counted in row word 1).
  * seg_base: global index of segment 0 (coins depend on it).  KRR_E_UNSUPPORTED for
- * segments longer than ~4.2 M slots. */
+ * segments longer than ~8 M slots (run levels past 15). */
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
                   uint64_t* rows, void* stream);
 
