@@ -40,6 +40,9 @@ def _fleet(rng, lens):
     x[(u >= 0.03) & (u < 0.04)] = -rng.random(int(((u >= 0.03) & (u < 0.04)).sum()))
     x[(u >= 0.04) & (u < 0.06)] = 0.25  # ties
     x[(u >= 0.06) & (u < 0.061)] = np.inf
+    x[(u >= 0.061) & (u < 0.063)] = -0.0  # folded into +0 by the sketch (and the restatement)
+    x[(u >= 0.063) & (u < 0.065)] = 5e-324 * rng.integers(1, 1000, int(((u >= 0.063) & (u < 0.065)).sum()))
+    x[(u >= 0.065) & (u < 0.066)] = -np.inf
     return offs, x
 
 
