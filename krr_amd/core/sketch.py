@@ -713,12 +713,11 @@ def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _nati
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    st = stream
-    if events is not None:
-        events[0].record(st) if st is not None else events[0].record()
+    if events is not None:  # around the build pass (its HBM time), on the launch stream
+        events[0].record(stream)
     rows = kll_build(ctx, series, cfg, slice_id=rank, stream=stream)
     if events is not None:
-        events[1].record(st) if st is not None else events[1].record()
+        events[1].record(stream)
     merged, W = kll_exchange(rows, group)
     out = kll_query(ctx, merged, W, cfg, params, stream)
     S = rows.shape[0]
