@@ -744,8 +744,9 @@ def main():
                       f"one thread, {args.numpy_seconds:.0f} s budget"}
         # the reference's own CPU path, measured in the build container only (cannot travel):
         result["reference_cpu_measured_in_build_container"] = {
-            "value": 492.0, "unit": "container-series/s", "cores": 1,
-            "source": "BASELINE.md (SimpleStrategy.run + _format_result, config 1)"}
+            "value": 492.0, "unit": "container-series/s", "cores": 1, "measured_in_this_run": False,
+            "source": "carried constant from BASELINE.md (SimpleStrategy.run + _format_result, config 1, "
+                      "measured once in the build container; the reference cannot travel to the GPU box)"}
 
     if rank == 0 and world == 1 and not args.no_host_path:
         phase("host path")

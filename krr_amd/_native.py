@@ -349,12 +349,15 @@ class Context:
             stream = torch.cuda.current_stream()
         return ctypes.c_void_p(stream.cuda_stream)
 
-    @staticmethod
-    def series(values, offsets, max_segment_len: int = 0, gaps_are_nan: bool = False) -> KrrSeries:
+    def series(self, values, offsets, max_segment_len: int = 0, gaps_are_nan: bool = False) -> KrrSeries:
         """Describe device tensors as a krr_series.  The struct keeps references to
-        both tensors, so their memory cannot be freed and reused while it is alive."""
+        both tensors, so their memory cannot be freed and reused while it is alive.
+        Both must live on this ctx's device: the kernels read only its HBM."""
         _check_tensor(values, "float64")
         _check_tensor(offsets, "int64")
+        for t in (values, offsets):
+            if t.is_cuda and t.device.index != self.device:
+                raise ValueError(f"tensor on {t.device}, ctx on cuda:{self.device}")
         ser = KrrSeries(values.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, values.numel(),
                         int(max_segment_len), int(bool(gaps_are_nan)), 0)
         ser._keep = (values, offsets)

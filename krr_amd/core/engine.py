@@ -72,6 +72,10 @@ class SimpleEngine:
 
         dev = torch.device("cuda", self.device)
         if isinstance(ps.values, torch.Tensor) and ps.values.is_cuda:  # already in HBM (device packer)
+            if ps.values.device != dev or ps.offsets.device != dev:
+                # packed on another GPU: the kernels read only this ctx's HBM
+                raise ValueError(f"series packed on {ps.values.device}, engine runs on {dev}: pack on the "
+                                 f"engine's device (or copy the fleet there first)")
             return ps.values, ps.offsets
         host = torch.from_numpy(np.ascontiguousarray(ps.values, dtype=np.float64))
         # page-locked values (pinned_alloc) go by DMA without blocking the host; the

@@ -110,17 +110,21 @@ class BatchedRunner:
         packer by default: each GPU's own PCIe link carries its shard's JSON) -> one kernel
         pass -> the records gathered to ``dst``, which returns every rank's rounded RunResults
         in fleet order (None elsewhere).  Collective: every rank calls it."""
+        from krr_amd.core.distributed import local_device
         from krr_amd.core.packing import PackedFleet
         from krr_amd.core.prom_native import pack_query_range_bodies
 
         if parser not in ("device", "host"):
             raise ValueError("parser must be 'device' or 'host'")
+        # ONE device for the pack and the kernel pass: this rank's GPU (LOCAL_RANK) unless
+        # the caller names one — the packer's own default (settings.device) is GPU 0
+        dev = local_device() if device is None else int(device)
         if parser == "device":
-            fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)
+            fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=dev)
         else:
             fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads),
                                 pack_query_range_bodies(mem_bodies, threads=threads))
-        return self.recommend_shard(fleet, group=group, dst=dst, device=device)
+        return self.recommend_shard(fleet, group=group, dst=dst, device=dev)
 
     def recommend_packed_sharded(self, fleet, group=None, dst: int = 0, device: Optional[int] = None):
         """Every rank holds the same packed fleet: each runs its sample-balanced contiguous

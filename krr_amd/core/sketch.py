@@ -491,6 +491,17 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
     between ``stream`` and a second stream (one part's drain overlaps the next one's start;
     launches over a few GiB stream faster than one over a whole 138-GB allocation)."""
     import torch
+
+    dev = _parts(series)[0][2]._keep[0].device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    # every allocation, copy and collective below is ordered on st (the caching allocator
+    # then recycles a buffer only after st has used it)
+    with torch.cuda.stream(st):
+        return _window_exact_body(ctx, series, params, ext_slots, group, st, events, key_cap)
+
+
+def _window_exact_body(ctx, series, params, ext_slots, group, st, events, key_cap):
+    import torch
     import torch.distributed as dist
 
     parts = _parts(series)
@@ -506,7 +517,6 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
     rows = per * world
     hdr = torch.empty((max(rows, 1), _native.HDR_WORDS), dtype=torch.int64, device=dev)
     keys = torch.empty((max(rows, 1), kc), dtype=torch.int64, device=dev)
-    st = stream if stream is not None else torch.cuda.current_stream(dev)
     if events is not None:
         events[0].record(st)
     side = None
@@ -539,7 +549,7 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
            "flags": torch.empty(max(nb, 1), dtype=torch.int32, device=dev)[:nb]}
     miss = torch.zeros(1, dtype=torch.int32, device=dev)
     ctx.window_merge(nb, world, stride, hdr_r, keys_r, kc, params, out["value"], out["count"], out["flags"], miss,
-                     stream)
+                     st)
     nmiss = int(miss.item())
     total = nmiss
     if world > 1:
@@ -548,7 +558,7 @@ def window_exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, p
         dist.all_reduce(t, group=group)
         total = int(t.item())
     if total:
-        finish_window_misses(ctx, parts, params, out, (lo, hi), group, stream)
+        finish_window_misses(ctx, parts, params, out, (lo, hi), group, st)
     out.update(block=(lo, hi), misses=nmiss, key_cap=kc, exchanged_bytes=sent, hdr=hdr[:S])
     return out
 

@@ -226,10 +226,15 @@ def _reorder(series: list, order: list, alloc=None):
     into object order 0..n-1 (numpy on the host, or torch for series already in HBM)."""
     from krr_amd.core.packing import PackedSeries
 
-    if series and not isinstance(series[0].values, np.ndarray):  # device packer output (torch, HBM)
+    on_dev = [s for s in series if not isinstance(s.values, np.ndarray)]
+    if on_dev:  # device packer output (torch, HBM) — one cluster's batch may have gone to the host packer
         import torch
 
-        dev = series[0].values.device
+        dev = on_dev[0].values.device
+        series = [s if not isinstance(s.values, np.ndarray) else
+                  PackedSeries(torch.from_numpy(np.ascontiguousarray(s.values, np.float64)).to(dev),
+                               torch.from_numpy(np.ascontiguousarray(s.offsets, np.int64)).to(dev), s.max_len)
+                  for s in series]
         lens = torch.cat([s.offsets[1:] - s.offsets[:-1] for s in series])
         bases = torch.tensor(np.cumsum([0] + [int(s.values.numel()) for s in series])[:-1], device=dev)
         srcs = torch.cat([s.offsets[:-1] + b for s, b in zip(series, bases)])

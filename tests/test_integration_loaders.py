@@ -131,3 +131,29 @@ def test_reorder_of_tensor_series_equals_numpy():
     assert np.array_equal(got.offsets.numpy(), want.offsets)
     assert np.array_equal(got.values.numpy(), want.values)
     assert got.max_len == want.max_len
+
+
+@pytest.mark.parametrize("host_part", [0, 1, 2])
+def test_reorder_mixed_host_and_device_parts(host_part):
+    """One cluster's batch fell back to the host packer (numpy) while the others came from
+    the device packer (tensors): _reorder normalises to the device side instead of failing
+    on torch.cat of numpy arrays (advisor round 3)."""
+    import torch
+
+    from krr_amd.core.packing import PackedSeries
+
+    rng = np.random.default_rng(10 + host_part)
+    parts = []
+    for k in range(3):
+        lens = rng.integers(0, 7, size=int(rng.integers(1, 6)))
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        parts.append(PackedSeries(rng.random(int(offs[-1])), offs, int(lens.max(initial=0))))
+    n = sum(p.n_segments for p in parts)
+    order = list(rng.permutation(n))
+    want = integration._reorder(parts, order)
+    mixed = [p if k == host_part else PackedSeries(torch.from_numpy(p.values), torch.from_numpy(p.offsets), p.max_len)
+             for k, p in enumerate(parts)]
+    got = integration._reorder(mixed, order)
+    assert isinstance(got.values, torch.Tensor)
+    assert np.array_equal(got.offsets.numpy(), want.offsets)
+    assert np.array_equal(got.values.numpy(), want.values)
