@@ -69,7 +69,10 @@ def parse():
                     help="config 5 --sketch-only: kll = KLL-style compactor sketch (rank error bounded whatever the "
                          "data, reported as sketch_error.rank_error_bound); loglinear = the log-linear histogram "
                          "(value error <= 2^-bits, rank error measured only)")
-    ap.add_argument("--kll-budget", type=int, default=512, help="config 5 kll: weighted keys kept per series slice")
+    ap.add_argument("--kll-budget", type=int, default=512, help="config 5 kll: body keys kept per row")
+    ap.add_argument("--kll-tail", type=int, default=-1,
+                    help="config 5 kll: exact top keys per row (-1: just enough for --percentile of the whole "
+                         "30d@15s series when p >= 90, i.e. p99 answered exactly; 256 below p90)")
     ap.add_argument("--c5-refine", action="store_true",
                     help="config 5 at N=1: run the time-sharded exact path (--c5-method) instead of the direct "
                          "single-window select (N>1 always uses it)")
@@ -1039,7 +1042,9 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     direct = exact and world == 1 and not args.c5_refine
     method = "direct" if direct else (args.c5_method if exact else ("kll" if args.sketch_kind == "kll" else
                                                                      "sketch-only"))
-    kcfg = sketch.KllConfig(budget=args.kll_budget)
+    ktail = args.kll_tail if args.kll_tail >= 0 else (
+        sketch.KllConfig.tail_for(T, args.percentile) if Decimal(args.percentile) >= 90 else 256)
+    kcfg = sketch.KllConfig(budget=args.kll_budget, tail=ktail)
     # the direct pass and the window export run per chunk of series in buffers of their own
     # (as configs 2-4, fleet_chunks); the sketch paths keep one buffer per rank
     chunked = direct or method == "window"
@@ -1163,7 +1168,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         kname = "k_kll_build"
         # every slot once + offsets + the exported rows
         kbytes = 8 * N + 8 * (S + 1) + 8 * kcfg.row_words * S
-        kernels_ms["merge_exchange_query_ms"] = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+        kernels_ms["exchange_merge_query_ms"] = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     elif method == "window":
         kname = "k_window_export"
         hdr = state["hdr"]
@@ -1195,8 +1200,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                             f"({Lr} samples/series/rank), log-linear sketch 2^{cfg.mantissa_bits} bins/octave, "
                             f"approximate"),
             "kll": (f"config5: {S} CPU series x {T} samples (30d@15s), time-sharded over {world} ranks ({Lr} "
-                    f"samples/series/rank), KLL-style compactor sketch ({kcfg.budget} keys per slice, "
-                    f"one build launch per rank), approximate")}[method]
+                    f"samples/series/rank), KLL sketch (row format 2: {kcfg.budget} body keys + {kcfg.tail} exact "
+                    f"tail keys per row, one build launch per rank, rows folded per series)")}[method]
     par = {"direct": "single GPU, whole series",
            "window": f"time-shard{world} (all-to-all of per-slice windows to the series' owners, RCCL)",
            "sketch": f"time-shard{world} (reduce-scatter of {cfg.width}-word sketches, RCCL)",
@@ -1317,20 +1322,28 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                 result["collected_samples_per_rank"] = int(state.get("collected", 0))
         elif method == "kll":
             rel = np.abs(got - exact_v) / np.abs(exact_v)
-            # the bound comes from the merged rows, which rank 0 holds for its owner block only
-            mb = min(m, state["rows"].shape[0] // state["rows_per_series"])
-            bound = sketch.kll_rank_bound(state["rows"][: mb * state["rows_per_series"]], state["rows_per_series"],
-                                          delta=0.01)
+            # the bound comes from the folded rows, which rank 0 holds for its owner block only
+            mb = min(m, state["rows"].shape[0])
+            rows_b = state["rows"][:mb]
+            body_bound = sketch.kll_rank_bound(rows_b, 1, delta=0.01)
+            # ranks of this percentile inside each row's exact tail have no error at all
+            rr = np.floor(target[:mb]).astype(np.int64)
+            in_tail = sketch.kll_tail_covers(rows_b, rr)
+            bound = np.where(in_tail, 0.0, body_bound)
             result["sketch_error"] = {
                 "kind": "kll", "sample_series": m, "rank_error_max": float(err.max()),
                 "rank_error_mean": float(err.mean()), "rank_error_bound_max": float(np.nanmax(bound)),
                 "rank_error_bound_mean": float(np.nanmean(bound)), "bound_confidence": 0.99,
-                "within_bound": bool(np.all(err[:mb] <= bound)), "bound_sample_series": mb,
+                "body_rank_error_bound_max": float(np.nanmax(body_bound)),
+                "within_bound": bool(np.all(err[:mb] <= bound + 1e-12)), "bound_sample_series": mb,
+                "rank_in_exact_tail_fraction": float(np.mean(in_tail)),
                 "value_rel_error_max": float(rel.max()), "value_rel_error_mean": float(rel.mean()),
-                "budget_keys_per_slice": kcfg.budget,
-                "guarantee": ("rank: |rank(answer) - (n-1)p/100| / n <= (2 sqrt(2 ln(6/delta) sum w^2) + w_max) / n "
-                              "with probability >= 1 - delta, from each series' compaction schedule only "
-                              "(krr_amd.core.sketch.kll_rank_bound); value: none"),
+                "budget_keys_per_row": kcfg.budget, "tail_keys_per_row": kcfg.tail,
+                "row_bytes": 8 * kcfg.row_words,
+                "guarantee": ("ranks r with n - r <= tail: exact (the row keeps the tail largest samples); other "
+                              "ranks: |rank(answer) - r| / n <= sqrt(2 ln(4/delta) sum w^2) / n with probability "
+                              ">= 1 - delta, sum w^2 fixed by the compaction schedule (presence pattern only; "
+                              "krr_amd.core.sketch.kll_rank_bound)"),
                 "definition": "rank error = distance of (n-1)p/100 from the sketch answer's rank interval "
                               "[#<v, #<=v - 1] over n; exact path = k_select/hselect on the gathered full series"}
         else:

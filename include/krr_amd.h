@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KRR_ABI_VERSION 1
+#define KRR_ABI_VERSION 2  /* 2: krr_kll_params gained `tail`; krr_kll_merge; krr_kll_query takes series_base */
 
 typedef enum {
     KRR_OK = 0,
@@ -257,43 +257,57 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
                      const double* vmax, const krr_sketch_params* sp, const krr_percentile_params* params,
                      double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);
 
-/* ---- KLL-style compactor sketch: a data-independent RANK-error bound ----
- * (north_star: "an optional mergeable t-digest/KLL sketch mode"; the log-linear sketch
- * above bounds the value error only.)  One HBM pass per series slice: blocks of 512
- * slots sorted on the wave and compacted (every other key from a coin-chosen offset,
- * weight x2), runs of <= 256 keys merged and compacted level by level, the lowest runs
- * compacted until at most `budget` keys remain; exported as one row of
- * krr_kll_row_words() uint64 words per series (layout in krr_amd/csrc/krr_kll.h).
- * A slice that fits one 1,024-slot chunk with <= budget present samples is kept whole
- * (exact).  Rows of one series' time slices merge by concatenation.  Row word 8 holds
- * sum(w^2) over the slice's compactions: with probability >= 1 - delta the weighted rank
- * of any value is off by at most sqrt(2 ln(2/delta) * sum(w^2)) (Hoeffding) — a bound in
- * n and the schedule only, whatever the values. */
+/* ---- KLL sketch (row format 2): a RANK-error bound whatever the data, an exact top tail,
+ * and a bounded fold ----
+ * (north_star: "an optional mergeable t-digest/KLL sketch mode"; the log-linear sketch above
+ * bounds the value error only.)  Specification: oracle/kll_ref.py; layout and schedule:
+ * krr_amd/csrc/krr_kll.h.  One HBM pass per series slice builds one row of
+ * krr_kll_row_words() uint64 words:
+ *   - body: a compactor hierarchy with a DETERMINISTIC schedule — every compaction takes an
+ *     even number of equal-weight keys (an odd largest key waits in its level's odd slot), so
+ *     level sizes and sum(w^2) (row word 4) depend on the input's presence pattern only, and
+ *     the total weight equals the present count exactly.  With probability >= 1 - delta every
+ *     body answer's rank is within sqrt(2 ln(4/delta) sum(w^2)) of the asked rank
+ *     (Azuma-Hoeffding; krr_amd.core.sketch.kll_rank_bound).  At most `budget` keys.
+ *   - tail: the `tail` largest present keys, exactly: a rank r with n - r <= min(n, tail)
+ *     (e.g. p99 of 172,800 samples with tail >= 1,729) is answered exactly.
+ * Rows of one series (time slices, days, ...) FOLD into one row of the same size
+ * (krr_kll_merge): counts add, the tails keep the `tail` largest of their union, the body
+ * levels are unioned and compacted from level 0 up until `budget` keys remain. */
 typedef struct {
-    int32_t budget;   /* keys kept per series slice, in [256, 4096] */
-    int32_t slice;    /* this slice's index (time shard): part of the compaction coin */
-    uint64_t seed;    /* compaction coins: splitmix64 of (seed, seg_base + s, slice, level, count) */
+    int32_t budget;   /* body keys per row: [256, 4096], a multiple of 64 */
+    int32_t slice;    /* build: this slice's index (coin key); merge / query: the fold epoch */
+    uint64_t seed;    /* coins: (seed, series, slice or epoch, event) hashed */
+    int32_t tail;     /* exact tail keys per row: [0, 4096] */
+    int32_t reserved;
 } krr_kll_params;
 
-/* uint64 words per exported row (10 + budget), or < 0 if invalid. */
+/* uint64 words per row (16 + budget + tail), or < 0 if invalid. */
 int64_t krr_kll_row_words(const krr_kll_params* kp);
 
 /* rows[S * row_words] (device): one row per segment of `series` (gaps_are_nan respected:
  * NaN gaps are absent; a NaN sample in the compact layout is counted in row word 1).
  * seg_base: global index of segment 0 (coins depend on it).  KRR_E_UNSUPPORTED for
- * segments longer than ~8 M slots (run levels past 15). */
+ * segments past ~130 M slots (run levels). */
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
                   uint64_t* rows, void* stream);
 
-/* Percentile of every series from its rows_per_series rows (rows[(s * W + w) * row_words],
- * e.g. W time slices after an all-to-all): SORTED_LOWER or LINEAR over n = sum(present);
- * rank r is answered by the smallest kept key whose weighted count c satisfies
- * c * n > r * total_weight (r = 0 and n - 1: the exact min / max).  out_flags:
- * KRR_FLAG_EMPTY, KRR_FLAG_NAN (value NaN), KRR_FLAG_CAPACITY (a row overflowed; never
- * expected).  REF_INDEX -> KRR_E_UNSUPPORTED. */
+/* Fold each series' rows_per_series rows (rows[(s * W + w) * row_words], e.g. its W time
+ * slices after an all-to-all, in time order) left to right into ONE row out_rows[s * row_words]
+ * of the same format: coins keyed by (kp->seed, series_base + s, kp->slice as the epoch, w).
+ * LDS (3 row_words + 5 budget) x 8 bytes per series: KRR_E_CAPACITY past the device's LDS. */
+int krr_kll_merge(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
+                  const krr_kll_params* kp, int64_t series_base, uint64_t* out_rows, void* stream);
+
+/* Percentile of every series from its rows (folded as krr_kll_merge first when W > 1):
+ * SORTED_LOWER or LINEAR over n = present samples; rank 0 and n - 1: the exact min / max;
+ * n - r <= tail length: the exact tail key; else the smallest body key whose weighted count
+ * of keys <= it exceeds r.  out_flags: KRR_FLAG_EMPTY, KRR_FLAG_NAN (value NaN),
+ * KRR_FLAG_CAPACITY (a row overflowed its levels or formats differ; never expected).
+ * REF_INDEX -> KRR_E_UNSUPPORTED. */
 int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
-                  const krr_kll_params* kp, const krr_percentile_params* params, double* out_value,
-                  int64_t* out_count, uint32_t* out_flags, void* stream);
+                  const krr_kll_params* kp, int64_t series_base, const krr_percentile_params* params,
+                  double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);
 
 /* ---- Exact refinement of merged sketches (config 5, exact percentiles) ----
  * The merged counts are exact, so they locate each needed rank's bin exactly:

@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_query",
     "krr_kll_row_words",
     "krr_kll_build",
+    "krr_kll_merge",
     "krr_kll_query",
     "krr_sketch_locate",
     "krr_sketch_range_count",
@@ -126,11 +127,13 @@ class KrrSketchParams(ctypes.Structure):
 
 
 class KrrKllParams(ctypes.Structure):
-    """include/krr_amd.h krr_kll_params: the KLL-style compactor sketch."""
+    """include/krr_amd.h krr_kll_params: the KLL sketch (row format 2)."""
     _fields_ = [
         ("budget", ctypes.c_int32),
         ("slice", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("tail", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -271,7 +274,9 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_kll_row_words.restype = i64
         lib.krr_kll_build.argtypes = [vp, sp, kkp, i64, vp, vp]
         lib.krr_kll_build.restype = ctypes.c_int
-        lib.krr_kll_query.argtypes = [vp, i64, i32, vp, kkp, pp, vp, vp, vp, vp]
+        lib.krr_kll_merge.argtypes = [vp, i64, i32, vp, kkp, i64, vp, vp]
+        lib.krr_kll_merge.restype = ctypes.c_int
+        lib.krr_kll_query.argtypes = [vp, i64, i32, vp, kkp, i64, pp, vp, vp, vp, vp]
         lib.krr_kll_query.restype = ctypes.c_int
         lib.krr_rank_of.argtypes = [vp, sp, vp, vp, vp, vp]
         lib.krr_rank_of.restype = ctypes.c_int
@@ -302,7 +307,7 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse_segments.restype = ctypes.c_int
         lib.krr_json_gather.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_gather.restype = ctypes.c_int
-        if lib.krr_abi_version() != 1:
+        if lib.krr_abi_version() != 2:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
         return lib
@@ -541,7 +546,7 @@ class Context:
     def kll_row_words(self, kp: KrrKllParams) -> int:
         w = int(self._lib.krr_kll_row_words(ctypes.byref(kp)))
         if w < 0:
-            raise ValueError("invalid kll parameters (budget must be in [256, 4096])")
+            raise ValueError("invalid kll parameters (budget in [256, 4096], a multiple of 64; tail in [0, 4096])")
         return w
 
     def kll_build(self, series: KrrSeries, kp: KrrKllParams, rows, seg_base: int = 0, stream=None) -> None:
@@ -551,16 +556,26 @@ class Context:
         self._check(self._lib.krr_kll_build(self._h, ctypes.byref(series), ctypes.byref(kp), int(seg_base),
                                             rows.data_ptr(), self._stream(stream)))
 
+    def kll_merge(self, rows, rows_per_series: int, kp: KrrKllParams, out_rows, series_base: int = 0,
+                  stream=None) -> None:
+        """rows: int64 [S * rows_per_series, kll_row_words] series-major -> out_rows [S, kll_row_words]."""
+        rw = self.kll_row_words(kp)
+        S = out_rows.numel() // rw
+        _check_tensor(rows, "int64", S * int(rows_per_series) * rw)
+        _check_tensor(out_rows, "int64", S * rw)
+        self._check(self._lib.krr_kll_merge(self._h, S, int(rows_per_series), rows.data_ptr(), ctypes.byref(kp),
+                                            int(series_base), out_rows.data_ptr(), self._stream(stream)))
+
     def kll_query(self, rows, rows_per_series: int, kp: KrrKllParams, params: KrrPercentileParams, out_value,
-                  out_count, out_flags, stream=None) -> None:
+                  out_count, out_flags, series_base: int = 0, stream=None) -> None:
         """rows: int64 [S * rows_per_series, kll_row_words], series-major."""
         S = out_value.numel()
         _check_tensor(rows, "int64", S * int(rows_per_series) * self.kll_row_words(kp))
         for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
             _check_tensor(t, dt, S)
         self._check(self._lib.krr_kll_query(self._h, S, int(rows_per_series), rows.data_ptr(), ctypes.byref(kp),
-                                            ctypes.byref(params), out_value.data_ptr(), out_count.data_ptr(),
-                                            out_flags.data_ptr(), self._stream(stream)))
+                                            int(series_base), ctypes.byref(params), out_value.data_ptr(),
+                                            out_count.data_ptr(), out_flags.data_ptr(), self._stream(stream)))
 
     def rank_of(self, series: KrrSeries, values, out_lt, out_le, stream=None) -> None:
         S = series.n_segments

@@ -641,21 +641,36 @@ def finish_window_misses(ctx: _native.Context, series: _native.KrrSeries, params
     out["value"][loc], out["count"][loc], out["flags"][loc] = v, n, f
 
 
-# ------------------------- KLL-style compactor sketch -------------------------
+# ------------------------- KLL sketch (row format 2) -------------------------
 
 @dataclass(frozen=True)
 class KllConfig:
-    """``budget`` weighted keys kept per series slice (krr_kll_params); ``seed`` drives the
-    compaction coins, so a run is reproducible (and checkable against a CPU restatement)."""
+    """``budget`` body keys kept per row, ``tail`` exact top keys per row (a rank within
+    ``tail`` of the top is answered exactly), ``seed`` drives the compaction coins, so a run
+    is reproducible (and checkable against oracle/kll_ref.py)."""
     budget: int = 512
+    tail: int = 0
     seed: int = 0x4B4C4C5345454431
 
     def params(self, slice_id: int = 0) -> _native.KrrKllParams:
-        return _native.KrrKllParams(self.budget, int(slice_id), self.seed & (2 ** 64 - 1))
+        return _native.KrrKllParams(self.budget, int(slice_id), self.seed & (2 ** 64 - 1), self.tail, 0)
 
     @property
     def row_words(self) -> int:
-        return 10 + self.budget
+        return 16 + self.budget + self.tail
+
+    @staticmethod
+    def tail_for(n_total: int, percentile, mode: str = "linear") -> int:
+        """The smallest tail (a multiple of 64) that answers ``percentile`` of an ``n_total``-sample
+        series exactly: it must hold every rank from the asked one (and LINEAR's next) to n - 1."""
+        from fractions import Fraction
+
+        if n_total <= 0:
+            return 0
+        p = Fraction(str(percentile))
+        r0 = int((n_total - 1) * p / 100)  # floor: SORTED_LOWER's rank, LINEAR's lower one
+        need = n_total - r0
+        return int(min(4096, -(-need // 64) * 64))
 
 
 def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, seg_base: int = 0,
@@ -665,7 +680,9 @@ def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, s
     import torch
 
     parts = _parts(series)
-    S = parts[-1][1] if parts else 0
+    if not parts:
+        raise ValueError("kll_build needs a KrrSeries or at least one (lo, hi, KrrSeries) part")
+    S = parts[-1][1]
     dev = parts[0][2]._keep[0].device
     rows = torch.empty((max(S, 1), cfg.row_words), dtype=torch.int64, device=dev)
     for lo, hi, ser in parts:
@@ -699,8 +716,24 @@ def kll_exchange(rows, group=None):
     return merged.view((hi - lo) * world, RW), world
 
 
+def kll_merge(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig, series_base: int = 0,
+              epoch: int = 0, stream=None):
+    """Fold each series' W rows (series-major, time order) into ONE row of the same format
+    (krr_kll_merge; coins keyed by (seed, series_base + s, epoch, w)).  W == 1: ``rows``."""
+    import torch
+
+    W = max(int(rows_per_series), 1)
+    if W == 1:
+        return rows
+    n = rows.shape[0] // W
+    out = torch.empty((max(n, 1), cfg.row_words), dtype=torch.int64, device=rows.device)[:n]
+    if n:
+        ctx.kll_merge(rows, W, cfg.params(epoch), out, series_base=series_base, stream=stream)
+    return out
+
+
 def kll_query(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig,
-              params: _native.KrrPercentileParams, stream=None) -> dict:
+              params: _native.KrrPercentileParams, series_base: int = 0, epoch: int = 0, stream=None) -> dict:
     import torch
 
     n = rows.shape[0] // max(rows_per_series, 1)
@@ -709,52 +742,66 @@ def kll_query(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig,
            "count": torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n],
            "flags": torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]}
     if n:
-        ctx.kll_query(rows, rows_per_series, cfg.params(), params, out["value"], out["count"], out["flags"], stream)
+        ctx.kll_query(rows, rows_per_series, cfg.params(epoch), params, out["value"], out["count"], out["flags"],
+                      series_base=series_base, stream=stream)
     return out
 
 
 def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _native.KrrPercentileParams,
                      group=None, stream=None, events=None) -> dict:
     """Sketch-only percentile of every time-sharded series: build (one pass over this
-    rank's slices; slice id = rank) -> all-to-all of the rows -> query on the owner.
-    value/count/flags of this rank's owner block, plus 'block' and 'rows' (the owner's
-    merged rows, series-major, for ``kll_rank_bound``)."""
+    rank's slices; slice id = rank) -> all-to-all of the rows -> fold each series' rows into
+    one (krr_kll_merge) -> query on the owner.  value/count/flags of this rank's owner block,
+    plus 'block' and 'rows' (the owner's folded rows, one per series, for ``kll_rank_bound``).
+    Everything runs on ``stream`` (or the current stream)."""
+    import torch
     import torch.distributed as dist
 
+    dev = _parts(series)[0][2]._keep[0].device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if events is not None:  # around the build pass (its HBM time), on the launch stream
-        events[0].record(stream)
-    rows = kll_build(ctx, series, cfg, slice_id=rank, stream=stream)
-    if events is not None:
-        events[1].record(stream)
-    merged, W = kll_exchange(rows, group)
-    out = kll_query(ctx, merged, W, cfg, params, stream)
-    S = rows.shape[0]
-    out.update(block=owner_blocks(S, world)[rank] if world > 1 else (0, S), rows=merged, rows_per_series=W)
+    with torch.cuda.stream(st):
+        if events is not None:  # around the build pass (its HBM time), on the launch stream
+            events[0].record(st)
+        rows = kll_build(ctx, series, cfg, slice_id=rank, stream=st)
+        if events is not None:
+            events[1].record(st)
+        S = rows.shape[0]
+        lo, hi = owner_blocks(S, world)[rank] if world > 1 else (0, S)
+        gathered, W = kll_exchange(rows, group)
+        merged = kll_merge(ctx, gathered, W, cfg, series_base=lo, stream=st)
+        out = kll_query(ctx, merged, 1, cfg, params, series_base=lo, stream=st)
+    out.update(block=(lo, hi), rows=merged, rows_per_series=1)
     return out
 
 
-def kll_rank_bound(rows, rows_per_series: int, delta: float = 0.01) -> np.ndarray:
-    """Per series, the normalised rank-error bound that holds with probability >= 1 - delta:
-    (2 sqrt(2 ln(6/delta) sum w^2) + w_max) / n, from the rows' headers (word 8: sum w^2
-    of the slice's compactions; run lengths: the heaviest kept key).
+def kll_rank_bound(rows, rows_per_series: int = 1, delta: float = 0.01) -> np.ndarray:
+    """Per series (one folded row each; fold them first with ``kll_merge`` when W > 1), the
+    normalised rank-error bound of BODY answers that holds with probability >= 1 - delta:
+    sqrt(2 ln(4/delta) sum w^2) / n, sum w^2 from row word 4.
 
-    Why: a compaction of weight-w keys changes the weighted count of keys <= x, for a
-    FIXED x, by 0 or +-w, zero-mean over its coin and independent of the others, so by
-    Hoeffding |E(x)| <= t = sqrt(2 ln(6/delta) sum w^2) except with probability delta/3.
-    Take x- and x+ = the true order statistics at ranks r -+ (2t + w_max) and the total
-    weight (x = +inf): on the three events, the query's threshold r * W / n is within t
-    of r, the answer's weighted count jumps by at most w_max, so its true rank lies
-    between those of x- and x+.  Data-independent: n and the compaction schedule only.
+    Why: a compaction of weight-w keys changes the weighted count of kept keys <= x, for a
+    FIXED x, by 0 or +-w, with conditional mean zero given every earlier coin — martingale
+    differences.  Their bounds w are FIXED in advance: every compaction takes an even number
+    of keys (an odd one is set aside), so which compactions happen, and at what weight,
+    depends on the input's presence pattern only.  Azuma-Hoeffding then gives
+    |error(x)| <= t = sqrt(2 ln(4/delta) sum w^2) except with probability delta/2, at
+    x_lo (the largest value of true count <= r - t) and x_hi (the smallest of true count
+    > r + t); on both events the answer (the smallest kept key of estimated count > r; the
+    total weight is exactly n) lies in (x_lo, x_hi], so its rank interval meets [r - t, r + t]
+    (DESIGN.md §8).  Ranks within the row's exact tail (n - r <= word 6) have no error.
     NaN for empty series."""
-    h = rows[:, :10].cpu().numpy().astype(np.uint64).reshape(-1, rows_per_series, 10)
-    n = h[:, :, 0].sum(axis=1).astype(np.float64)
-    w2 = h[:, :, 8].astype(np.float64).sum(axis=1)
-    lens = np.stack([(h[:, :, 4 + (lv >> 2)] >> np.uint64(16 * (lv & 3))) & np.uint64(0xFFFF) for lv in range(16)],
-                    axis=-1)  # [S, W, 16]
-    present = (lens > 0).any(axis=1)  # [S, 16]
-    top = np.where(present.any(axis=1), 15 - np.argmax(present[:, ::-1], axis=1), 0)
-    wmax = np.where(present.any(axis=1), 2.0 ** top, 0.0)
+    if int(rows_per_series) != 1:
+        raise ValueError("fold the rows first (kll_merge): the bound is read from one row per series")
+    h = rows[:, :16].cpu().numpy().astype(np.uint64)
+    n = h[:, 0].astype(np.float64)
+    w2 = h[:, 4].astype(np.float64)
     with np.errstate(invalid="ignore", divide="ignore"):
-        return (2.0 * np.sqrt(2.0 * np.log(6.0 / delta) * w2) + wmax) / n
+        return np.sqrt(2.0 * np.log(4.0 / delta) * w2) / n
+
+
+def kll_tail_covers(rows, rank: np.ndarray) -> np.ndarray:
+    """Per series, whether ``rank`` (0-based ascending) is answered from the exact tail."""
+    h = rows[:, :16].cpu().numpy().astype(np.int64)
+    return (h[:, 0] - np.asarray(rank, dtype=np.int64)) <= h[:, 6]

@@ -3486,7 +3486,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
                               (int)c->max_lds);
     for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
                           (const void*)k_window_export<false>, (const void*)k_window_merge,
-                          (const void*)k_kll_build, (const void*)k_kll_query})
+                          (const void*)k_kll_build, (const void*)k_kll_merge, (const void*)k_kll_query})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -3837,12 +3837,25 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
 }
 
 int64_t krr_kll_row_words(const krr_kll_params* kp) {
-    if (!kp || kp->budget < kKllRun || kp->budget > 4096) return -1;
-    return (int64_t)kKllHdr + kp->budget;
+    if (!kp || kp->budget < kKllRun || kp->budget > 4096 || (kp->budget & 63) || kp->tail < 0 || kp->tail > 4096)
+        return -1;
+    return (int64_t)kKllHdr + kp->budget + kp->tail;
 }
 
-static size_t kll_build_lds(int levels) {  // two work runs + levels kKllFirst..levels + lens/counters
-    return (size_t)(2 + levels - (int)kKllFirst + 1) * kKllRun * 8 + 2 * kKllLevels * 4;
+// tail buffer keys: a refresh leaves <= tail + slack, a chunk adds <= 1,024; the final
+// compression's workspace (1,024 level keys + 512 carry) reuses it
+static uint32_t kll_tcap(int32_t tail) {
+    const uint32_t t = tail > 0 ? (uint32_t)tail + 1024u + kKllTailSlack : 0u;
+    return t > 1536u ? t : 1536u;
+}
+
+static size_t kll_build_lds(int nrl, uint32_t tcap) {
+    return ((size_t)(nrl + 2) * kKllRun + tcap + kKllLevels) * 8 + (3 * kKllLevels + 2) * 4;
+}
+
+static size_t kll_merge_lds(const krr_kll_params* kp, bool query) {
+    const size_t rw = (size_t)kKllHdr + kp->budget + kp->tail;
+    return (3 * rw + 5 * (size_t)kp->budget) * 8 + (query ? (size_t)kp->budget : 0);
 }
 
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
@@ -3850,7 +3863,8 @@ int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* 
     if (!ctx) return KRR_E_INVALID;
     int rc = check_series(ctx, series);
     if (rc) return rc;
-    if (krr_kll_row_words(kp) < 0) return set_err(ctx, KRR_E_INVALID, "kll budget must be in [256, 4096]%s", "");
+    if (krr_kll_row_words(kp) < 0)
+        return set_err(ctx, KRR_E_INVALID, "kll: budget in [256, 4096] (a multiple of 64), tail in [0, 4096]%s", "");
     if (seg_base < 0) return set_err(ctx, KRR_E_INVALID, "negative seg_base%s", "");
     const int64_t S = series->n_segments;
     if (S == 0) return KRR_OK;
@@ -3860,38 +3874,67 @@ int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* 
     int64_t maxlen = 0;
     rc = resolve_maxlen(ctx, series, (hipStream_t)stream, &maxlen);
     if (rc) return rc;
-    const int levels = kll_levels(maxlen);
-    if (levels > kKllLevels - 1)
+    const int nrl = kll_run_levels(maxlen);
+    if (kKllFirstRun + nrl > kKllLevels - 1)
         return set_err(ctx, KRR_E_UNSUPPORTED, "kll: segments of %s%lld slots need more run levels", "",
                        (long long)maxlen);
-    const size_t lds = kll_build_lds(levels);
-    if (lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "kll needs %s%lld B of LDS", "", (long long)lds);
-    KllBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, kp->budget, levels,
+    const uint32_t tcap = kll_tcap(kp->tail);
+    const size_t lds = kll_build_lds(nrl, tcap);
+    if (lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "kll build needs %s%lld B of LDS", "", (long long)lds);
+    KllBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, kp->budget, kp->tail, nrl, tcap,
                    (uint32_t)kp->slice, kp->seed, seg_base, rows};
     hipLaunchKernelGGL(k_kll_build, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
 
+static int kll_merge_common(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
+                            const krr_kll_params* kp, int64_t series_base, bool query, size_t* lds) {
+    if (krr_kll_row_words(kp) < 0)
+        return set_err(ctx, KRR_E_INVALID, "kll: budget in [256, 4096] (a multiple of 64), tail in [0, 4096]%s", "");
+    if (n_series < 0 || rows_per_series < 1 || series_base < 0)
+        return set_err(ctx, KRR_E_INVALID, "bad n_series / rows_per_series / series_base%s", "");
+    if (n_series && !rows) return set_err(ctx, KRR_E_INVALID, "null rows%s", "");
+    *lds = kll_merge_lds(kp, query);
+    if (*lds > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll fold of rows this wide needs %s%lld B of LDS", "", (long long)*lds);
+    return KRR_OK;
+}
+
+int krr_kll_merge(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
+                  const krr_kll_params* kp, int64_t series_base, uint64_t* out_rows, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    size_t lds = 0;
+    int rc = kll_merge_common(ctx, n_series, rows_per_series, rows, kp, series_base, false, &lds);
+    if (rc) return rc;
+    if (n_series == 0) return KRR_OK;
+    if (!out_rows) return set_err(ctx, KRR_E_INVALID, "null out_rows%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    KllMergeArgs A{n_series, rows_per_series, kp->budget, kp->tail, (uint32_t)kp->slice, kp->seed, series_base, rows,
+                   out_rows, 0, 0, 1, 0.0, nullptr, nullptr, nullptr};
+    hipLaunchKernelGGL(k_kll_merge, dim3(grid_for(n_series)), dim3(64), lds, (hipStream_t)stream, A);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
 int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
-                  const krr_kll_params* kp, const krr_percentile_params* params, double* out_value,
-                  int64_t* out_count, uint32_t* out_flags, void* stream) {
+                  const krr_kll_params* kp, int64_t series_base, const krr_percentile_params* params,
+                  double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream) {
     if (!ctx) return KRR_E_INVALID;
     int rc = check_params(ctx, params);
     if (rc) return rc;
     if (params->mode == KRR_PCT_REF_INDEX)
         return set_err(ctx, KRR_E_UNSUPPORTED, "REF_INDEX has no sketch form: use krr_select_present%s", "");
-    if (krr_kll_row_words(kp) < 0) return set_err(ctx, KRR_E_INVALID, "kll budget must be in [256, 4096]%s", "");
-    if (n_series < 0 || rows_per_series < 1) return set_err(ctx, KRR_E_INVALID, "bad n_series / rows_per_series%s", "");
+    size_t lds = 0;
+    rc = kll_merge_common(ctx, n_series, rows_per_series, rows, kp, series_base, true, &lds);
+    if (rc) return rc;
     if (n_series == 0) return KRR_OK;
-    if (!rows || !out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
-    const size_t lds = (size_t)rows_per_series * kp->budget * 9;
-    if (lds > ctx->max_lds)
-        return set_err(ctx, KRR_E_CAPACITY, "kll query of %s%lld rows needs more LDS", "", (long long)rows_per_series);
+    if (!out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
-    KllQueryArgs A{n_series, rows_per_series, kp->budget, rows, params->mode, params->p_num, params->p_den,
-                   params->q, out_value, out_count, out_flags};
+    KllMergeArgs A{n_series, rows_per_series, kp->budget, kp->tail, (uint32_t)kp->slice, kp->seed, series_base, rows,
+                   nullptr, params->mode, params->p_num, params->p_den, params->q, out_value, out_count, out_flags};
     hipLaunchKernelGGL(k_kll_query, dim3(grid_for(n_series)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;

@@ -1,69 +1,71 @@
-// krr_kll.h — KLL-style compactor sketch with a data-independent rank-error bound
-// (config 5, sketch-only mode; included by krr_kernels.hip after the streaming skeleton).
+// krr_kll.h — KLL sketch, row format 2: a compactor hierarchy with a DETERMINISTIC schedule,
+// an exact top tail, and a bounded fold (config 5 sketch mode; included by krr_kernels.hip after
+// the streaming skeleton).  The specification, word for word, is oracle/kll_ref.py; rows and
+// answers are compared with it bit for bit (tests/test_gpu_kll.py).
 //
 // north_star names "an optional mergeable t-digest/KLL sketch mode" whose rank error is
-// reported.  The log-linear histogram (k_sketch_build) bounds the VALUE error only; this
-// one bounds the RANK error whatever the data (low dispersion, heavy quantisation, ties).
+// reported.  Three properties make it fit for that:
+//  * deterministic schedule — a compaction takes an EVEN number of equal-weight keys (an odd
+//    largest key is SET ASIDE in its level's odd slot first), so every level's key count, and
+//    sum w^2, depend on the presence pattern only, never on coins or values: the Azuma-Hoeffding
+//    bound holds as written, and weight is conserved exactly (body weight == n);
+//  * exact tail — the `tail` largest present keys are kept exactly, so any rank within `tail`
+//    of the top (p99 of 172,800 samples needs 1,729) is answered with no error;
+//  * bounded fold — krr_kll_merge folds W rows into ONE row of the same size (tails: the largest
+//    `tail` of the union; body: levels unioned, then compacted from level 0 up until `budget`
+//    keys remain), so a new slice folds into an old state without the old data.
 //
-// One wave per series slice streams it once (stream_segment, 1,024 slots per chunk).  A
-// COMPACTION keeps the keys at sorted positions off, off+2, ... (off a coin from a counter
-// hash of (seed, series, slice, level, count)) and doubles their weight:
-//   * level 0, per lane: the lane's 16 slots of a chunk are sorted in registers (NaN slots
-//     sort last and are dropped) and compacted to <= 8 keys of weight 2;
-//   * level 1, per lane: the runs of two consecutive chunks are merged in registers and
-//     compacted to <= 8 keys of weight 4;
-//   * level 2, per wave (every other chunk): the 64 lanes' weight-4 keys are sorted across
-//     the wave (bitonic network: DPP / ds_swizzle exchanges) and compacted to a run of
-//     <= 256 keys of weight 8, pushed to level 3;
-//   * level h >= 3 holds at most one sorted run (LDS).  Pushing a run onto a full level
-//     merges the two runs (merge-path positions by binary search) and compacts the merge:
-//     <= 256 keys of weight 2^(h+1) go up — a binary counter of runs;
-//   * at the end, while more than `budget` keys remain, the lowest run is compacted alone
-//     and pushed up; the runs are exported as one fixed-size row.
-// A slice of <= budget present samples that fits one chunk is exported whole (weight 1):
-// short series are exact.
-//
-// Rank error: a compaction of weight-w keys moves the weighted rank of any fixed value by
-// 0 or +-w, zero-mean over its coin, independently; so |error| <= sqrt(2 ln(2/delta) sum w^2)
-// with probability >= 1 - delta (Hoeffding), plus one key's weight for the answer's own
-// granularity.  sum w^2 is exported per row and merged by addition: the bound depends on
-// n and the compaction schedule only, never on the values.
-//
-// Rows merge across time slices by concatenation (all-to-all to the series' owner, as the
-// window export); k_kll_query stages a series' W rows in LDS and bisects the 64-bit key
-// space for the smallest key whose weighted count passes rank r * total_weight / n.
+// Build, one wave per series slice, one HBM pass (1,024-slot chunks; lane l holds slots
+// u*128 + 2l + h):
+//   level 0  every chunk, per lane: slot pair u (a double2 load) with both samples present ->
+//            one 2-key compaction (coin bit u); a lone present sample -> the lane's level-0 odd slot;
+//   level 1  odd chunks: the lane's pending 8 and new 8 weight-2 keys sorted (16-key bitonic
+//            network), odd largest set aside, compacted -> <= 8 weight-4 keys;
+//   level 2, 3  every 4th / 8th chunk: two runs of <= 8 merged (bitonic merge 16), compacted;
+//   level 4  every 8th chunk, the wave: 64 lanes x 8 weight-16 keys sorted across the wave
+//            (DPP / swizzle exchanges), compacted into a run of <= 256 weight-32 keys;
+//   h >= 5   one LDS run per level; a run pushed onto an occupied level is merged with it
+//            (merge-path positions), the odd largest set aside, compacted and carried up.
+// An odd slot that receives a second key makes a 2-key compaction whose kept key goes to the
+// next level's slot (per lane below level 4, per wave above).  The tail: candidates above a
+// running threshold tau are appended to an LDS buffer; when it fills, tau rises to a sampled
+// pivot that keeps >= `tail` keys (counted exactly, ties kept by count).  At the end: flush by
+// all-absent chunks to a multiple of 8, the tail sorted and its top `tail` exported, the body
+// compacted from level 0 up until `budget` keys remain, each level exported ascending.
 #pragma once
 
 namespace krr {
 
-constexpr int kKllBlock = 512;   // level-0 block (half a streaming chunk)
-constexpr int kKllRun = 256;     // keys per run at levels >= 1
-constexpr int kKllLevels = 16;   // run slots: level 0 (whole short slices) .. 15
-constexpr int kKllHdr = 10;      // header words of an exported row
-constexpr uint64_t kKllNanKey = ~0ull;  // okey space: above every key (query bisection bound)
-constexpr uint64_t kKllAbsent = 0x7FF0000000000000ull;  // +inf: an absent (NaN) slot sorts last
-constexpr uint32_t kKllFirst = 3;  // first LDS run level (levels 0-2 are the lane and wave stages)
-constexpr uint32_t kKllLane0 = 32, kKllLane1 = 96;  // coin "levels" of lane l's compactions: 32 + l, 96 + l
+constexpr int kKllHdr = 16;
+constexpr int kKllLevels = 24;
+constexpr int kKllRun = 256;
+constexpr int kKllFirstRun = 5;
+constexpr uint32_t kKllTailSlack = 128;  // a refresh leaves <= tail + slack keys in the buffer
+// coin tags (oracle/kll_ref.py T_*)
+constexpr uint32_t kT_L0 = 0x100, kT_L1 = 0x200, kT_L2 = 0x300, kT_L3 = 0x400, kT_LODD = 0x800, kT_WAVE = 0x1000,
+                   kT_RUN = 0x1100, kT_WODD = 0x1200, kT_FINAL = 0x1300, kT_FOLD = 0x2000;
+constexpr uint64_t kKllInfBits = 0x7FF0000000000000ull;
+// row flags (word 15)
+constexpr uint64_t kKllRowOverflow = 1;  // a level past the provisioned runs (never expected): row unusable
 
-// Row layout (uint64 words): [0] present samples  [1] NaN samples (compact layout; 0 with
-// gaps)  [2] min  [3] max (f64 bits, NaN when empty)  [4..7] run lengths, u16 x 16, level
-// h at bits 16(h & 3) of word 4 + h/4  [8] sum over compactions of w^2  [9] total weight
-// (sum of len_h 2^h)  [10 ..] keys (f64 bits), level 0 first, then level 1, 2, ...
-// Keys are the sample values with -0 folded into +0 (the sketch keeps no zero sign), so
-// f64 min / max and compares order them totally (NaN slots are absent and never kept).
-// Within a run the keys ascend, except level 0 = block 0's keys then block 1's.
-
-__host__ __device__ inline uint64_t kll_mix(uint64_t z) {  // splitmix64 finaliser
+__host__ __device__ inline uint64_t kll_mix64(uint64_t z) {  // splitmix64 finaliser
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-// Compaction offset (0 or 1) of the `cnt`-th compaction at `level` of a series' slice.
-__host__ __device__ inline uint32_t kll_coin(uint64_t seed, uint64_t series, uint32_t slice, uint32_t level,
-                                             uint32_t cnt) {
-    const uint64_t x = seed + 0x9E3779B97F4A7C15ull * (series + 1) + 0xD1B54A32D192ED03ull * ((uint64_t)slice + 1) +
-                       0x8CB92BA72F3D8DD7ull * (((uint64_t)level << 32) | cnt);
-    return (uint32_t)(kll_mix(x) >> 63);
+__host__ __device__ inline uint64_t kll_slice_base(uint64_t seed, uint64_t series, uint64_t slc) {
+    return kll_mix64(seed + 0x9E3779B97F4A7C15ull * (series + 1) + 0xD1B54A32D192ED03ull * (slc + 1));
+}
+__host__ __device__ inline uint32_t kll_fmix32(uint32_t h) {  // murmur3 finaliser
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    return h ^ (h >> 16);
+}
+// 32 coin bits of event (tag, idx) of the slice (or fold epoch) keyed by `base`.
+__host__ __device__ inline uint32_t kll_coin32(uint64_t base, uint32_t tag, uint32_t idx) {
+    return kll_fmix32((uint32_t)base ^ kll_fmix32((uint32_t)(base >> 32) + tag * 0x9E3779B9u + idx * 0x85EBCA6Bu));
 }
 
 // Chunks stream_segment delivers for [beg, end) (the same arithmetic).
@@ -77,35 +79,28 @@ __host__ __device__ inline int64_t kll_nchunks(int64_t beg, int64_t end) {
     return nfull + ((rem > 0 || a0 > beg || a1 < end) ? 1 : 0);
 }
 
-// Highest run level a segment of `len` slots can reach: level 3 receives one run per two
-// chunks, the runs form a binary counter, the final compression may carry one level more.
-__host__ __device__ inline int kll_levels(int64_t len) {
-    const int64_t pushes = (kll_nchunks(0, len) + 2) / 2 + 1;
+// Run levels (5 ..) a segment of `len` slots can fill: one push at level 5 per 8 chunks,
+// a binary counter above it.
+__host__ __device__ inline int kll_run_levels(int64_t len) {
+    const int64_t pushes = (kll_nchunks(0, len) + 7) / 8;
     int lg = 0;
     while ((int64_t(1) << (lg + 1)) <= pushes) ++lg;
-    return (int)kKllFirst + lg + 1;
+    return lg + 1;
 }
 
-struct KllBuildArgs {
-    const double* vals;
-    const int64_t* offs;
-    int64_t S;
-    int32_t gaps;
-    int32_t budget;
-    int32_t levels;   // highest run level (LDS slots for levels kKllFirst..levels)
-    uint32_t slice;
-    uint64_t seed;
-    int64_t seg_base;
-    uint64_t* rows;   // [S][kKllHdr + budget]
-};
+// ---- sorting networks on f64 keys (no NaN; -0 folded into +0, so min/max order totally) ----
+__device__ __forceinline__ void kll_cxd(double& a, double& b) {  // ascending
+    const double lo = fmin(a, b), hi = fmax(a, b);
+    a = lo;
+    b = hi;
+}
 
-// Compare-exchange of two keys (f64 bits; no NaN, no -0): after it, a holds the min if asc,
-// else the max — v_min_f64 / v_max_f64, two instructions when asc is known at compile time.
-__device__ __forceinline__ void kll_cx(uint64_t& a, uint64_t& b, bool asc) {
-    const double x = bitsd(a), y = bitsd(b);
-    const double lo = fmin(x, y), hi = fmax(x, y);
-    a = dbits(asc ? lo : hi);
-    b = dbits(asc ? hi : lo);
+// c ? b : a as a bit blend: a select between two adjacent array elements would otherwise be
+// folded into a dynamically indexed load (an array in scratch memory).
+__device__ __forceinline__ double kll_pick(bool c, double a, double b) {
+    uint64_t m = c ? ~0ull : 0ull;
+    asm volatile("" : "+v"(m));
+    return bitsd((dbits(a) & ~m) | (dbits(b) & m));
 }
 
 // x of lane ^ M (M in {1, 2, 4, 8, 16}: never across the 32-lane halves): DPP quad_perm for
@@ -119,81 +114,45 @@ __device__ __forceinline__ uint32_t kll_xor32(uint32_t v) {
     else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));
 }
 template <int M>
-__device__ __forceinline__ uint64_t kll_xor64(uint64_t x) {
+__device__ __forceinline__ double kll_xord(double d) {
+    const uint64_t x = dbits(d);
     if constexpr (M == 32) {  // across the 32-lane halves
         const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, 32, kWave);
         const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), 32, kWave);
-        return ((uint64_t)hi << 32) | lo;
+        return bitsd(((uint64_t)hi << 32) | lo);
     }
-    return ((uint64_t)kll_xor32<M>((uint32_t)(x >> 32)) << 32) | kll_xor32<M>((uint32_t)x);
+    return bitsd(((uint64_t)kll_xor32<M>((uint32_t)(x >> 32)) << 32) | kll_xor32<M>((uint32_t)x));
 }
-
 template <int M, int N>
-__device__ __forceinline__ void kll_cross(uint64_t (&x)[N], bool take_min) {
+__device__ __forceinline__ void kll_cross(double (&x)[N], bool take_min) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const double o = bitsd(kll_xor64<M>(x[i])), v = bitsd(x[i]);
-        x[i] = dbits(take_min ? fmin(v, o) : fmax(v, o));
-    }
-}
-
-// In-lane substeps j = J, J/2, .., 1 of bitonic stage k on the lane's 16 keys
-// (position = lane * 16 + i; direction from bit k of the position, all ascending at k = 512).
-template <int J>
-__device__ __forceinline__ void kll_inlane(uint64_t (&x)[16], uint32_t k, int lane) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (i & J) continue;
-        const uint32_t pos = (uint32_t)lane * 16u + (uint32_t)i;
-        const bool asc = k >= (uint32_t)kKllBlock || (pos & k) == 0;
-        kll_cx(x[i], x[i + J], asc);
-    }
-    if constexpr (J > 1) kll_inlane<J / 2>(x, k, lane);
-}
-
-// Sort each 512-key block (lanes 0-31: block 0, lanes 32-63: block 1) ascending.
-__device__ __forceinline__ void kll_sort_blocks(uint64_t (&x)[16], int lane) {
-    kll_inlane<1>(x, 2, lane);
-    kll_inlane<2>(x, 4, lane);
-    kll_inlane<4>(x, 8, lane);
-    kll_inlane<8>(x, 16, lane);
-#pragma unroll 1
-    for (uint32_t k = 32; k <= (uint32_t)kKllBlock; k <<= 1) {
-        const bool asc = k >= (uint32_t)kKllBlock || (((uint32_t)lane * 16u) & k) == 0;
-#pragma unroll 1
-        for (uint32_t j = k >> 1; j >= 16; j >>= 1) {
-            const int m = (int)(j >> 4);
-            const bool take_min = ((lane & m) == 0) == asc;  // the lower lane of the pair keeps the min if ascending
-            switch (m) {  // wave-uniform
-                case 1: kll_cross<1, 16>(x, take_min); break;
-                case 2: kll_cross<2, 16>(x, take_min); break;
-                case 4: kll_cross<4, 16>(x, take_min); break;
-                case 8: kll_cross<8, 16>(x, take_min); break;
-                default: kll_cross<16, 16>(x, take_min); break;
-            }
-        }
-        kll_inlane<8>(x, k, lane);
+        const double o = kll_xord<M>(x[i]);
+        x[i] = take_min ? fmin(x[i], o) : fmax(x[i], o);
     }
 }
 
 // The lane's 16 keys ascending (a full bitonic sort in registers).
-__device__ __forceinline__ void kll_sort16(uint64_t (&x)[16]) {
+__device__ __forceinline__ void kll_sort16(double (&x)[16]) {
 #pragma unroll
     for (int k = 2; k <= 16; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                if (!(i & j)) kll_cx(x[i], x[i + j], k == 16 || (i & k) == 0);
+                if (!(i & j)) {
+                    if (k == 16 || (i & k) == 0) kll_cxd(x[i], x[i + j]);
+                    else kll_cxd(x[i + j], x[i]);
+                }
         }
     }
 }
 
 // z[0, 8) and z[8, 16) ascending -> z ascending (reverse the second half: bitonic; clean).
-__device__ __forceinline__ void kll_merge16(uint64_t (&z)[16]) {
+__device__ __forceinline__ void kll_merge16(double (&z)[16]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint64_t t = z[8 + i];
+        const double t = z[8 + i];
         z[8 + i] = z[15 - i];
         z[15 - i] = t;
     }
@@ -201,17 +160,17 @@ __device__ __forceinline__ void kll_merge16(uint64_t (&z)[16]) {
     for (int j = 8; j > 0; j >>= 1) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-            if (!(i & j)) kll_cx(z[i], z[i + j], true);
+            if (!(i & j)) kll_cxd(z[i], z[i + j]);
     }
 }
 
 // 512 keys ascending across the wave: lane l holds positions 8l .. 8l+7, each lane's 8
 // already ascending (odd lanes' runs are reversed first, so stage 16 starts bitonic).
-__device__ __forceinline__ void kll_sort512(uint64_t (&y)[8], int lane) {
+__device__ __forceinline__ void kll_sort512(double (&y)[8], int lane) {
     if (lane & 1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint64_t t = y[i];
+            const double t = y[i];
             y[i] = y[7 - i];
             y[7 - i] = t;
         }
@@ -236,19 +195,78 @@ __device__ __forceinline__ void kll_sort512(uint64_t (&y)[8], int lane) {
         for (int j = 4; j > 0; j >>= 1) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                if (!(i & j)) kll_cx(y[i], y[i + j], asc);
+                if (!(i & j)) {
+                    if (asc) kll_cxd(y[i], y[i + j]);
+                    else kll_cxd(y[i + j], y[i]);
+                }
         }
     }
 }
 
-// Merge-path step of a merge-compaction: every key X[i] (i = lane + 64 q, i < nx <= 256)
-// lands at merged position p = i + #(Y < X[i]) (STRICT: X's keys go before Y's equal keys)
-// or i + #(Y <= X[i]); positions off, off + 2, ... are kept, at O[(p - off) / 2].  The four
-// binary searches of a lane advance together (their LDS reads overlap), 9 halvings each
-// (ny <= 256).
+// One key per lane, ascending over the 64 lanes (refresh samples).
+__device__ __forceinline__ double kll_sort64(double v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t x = dbits(v);
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, j, kWave);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j, kWave);
+            const double o = bitsd(((uint64_t)hi << 32) | lo);
+            const bool asc = (lane & k) == 0 || k == 64;
+            const bool lower = (lane & j) == 0;
+            v = (lower == asc) ? fmin(v, o) : fmax(v, o);
+        }
+    }
+    return v;
+}
+
+// Ascending sort of a[0, n) in LDS by one wave, any n: bitonic with the flip first step (every
+// block sorted ascending), so the virtual +inf past n never moves and its pairs are skipped.
+__device__ void kll_lds_sort(uint64_t* a, uint32_t n, int lane) {
+    if (n < 2) return;
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+#pragma unroll 1
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+#pragma unroll 1
+        for (uint32_t j = k >> 1; j >= 1; j >>= 1) {
+            const bool flip = j == (k >> 1);
+#pragma unroll 1
+            for (uint32_t t = lane; t < (P >> 1); t += kWave) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const uint32_t p = flip ? (i ^ (k - 1)) : (i + j);
+                if (p < n) {
+                    const double x = bitsd(a[i]), y = bitsd(a[p]);
+                    a[i] = dbits(fmin(x, y));
+                    a[p] = dbits(fmax(x, y));
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// #{i < n : a[i] < v} (STRICT) or #{a[i] <= v} of an ascending LDS / global array.
+template <bool STRICT>
+__device__ __forceinline__ uint32_t kll_bound(const uint64_t* a, uint32_t n, double v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const double y = bitsd(a[mid]);
+        if (STRICT ? y < v : y <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Merge-compaction step: every key X[i] (i = lane + 64 q, i < nx <= 256) lands at merged
+// position p = i + #(Y < X[i]) (STRICT: X's keys go first among equal keys) or i + #(Y <= X[i]);
+// positions p < lim with p = off, off + 2, ... are kept at O[(p - off) / 2].  The four binary
+// searches of a lane advance together (their LDS reads overlap), 9 halvings each (ny <= 256).
 template <bool STRICT>
 __device__ __forceinline__ void kll_merge_half(const uint64_t* X, uint32_t nx, const uint64_t* Y, uint32_t ny,
-                                               uint32_t off, uint64_t* O, int lane) {
+                                               uint32_t off, uint32_t lim, uint64_t* O, int lane) {
     constexpr int Q = kKllRun / kWave;
     uint64_t v[Q];
     uint32_t lo[Q], hi[Q];
@@ -278,290 +296,809 @@ __device__ __forceinline__ void kll_merge_half(const uint64_t* X, uint32_t nx, c
     for (int q = 0; q < Q; ++q) {
         const uint32_t i = (uint32_t)lane + (uint32_t)q * kWave;
         const uint32_t p = i + lo[q];
-        if (i < nx && p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v[q];
+        if (i < nx && p < lim && p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = v[q];
     }
 }
 
-struct KllState {
-    uint64_t* tmp;      // two LDS runs of kKllRun keys (tb(0), tb(1))
-    uint64_t* lv;       // LDS runs, level h at lv + (h - 1) * kKllRun
-    uint32_t* lens;     // LDS [kKllLevels]
-    uint32_t* cnt;      // LDS [kKllLevels] compactions done per level
-    uint64_t seed, series;
+// Full merge of ascending X (nx) and Y (ny), any sizes, into O (X first among equal keys;
+// equal keys have equal bits, so the order is immaterial to the result).
+__device__ void kll_lds_merge(const uint64_t* X, uint32_t nx, const uint64_t* Y, uint32_t ny, uint64_t* O,
+                              int lane) {
+#pragma unroll 1
+    for (uint32_t i = lane; i < nx; i += kWave) O[i + kll_bound<true>(Y, ny, bitsd(X[i]))] = X[i];
+#pragma unroll 1
+    for (uint32_t j = lane; j < ny; j += kWave) O[j + kll_bound<false>(X, nx, bitsd(Y[j]))] = Y[j];
+}
+
+// Uniform build state in LDS.
+struct KllShared {
+    uint64_t* lv;    // runs, level h at lv + (h - kKllFirstRun) * kKllRun
+    uint64_t* tmp;   // two work runs of kKllRun keys
+    uint64_t* tb;    // tail buffer (tcap keys); the final compression's workspace at the end
+    uint64_t* wk;    // [kKllLevels] wave odd-slot keys
+    uint32_t* lens;  // [kKllLevels] run lengths
+    uint32_t* rcnt;  // [kKllLevels] run merge-compactions per level
+    uint32_t* wcnt;  // [kKllLevels] wave odd-pair compactions per level
+    uint32_t* misc;  // [0] wave odd-slot presence bits  [1] overflow
+};
+
+struct KllBuildArgs {
+    const double* vals;
+    const int64_t* offs;
+    int64_t S;
+    int32_t gaps;
+    int32_t budget;
+    int32_t tail;
+    int32_t nrl;      // run levels in LDS: kKllFirstRun .. kKllFirstRun + nrl - 1
+    uint32_t tcap;    // tail buffer / workspace keys
     uint32_t slice;
-    uint64_t sum_w2;    // wave-uniform
-    uint32_t overflow;  // a run above the provisioned levels (never expected)
+    uint64_t seed;
+    int64_t seg_base;
+    uint64_t* rows;   // [S][kKllHdr + budget + tail]
+};
+
+// ---- wave-level pieces, free functions of value arguments (the per-wave state below stays in
+// registers: nothing of it is ever address-taken) ----
+
+// A set-aside key at wave level h (>= 4): stored in the level's odd slot, or compacted with the
+// key already there (coin) and carried up.  Returns the sum of w^2 it added.
+__device__ uint64_t kll_wave_odd(KllShared sh, uint64_t base, uint32_t h, double v, int lane) {
+    uint64_t w2 = 0;
+#pragma unroll 1
+    while (true) {
+        if (h >= (uint32_t)kKllLevels) {
+            if (lane == 0) sh.misc[1] = 1;
+            __syncthreads();
+            return w2;
+        }
+        const uint32_t pm = uni32(sh.misc[0]);
+        if (!((pm >> h) & 1u)) {
+            if (lane == 0) {
+                sh.wk[h] = dbits(v);
+                sh.misc[0] = pm | (1u << h);
+            }
+            __syncthreads();
+            return w2;
+        }
+        const double k = bitsd(uni64(sh.wk[h]));
+        const uint32_t c = uni32(sh.wcnt[h]);
+        const uint32_t bit = kll_coin32(base, kT_WODD + h, c) & 1u;
+        v = bit ? fmax(k, v) : fmin(k, v);
+        w2 += 1ull << (2 * h);
+        __syncthreads();
+        if (lane == 0) {
+            sh.wcnt[h] = c + 1;
+            sh.misc[0] = pm & ~(1u << h);
+        }
+        __syncthreads();
+        ++h;
+    }
+}
+
+// Push the run tmp[t_sel][0, t) at level h (>= 5): store it, or merge-compact and carry up.
+// Returns the sum of w^2 it added.
+__device__ uint64_t kll_push(KllShared sh, uint64_t base, int32_t nrl, uint32_t t_sel, uint32_t t, uint32_t h,
+                             int lane) {
+    uint64_t w2 = 0;
+#pragma unroll 1
+    while (t) {
+        if ((int)h >= kKllFirstRun + nrl) {
+            if (lane == 0) sh.misc[1] = 1;
+            __syncthreads();
+            return w2;
+        }
+        const uint32_t a = uni32(sh.lens[h]);
+        const uint64_t* T = sh.tmp + (size_t)t_sel * kKllRun;
+        uint64_t* L = sh.lv + (size_t)(h - kKllFirstRun) * kKllRun;
+        if (a == 0) {
+            for (uint32_t i = lane; i < t; i += kWave) L[i] = T[i];
+            __syncthreads();
+            if (lane == 0) sh.lens[h] = t;
+            __syncthreads();
+            return w2;
+        }
+        const uint32_t m = a + t, lim = m & ~1u;
+        if (m & 1u)  // the largest key of the merge is set aside at level h
+            w2 += kll_wave_odd(sh, base, h, fmax(bitsd(L[a - 1]), bitsd(T[t - 1])), lane);
+        const uint32_t c = uni32(sh.rcnt[h]);
+        const uint32_t off = kll_coin32(base, kT_RUN + h, c) & 1u;
+        uint64_t* O = sh.tmp + (size_t)(t_sel ^ 1) * kKllRun;
+        kll_merge_half<true>(L, a, T, t, off, lim, O, lane);  // the run's keys before T's equal keys
+        kll_merge_half<false>(T, t, L, a, off, lim, O, lane);
+        w2 += 1ull << (2 * h);
+        __syncthreads();
+        if (lane == 0) {
+            sh.lens[h] = 0;
+            sh.rcnt[h] = c + 1;
+        }
+        __syncthreads();
+        t = lim >> 1;
+        t_sel ^= 1;
+        ++h;
+    }
+    return w2;
+}
+
+// The tail buffer's uniform state.
+struct KllTail {
+    uint32_t tl;    // keys in the buffer
+    uint32_t full;  // tau is active
+    double tau;     // keys <= tau are not candidates
+};
+
+// In-place stable compaction: keep keys > v and the first `eq` copies of v.
+__device__ KllTail kll_tail_keep(KllShared sh, KllTail ts, double v, uint32_t eq, int lane) {
+    uint32_t out = 0;
+#pragma unroll 1
+    for (uint32_t r = 0; r < ts.tl; r += kWave) {
+        const uint32_t i = r + (uint32_t)lane;
+        const double x = i < ts.tl ? bitsd(sh.tb[i]) : -__builtin_inf();
+        const bool isgt = i < ts.tl && x > v;
+        const uint64_t em = ballot(i < ts.tl && x == v);
+        const bool keep = isgt || (((em >> lane) & 1ull) && lane_prefix(em) < eq);
+        const uint64_t km = ballot(keep);
+        const uint32_t ne = popc64(em);
+        eq -= ne < eq ? ne : eq;
+        if (keep) sh.tb[out + lane_prefix(km)] = dbits(x);
+        out += popc64(km);
+    }
+    __syncthreads();
+    return KllTail{out, 1u, v};
+}
+
+// Keep the buffer's largest keys: raise tau to a sampled pivot v that leaves between `tail`
+// and tail + slack keys (> v, plus copies of v to reach `tail` when ties straddle it), all
+// counted exactly; if no sample does, sort the buffer and keep exactly `tail`.
+__device__ KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
+    const uint32_t m = ts.tl;
+    double s = bitsd(sh.tb[(uint32_t)(((uint64_t)(uint32_t)lane * m) >> 6)]);
+    s = kll_sort64(s, lane);
+    int idx = (int)(((uint64_t)(m - tail) * 64u) / m) - 1;
+    idx = idx < 0 ? 0 : (idx > 63 ? 63 : idx);
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+        const double v = bitsd(lane_bcast64(dbits(s), idx));
+        uint32_t gt = 0, ge = 0;
+        for (uint32_t i = lane; i < m; i += kWave) {
+            const double x = bitsd(sh.tb[i]);
+            gt += x > v ? 1u : 0u;
+            ge += x >= v ? 1u : 0u;
+        }
+        gt = wave_sum_u32(gt);
+        ge = wave_sum_u32(ge);
+        if (gt >= tail && gt <= tail + kKllTailSlack) return kll_tail_keep(sh, ts, v, 0, lane);
+        if (gt < tail && ge >= tail) return kll_tail_keep(sh, ts, v, tail - gt, lane);
+        if (ge < tail) {  // pivot too high
+            if (idx == 0) break;
+            --idx;
+        } else {  // keeps too many
+            if (idx == 63) break;
+            ++idx;
+        }
+    }
+    kll_lds_sort(sh.tb, m, lane);  // exact fallback
+    for (uint32_t i = lane; i < tail; i += kWave) sh.tb[i] = sh.tb[m - tail + i];
+    __syncthreads();
+    return KllTail{tail, 1u, bitsd(uni64(sh.tb[0]))};
+}
+
+// Per-wave build state; one instance per series slice (by value: nothing is address-taken).
+struct KllProc {
+    KllShared sh;
+    uint64_t base;
+    uint64_t w2u;      // sum w^2 of the wave-level compactions (uniform)
+    uint32_t ci;       // chunk index (uniform)
     int lane;
+    int32_t nrl;
+    uint32_t tail, tcap;
+    KllTail ts;
+    // per lane
+    double pend1[8], pend2[8], pend3[8];
+    uint32_t cp1, cp2, cp3;
+    double K[4];
+    uint32_t kmask;
+    uint32_t kcnt[4];
+    double arr;
+    bool has_arr;
+    uint32_t w2l, pres;
+    double kmin, kmax;
 
-    __device__ __forceinline__ uint64_t* run(uint32_t h) const { return lv + (size_t)(h - kKllFirst) * kKllRun; }
-    __device__ __forceinline__ uint64_t* tb(uint32_t sel) const { return tmp + (size_t)sel * kKllRun; }
+    // ---- per-lane odd slots (levels 0..3); a carry past level 3 arrives at the wave ----
+    // Branch-free over the levels (a per-level early return would be merged into one store
+    // through a dynamic index, putting K in scratch memory).
+    template <int H0>
+    __device__ __forceinline__ void lane_odd(double v, bool active = true) {
+#pragma unroll
+        for (int h = H0; h < 4; ++h) {
+            const bool occ = (kmask >> h) & 1u;
+            const bool here = active && !occ, comp = active && occ;
+            const uint32_t bit = kll_coin32(base, kT_LODD + 4u * (uint32_t)lane + (uint32_t)h, kcnt[h]) & 1u;
+            const double kept = bit ? fmax(K[h], v) : fmin(K[h], v);
+            K[h] = kll_pick(here, K[h], v);
+            kcnt[h] += comp ? 1u : 0u;
+            kmask = here ? (kmask | (1u << h)) : (comp ? (kmask & ~(1u << h)) : kmask);
+            w2l += comp ? (1u << (2 * h)) : 0u;
+            v = kll_pick(comp, v, kept);
+            active = comp;
+        }
+        arr = kll_pick(active, arr, v);
+        has_arr = has_arr || active;
+    }
 
-    // Level 2: the lanes' weight-4 keys (y ascending per lane, NaN keys past cy) sorted
-    // across the wave, compacted to <= 256 keys of weight 8, pushed to level 3.
-    __device__ void wave_stage(uint64_t (&y)[8], uint32_t cy, int levels) {
-        const uint32_t C = wave_sum_u32(cy);
+    __device__ __forceinline__ void arrivals() {
+        uint64_t am = ballot(has_arr);
+        if (am) {  // rare: a per-lane odd carry reached level 4
+#pragma unroll 1
+            while (am) {
+                const int l = __ffsll((long long)am) - 1;
+                w2u += kll_wave_odd(sh, base, 4, bitsd(lane_bcast64(dbits(arr), l)), lane);
+                am &= am - 1;
+            }
+            has_arr = false;
+        }
+    }
+
+    // Odd largest set aside (slow path), then every other key from the coin: z (16, ascending,
+    // absent keys +inf at the end, c present) -> y (8), cy.
+    template <int H>
+    __device__ __forceinline__ void lane_level(double (&z)[16], uint32_t c, uint32_t tag, uint32_t idx, double (&y)[8],
+                                               uint32_t& cy) {
+        if (ballot(c & 1u)) {
+            const bool odd = c & 1u;
+            double v = z[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) v = kll_pick((uint32_t)i == c - 1, v, z[i]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) z[i] = kll_pick(odd && (uint32_t)i == c - 1, z[i], bitsd(kKllInfBits));
+            lane_odd<H>(v, odd);
+            c -= odd ? 1u : 0u;
+        }
+        const uint32_t off = kll_coin32(base, tag + (uint32_t)lane, idx) & 1u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = kll_pick(off != 0, z[2 * k], z[2 * k + 1]);
+        cy = c >> 1;
+        w2l += c >= 2 ? (1u << (2 * H)) : 0u;
+    }
+
+    // ---- level 4: the wave ----
+    __device__ __forceinline__ void wave_stage(double (&y)[8], uint32_t cy) {
+        uint32_t C = wave_sum_u32(cy);
         if (C == 0) return;
         kll_sort512(y, lane);
-        const uint32_t c = uni32(cnt[2]);
-        const uint32_t off = kll_coin(seed, series, slice, 2, c);
+        if (C & 1u) {  // the largest present key (position C - 1) is set aside at level 4
+            const uint32_t src = (C - 1) >> 3, slot = (C - 1) & 7u;
+            double v = y[0];
+#pragma unroll
+            for (int i = 1; i < 8; ++i) v = kll_pick((uint32_t)i == slot, v, y[i]);
+            w2u += kll_wave_odd(sh, base, 4, bitsd(lane_bcast64(dbits(v), (int)src)), lane);
+            C -= 1;
+        }
+        const uint32_t off = kll_coin32(base, kT_WAVE, ci >> 3) & 1u;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t p = (uint32_t)lane * 8u + (uint32_t)i;
-            if (p < C && p >= off && ((p - off) & 1u) == 0) tb(0)[(p - off) >> 1] = y[i];
+            if (p < C && p >= off && ((p - off) & 1u) == 0) sh.tmp[(p - off) >> 1] = dbits(y[i]);
         }
-        sum_w2 += 16;
+        if (C >= 2) w2u += 1ull << 8;
         __syncthreads();
-        if (lane == 0) cnt[2] = c + 1;
-        __syncthreads();
-        push(0, C > off ? (C - off + 1) >> 1 : 0u, kKllFirst, levels);
+        w2u += kll_push(sh, base, nrl, 0, C >> 1, kKllFirstRun, lane);
     }
 
-    // Push the run tmp[t_sel][0, t) at level h (>= kKllFirst): store it, or merge-compact and carry.
-    __device__ void push(uint32_t t_sel, uint32_t t, uint32_t h, int levels) {
-        while (t) {  // an empty run changes nothing
-            if ((int)h > levels) {
-                overflow = 1;
-                return;
-            }
-            const uint32_t a = uni32(lens[h]);
-            const uint64_t* T = tb(t_sel);
-            if (a == 0) {
-                uint64_t* L = run(h);
-                for (uint32_t i = lane; i < t; i += kWave) L[i] = T[i];
-                __syncthreads();
-                if (lane == 0) lens[h] = t;
-                __syncthreads();
-                return;
-            }
-            const uint32_t c = uni32(cnt[h]);
-            const uint32_t off = kll_coin(seed, series, slice, h, c);
-            const uint64_t* A = run(h);
-            uint64_t* O = tb(t_sel ^ 1);
-            kll_merge_half<true>(A, a, T, t, off, O, lane);  // A's keys before T's equal keys
-            kll_merge_half<false>(T, t, A, a, off, O, lane);
-            sum_w2 += (uint64_t)1 << (2 * h);
-            __syncthreads();
-            if (lane == 0) {
-                lens[h] = 0;
-                cnt[h] = c + 1;
-            }
-            __syncthreads();
-            t = (a + t > off) ? (a + t - off + 1) >> 1 : 0;
-            t_sel ^= 1;
-            ++h;
+    __device__ __forceinline__ void tail_filter(const double (&a)[8], const double (&b)[8]) {
+        uint64_t m[16];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
+            m[j] = ballot(ts.full ? x > ts.tau : x == x);
+            tot += popc64(m[j]);
         }
+        if (!tot) return;
+        if (ts.tl + tot > tcap) {
+            ts = kll_tail_refresh(sh, ts, tail, lane);
+            tot = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
+                m[j] = ballot(x > ts.tau);
+            }
+        }
+        uint32_t tl = ts.tl;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (m[j]) {
+                const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
+                if ((m[j] >> lane) & 1ull) sh.tb[tl + lane_prefix(m[j])] = dbits(x);
+                tl += popc64(m[j]);
+            }
+        }
+        ts.tl = tl;
+    }
+
+    // ---- one chunk ----
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+        double a[8], b[8];
+        bool lane_nan = false;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a[u] = c[u].x + 0.0;  // -0 -> +0; NaN stays NaN
+            b[u] = c[u].y + 0.0;
+            lane_nan |= __builtin_isnan(a[u]) || __builtin_isnan(b[u]);
+        }
+        const uint64_t nanm = ballot(lane_nan);
+        if (tail) tail_filter(a, b);
+        double out[8];
+        uint32_t c0 = 0;
+        if (nanm == 0) {  // every slot present: 8 two-key compactions per lane
+            const uint32_t bits = kll_coin32(base, kT_L0 + (uint32_t)lane, ci);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double lo = fmin(a[u], b[u]), hi = fmax(a[u], b[u]);
+                out[u] = ((bits >> u) & 1u) ? hi : lo;
+                kmin = fmin(kmin, lo);
+                kmax = fmax(kmax, hi);
+            }
+            c0 = 8;
+            w2l += 8;
+            pres += 16;
+        } else {
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) any |= !__builtin_isnan(a[u]) || !__builtin_isnan(b[u]);
+            if (ballot(any)) {
+                const uint32_t bits = kll_coin32(base, kT_L0 + (uint32_t)lane, ci);
+                uint32_t lone = 0;  // pairs with one present sample, bit u
+                double lv[8];       // ... that sample
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool pa = !__builtin_isnan(a[u]), pb = !__builtin_isnan(b[u]);
+                    kmin = fmin(kmin, fmin(a[u], b[u]));
+                    kmax = fmax(kmax, fmax(a[u], b[u]));
+                    pres += (pa ? 1u : 0u) + (pb ? 1u : 0u);
+                    const double lo = fmin(a[u], b[u]), hi = fmax(a[u], b[u]);
+                    out[u] = (pa && pb) ? (((bits >> u) & 1u) ? hi : lo) : bitsd(kKllInfBits);
+                    c0 += (pa && pb) ? 1u : 0u;
+                    lone |= (pa != pb) ? (1u << u) : 0u;
+                    lv[u] = lo;  // fmin of a present and a NaN sample is the present one
+                }
+                w2l += c0;
+                // lone samples into the level-0 odd slot, in pair order (one slot update per round)
+#pragma unroll 1
+                while (ballot(lone != 0)) {
+                    const uint32_t u0 = lone ? (uint32_t)__builtin_ctz(lone) : 0u;
+                    double v = lv[0];
+#pragma unroll
+                    for (int u = 1; u < 8; ++u) v = kll_pick((uint32_t)u == u0, v, lv[u]);
+                    lane_odd<0>(v, lone != 0);
+                    lone &= lone - 1;
+                }
+                arrivals();
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) out[u] = bitsd(kKllInfBits);
+            }
+        }
+        if ((ci & 1u) == 0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pend1[u] = out[u];
+            cp1 = c0;
+        } else {
+            double z[16], y[8];
+            uint32_t cy;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                z[u] = pend1[u];
+                z[8 + u] = out[u];
+            }
+            kll_sort16(z);
+            lane_level<1>(z, cp1 + c0, kT_L1, ci >> 1, y, cy);
+            arrivals();
+            if (((ci >> 1) & 1u) == 0) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) pend2[u] = y[u];
+                cp2 = cy;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    z[u] = pend2[u];
+                    z[8 + u] = y[u];
+                }
+                kll_merge16(z);
+                lane_level<2>(z, cp2 + cy, kT_L2, ci >> 2, y, cy);
+                arrivals();
+                if (((ci >> 2) & 1u) == 0) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) pend3[u] = y[u];
+                    cp3 = cy;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        z[u] = pend3[u];
+                        z[8 + u] = y[u];
+                    }
+                    kll_merge16(z);
+                    lane_level<3>(z, cp3 + cy, kT_L3, ci >> 3, y, cy);
+                    arrivals();
+                    wave_stage(y, cy);
+                }
+            }
+        }
+        ++ci;
     }
 };
 
-__global__ __launch_bounds__(64) void k_kll_build(KllBuildArgs A) {
+// The streaming loop of stream_segment (ONE_SITE, one chunk in flight), run for npad chunks:
+// chunks past the segment's last are all NaN (the flush), and the head / tail slots ride the
+// last real chunk only.
+template <class Proc>
+__device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int64_t beg, int64_t end, int64_t npad,
+                                           Proc& proc, int lane) {
+    int64_t a0 = (beg + 1) & ~(int64_t)1;
+    if (a0 > end) a0 = end;
+    int64_t a1 = end & ~(int64_t)1;
+    if (a1 < a0) a1 = a0;
+    const double2* __restrict__ v2 = reinterpret_cast<const double2*>(vals);
+    const int64_t i0 = a0 >> 1;
+    const int64_t nunits = (a1 >> 1) - i0;
+    constexpr int CH = kUnroll * kWave;
+    const int64_t nfull = nunits / CH;
+    const bool head = a0 > beg, tail = a1 < end;
+    const int64_t nch = nfull + ((nunits - nfull * CH) > 0 || head || tail ? 1 : 0);
+    if (npad == 0) return;
+    const double2* __restrict__ p = v2 + i0 + lane;
+    const double qnan = __builtin_nan("");
+    double hv = qnan, tv = qnan;
+    if (head) hv = vals[beg];
+    if (tail) tv = vals[a1];
+    const double2* __restrict__ zp = g_zero_chunk + lane;
+    auto fill_u = [&](double2 (&c)[kUnroll], int64_t ci) {
+        if (ci < nfull) {
+            load_chunk(c, p + ci * CH);
+        } else {
+            const double2* zpl = zp;
+            int ln = lane;
+            asm volatile("" : "+v"(zpl), "+v"(ln));
+            const double2* q[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t j = ci * CH + u * kWave + ln;
+                q[u] = (ci < nch && j < nunits) ? v2 + i0 + j : zpl + u * kWave;
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) c[u] = load16(q[u]);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t j = ci * CH + u * kWave + ln;
+                if (j >= nunits) c[u] = make_double2(qnan, qnan);
+            }
+            if (lane == kWave - 1 && ci == nch - 1) {
+                c[kUnroll - 1].x = hv;
+                c[kUnroll - 1].y = tv;
+            }
+        }
+    };
+    double2 cur[kUnroll], nxt[kUnroll];
+    fill_u(nxt, 0);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        double x = nxt[u].x, y = nxt[u].y;
+        asm volatile("" : "+v"(x), "+v"(y));
+        cur[u] = make_double2(x, y);
+    }
+#pragma unroll 1
+    for (int64_t ci = 0; ci < npad; ++ci) {
+        fill_u(nxt, ci + 1);
+        proc.chunk(cur);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
+    }
+}
+
+// Level h's keys after the build (per-lane odd slots below 4: `has` / `kv` of this lane, the
+// wave slot, the run) plus `carry` (ascending, nc) gathered into ws, ascending; returns how many.
+__device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t h, bool has, double kv,
+                                     const uint64_t* carry, uint32_t nc, uint64_t* ws, int lane) {
+    const uint32_t a = (h >= (uint32_t)kKllFirstRun && (int)h < kKllFirstRun + nrl) ? uni32(sh.lens[h]) : 0u;
+    uint32_t m = 0, sources = 0;
+    if (a) {
+        const uint64_t* R = sh.lv + (size_t)(h - kKllFirstRun) * kKllRun;
+        for (uint32_t i = lane; i < a; i += kWave) ws[i] = R[i];
+        m = a;
+        ++sources;
+    }
+    if (nc) {
+        for (uint32_t i = lane; i < nc; i += kWave) ws[m + i] = carry[i];
+        m += nc;
+        ++sources;
+    }
+    const uint64_t km = ballot(has);
+    if (km) {
+        if (has) ws[m + lane_prefix(km)] = dbits(kv);
+        m += popc64(km);
+        sources += 2;  // unsorted
+    }
+    if ((uni32(sh.misc[0]) >> h) & 1u) {
+        if (lane == 0) ws[m] = sh.wk[h];
+        m += 1;
+        ++sources;
+    }
+    __syncthreads();
+    if (sources > 1) kll_lds_sort(ws, m, lane);
+    return m;
+}
+
+__global__ __launch_bounds__(64, 2) void k_kll_build(KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
-    KllState K;
-    K.tmp = reinterpret_cast<uint64_t*>(smem);
-    K.lv = K.tmp + 2 * kKllRun;
-    K.lens = reinterpret_cast<uint32_t*>(K.lv + (size_t)(A.levels - (int)kKllFirst + 1) * kKllRun);
-    K.cnt = K.lens + kKllLevels;
-    K.seed = A.seed;
-    K.slice = A.slice;
-    K.lane = lane;
-    const uint32_t RW = (uint32_t)(kKllHdr + A.budget);
-    const int blk = lane >> 5;                 // this lane's level-0 block
-    const uint32_t bpos = (uint32_t)(lane & 31) * 16u;  // its first position in the block
+    KllShared sh;
+    sh.lv = reinterpret_cast<uint64_t*>(smem);
+    sh.tmp = sh.lv + (size_t)A.nrl * kKllRun;
+    sh.tb = sh.tmp + 2 * kKllRun;
+    sh.wk = sh.tb + A.tcap;
+    sh.lens = reinterpret_cast<uint32_t*>(sh.wk + kKllLevels);
+    sh.rcnt = sh.lens + kKllLevels;
+    sh.wcnt = sh.rcnt + kKllLevels;
+    sh.misc = sh.wcnt + kKllLevels;
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         if (lane < kKllLevels) {
-            K.lens[lane] = 0;
-            K.cnt[lane] = 0;
+            sh.lens[lane] = 0;
+            sh.rcnt[lane] = 0;
+            sh.wcnt[lane] = 0;
         }
+        if (lane < 2) sh.misc[lane] = 0;
         __syncthreads();
-        K.series = (uint64_t)(A.seg_base + s);
-        K.sum_w2 = 0;
-        K.overflow = 0;
-        const bool whole = kll_nchunks(beg, end) <= 1;  // one chunk: kept exactly if it fits the budget
+        const uint64_t series = (uint64_t)(A.seg_base + s);
         uint64_t* row = A.rows + (size_t)s * RW;
-
-        struct Proc {  // by value: nothing here is address-taken (no scratch)
-            KllState K;
-            int budget, levels;
-            uint64_t* row;
-            int lane, blk;
-            uint32_t bpos;
-            bool whole;
-            uint32_t nan_l, pres_l;
-            uint32_t c_whole[2];
-            double kmin, kmax;   // NaN until a present sample
-            bool have;           // a level-1 run is pending in pend (wave-uniform)
-            uint32_t cpend;      // its present keys
-            uint32_t ci;         // chunks seen
-            uint64_t pend[8];
-            __device__ void chunk(const double2 (&c)[kUnroll]) {
-                uint64_t x[16];
-                uint32_t valid = 0;
+        const int64_t nch = kll_nchunks(beg, end);
+        const int64_t npad = (nch + 7) & ~(int64_t)7;
+        KllProc P;
+        P.sh = sh;
+        P.base = kll_slice_base(A.seed, series, A.slice);
+        P.w2u = 0;
+        P.ci = 0;
+        P.lane = lane;
+        P.nrl = A.nrl;
+        P.tail = tail;
+        P.tcap = A.tcap;
+        P.ts = KllTail{0u, 0u, 0.0};
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const double d = slot_val(c, j);
-                    const bool nan = __builtin_isnan(d);
-                    const double v = d == 0.0 ? 0.0 : d;  // -0 -> +0
-                    x[j] = nan ? kKllAbsent : dbits(v);
-                    valid += nan ? 0u : 1u;
-                    kmin = fmin(kmin, d == 0.0 ? 0.0 : d);  // fmin / fmax skip NaN
-                    kmax = fmax(kmax, d == 0.0 ? 0.0 : d);
-                }
-                nan_l += 16u - valid;
-                pres_l += valid;
-                if (whole) {  // the only chunk: kept whole if it fits the budget
-                    // present keys per block (lanes 0-31 / 32-63)
-                    const uint32_t incl = wave_scan32(valid, 0u, OpAdd32{});
-                    const uint32_t c0 = lane_bcast32(incl, 31), c1 = lane_bcast32(incl, kWave - 1) - c0;
-                    c_whole[0] = c0;
-                    c_whole[1] = c1;
-                    if (c0 + c1 <= (uint32_t)budget) {  // level 0, block 0's keys then block 1's, sorted
-                        kll_sort_blocks(x, lane);
-                        const uint32_t base = blk ? c0 : 0u, cb = blk ? c1 : c0;
+        for (int u = 0; u < 8; ++u) P.pend1[u] = P.pend2[u] = P.pend3[u] = bitsd(kKllInfBits);
+        P.cp1 = P.cp2 = P.cp3 = 0;
 #pragma unroll
-                        for (int i = 0; i < 16; ++i)
-                            if (bpos + (uint32_t)i < cb) row[kKllHdr + base + bpos + i] = x[i];
-                        return;
-                    }
-                }
-                // level 0 (per lane): sort the lane's 16 slots, keep every other from a coin
-                kll_sort16(x);
-                const uint32_t off = kll_coin(K.seed, K.series, K.slice, kKllLane0 + lane, ci);
-                uint64_t y[8];
-#pragma unroll
-                for (int m = 0; m < 8; ++m) y[m] = off ? x[2 * m + 1] : x[2 * m];  // NaN keys stay past cy
-                const uint32_t cy = valid > off ? (valid - off + 1) >> 1 : 0u;
-                K.sum_w2 += popc64(ballot(valid > 0));
-                if (!have) {
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) pend[m] = y[m];
-                    cpend = cy;
-                    have = true;
-                } else {  // level 1 (per lane): merge with the pending run, compact
-                    uint64_t z[16];
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) {
-                        z[m] = pend[m];
-                        z[8 + m] = y[m];
-                    }
-                    kll_merge16(z);
-                    const uint32_t cz = cpend + cy;
-                    const uint32_t off1 = kll_coin(K.seed, K.series, K.slice, kKllLane1 + lane, ci >> 1);
-                    uint64_t y2[8];
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) y2[m] = off1 ? z[2 * m + 1] : z[2 * m];
-                    K.sum_w2 += 4ull * popc64(ballot(cz > 0));
-                    have = false;
-                    K.wave_stage(y2, cz > off1 ? (cz - off1 + 1) >> 1 : 0u, levels);
-                }
-                ++ci;
-            }
-        } P{K, A.budget, A.levels, row, lane, blk, bpos, whole, 0u, 0u, {0u, 0u}, bitsd(kQuietNaN), bitsd(kQuietNaN),
-            false, 0u, 0u, {}};
-
-        const uint32_t pad = stream_segment<true>(A.vals, beg, end, P, lane);
-        if (P.have) {  // an odd last chunk: its level-1 run is compacted alone
-            const uint32_t off1 = kll_coin(P.K.seed, P.K.series, P.K.slice, kKllLane1 + lane, P.ci >> 1);
-            uint64_t y2[8];
-#pragma unroll
-            for (int m = 0; m < 8; ++m) y2[m] = (m < 4) ? (off1 ? P.pend[2 * m + 1] : P.pend[2 * m]) : kKllAbsent;
-            P.K.sum_w2 += 4ull * popc64(ballot(P.cpend > 0));
-            P.K.wave_stage(y2, P.cpend > off1 ? (P.cpend - off1 + 1) >> 1 : 0u, A.levels);
+        for (int h = 0; h < 4; ++h) {
+            P.K[h] = 0.0;
+            P.kcnt[h] = 0;
         }
-        K = P.K;
-        const uint32_t nan_l = P.nan_l, pres_l = P.pres_l, c_whole[2] = {P.c_whole[0], P.c_whole[1]};
-        const uint64_t n_nan = (uint64_t)wave_sum_u32(nan_l) - pad;
-        const uint64_t n_pres = wave_sum_u32(pres_l);
+        P.kmask = 0;
+        P.arr = 0.0;
+        P.has_arr = false;
+        P.w2l = 0;
+        P.pres = 0;
+        P.kmin = P.kmax = bitsd(kQuietNaN);
+        kll_stream(A.vals, beg, end, npad, P, lane);
+
+        const uint32_t kmask = P.kmask;
+        const double K0[4] = {P.K[0], P.K[1], P.K[2], P.K[3]};
+        const uint64_t n_pres = lane_bcast64(wave_scan64((uint64_t)P.pres, 0ull, OpAdd64{}), kWave - 1);
+        const uint64_t w2lanes = lane_bcast64(wave_scan64((uint64_t)P.w2l, 0ull, OpAdd64{}), kWave - 1);
         const uint64_t gmin = lane_bcast64(wave_scan64(dbits(P.kmin), kQuietNaN, OpMinF64Bits{}), kWave - 1);
         const uint64_t gmax = lane_bcast64(wave_scan64(dbits(P.kmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1);
-        const bool exact0 = whole && c_whole[0] + c_whole[1] <= (uint32_t)A.budget;
-        // final compression: the lowest run alone, until the budget holds
-        if (!exact0) {
-#pragma unroll 1
-            while (true) {
-                uint32_t total = 0, low = 0;
-#pragma unroll 1
-                for (int h = A.levels; h >= (int)kKllFirst; --h) {
-                    const uint32_t l = uni32(K.lens[h]);
-                    total += l;
-                    low = l ? (uint32_t)h : low;
-                }
-                if (total <= (uint32_t)A.budget || low == 0 || K.overflow) break;
-                const uint32_t a = uni32(K.lens[low]);
-                const uint32_t c = uni32(K.cnt[low]);
-                const uint32_t off = kll_coin(K.seed, K.series, K.slice, low, c);
-                const uint64_t* L = K.run(low);
-                uint64_t keep[kKllRun / kWave / 2];
-#pragma unroll
-                for (int q = 0; q < kKllRun / kWave / 2; ++q) {
-                    const uint32_t p = off + 2u * ((uint32_t)lane + (uint32_t)q * kWave);  // output index -> position
-                    keep[q] = p < a ? L[p] : 0ull;
-                }
-                K.sum_w2 += (uint64_t)1 << (2 * low);
-                __syncthreads();
-                const uint32_t t = a > off ? (a - off + 1) >> 1 : 0u;
-#pragma unroll
-                for (int q = 0; q < kKllRun / kWave / 2; ++q) {
-                    const uint32_t m = (uint32_t)lane + (uint32_t)q * kWave;
-                    if (m < t) K.tb(0)[m] = keep[q];
-                }
-                if (lane == 0) {
-                    K.lens[low] = 0;
-                    K.cnt[low] = c + 1;
-                }
-                __syncthreads();
-                K.push(0, t, low + 1, A.levels);
-            }
+
+        // tail: the min(n, tail) largest present keys, ascending
+        uint32_t tl_out = 0;
+        if (tail) {
+            KllTail ts = P.ts;
+            if (ts.tl > tail + kKllTailSlack) ts = kll_tail_refresh(sh, ts, tail, lane);
+            kll_lds_sort(sh.tb, ts.tl, lane);
+            tl_out = ts.tl < tail ? ts.tl : tail;
+            for (uint32_t i = lane; i < tl_out; i += kWave) row[kKllHdr + budget + i] = sh.tb[ts.tl - tl_out + i];
+            __syncthreads();
         }
-        // export: header, then the runs in level order
-        uint64_t wtot = 0, lw0 = 0, lw1 = 0, lw2 = 0, lw3 = 0;  // run lengths, u16 x 4 per word
-        uint32_t pos = 0;
-        if (exact0) {
-            wtot = c_whole[0] + c_whole[1];
-            lw0 = wtot;
-            pos = (uint32_t)wtot;
-        } else {
+
+        // body: from level 0 up, while more than `budget` keys remain, compact each level of
+        // >= 2 keys once (odd largest set aside) into the next; export every level ascending
+        uint64_t* ws = sh.tb;                // level keys (<= 256 + carry + 64 + 1)
+        uint64_t* cbuf = sh.tb + 1024;       // carry (<= 512)
+        uint64_t total = 0;
 #pragma unroll 1
-            for (int h = (int)kKllFirst; h <= A.levels && h < kKllLevels; ++h) {
-                const uint32_t l = uni32(K.lens[h]);
-                if (!l) continue;
-                if (pos + l > (uint32_t)A.budget) {  // only after an overflow
-                    K.overflow = 1;
+        for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+            uint32_t n_h = 0;
+            if (h < 4) n_h = popc64(ballot((kmask >> h) & 1u));
+            if (h >= (uint32_t)kKllFirstRun && (int)h < kKllFirstRun + A.nrl) n_h += uni32(sh.lens[h]);
+            n_h += (uni32(sh.misc[0]) >> h) & 1u;
+            total += n_h;
+        }
+        uint32_t nc = 0, pos = 0;
+        uint64_t lw[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t weight = 0, w2f = 0;
+#pragma unroll 1
+        for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+            const bool has = h < 4 && ((kmask >> h) & 1u);
+            const double kv = h == 0 ? K0[0] : (h == 1 ? K0[1] : (h == 2 ? K0[2] : K0[3]));
+            const uint32_t m = kll_gather_level(sh, A.nrl, h, has, kv, cbuf, nc, ws, lane);
+            uint32_t keep = m;  // keys exported at level h
+            nc = 0;
+            if (total > budget && m >= 2) {
+                if (h + 1 >= (uint32_t)kKllLevels) {
+                    if (lane == 0) sh.misc[1] = 1;
+                    __syncthreads();
                     break;
                 }
-                const uint64_t* L = K.run((uint32_t)h);
-                for (uint32_t i = lane; i < l; i += kWave) row[kKllHdr + pos + i] = L[i];
-                pos += l;
-                wtot += (uint64_t)l << h;
-                const uint64_t f = (uint64_t)l << (16 * (h & 3));
-                lw0 |= (h >> 2) == 0 ? f : 0ull;
-                lw1 |= (h >> 2) == 1 ? f : 0ull;
-                lw2 |= (h >> 2) == 2 ? f : 0ull;
-                lw3 |= (h >> 2) == 3 ? f : 0ull;
+                const uint32_t me = m & ~1u;
+                const uint32_t off = kll_coin32(P.base, kT_FINAL + h, 0) & 1u;
+                for (uint32_t k = lane; k < (me >> 1); k += kWave) cbuf[k] = ws[off + 2 * k];
+                nc = me >> 1;
+                w2f += 1ull << (2 * h);
+                total -= me - nc;
+                keep = m - me;  // the set-aside key, ws[m - 1]
+                if (keep && lane == 0) ws[0] = ws[m - 1];
+                __syncthreads();
             }
+            if (keep) {
+                if (pos + keep > budget) {  // only after an overflow
+                    if (lane == 0) sh.misc[1] = 1;
+                    __syncthreads();
+                    break;
+                }
+                for (uint32_t i = lane; i < keep; i += kWave) row[kKllHdr + pos + i] = ws[i];
+                pos += keep;
+                weight += (uint64_t)keep << h;
+                lw[h >> 2] |= (uint64_t)keep << (16 * (h & 3));
+            }
+            __syncthreads();
         }
+        const bool overflow = uni32(sh.misc[1]) != 0;
+        for (uint32_t i = pos + lane; i < budget; i += kWave) row[kKllHdr + i] = 0;  // canonical rows: unused words 0
+        for (uint32_t i = tl_out + lane; i < tail; i += kWave) row[kKllHdr + budget + i] = 0;
         if (lane == 0) {
             row[0] = n_pres;
-            row[1] = A.gaps ? 0ull : n_nan;
+            row[1] = A.gaps ? 0ull : (uint64_t)(end - beg) - n_pres;
             row[2] = n_pres ? gmin : kQuietNaN;
             row[3] = n_pres ? gmax : kQuietNaN;
-            row[4] = lw0;
-            row[5] = lw1;
-            row[6] = lw2;
-            row[7] = lw3;
-            row[8] = K.overflow ? ~0ull : K.sum_w2;
-            row[9] = wtot;
+            row[4] = P.w2u + w2lanes + w2f;
+            row[5] = weight;
+            row[6] = tl_out;
+            row[7] = ((uint64_t)budget << 32) | tail;
+#pragma unroll
+            for (int w = 0; w < 6; ++w) row[8 + w] = lw[w];
+            row[14] = 0;
+            row[15] = overflow ? kKllRowOverflow : 0ull;
         }
         __syncthreads();
     }
 }
 
-struct KllQueryArgs {
+// ---------------------------------------------------------------------------------------------
+// Fold / merge / query.  A row image in LDS: header, body, tail words exactly as in memory.
+
+__device__ __forceinline__ uint32_t kll_len(const uint64_t* row, uint32_t h) {
+    return (uint32_t)(row[8 + (h >> 2)] >> (16 * (h & 3))) & 0xFFFFu;
+}
+
+__device__ void kll_copy_row(const uint64_t* src, uint64_t* dst, uint32_t RW, int lane) {
+    for (uint32_t i = lane; i < RW; i += kWave) dst[i] = src[i];
+    __syncthreads();
+}
+
+// Three ascending lists merged into O (A, then C, then K among equal keys).
+__device__ void kll_merge3(const uint64_t* A, uint32_t na, const uint64_t* C, uint32_t nc, const uint64_t* K,
+                           uint32_t nk, uint64_t* O, int lane) {
+#pragma unroll 1
+    for (uint32_t i = lane; i < na; i += kWave) {
+        const double x = bitsd(A[i]);
+        O[i + kll_bound<true>(C, nc, x) + kll_bound<true>(K, nk, x)] = A[i];
+    }
+#pragma unroll 1
+    for (uint32_t j = lane; j < nc; j += kWave) {
+        const double x = bitsd(C[j]);
+        O[j + kll_bound<false>(A, na, x) + kll_bound<true>(K, nk, x)] = C[j];
+    }
+#pragma unroll 1
+    for (uint32_t k = lane; k < nk; k += kWave) {
+        const double x = bitsd(K[k]);
+        O[k + kll_bound<false>(A, na, x) + kll_bound<false>(C, nc, x)] = K[k];
+    }
+    __syncthreads();
+}
+
+// O = fold(A, C): A, C, O row images in LDS (the same budget / tail cap); S scratch
+// (>= 3 budget keys), CB carry (>= 2 budget keys).  Coins: (base, kT_FOLD + h, idx).
+__device__ void kll_fold(const uint64_t* A, const uint64_t* C, uint64_t* O, uint64_t* S, uint64_t* CB, uint64_t base,
+                         uint32_t idx, uint32_t budget, uint32_t tail, int lane) {
+    const uint64_t na = A[0], ncn = C[0];
+    const uint32_t ta = (uint32_t)A[6], tc = (uint32_t)C[6];
+    const uint64_t n = na + ncn;
+    const uint32_t tn = (uint64_t)tail < n ? tail : (uint32_t)n;  // min(tail, n) <= ta + tc
+    // tail: the tn largest of the union (merged positions >= ta + tc - tn)
+    {
+        const uint64_t* X = A + kKllHdr + budget;
+        const uint64_t* Y = C + kKllHdr + budget;
+        uint64_t* Z = O + kKllHdr + budget;
+        const uint32_t drop = ta + tc - tn;
+        for (uint32_t i = lane; i < ta; i += kWave) {
+            const uint32_t p = i + kll_bound<true>(Y, tc, bitsd(X[i]));
+            if (p >= drop) Z[p - drop] = X[i];
+        }
+        for (uint32_t j = lane; j < tc; j += kWave) {
+            const uint32_t p = j + kll_bound<false>(X, ta, bitsd(Y[j]));
+            if (p >= drop) Z[p - drop] = Y[j];
+        }
+    }
+    // body
+    uint64_t total = 0;
+    for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) total += kll_len(A, h) + kll_len(C, h);
+    uint32_t offA = 0, offC = 0, pos = 0, ncarry = 0;
+    uint64_t lw[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t weight = 0, w2 = 0;
+    bool bad = (A[15] | C[15]) != 0;
+#pragma unroll 1
+    for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+        const uint32_t la = kll_len(A, h), lc = kll_len(C, h);
+        kll_merge3(A + kKllHdr + offA, la, C + kKllHdr + offC, lc, CB, ncarry, S, lane);
+        offA += la;
+        offC += lc;
+        const uint32_t m = la + lc + ncarry;
+        uint32_t keep = m;
+        ncarry = 0;
+        if (total > budget && m >= 2) {
+            if (h + 1 >= (uint32_t)kKllLevels) {
+                bad = true;
+                break;
+            }
+            const uint32_t me = m & ~1u;
+            const uint32_t off = kll_coin32(base, kT_FOLD + h, idx) & 1u;
+            for (uint32_t k = lane; k < (me >> 1); k += kWave) CB[k] = S[off + 2 * k];
+            ncarry = me >> 1;
+            w2 += 1ull << (2 * h);
+            total -= me - ncarry;
+            keep = m - me;
+            if (keep && lane == 0) S[0] = S[m - 1];
+            __syncthreads();
+        }
+        if (keep) {
+            if (pos + keep > budget) {
+                bad = true;
+                break;
+            }
+            for (uint32_t i = lane; i < keep; i += kWave) O[kKllHdr + pos + i] = S[i];
+            pos += keep;
+            weight += (uint64_t)keep << h;
+            lw[h >> 2] |= (uint64_t)keep << (16 * (h & 3));
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = pos + lane; i < budget; i += kWave) O[kKllHdr + i] = 0;  // canonical rows: unused words 0
+    for (uint32_t i = tn + lane; i < tail; i += kWave) O[kKllHdr + budget + i] = 0;
+    if (lane == 0) {
+        O[0] = n;
+        O[1] = A[1] + C[1];
+        O[2] = dbits(fmin(bitsd(A[2]), bitsd(C[2])));  // fmin / fmax: the non-NaN operand wins
+        O[3] = dbits(fmax(bitsd(A[3]), bitsd(C[3])));
+        O[4] = A[4] + C[4] + w2;
+        O[5] = weight;
+        O[6] = tn;
+        O[7] = A[7];
+#pragma unroll
+        for (int w = 0; w < 6; ++w) O[8 + w] = lw[w];
+        O[14] = 0;
+        O[15] = (bad || A[7] != C[7]) ? kKllRowOverflow : 0ull;
+    }
+    __syncthreads();
+}
+
+struct KllMergeArgs {
     int64_t S;
-    int32_t W;        // rows per series (time slices)
-    int32_t budget;
-    const uint64_t* rows;  // [S][W][kKllHdr + budget]
-    int32_t mode;
+    int32_t W;
+    int32_t budget, tail;
+    uint32_t epoch;
+    uint64_t seed;
+    int64_t series_base;
+    const uint64_t* rows;  // [S][W][RW]
+    uint64_t* out;         // [S][RW] (merge)
+    int32_t mode;          // query
     int64_t p_num, p_den;
     double q;
     double* out_v;
@@ -569,64 +1106,77 @@ struct KllQueryArgs {
     uint32_t* out_f;
 };
 
-// Smallest key K with (weighted count of keys <= K) * n > r * wtot (an item's key).
-__device__ uint64_t kll_select(const uint64_t* key, const uint8_t* lvl, uint32_t m, uint64_t r, uint64_t n,
-                               uint64_t wtot, int lane) {
-    uint64_t lo = 0, hi = kKllNanKey;
+// The series' W rows folded left to right into the image returned (LDS).
+__device__ uint64_t* kll_fold_rows(const KllMergeArgs& A, int64_t s, unsigned char* smem, int lane) {
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
+    uint64_t* im0 = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* im1 = im0 + RW;
+    uint64_t* imc = im1 + RW;
+    uint64_t* S = imc + RW;
+    uint64_t* CB = S + 3 * (size_t)budget;
+    const uint64_t* rows = A.rows + (size_t)s * A.W * RW;
+    kll_copy_row(rows, im0, RW, lane);
+    const uint64_t base = kll_slice_base(A.seed, (uint64_t)(A.series_base + s), A.epoch);
+#pragma unroll 1
+    for (int w = 1; w < A.W; ++w) {
+        kll_copy_row(rows + (size_t)w * RW, imc, RW, lane);
+        kll_fold(im0, imc, im1, S, CB, base, (uint32_t)w, budget, tail, lane);
+        uint64_t* t = im0;
+        im0 = im1;
+        im1 = t;
+    }
+    return im0;
+}
+
+__global__ __launch_bounds__(64) void k_kll_merge(KllMergeArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const uint32_t RW = (uint32_t)kKllHdr + (uint32_t)A.budget + (uint32_t)A.tail;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const uint64_t* im = kll_fold_rows(A, s, smem, lane);
+        uint64_t* o = A.out + (size_t)s * RW;
+        for (uint32_t i = lane; i < RW; i += kWave) o[i] = im[i];
+        __syncthreads();
+    }
+}
+
+// Smallest body key K with (weight of body keys <= K) > r: bisection of the 64-bit
+// order-preserving key space over the image's keys.
+__device__ uint64_t kll_body_select(const uint64_t* im, const uint8_t* lvl, uint32_t m, uint64_t r, int lane) {
+    uint64_t lo = 0, hi = ~0ull;
 #pragma unroll 1
     while (lo < hi) {
         const uint64_t mid = lo + ((hi - lo) >> 1);
         uint64_t c = 0;
-        for (uint32_t i = lane; i < m; i += kWave) c += key[i] <= mid ? (uint64_t)1 << lvl[i] : 0ull;
+        for (uint32_t i = lane; i < m; i += kWave) c += okey(im[kKllHdr + i]) <= mid ? (uint64_t)1 << lvl[i] : 0ull;
         c = lane_bcast64(wave_scan64(c, 0ull, OpAdd64{}), kWave - 1);
-        const bool ok = (unsigned __int128)c * n > (unsigned __int128)r * wtot;
-        lo = ok ? lo : mid + 1;
-        hi = ok ? mid : hi;
+        lo = c > r ? lo : mid + 1;
+        hi = c > r ? mid : hi;
     }
     return lo;
 }
 
-__global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
+__global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
-    const uint32_t RW = (uint32_t)(kKllHdr + A.budget);
-    uint64_t* key = reinterpret_cast<uint64_t*>(smem);
-    uint8_t* lvl = reinterpret_cast<uint8_t*>(key + (size_t)A.W * A.budget);
+    const uint32_t budget = (uint32_t)A.budget;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + (uint32_t)A.tail;
+    uint8_t* lvl = reinterpret_cast<uint8_t*>(reinterpret_cast<uint64_t*>(smem) + 3 * (size_t)RW + 5 * (size_t)budget);
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        const uint64_t* rows = A.rows + (size_t)s * A.W * RW;
-        uint64_t n = 0, nan = 0, wtot = 0;
-        double mn = bitsd(kQuietNaN), mx = bitsd(kQuietNaN);
-        bool bad = false;
+        const uint64_t* im = kll_fold_rows(A, s, smem, lane);
+        const uint64_t n = im[0], nan = im[1];
+        const uint32_t tl = (uint32_t)im[6];
         uint32_t m = 0;
-#pragma unroll 1
-        for (int w = 0; w < A.W; ++w) {
-            const uint64_t* row = rows + (size_t)w * RW;
-            n += row[0];
-            nan += row[1];
-            mn = fmin(mn, bitsd(row[2]));
-            mx = fmax(mx, bitsd(row[3]));
-            bad = bad || row[8] == ~0ull;
-            wtot += row[9];
-            uint32_t pos = 0;
-#pragma unroll 1
-            for (int h = 0; h < kKllLevels; ++h) {
-                const uint32_t l = (uint32_t)(row[4 + (h >> 2)] >> (16 * (h & 3))) & 0xFFFFu;
-                if (pos + l > (uint32_t)A.budget) {  // not a row krr_kll_build wrote: never stage past it
-                    bad = true;
-                    break;
-                }
-                for (uint32_t i = lane; i < l; i += kWave) {
-                    key[m + i] = okey(row[kKllHdr + pos + i]);  // f64 bits -> order-preserving
-                    lvl[m + i] = (uint8_t)h;
-                }
-                pos += l;
-                m += l;
-            }
+        for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+            const uint32_t l = kll_len(im, h);
+            for (uint32_t i = lane; i < l; i += kWave) lvl[m + i] = (uint8_t)h;
+            m += l;
         }
         __syncthreads();
         uint32_t flags = 0;
         double result = bitsd(kQuietNaN);
-        if (bad) {
+        if (im[15] != 0 || im[7] != (((uint64_t)budget << 32) | (uint32_t)A.tail)) {
             flags = KRR_FLAG_CAPACITY;
         } else if (nan) {
             flags = KRR_FLAG_NAN;
@@ -657,11 +1207,10 @@ __global__ __launch_bounds__(64) void k_kll_query(KllQueryArgs A) {
                     v[1] = v[0];
                     continue;
                 }
-                // every kept key compacted away (a few samples spread over several chunks):
-                // only the exact min / max remain
-                v[qi] = r == 0 ? mn : (r == n - 1 ? mx : (wtot == 0 ? (2 * r < n ? mn : mx)
-                                                                     : bitsd(okey_inv(kll_select(key, lvl, m, r, n,
-                                                                                                 wtot, lane)))));
+                if (r == 0) v[qi] = bitsd(im[2]);
+                else if (r == n - 1) v[qi] = bitsd(im[3]);
+                else if (n - r <= tl) v[qi] = bitsd(im[kKllHdr + budget + tl - (n - r)]);
+                else v[qi] = bitsd(okey_inv(kll_body_select(im, lvl, m, r, lane)));
             }
             result = A.mode == KRR_PCT_SORTED_LOWER ? v[0] : np_lerp(v[0], v[1], gamma);
         }

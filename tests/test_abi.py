@@ -56,7 +56,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_abi_version_and_null_handling(lib):
-    assert lib.krr_abi_version() == 1
+    assert lib.krr_abi_version() == 2
     assert lib.krr_last_error(None) == b"null krr_ctx"
     assert lib.krr_segmented_percentile(None, None, None, None, None, None, None) == -1
     assert lib.krr_segmented_max(None, None, None, None, None, None) == -1

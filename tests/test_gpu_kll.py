@@ -1,10 +1,13 @@
-"""GPU: the KLL-style compactor sketch (krr_kll_build / krr_kll_query) through the C ABI.
+"""GPU: the KLL sketch, row format 2 (krr_kll_build / krr_kll_merge / krr_kll_query) through the
+C ABI.
 
-Rows and answers are compared bit for bit with the CPU restatement (oracle/kll_ref.py:
-the same blocks, coins, merge/carry order and query rule); at full config-5 length the
-answers' rank errors, measured against the exact order statistics, stay within the
+Rows, folded rows and answers are compared bit for bit with the CPU restatement
+(oracle/kll_ref.py: the same pairings, coins, level steps, set-asides, tail, final
+compression, fold and query rule).  At full config-5 length the answers are checked against
+exact order statistics: top ranks inside the exact tail have no error at all (p99 of 172,800
+samples folded from 64 slices — VERDICT r3 item 1), and body answers stay within the
 data-independent bound the rows carry (krr_amd.core.sketch.kll_rank_bound), on the data
-shapes where the log-linear histogram has no rank bound (low dispersion, quantised)."""
+shapes where a value-binned sketch has no rank bound (low dispersion, quantised, sorted)."""
 from decimal import Decimal
 
 import numpy as np
@@ -46,82 +49,140 @@ def _fleet(rng, lens):
     return offs, x
 
 
-LENS = [0, 1, 2, 3, 300, 511, 512, 513, 1023, 1024, 1025, 1026, 2047, 2048, 5000, 9999, 20_160, 43_200]
+LENS = [0, 1, 2, 3, 300, 511, 512, 513, 1023, 1024, 1025, 1026, 2047, 2048, 5000, 8191, 8193, 9999, 20_160,
+        43_200]
 
 
-def _rows(ctx, x, offs, gaps, budget=512, slice_id=0, seg_base=0):
+def _cfg(budget=512, tail=0):
+    from krr_amd.core import sketch
+
+    return sketch.KllConfig(budget=budget, tail=tail, seed=SEED)
+
+
+def _rows(ctx, x, offs, gaps, budget=512, tail=0, slice_id=0, seg_base=0):
     import torch
 
     from krr_amd.core import sketch
 
-    cfg = sketch.KllConfig(budget=budget, seed=SEED)
+    cfg = _cfg(budget, tail)
     ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, gaps)
     rows = sketch.kll_build(ctx, ser, cfg, slice_id=slice_id, seg_base=seg_base)
     torch.cuda.synchronize()
     return cfg, rows.cpu().numpy().view(np.uint64)
 
 
-def _check_rows(got, x, offs, gaps, budget, slice_id=0, seg_base=0):
+def _check_rows(got, x, offs, gaps, budget, tail, slice_id=0, seg_base=0):
     for s in range(offs.size - 1):
-        want = R.build_row(x, int(offs[s]), int(offs[s + 1]), budget=budget, seed=SEED, series=seg_base + s,
-                           slc=slice_id, gaps=gaps)
-        used = R.HDR + sum((int(want[4 + (h >> 2)]) >> (16 * (h & 3))) & 0xFFFF for h in range(16))
-        assert np.array_equal(got[s, :used], want[:used]), (s, int(offs[s + 1] - offs[s]),
-                                                           got[s, :R.HDR].tolist(), want[:R.HDR].tolist())
+        want = R.build_row(x, int(offs[s]), int(offs[s + 1]), budget=budget, tail=tail, seed=SEED,
+                           series=seg_base + s, slc=slice_id, gaps=gaps)
+        assert np.array_equal(got[s], want), (s, int(offs[s + 1] - offs[s]), got[s, :R.HDR].tolist(),
+                                              want[:R.HDR].tolist())
 
 
 @pytest.mark.parametrize("gaps", [False, True])
-@pytest.mark.parametrize("budget", [256, 512, 1024])
-def test_rows_match_restatement(ctx, gaps, budget):
-    rng = np.random.default_rng(budget + gaps)
+@pytest.mark.parametrize("budget,tail", [(256, 0), (512, 64), (1024, 1792)])
+def test_rows_match_restatement(ctx, gaps, budget, tail):
+    rng = np.random.default_rng(budget + gaps + tail)
     lens = rng.permutation(np.array(LENS * 2))
     offs, x = _fleet(rng, lens)
     if gaps:
         x[rng.random(x.size) < 0.15] = np.nan
-    _, got = _rows(ctx, x, offs, gaps, budget=budget, seg_base=17)
-    _check_rows(got, x, offs, gaps, budget, seg_base=17)
+    _, got = _rows(ctx, x, offs, gaps, budget=budget, tail=tail, seg_base=17)
+    _check_rows(got, x, offs, gaps, budget, tail, seg_base=17)
 
 
-def test_odd_offsets_and_heads(ctx):
-    """Segments starting at odd slots (stream_segment's head/tail slots) and one long
-    segment whose level counter carries to the top."""
+def test_odd_offsets_heads_and_long_carry(ctx):
+    """Segments starting at odd slots (stream_segment's head/tail slots) and long segments
+    whose run counter carries to the top."""
     rng = np.random.default_rng(5)
-    lens = np.array([3, 1025, 7, 1027, 1, 172_801, 2049])
+    lens = np.array([3, 1025, 7, 1027, 1, 172_801, 2049, 70_001])
     offs, x = _fleet(rng, lens)
-    _, got = _rows(ctx, x, offs, False)
-    _check_rows(got, x, offs, False, 512)
+    _, got = _rows(ctx, x, offs, False, tail=256)
+    _check_rows(got, x, offs, False, 512, 256)
 
 
-def _query(ctx, rows_u64, W, cfg, mode, p):
+@pytest.mark.parametrize("shape", ["increasing", "quantized", "decreasing", "runs_of_gaps"])
+def test_tail_refresh_paths_match_restatement(ctx, shape):
+    """Inputs that drive the tail buffer's refresh hard: sorted ascending (every key is a new
+    candidate), heavy ties around the cut (the tie-keeping rule), descending (one fill, no
+    refresh), and long gap runs."""
+    rng = np.random.default_rng(31)
+    lens = np.array([30_000, 12_345, 4_097, 65_536])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    parts = []
+    for n in lens:
+        if shape == "increasing":
+            parts.append(np.sort(rng.gamma(2.0, 0.05, n)))
+        elif shape == "decreasing":
+            parts.append(np.sort(rng.gamma(2.0, 0.05, n))[::-1])
+        elif shape == "quantized":
+            parts.append(rng.choice([0.1, 0.2, 0.3, 0.5], n, p=[0.5, 0.3, 0.15, 0.05]))
+        else:
+            v = rng.gamma(2.0, 0.05, n)
+            v[(np.arange(n) // 700) % 3 == 1] = np.nan
+            parts.append(v)
+    x = np.concatenate(parts)
+    gaps = shape == "runs_of_gaps"
+    for tail in (64, 1000, 2048):
+        _, got = _rows(ctx, x, offs, gaps, budget=512, tail=tail)
+        _check_rows(got, x, offs, gaps, 512, tail)
+
+
+def _query(ctx, rows_u64, W, cfg, mode, p, series_base=0, epoch=0):
     import torch
 
     from krr_amd.core import sketch
     from krr_amd.core.engine import percentile_params
 
     prm = percentile_params(Decimal(p), mode)
-    out = sketch.kll_query(ctx, _dev(rows_u64.view(np.int64), np.int64), W, cfg, prm)
+    out = sketch.kll_query(ctx, _dev(rows_u64.view(np.int64), np.int64), W, cfg, prm, series_base=series_base,
+                           epoch=epoch)
     torch.cuda.synchronize()
     return prm, {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def _slices(ctx, rng, lens, W, budget=512, tail=0):
+    """W time slices of every series built as separate launches (slice ids 0..W-1), rows
+    interleaved series-major as kll_exchange delivers them."""
+    S = lens.size
+    out = []
+    for w in range(W):
+        offs, x = _fleet(rng, np.maximum(lens // W, np.minimum(lens, 1)))
+        cfg, rows = _rows(ctx, x, offs, False, budget=budget, tail=tail, slice_id=w)
+        out.append(rows)
+    return cfg, np.stack(out, axis=1).reshape(S * W, -1)
+
+
+@pytest.mark.parametrize("W", [2, 5])
+@pytest.mark.parametrize("budget,tail", [(256, 64), (512, 1792)])
+def test_merge_matches_restatement(ctx, W, budget, tail):
+    import torch
+
+    from krr_amd.core import sketch
+
+    rng = np.random.default_rng(W * 100 + tail)
+    lens = np.array([0, 1, 5, 900, 3000, 20_000, 60_000, 1024, 4097, 172_800])
+    cfg, merged_in = _slices(ctx, rng, lens, W, budget, tail)
+    got = sketch.kll_merge(ctx, _dev(merged_in.view(np.int64), np.int64), W, cfg, series_base=40, epoch=3)
+    torch.cuda.synchronize()
+    got = got.cpu().numpy().view(np.uint64)
+    for s in range(lens.size):
+        want = R.merge_rows(merged_in[s * W:(s + 1) * W], seed=SEED, series=40 + s, epoch=3)
+        assert np.array_equal(got[s], want), (s, got[s, :R.HDR].tolist(), want[:R.HDR].tolist())
 
 
 @pytest.mark.parametrize("W", [1, 3])
 @pytest.mark.parametrize("mode,p", [("linear", "99"), ("sorted_lower", "99"), ("linear", "50"),
                                     ("sorted_lower", "95.5")])
 def test_query_matches_restatement(ctx, W, mode, p):
-    """W time slices of every series built as separate launches (slice ids 0..W-1), rows
-    interleaved series-major as kll_exchange delivers them, queried together."""
+    """krr_kll_query over W rows per series (folded in the kernel) == the restatement."""
     rng = np.random.default_rng(W * 10 + len(p))
     lens = np.array([0, 1, 5, 900, 3000, 20_000, 60_000, 1024, 4097])
-    S = lens.size
-    slices = []
-    for w in range(W):
-        offs, x = _fleet(rng, np.maximum(lens // W, np.minimum(lens, 1)))
-        cfg, rows = _rows(ctx, x, offs, False, slice_id=w)
-        slices.append(rows)
-    merged = np.stack(slices, axis=1).reshape(S * W, -1)
-    prm, out = _query(ctx, merged, W, cfg, mode, p)
-    for s in range(S):
-        v, n, f = R.query(merged[s * W:(s + 1) * W], prm.mode, prm.p_num, prm.p_den, prm.q)
+    cfg, merged = _slices(ctx, rng, lens, W, 512, 128)
+    prm, out = _query(ctx, merged, W, cfg, mode, p, series_base=7, epoch=2)
+    for s in range(lens.size):
+        v, n, f = R.query(merged[s * W:(s + 1) * W], prm.mode, prm.p_num, prm.p_den, prm.q, seed=SEED, series=7 + s,
+                          epoch=2)
         assert out["count"][s] == n and out["flags"][s] == f
         assert (np.isnan(v) and np.isnan(out["value"][s])) or out["value"][s] == v, (s, out["value"][s], v)
 
@@ -131,7 +192,7 @@ def test_short_series_exact_and_flags(ctx):
     lens = np.array([0, 1, 2, 100, 511])
     offs, x = _fleet(rng, lens)
     x[offs[3] + 4] = np.nan  # a NaN sample in the compact layout: KRR_FLAG_NAN
-    cfg, rows = _rows(ctx, x, offs, False)
+    cfg, rows = _rows(ctx, x, offs, False, tail=512)
     prm, out = _query(ctx, rows, 1, cfg, "linear", "99")
     assert out["flags"][0] == 4 and np.isnan(out["value"][0])
     assert out["flags"][3] == 1 and np.isnan(out["value"][3])
@@ -141,15 +202,17 @@ def test_short_series_exact_and_flags(ctx):
 
 
 @pytest.mark.parametrize("shape", ["gamma", "low_dispersion", "quantized", "increasing"])
-def test_full_length_rank_error_within_bound(ctx, shape):
-    """Config-5 length (172,800 samples) over 1 and 8 emulated time slices: the measured
-    rank error of p50/p90/p99 against the exact order statistic <= the rows' bound."""
+def test_full_length_folded_64_slices(ctx, shape):
+    """Config-5 length (172,800 samples) in 1, 8 and 64 time slices, folded into one row per
+    series: p99 (LINEAR and SORTED_LOWER) exact — value error 0, inside the exact tail;
+    p50 / p90 rank error of the body answers <= the rows' bound; folded rows bit-identical to
+    the restatement."""
     import torch
 
     from krr_amd.core import sketch
     from krr_amd.core.engine import percentile_params
 
-    T, S = 172_800, 64
+    T, S = 172_800, 32
     rng = np.random.default_rng({"gamma": 1, "low_dispersion": 2, "quantized": 3, "increasing": 4}[shape])
     if shape == "gamma":
         x = rng.gamma(2.0, 0.05, (S, T))
@@ -160,8 +223,8 @@ def test_full_length_rank_error_within_bound(ctx, shape):
     else:
         x = np.sort(rng.gamma(2.0, 0.05, (S, T)), axis=1)
     xs = np.sort(x, axis=1)
-    cfg = sketch.KllConfig(budget=512, seed=SEED)
-    for W in (1, 8):
+    cfg = sketch.KllConfig(budget=512, tail=sketch.KllConfig.tail_for(T, "99"), seed=SEED)
+    for W in (1, 8, 64):
         cuts = [T * w // W for w in range(W + 1)]
         parts = []
         for w in range(W):
@@ -169,13 +232,24 @@ def test_full_length_rank_error_within_bound(ctx, shape):
             offs = (np.arange(S + 1) * sl.shape[1]).astype(np.int64)
             ser = ctx.series(_dev(sl.ravel()), _dev(offs, np.int64), sl.shape[1], False)
             parts.append(sketch.kll_build(ctx, ser, cfg, slice_id=w))
-        merged = torch.stack(parts, dim=1).reshape(S * W, -1)
-        bound = sketch.kll_rank_bound(merged, W)
-        assert np.all(bound < (0.03 if W == 1 else 0.015))
-        for p in ("50", "90", "99"):
-            prm = percentile_params(Decimal(p), "sorted_lower")
-            out = sketch.kll_query(ctx, merged, W, cfg, prm)
+        stacked = torch.stack(parts, dim=1).reshape(S * W, -1)
+        row = sketch.kll_merge(ctx, stacked, W, cfg, epoch=5)
+        torch.cuda.synchronize()
+        if W == 64:  # the folded rows against the restatement, on a few series
+            st = stacked.cpu().numpy().view(np.uint64)
+            for s in (0, S - 1):
+                want = R.merge_rows(st[s * W:(s + 1) * W], seed=SEED, series=s, epoch=5)
+                assert np.array_equal(row[s].cpu().numpy().view(np.uint64), want), (shape, s)
+        bound = sketch.kll_rank_bound(row)
+        assert np.all(bound < 0.03), (shape, W, float(bound.max()))
+        for p, mode in (("99", "linear"), ("99", "sorted_lower"), ("50", "sorted_lower"), ("90", "sorted_lower")):
+            prm = percentile_params(Decimal(p), mode)
+            out = sketch.kll_query(ctx, row, 1, cfg, prm)
             v = out["value"].cpu().numpy()
+            if p == "99":
+                want = np.percentile(x, 99.0, axis=1) if mode == "linear" else xs[:, (T - 1) * 99 // 100]
+                assert np.array_equal(v, want), (shape, W, mode)  # exact: inside the tail
+                continue
             k = (T - 1) * int(p) // 100
             lt = np.array([np.searchsorted(xs[s], v[s], "left") for s in range(S)])
             le = np.array([np.searchsorted(xs[s], v[s], "right") for s in range(S)])
@@ -183,7 +257,9 @@ def test_full_length_rank_error_within_bound(ctx, shape):
             assert np.all(err <= bound), (shape, W, p, float(err.max()), float(bound.min()))
 
 
-def test_time_sharded_helper_world1(ctx):
+def test_time_sharded_helper_world1_on_a_side_stream(ctx):
+    """kll_time_sharded on a stream that is NOT the current one (advisor r3): every kernel and
+    copy is ordered on it."""
     import torch
 
     from krr_amd.core import sketch
@@ -192,31 +268,45 @@ def test_time_sharded_helper_world1(ctx):
     rng = np.random.default_rng(4)
     offs, x = _fleet(rng, np.array([10_080] * 8 + [0, 3]))
     ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, False)
-    cfg = sketch.KllConfig(budget=512, seed=SEED)
+    cfg = _cfg(512, 128)
     prm = percentile_params(Decimal("99"), "linear")
-    out = sketch.kll_time_sharded(ctx, ser, cfg, prm)
-    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    out = sketch.kll_time_sharded(ctx, ser, cfg, prm, stream=side)
+    side.synchronize()
     assert out["block"] == (0, 10) and out["rows_per_series"] == 1
     rows = out["rows"].cpu().numpy().view(np.uint64)
     for s in range(10):
+        want = R.build_row(x, int(offs[s]), int(offs[s + 1]), budget=512, tail=128, seed=SEED, series=s)
+        assert np.array_equal(rows[s], want)
         v, n, f = R.query(rows[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q)
         got = out["value"][s].item()
         assert out["count"][s].item() == n and (got == v or (np.isnan(got) and np.isnan(v)))
 
 
 def test_sparse_gapped_series_match_restatement(ctx):
-    """A few present samples spread over several chunks (NaN gaps), for many series: kept
-    keys may all be compacted away, and the answer then comes from the exact min / max."""
+    """A few present samples spread over several chunks (NaN gaps), no tail, for many series:
+    lone samples go through the odd slots; answers are real samples."""
     rng = np.random.default_rng(21)
     S, L = 64, 5000
     x = np.full(S * L, np.nan)
     for s in range(S):
-        idx = rng.choice(L, size=int(rng.integers(1, 6)), replace=False)
+        idx = rng.choice(L, size=int(rng.integers(1, 40)), replace=False)
         x[s * L + idx] = rng.gamma(2.0, 0.05, idx.size)
     offs = (np.arange(S + 1) * L).astype(np.int64)
-    cfg, rows = _rows(ctx, x, offs, True, budget=256)
-    _check_rows(rows, x, offs, True, 256)
+    cfg, rows = _rows(ctx, x, offs, True, budget=256, tail=0)
+    _check_rows(rows, x, offs, True, 256, 0)
     prm, out = _query(ctx, rows, 1, cfg, "sorted_lower", "50")
     for s in range(S):
         v, n, f = R.query(rows[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q)
         assert out["count"][s] == n and out["flags"][s] == f == 0 and out["value"][s] == v and np.isfinite(v)
+
+
+def test_alternating_gaps_drive_odd_slot_cascades(ctx):
+    """Every other slot absent: every slot pair holds one sample, so every key enters through
+    the per-lane odd slots and their cascades reach the wave level."""
+    rng = np.random.default_rng(8)
+    lens = np.array([40_000, 9_000, 1_500])
+    offs, x = _fleet(rng, lens)
+    x[::2] = np.nan
+    _, got = _rows(ctx, x, offs, True, budget=512, tail=64)
+    _check_rows(got, x, offs, True, 512, 64)

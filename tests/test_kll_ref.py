@@ -1,7 +1,9 @@
-"""The KLL-style sketch's specification on the CPU (oracle/kll_ref.py): short series are
-exact, and on every data shape the answer's rank error stays inside the data-independent
-bound the rows carry (krr_amd.core.sketch.kll_rank_bound).  The GPU kernel is compared
-with this model bit for bit in tests/test_gpu_kll.py."""
+"""The KLL sketch's specification on the CPU (oracle/kll_ref.py, row format 2): the schedule
+is deterministic (level sizes and sum w^2 depend on the presence pattern only), weight is
+conserved, the exact tail answers top ranks with no error, folds stay bounded, and on every
+data shape the body answers' rank error stays inside the bound the rows carry
+(krr_amd.core.sketch.kll_rank_bound).  The GPU kernels are compared with this model bit for
+bit in tests/test_gpu_kll.py."""
 from __future__ import annotations
 
 from decimal import Decimal
@@ -25,83 +27,162 @@ def _shapes(n: int, rng):
     }
 
 
-def _rank_error(x: np.ndarray, v: float, target: float) -> float:
+def _rank_error(x: np.ndarray, v: float, target: int) -> int:
     lt = int((x < v).sum())
     le = int((x <= v).sum())
-    return max(0.0, lt - target, target - (le - 1)) / x.size
+    return max(0, lt - target, target - (le - 1))
 
 
-@pytest.mark.parametrize("n", [1, 7, 300, 511, 512, 1023])
-def test_short_series_are_exact(n):
+def _q(rows, p, mode, **kw):
+    prm = percentile_params(Decimal(p), mode)
+    return M.query(rows, prm.mode, prm.p_num, prm.p_den, prm.q, **kw)
+
+
+@pytest.mark.parametrize("n", [1, 7, 300, 511, 512, 1023, 1025, 2000])
+def test_series_within_the_tail_are_exact(n):
     rng = np.random.default_rng(n)
     x = rng.gamma(2.0, 0.05, n)
-    row = M.build_row(x, 0, n, budget=1024)
-    assert int(row[9]) == n and int(row[8]) == 0  # kept whole: weight n, no compaction
-    for p, mode in (("99", "linear"), ("50", "sorted_lower"), ("95", "linear")):
-        prm = percentile_params(Decimal(p), mode)
-        v, cnt, fl = M.query(row[None], prm.mode, prm.p_num, prm.p_den, prm.q)
+    row = M.build_row(x, 0, n, budget=512, tail=2048, seed=5)
+    assert int(row[6]) == n and int(row[5]) == n  # tail holds everything; body weight == n
+    for p, mode in (("99", "linear"), ("50", "sorted_lower"), ("95", "linear"), ("0.1", "linear")):
+        v, cnt, fl = _q(row[None], p, mode)
         want = np.percentile(x, float(p)) if mode == "linear" else np.sort(x)[(n - 1) * int(p) // 100]
         assert cnt == n and fl == 0 and v == want
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 100, 1023, 1024, 1025, 8191, 8192, 8193, 20_000, 43_201])
+def test_weight_is_conserved_and_rows_are_bounded(n):
+    rng = np.random.default_rng(n + 1)
+    x = rng.gamma(2.0, 0.05, n)
+    row = M.build_row(x, 0, n, budget=256, tail=64, seed=3)
+    L = M.row_levels(row)
+    assert sum(l.size << h for h, l in enumerate(L)) == n == int(row[5])
+    assert sum(l.size for l in L) <= 256 and int(row[6]) == min(n, 64)
+    for l in L:
+        assert np.all(np.diff(l) >= 0)
+
+
+def test_schedule_is_deterministic():
+    """Item of VERDICT r3: the level sizes and sum w^2 depend on the presence pattern only —
+    not on the coins (seed, series, slice) and not on the values."""
+    rng = np.random.default_rng(1)
+    n = 50_000
+    gaps = rng.random(n) < 0.1
+    shapes = []
+    for k in range(4):
+        x = rng.gamma(2.0, 0.05, n) if k < 2 else rng.choice([0.1, 0.2], n)
+        x[gaps] = np.nan
+        row = M.build_row(x, 3, n - 2, budget=512, tail=128, seed=k, series=k * 7, slc=k, gaps=True)
+        shapes.append((int(row[4]), [l.size for l in M.row_levels(row)]))
+    assert all(s == shapes[0] for s in shapes)
+
+
 @pytest.mark.parametrize("shape", ["gamma", "low_dispersion", "quantized", "increasing", "decreasing", "constant",
                                    "signed"])
-@pytest.mark.parametrize("W", [1, 3])
-def test_rank_error_within_bound(shape, W):
-    rng = np.random.default_rng(7 + W)
+def test_body_rank_error_within_bound(shape):
+    rng = np.random.default_rng(7)
     n = 43_200
     x = _shapes(n, rng)[shape]
-    cuts = [n * w // W for w in range(W + 1)]
-    rows = np.stack([M.build_row(x, cuts[w], cuts[w + 1], budget=512, seed=11, series=3, slc=w)
+    for W in (1, 3, 8):
+        cuts = [n * w // W for w in range(W + 1)]
+        rows = np.stack([M.build_row(x, cuts[w], cuts[w + 1], budget=512, tail=64, seed=11, series=3, slc=w)
+                         for w in range(W)])
+        row = M.merge_rows(rows, seed=11, series=3, epoch=4)
+        assert int(row[0]) == n and int(row[5]) == n
+        bound = M.rank_bound(row, delta=0.01)
+        assert bound < 0.03
+        for p in ("10", "50", "90"):
+            v, cnt, fl = _q(row[None], p, "sorted_lower")
+            assert cnt == n and fl == 0
+            assert _rank_error(x, v, (n - 1) * int(p) // 100) <= bound * n, (shape, W, p)
+
+
+@pytest.mark.parametrize("shape", ["gamma", "low_dispersion", "quantized", "increasing"])
+def test_p99_exact_after_folding_64_slices(shape):
+    """172,800 samples in 64 slices folded into one row; p99 rank bound
+    <= 10% of the tail (here 0: the exact tail covers it) and value error <= 1% (here 0)."""
+    from krr_amd.core.sketch import KllConfig
+
+    rng = np.random.default_rng(99)
+    T = 172_800
+    x = _shapes(T, rng)[shape]
+    tail = KllConfig.tail_for(T, "99")
+    W = 64
+    cuts = [T * w // W for w in range(W + 1)]
+    rows = np.stack([M.build_row(x, cuts[w], cuts[w + 1], budget=512, tail=tail, seed=2, series=0, slc=w)
                      for w in range(W)])
-    assert int(rows[:, 0].sum()) == n
-    bound = M.rank_bound(rows, delta=0.01)
-    assert bound < 0.05  # 43,200 samples into 512 keys per slice
-    for p in ("50", "90", "99"):
-        prm = percentile_params(Decimal(p), "sorted_lower")
-        v, cnt, fl = M.query(rows, prm.mode, prm.p_num, prm.p_den, prm.q)
-        assert cnt == n and fl == 0
-        assert _rank_error(x, v, (n - 1) * int(p) // 100) <= bound, (shape, p)
+    row = M.merge_rows(rows, seed=2, series=0, epoch=1)
+    assert int(row[0]) == T and int(row[6]) == tail and M.row_words(512, tail) == row.size
+    assert np.array_equal(M.row_tail(row), np.sort(x)[T - tail:])
+    for mode in ("linear", "sorted_lower"):
+        v, n, f = _q(row[None], "99", mode)
+        want = np.percentile(x, 99.0) if mode == "linear" else np.sort(x)[(T - 1) * 99 // 100]
+        assert n == T and f == 0 and v == want
 
 
-def test_weight_and_nan_accounting():
+def test_fold_is_bounded_and_counts_add():
+    rng = np.random.default_rng(4)
+    a = M.build_row(rng.gamma(2, 0.05, 30_000), 0, 30_000, budget=256, tail=128, seed=1, slc=0)
+    b = M.build_row(rng.gamma(2, 0.05, 12_345), 0, 12_345, budget=256, tail=128, seed=1, slc=1)
+    c = M.fold(a, b, M.slice_base(1, 0, 9), 1)
+    assert int(c[0]) == 42_345 == int(c[5]) and int(c[4]) >= int(a[4]) + int(b[4])
+    assert sum(l.size for l in M.row_levels(c)) <= 256
+    assert np.array_equal(M.row_tail(c), np.sort(np.concatenate([M.row_tail(a), M.row_tail(b)]))[-128:])
+    assert c[2:3].view(np.float64)[0] == min(a[2:3].view(np.float64)[0], b[2:3].view(np.float64)[0])
+    # a folded state absorbs a new day without the old data: fold(fold(a, b), d) is a row again
+    d = M.build_row(rng.gamma(2, 0.05, 5_000), 0, 5_000, budget=256, tail=128, seed=1, slc=2)
+    e = M.fold(c, d, M.slice_base(1, 0, 9), 2)
+    assert int(e[0]) == 47_345 and e.size == c.size
+    with pytest.raises(ValueError):
+        M.fold(a, M.build_row(np.ones(10), 0, 10, budget=256, tail=64), M.slice_base(1, 0, 9), 1)
+
+
+def test_nan_accounting_and_flags():
     rng = np.random.default_rng(3)
     x = rng.gamma(2.0, 0.05, 20_000)
     x[::97] = np.nan
-    row = M.build_row(x, 5, 19_999, budget=512, gaps=True)
+    row = M.build_row(x, 5, 19_999, budget=512, tail=64, gaps=True)
     present = int((~np.isnan(x[5:19_999])).sum())
-    assert int(row[0]) == present and int(row[1]) == 0
-    w = int(row[9])
-    assert abs(w - present) < 0.05 * present  # total weight tracks n (coins are zero-mean)
-    keys, lvl = M.row_keys(row)
-    assert keys.size <= 512 and np.all(np.diff(keys[lvl == lvl.max()].astype(np.float64)) >= 0)
-    compact = M.build_row(x, 5, 19_999, budget=512, gaps=False)
+    assert int(row[0]) == present and int(row[1]) == 0 and int(row[5]) == present
+    compact = M.build_row(x, 5, 19_999, budget=512, tail=64, gaps=False)
     assert int(compact[1]) == int(np.isnan(x[5:19_999]).sum())
-    prm = percentile_params(Decimal("99"), "linear")
-    assert M.query(compact[None], prm.mode, prm.p_num, prm.p_den, prm.q)[2] == 1  # KRR_FLAG_NAN
+    assert _q(compact[None], "99", "linear")[2] == M.FLAG_NAN
+    empty = M.build_row(x, 7, 7, budget=512, tail=64)
+    v, n, f = _q(empty[None], "99", "linear")
+    assert n == 0 and f == M.FLAG_EMPTY and np.isnan(v)
 
 
 def test_rank_bound_helper_matches_restatement():
     """krr_amd.core.sketch.kll_rank_bound (the bench's bound, from device rows) equals the
-    restatement's per-series bound."""
+    restatement's per-row bound."""
     import torch
 
     from krr_amd.core import sketch
 
     rng = np.random.default_rng(12)
-    W, rows = 3, []
+    rows = []
     for s, n in enumerate((0, 900, 30_000, 90_000)):
         x = rng.gamma(2.0, 0.05, n)
-        cuts = [n * w // W for w in range(W + 1)]
-        rows.append(np.stack([M.build_row(x, cuts[w], cuts[w + 1], budget=256, seed=2, series=s, slc=w)
-                              for w in range(W)]))
-    got = sketch.kll_rank_bound(torch.from_numpy(np.concatenate(rows).view(np.int64)), W)
+        rows.append(M.build_row(x, 0, n, budget=256, tail=64, seed=2, series=s))
+    got = sketch.kll_rank_bound(torch.from_numpy(np.stack(rows).view(np.int64)))
     assert np.isnan(got[0])
     for s in range(1, 4):
         assert got[s] == pytest.approx(M.rank_bound(rows[s]), rel=1e-12)
 
 
-def _exchange_worker(rank, world, port, q, n_series, T, budget):
+def test_sparse_series_whose_keys_all_vanish():
+    """Three present samples spread over many chunks (NaN gaps), no tail: every level-0 key is
+    a lone sample (odd slots); answers are real samples, never NaN."""
+    x = np.full(5000, np.nan)
+    x[[10, 2500, 4990]] = [0.3, 0.1, 0.2]
+    for seed in range(16):
+        row = M.build_row(x, 0, x.size, budget=256, tail=0, seed=seed, gaps=True)
+        assert int(row[5]) == 3
+        v, n, f = _q(row[None], "50", "sorted_lower")
+        assert n == 3 and f == 0 and v in (0.1, 0.2, 0.3)
+
+
+def _exchange_worker(rank, world, port, q, n_series, T, budget, tail):
     import os
 
     import torch
@@ -115,7 +196,7 @@ def _exchange_worker(rank, world, port, q, n_series, T, budget):
         rng = np.random.default_rng(0)
         x = rng.gamma(2.0, 0.05, (n_series, T))
         t0, t1 = T * rank // world, T * (rank + 1) // world
-        rows = np.stack([M.build_row(x[s], t0, t1, budget=budget, seed=9, series=s, slc=rank)
+        rows = np.stack([M.build_row(x[s], t0, t1, budget=budget, tail=tail, seed=9, series=s, slc=rank)
                          for s in range(n_series)])
         merged, W = sketch.kll_exchange(torch.from_numpy(rows.view(np.int64)))
         lo, hi = sketch.owner_blocks(n_series, world)[rank]
@@ -134,10 +215,10 @@ def test_exchange_hands_each_owner_its_series_rows(world):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    n_series, T, budget = 7, 5000, 256
+    n_series, T, budget, tail = 7, 5000, 256, 64
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, n_series, T, budget))
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, n_series, T, budget, tail))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -146,25 +227,12 @@ def test_exchange_hands_each_owner_its_series_rows(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     x = np.random.default_rng(0).gamma(2.0, 0.05, (n_series, T))
-    prm = percentile_params(Decimal("99"), "linear")
     for rank, lo, hi, W, merged in got:
         assert W == world and merged.shape[0] == (hi - lo) * world
         for s in range(lo, hi):
-            want = np.stack([M.build_row(x[s], T * w // world, T * (w + 1) // world, budget=budget, seed=9, series=s,
-                                         slc=w) for w in range(world)])
+            want = np.stack([M.build_row(x[s], T * w // world, T * (w + 1) // world, budget=budget, tail=tail,
+                                         seed=9, series=s, slc=w) for w in range(world)])
             have = merged[(s - lo) * world:(s - lo + 1) * world]
             assert np.array_equal(have, want)
-            v, n, f = M.query(have, prm.mode, prm.p_num, prm.p_den, prm.q)
-            assert n == T and f == 0 and np.isfinite(v)
-
-
-def test_sparse_series_whose_keys_all_vanish():
-    """Three present samples spread over many chunks (NaN gaps): every kept key can be
-    compacted away; the answer then comes from the exact min / max, never a NaN."""
-    x = np.full(5000, np.nan)
-    x[[10, 2500, 4990]] = [0.3, 0.1, 0.2]
-    prm = percentile_params(Decimal("50"), "sorted_lower")
-    for seed in range(16):
-        row = M.build_row(x, 0, x.size, budget=256, seed=seed, gaps=True)
-        v, n, f = M.query(row[None], prm.mode, prm.p_num, prm.p_den, prm.q)
-        assert n == 3 and f == 0 and v in (0.1, 0.2, 0.3)
+            v, n, f = _q(have, "99", "linear", seed=9, series=s)
+            assert n == T and f == 0 and v == np.percentile(x[s], 99.0)  # within the folded tail
