@@ -751,6 +751,9 @@ def main():
             "source": "carried constant from BASELINE.md (SimpleStrategy.run + _format_result, config 1, "
                       "measured once in the build container; the reference cannot travel to the GPU box)"}
 
+    if rank == 0:
+        phase("right-size")
+        result.update(right_size(args, host_rec[:containers_total].numpy()))
     if rank == 0 and world == 1 and not args.no_host_path:
         phase("host path")
         result.update(host_path(args, dev, c_host_sample=parts[0][2]))
@@ -935,6 +938,46 @@ def pg_comm(dev):
         return int(fn()) if fn is not None else None
     except (RuntimeError, AttributeError):
         return None
+
+
+def right_size(args, records) -> dict:
+    """After the timed region, on rank 0: the run's records (every rank's, gathered) -> the
+    reference's Runner output, one ResourceAllocations per container (runner.py:113-120, after
+    Runner._format_result's exact rounding, runner.py:49-86): native rounding +
+    bulk-built models (krr_amd.core.fast_round.allocations_batch).  Checked against the
+    per-object path (SimpleStrategy result -> Decimal rounding -> the pydantic-validated
+    model) on a sample."""
+    from krr_amd.core.distributed import raw_from_records
+    from krr_amd.core.engine import RawResults
+    from krr_amd.core.fast_round import allocations_batch
+    from krr_amd.core.rounding import format_result
+    from krr_amd.core.runner import to_allocations
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    settings = SimpleStrategySettings(cpu_percentile=str(args.percentile), memory_buffer_percentage="5")
+    raw = raw_from_records(records)
+    n = int(raw.cpu_value.size)
+    threads = args.cpu_threads or cpu_lease()["threads"]
+    k = min(500, n)
+    sub = RawResults(*(np.asarray(a)[:k] for a in (raw.cpu_value, raw.cpu_count, raw.cpu_flags, raw.mem_value,
+                                                   raw.mem_count, raw.mem_flags)))
+    allocations_batch(sub, settings, threads=threads)  # loads the host libraries
+    times = []
+    for _ in range(3):
+        t_a = time.perf_counter()
+        got = allocations_batch(raw, settings, threads=threads)
+        times.append(time.perf_counter() - t_a)
+    dt = sorted(times)[1]
+    want = [to_allocations(format_result(r)) for r in SimpleStrategy(settings).results_from_raw(sub)]
+    same = all(g == w and g.json() == w.json() for g, w in zip(got[:k], want))
+    return {"round_objects_per_s": n / dt,
+            "round_ms": dt * 1e3,
+            "round_objects": n,
+            "round_equal_per_object_path": bool(same and len(got) == n),
+            "round_definition": (f"all {n} containers' 32-B records -> native exact-decimal rounding (krr_round_simple, "
+                                 f"{threads} threads) -> one ResourceAllocations per container built in bulk; median "
+                                 f"of 3; checked equal (values, exponents, JSON) to the per-object reference path on "
+                                 f"the first {k}")}
 
 
 def parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed) -> dict:

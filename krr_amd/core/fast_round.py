@@ -32,6 +32,30 @@ CPU_FALLBACK = 1
 MEM_FALLBACK = 2
 
 
+def _load_pyobj():
+    """krr_amd/lib/_krr_pyobj.so (krr_amd/csrc/krr_pyobj.c, built by __graft_entry__.build()):
+    the per-object construction loops in C.  None when it is not built: the Python forms below
+    build the same objects."""
+    import importlib.machinery
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "_krr_pyobj.so")
+    if not os.path.exists(path):
+        return None
+    try:
+        loader = importlib.machinery.ExtensionFileLoader("_krr_pyobj", path)
+        spec = importlib.util.spec_from_file_location("_krr_pyobj", path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        return mod
+    except ImportError:  # pragma: no cover - built for another interpreter
+        return None
+
+
+_PYOBJ = _load_pyobj()
+
+
 class _Params:
     def __init__(self, buffer: Decimal, cpu_min: Decimal, mem_min: Decimal):
         import ctypes
@@ -77,40 +101,104 @@ def format_simple_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALU
     buffer = settings.memory_buffer()
     cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
                                memory_min_value, threads)
-    # Decimals are immutable: one object per distinct string (1m / 1M granularity
-    # makes fleets highly repetitive).  Each object still gets its own models.
-    cache: dict[bytes, Decimal] = {}
-
-    def dec(b: bytes) -> Decimal:
-        d = cache.get(b)
-        if d is None:
-            d = cache[b] = Decimal(b.decode())
-        return d
-
+    # Decimals are immutable: one object per distinct string (1m / 1M granularity makes
+    # fleets highly repetitive), found by a sort of the string columns, not per object.
+    # Each object still gets its own models.
+    cpu_col, mem_col = decimal_column(cs), decimal_column(ms)
     out: list[RunResult] = []
     cpu_rt, mem_rt = ResourceType.CPU, ResourceType.Memory
     # millions of small acyclic objects: keep the cyclic GC from rescanning them
     gc_was = gc.isenabled()
     gc.disable()
     try:
-        _fill(out, st.tolist(), cs, ms, dec, raw, settings, buffer, cpu_min_value, memory_min_value, cpu_rt, mem_rt)
+        _apply_fallbacks(cpu_col, mem_col, st, raw, settings, buffer, cpu_min_value, memory_min_value)
+        if _PYOBJ is not None:
+            out = _PYOBJ.run_results(ResourceRecommendation, cpu_rt, mem_rt, cpu_col, mem_col)
+        else:
+            rec = _recommendation
+            out = [{cpu_rt: rec(c, None), mem_rt: rec(m, m)} for c, m in zip(cpu_col, mem_col)]
     finally:
         if gc_was:
             gc.enable()
     return out
 
 
-def _fill(out, status, cs, ms, dec, raw, settings, buffer, cpu_min_value, memory_min_value, cpu_rt, mem_rt):
-    for i, s in enumerate(status):
+def decimal_column(strings: np.ndarray, nan=None) -> list:
+    """Decimal(s) for every string of a numpy bytes column, as a list: one Decimal object per
+    distinct string (Decimal() runs once per distinct value); rows "NaN" become ``nan`` when
+    given (e.g. the "?" ResourceAllocations shows), empty rows (fallback objects) None."""
+    n = int(strings.size)
+    if n == 0:
+        return []
+    if _PYOBJ is not None:
+        col = np.ascontiguousarray(strings)
+        return _PYOBJ.decimal_column(col.view(np.uint8).reshape(-1), n, col.dtype.itemsize, Decimal, None, nan)
+    uniq, inv = np.unique(strings, return_inverse=True)
+    decs = np.empty(uniq.size, dtype=object)
+    decs[:] = [(nan if (nan is not None and u == b"NaN") else Decimal(u.decode())) if u else None
+               for u in uniq.tolist()]  # '': a fallback object
+    return decs[inv.reshape(-1)].tolist()
+
+
+def _apply_fallbacks(cpu_col, mem_col, status, raw, settings, buffer, cpu_min_value, memory_min_value) -> None:
+    """The objects the native rounding did not cover, through the Python restatement (which
+    raises what the reference raises)."""
+    cpu_rt, mem_rt = ResourceType.CPU, ResourceType.Memory
+    for i in np.nonzero(status)[0].tolist():
+        s = int(status[i])
         if s & CPU_FALLBACK:
-            cpu = round_value(settings.cpu_from_raw(raw, i), cpu_rt, cpu_min_value, memory_min_value)
-        else:
-            cpu = dec(cs[i])
+            cpu_col[i] = round_value(settings.cpu_from_raw(raw, i), cpu_rt, cpu_min_value, memory_min_value)
         if s & MEM_FALLBACK:
-            mem = round_value(settings.memory_from_raw(raw, i, buffer), mem_rt, cpu_min_value, memory_min_value)
-        else:
-            mem = dec(ms[i])
-        out.append({cpu_rt: _recommendation(cpu, None), mem_rt: _recommendation(mem, mem)})
+            mem_col[i] = round_value(settings.memory_from_raw(raw, i, buffer), mem_rt, cpu_min_value,
+                                     memory_min_value)
+
+
+def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
+                      memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE, threads: int = 0, model=None,
+                      resource_type=None) -> list:
+    """Runner._gather_objects_recommendations's list (runner.py:113-120) straight from raw kernel
+    results: one ``ResourceAllocations`` per object, equal to
+    ``ResourceAllocations(requests={rt: r[rt].request ...}, limits={rt: r[rt].limit ...})`` of the
+    rounded RunResult r, built in bulk.  The values are what the model's validator would leave
+    (allocations.py:33-51: Decimal unchanged, NaN -> "?", the CPU limit None), so each model is
+    made without a per-object validation walk (pydantic v1 ``construct``'s layout: the field
+    dict and the fields-set).  ``model`` / ``resource_type``: the reference's own classes
+    (krr_amd.integration) or, by default, this package's mirror."""
+    from krr_amd.core.models.allocations import ResourceAllocations
+
+    model = model or ResourceAllocations
+    rtypes = list(resource_type or ResourceType)
+    cpu_k, mem_k = rtypes[0], rtypes[1]
+    buffer = settings.memory_buffer()
+    cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
+                               memory_min_value, threads)
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        q = "?"
+        cpu_col, mem_col = decimal_column(cs, q), decimal_column(ms, q)
+        fb = np.nonzero(st)[0].tolist()
+        _apply_fallbacks(cpu_col, mem_col, st, raw, settings, buffer, cpu_min_value, memory_min_value)
+        for i in fb:  # the validator's NaN -> "?" (allocations.py:40-41) for the Python-rounded ones
+            if isinstance(cpu_col[i], Decimal) and cpu_col[i].is_nan():
+                cpu_col[i] = q
+            if isinstance(mem_col[i], Decimal) and mem_col[i].is_nan():
+                mem_col[i] = q
+        fields = {"requests", "limits"}
+        if _PYOBJ is not None:
+            return _PYOBJ.allocations(model, fields, cpu_k, mem_k, cpu_col, mem_col)
+        new, setattr_ = object.__new__, object.__setattr__
+
+        def mk(c, m):
+            o = new(model)
+            setattr_(o, "__dict__", {"requests": {cpu_k: c, mem_k: m}, "limits": {cpu_k: None, mem_k: m}})
+            setattr_(o, "__fields_set__", fields)
+            return o
+
+        return list(map(mk, cpu_col, mem_col))
+    finally:
+        if gc_was:
+            gc.enable()
 
 
 _FIELDS = ("request", "limit")
@@ -125,4 +213,4 @@ def _recommendation(request, limit) -> ResourceRecommendation:
     return m
 
 
-__all__ = ["format_simple_batch", "round_strings"]
+__all__ = ["allocations_batch", "decimal_column", "format_simple_batch", "round_strings"]

@@ -155,6 +155,33 @@ class BatchedRunner:
         res = await asyncio.to_thread(self.recommend_shard, fleet, group, dst, device)
         return None if res is None else [to_allocations(r) for r in res]
 
+    def allocations_packed(self, fleet, model=None, resource_type=None) -> list:
+        """Runner._gather_objects_recommendations's list (runner.py:113-120) for a PackedFleet:
+        one kernel pass, native rounding, and the ResourceAllocations built in bulk
+        (krr_amd.core.fast_round.allocations_batch; ``model`` / ``resource_type``: the
+        reference's own classes, default this package's mirror)."""
+        from krr_amd.core.fast_round import allocations_batch
+
+        self._require_packed()
+        raw = self.strategy.settings.run_fleet(fleet)
+        return allocations_batch(raw, self.strategy.settings, self.cpu_min_value, self.memory_min_value, model=model,
+                                 resource_type=resource_type)
+
+    def pack_from_bodies(self, cpu_bodies, mem_bodies, threads: int = 0, parser: str = "device"):
+        """The PackedFleet of raw per-pod query_range bodies (see recommend_from_bodies)."""
+        from krr_amd.core.packing import PackedFleet
+        from krr_amd.core.prom_native import pack_query_range_bodies
+
+        if len(cpu_bodies) != len(mem_bodies):
+            raise ValueError("cpu and memory bodies need one entry per object each")
+        if parser not in ("device", "host"):
+            raise ValueError("parser must be 'device' or 'host'")
+        if parser == "device":
+            return self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads)
+        alloc = _pinned_alloc_or_none()
+        return PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
+                           pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
+
     def recommend_from_bodies(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
                               threads: int = 0, parser: str = "device") -> list[RunResult]:
         """The whole loader -> strategy -> rounding path from raw Prometheus query_range
@@ -164,20 +191,7 @@ class BatchedRunner:
         (krr_amd.core.device_pack; a batch with bodies outside Prometheus' canonical form
         goes to the host packer); ``"host"``: the native host packer (libkrr_host.so).
         No Decimal lists either way; one kernel pass, native rounding."""
-        from krr_amd.core.packing import PackedFleet
-        from krr_amd.core.prom_native import pack_query_range_bodies
-
-        if len(cpu_bodies) != len(mem_bodies):
-            raise ValueError("cpu and memory bodies need one entry per object each")
-        if parser not in ("device", "host"):
-            raise ValueError("parser must be 'device' or 'host'")
-        if parser == "device":
-            fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads)
-        else:
-            alloc = _pinned_alloc_or_none()
-            fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
-                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))
-        return self.recommend_packed(fleet)
+        return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
 
     @staticmethod
     def body_shard_bounds(objects: Sequence[K8sObjectData], world: int) -> list:
@@ -228,6 +242,10 @@ class BatchedRunner:
 
     def allocations(self, objects: Sequence[K8sObjectData],
                     histories: Sequence[HistoryData]) -> list[ResourceAllocations]:
+        if len(objects) != len(histories):
+            raise ValueError("one HistoryData per object")
+        if supports_packed(self.strategy):  # bulk-built models (fast_round.allocations_batch)
+            return self.allocations_packed(self.strategy.pack(histories))
         return [to_allocations(r) for r in self.recommend(objects, histories)]
 
     def collect_result(self, objects: Sequence[K8sObjectData], histories: Sequence[HistoryData]):

@@ -426,60 +426,163 @@ struct KllTail {
     double tau;     // keys <= tau are not candidates
 };
 
-// In-place stable compaction: keep keys > v and the first `eq` copies of v.
+// In-place stable compaction: keep keys > v and the first `eq` copies of v.  Four keys per
+// lane per round, their LDS reads issued together.
 __device__ KllTail kll_tail_keep(KllShared sh, KllTail ts, double v, uint32_t eq, int lane) {
     uint32_t out = 0;
 #pragma unroll 1
-    for (uint32_t r = 0; r < ts.tl; r += kWave) {
-        const uint32_t i = r + (uint32_t)lane;
-        const double x = i < ts.tl ? bitsd(sh.tb[i]) : -__builtin_inf();
-        const bool isgt = i < ts.tl && x > v;
-        const uint64_t em = ballot(i < ts.tl && x == v);
-        const bool keep = isgt || (((em >> lane) & 1ull) && lane_prefix(em) < eq);
-        const uint64_t km = ballot(keep);
-        const uint32_t ne = popc64(em);
-        eq -= ne < eq ? ne : eq;
-        if (keep) sh.tb[out + lane_prefix(km)] = dbits(x);
-        out += popc64(km);
+    for (uint32_t r = 0; r < ts.tl; r += 4 * kWave) {
+        double x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = r + (uint32_t)q * kWave + (uint32_t)lane;
+            x[q] = i < ts.tl ? bitsd(sh.tb[i]) : -__builtin_inf();
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // in buffer order: q-th group of 64 after the (q-1)-th
+            const uint32_t i = r + (uint32_t)q * kWave + (uint32_t)lane;
+            const uint64_t em = ballot(i < ts.tl && x[q] == v);
+            const bool keep = (i < ts.tl && x[q] > v) || (((em >> lane) & 1ull) && lane_prefix(em) < eq);
+            const uint64_t km = ballot(keep);
+            const uint32_t ne = popc64(em);
+            eq -= ne < eq ? ne : eq;
+            if (keep) sh.tb[out + lane_prefix(km)] = dbits(x[q]);
+            out += popc64(km);
+        }
     }
     __syncthreads();
     return KllTail{out, 1u, v};
 }
 
+// (#keys > v, #keys >= v) of the tail buffer, eight LDS reads per lane in flight.
+__device__ __forceinline__ void kll_tail_count(const uint64_t* tb, uint32_t m, double v, uint32_t& gt, uint32_t& ge,
+                                               int lane) {
+    uint32_t g = 0, e = 0;
+#pragma unroll 1
+    for (uint32_t r = 0; r < m; r += 8 * kWave) {
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t i = r + (uint32_t)q * kWave + (uint32_t)lane;
+            x[q] = i < m ? bitsd(tb[i]) : -__builtin_inf();
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            g += x[q] > v ? 1u : 0u;
+            e += x[q] >= v ? 1u : 0u;
+        }
+    }
+    gt = wave_sum_u32(g);
+    ge = wave_sum_u32(e);
+}
+
 // Keep the buffer's largest keys: raise tau to a sampled pivot v that leaves between `tail`
 // and tail + slack keys (> v, plus copies of v to reach `tail` when ties straddle it), all
-// counted exactly; if no sample does, sort the buffer and keep exactly `tail`.
+// counted exactly.  The first pivot is where 64 strided samples put the cut; a miss jumps by
+// the counted distance.  If no sample does, sort the buffer and keep exactly `tail`.
 __device__ KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
     const uint32_t m = ts.tl;
     double s = bitsd(sh.tb[(uint32_t)(((uint64_t)(uint32_t)lane * m) >> 6)]);
     s = kll_sort64(s, lane);
-    int idx = (int)(((uint64_t)(m - tail) * 64u) / m) - 1;
+    const uint32_t want = tail + kKllTailSlack / 2;
+    int idx = (int)(((uint64_t)(m - want) * 64u) / m);
     idx = idx < 0 ? 0 : (idx > 63 ? 63 : idx);
+    int lo = -1, hi = 64;  // samples known too low (keep too many) / too high
 #pragma unroll 1
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 6 && hi - lo > 1; ++it) {
         const double v = bitsd(lane_bcast64(dbits(s), idx));
-        uint32_t gt = 0, ge = 0;
-        for (uint32_t i = lane; i < m; i += kWave) {
-            const double x = bitsd(sh.tb[i]);
-            gt += x > v ? 1u : 0u;
-            ge += x >= v ? 1u : 0u;
-        }
-        gt = wave_sum_u32(gt);
-        ge = wave_sum_u32(ge);
+        uint32_t gt, ge;
+        kll_tail_count(sh.tb, m, v, gt, ge, lane);
         if (gt >= tail && gt <= tail + kKllTailSlack) return kll_tail_keep(sh, ts, v, 0, lane);
         if (gt < tail && ge >= tail) return kll_tail_keep(sh, ts, v, tail - gt, lane);
+        // jump by the counted distance (about m / 64 keys between neighbouring samples)
+        const int step = (int)(((int64_t)ge - (int64_t)want) * 64 / (int64_t)m);
         if (ge < tail) {  // pivot too high
-            if (idx == 0) break;
-            --idx;
+            hi = idx;
+            idx += step < -1 ? step : -1;
         } else {  // keeps too many
-            if (idx == 63) break;
-            ++idx;
+            lo = idx;
+            idx += step > 1 ? step : 1;
         }
+        idx = idx <= lo ? lo + 1 : (idx >= hi ? hi - 1 : idx);
     }
     kll_lds_sort(sh.tb, m, lane);  // exact fallback
     for (uint32_t i = lane; i < tail; i += kWave) sh.tb[i] = sh.tb[m - tail + i];
     __syncthreads();
     return KllTail{tail, 1u, bitsd(uni64(sh.tb[0]))};
+}
+
+// 2,048 keys ascending across the wave in registers (lane l holds positions 32 l .. 32 l + 31):
+// bitonic with the flip first step of every stage, so every compare-exchange is ascending.
+__device__ __forceinline__ void kll_regsort2048(double (&x)[32], int lane) {
+#pragma unroll
+    for (int k = 2; k <= 32; k <<= 1) {  // in-lane stages
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int p = i ^ (k - 1);
+            if ((i & (k >> 1)) == 0 && p > i) kll_cxd(x[i], x[p]);
+        }
+#pragma unroll
+        for (int j = k >> 2; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+                if (!(i & j)) kll_cxd(x[i], x[i + j]);
+        }
+    }
+#pragma unroll 1
+    for (int k = 64; k <= 2048; k <<= 1) {
+        // flip: position p pairs with p ^ (k - 1) = lane ^ ((k - 1) >> 5), slot 31 - i
+        const int mk = (k - 1) >> 5;
+        const bool lower = (lane & ((k >> 1) >> 5)) == 0;
+        double o[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const uint64_t xb = dbits(x[31 - i]);
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)xb, mk, kWave);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(xb >> 32), mk, kWave);
+            o[i] = bitsd(((uint64_t)hi << 32) | lo);
+        }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x[i] = lower ? fmin(x[i], o[i]) : fmax(x[i], o[i]);
+        // half-cleaners across lanes (j >= 32), then in-lane
+#pragma unroll 1
+        for (int j = k >> 2; j >= 32; j >>= 1) {
+            const int mj = j >> 5;
+            const bool low = (lane & mj) == 0;
+            switch (mj) {  // wave-uniform
+                case 1: kll_cross<1, 32>(x, low); break;
+                case 2: kll_cross<2, 32>(x, low); break;
+                case 4: kll_cross<4, 32>(x, low); break;
+                case 8: kll_cross<8, 32>(x, low); break;
+                case 16: kll_cross<16, 32>(x, low); break;
+                default: kll_cross<32, 32>(x, low); break;
+            }
+        }
+#pragma unroll
+        for (int j = 16; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+                if (!(i & j)) kll_cxd(x[i], x[i + j]);
+        }
+    }
+}
+
+// The tail buffer tb[0, m) (m <= 2,048) ascending in place, through registers.
+__device__ void kll_tail_sort(uint64_t* tb, uint32_t m, int lane) {
+    double x[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t p = (uint32_t)lane * 32u + (uint32_t)i;
+        x[i] = p < m ? bitsd(tb[p]) : __builtin_inf();
+    }
+    __syncthreads();
+    kll_regsort2048(x, lane);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t p = (uint32_t)lane * 32u + (uint32_t)i;
+        if (p < m) tb[p] = dbits(x[i]);
+    }
+    __syncthreads();
 }
 
 // Per-wave build state; one instance per series slice (by value: nothing is address-taken).
@@ -584,59 +687,70 @@ struct KllProc {
         w2u += kll_push(sh, base, nrl, 0, C >> 1, kKllFirstRun, lane);
     }
 
-    __device__ __forceinline__ void tail_filter(const double (&a)[8], const double (&b)[8]) {
-        uint64_t m[16];
-        uint32_t tot = 0;
+    // Candidates: keys > tau (every present key until the buffer first fills).  A pair whose
+    // larger key is no candidate has none, so the per-slot tests run for hit pair columns only;
+    // a chunk adds at most 1,024 keys, so the buffer is refreshed first when less room is left.
+    template <bool FULL>
+    __device__ __forceinline__ bool cand(double x) const {
+        return FULL ? x > ts.tau : x == x;
+    }
+    template <bool FULL>
+    __device__ __forceinline__ void tail_append(const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
+        uint64_t pm[8], any = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
-            m[j] = ballot(ts.full ? x > ts.tau : x == x);
-            tot += popc64(m[j]);
+        for (int u = 0; u < 8; ++u) {
+            pm[u] = ballot(cand<FULL>(hi[u]));
+            any |= pm[u];
         }
-        if (!tot) return;
-        if (ts.tl + tot > tcap) {
-            ts = kll_tail_refresh(sh, ts, tail, lane);
-            tot = 0;
+        if (!any) return;
+        if (ts.tl + 16u * kWave > tcap) {
+            ts = kll_tail_refresh(sh, ts, tail, lane);  // tau rises: recheck the pairs
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
-                m[j] = ballot(x > ts.tau);
-            }
+            for (int u = 0; u < 8; ++u) pm[u] = ballot(hi[u] > ts.tau);
         }
         uint32_t tl = ts.tl;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (m[j]) {
-                const double x = (j & 1) ? b[j >> 1] : a[j >> 1];
-                if ((m[j] >> lane) & 1ull) sh.tb[tl + lane_prefix(m[j])] = dbits(x);
-                tl += popc64(m[j]);
+        for (int u = 0; u < 8; ++u) {
+            if (pm[u]) {
+                const uint64_t ma = ballot(ts.full ? a[u] > ts.tau : a[u] == a[u]);
+                const uint64_t mb = ballot(ts.full ? b[u] > ts.tau : b[u] == b[u]);
+                if ((ma >> lane) & 1ull) sh.tb[tl + lane_prefix(ma)] = dbits(a[u] + 0.0);  // -0 -> +0
+                tl += popc64(ma);
+                if ((mb >> lane) & 1ull) sh.tb[tl + lane_prefix(mb)] = dbits(b[u] + 0.0);
+                tl += popc64(mb);
             }
         }
         ts.tl = tl;
     }
+    __device__ __forceinline__ void tail_filter(const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
+        if (ts.full) tail_append<true>(a, b, hi);
+        else tail_append<false>(a, b, hi);
+    }
 
     // ---- one chunk ----
     __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
-        double a[8], b[8];
-        bool lane_nan = false;
+        // keys are folded (-0 -> +0) where they are kept: the selected pair key, lone and tail
+        // keys, min / max at the end; compares treat -0 and +0 alike
+        double a[8], b[8], lo[8], hi[8];
+        uint64_t nanm = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            a[u] = c[u].x + 0.0;  // -0 -> +0; NaN stays NaN
-            b[u] = c[u].y + 0.0;
-            lane_nan |= __builtin_isnan(a[u]) || __builtin_isnan(b[u]);
+            a[u] = c[u].x;
+            b[u] = c[u].y;
+            nanm |= ballot(__builtin_isunordered(a[u], b[u]));
+            lo[u] = fmin(a[u], b[u]);  // one NaN: both are the present sample
+            hi[u] = fmax(a[u], b[u]);
         }
-        const uint64_t nanm = ballot(lane_nan);
-        if (tail) tail_filter(a, b);
+        if (tail) tail_filter(a, b, hi);
         double out[8];
         uint32_t c0 = 0;
         if (nanm == 0) {  // every slot present: 8 two-key compactions per lane
             const uint32_t bits = kll_coin32(base, kT_L0 + (uint32_t)lane, ci);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const double lo = fmin(a[u], b[u]), hi = fmax(a[u], b[u]);
-                out[u] = ((bits >> u) & 1u) ? hi : lo;
-                kmin = fmin(kmin, lo);
-                kmax = fmax(kmax, hi);
+                out[u] = (((bits >> u) & 1u) ? hi[u] : lo[u]) + 0.0;
+                kmin = fmin(kmin, lo[u]);
+                kmax = fmax(kmax, hi[u]);
             }
             c0 = 8;
             w2l += 8;
@@ -644,32 +758,29 @@ struct KllProc {
         } else {
             bool any = false;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) any |= !__builtin_isnan(a[u]) || !__builtin_isnan(b[u]);
+            for (int u = 0; u < 8; ++u) any |= hi[u] == hi[u];
             if (ballot(any)) {
                 const uint32_t bits = kll_coin32(base, kT_L0 + (uint32_t)lane, ci);
                 uint32_t lone = 0;  // pairs with one present sample, bit u
-                double lv[8];       // ... that sample
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const bool pa = !__builtin_isnan(a[u]), pb = !__builtin_isnan(b[u]);
-                    kmin = fmin(kmin, fmin(a[u], b[u]));
-                    kmax = fmax(kmax, fmax(a[u], b[u]));
+                    kmin = fmin(kmin, lo[u]);
+                    kmax = fmax(kmax, hi[u]);
                     pres += (pa ? 1u : 0u) + (pb ? 1u : 0u);
-                    const double lo = fmin(a[u], b[u]), hi = fmax(a[u], b[u]);
-                    out[u] = (pa && pb) ? (((bits >> u) & 1u) ? hi : lo) : bitsd(kKllInfBits);
+                    out[u] = (pa && pb) ? ((((bits >> u) & 1u) ? hi[u] : lo[u]) + 0.0) : bitsd(kKllInfBits);
                     c0 += (pa && pb) ? 1u : 0u;
                     lone |= (pa != pb) ? (1u << u) : 0u;
-                    lv[u] = lo;  // fmin of a present and a NaN sample is the present one
                 }
                 w2l += c0;
                 // lone samples into the level-0 odd slot, in pair order (one slot update per round)
 #pragma unroll 1
                 while (ballot(lone != 0)) {
                     const uint32_t u0 = lone ? (uint32_t)__builtin_ctz(lone) : 0u;
-                    double v = lv[0];
+                    double v = lo[0];
 #pragma unroll
-                    for (int u = 1; u < 8; ++u) v = kll_pick((uint32_t)u == u0, v, lv[u]);
-                    lane_odd<0>(v, lone != 0);
+                    for (int u = 1; u < 8; ++u) v = kll_pick((uint32_t)u == u0, v, lo[u]);
+                    lane_odd<0>(v + 0.0, lone != 0);
                     lone &= lone - 1;
                 }
                 arrivals();
@@ -719,7 +830,11 @@ struct KllProc {
                     kll_merge16(z);
                     lane_level<3>(z, cp3 + cy, kT_L3, ci >> 3, y, cy);
                     arrivals();
+#ifndef KRR_KLL_X_NOWAVE  // profiling variant: no wave stage (rows are not valid)
                     wave_stage(y, cy);
+#else
+                    kmax = fmax(kmax, y[0]);
+#endif
                 }
             }
         }
@@ -827,7 +942,10 @@ __device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t 
     return m;
 }
 
-__global__ __launch_bounds__(64, 2) void k_kll_build(KllBuildArgs A) {
+#ifndef KRR_KLL_WAVES_PER_SIMD
+#define KRR_KLL_WAVES_PER_SIMD 1  // the build's LDS (runs + tail buffer) allows one wave per SIMD anyway
+#endif
+__global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     KllShared sh;
@@ -884,15 +1002,16 @@ __global__ __launch_bounds__(64, 2) void k_kll_build(KllBuildArgs A) {
         const double K0[4] = {P.K[0], P.K[1], P.K[2], P.K[3]};
         const uint64_t n_pres = lane_bcast64(wave_scan64((uint64_t)P.pres, 0ull, OpAdd64{}), kWave - 1);
         const uint64_t w2lanes = lane_bcast64(wave_scan64((uint64_t)P.w2l, 0ull, OpAdd64{}), kWave - 1);
-        const uint64_t gmin = lane_bcast64(wave_scan64(dbits(P.kmin), kQuietNaN, OpMinF64Bits{}), kWave - 1);
-        const uint64_t gmax = lane_bcast64(wave_scan64(dbits(P.kmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1);
+        const uint64_t gmin = dbits(bitsd(lane_bcast64(wave_scan64(dbits(P.kmin), kQuietNaN, OpMinF64Bits{}), kWave - 1)) + 0.0);
+        const uint64_t gmax = dbits(bitsd(lane_bcast64(wave_scan64(dbits(P.kmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1)) + 0.0);
 
         // tail: the min(n, tail) largest present keys, ascending
         uint32_t tl_out = 0;
         if (tail) {
             KllTail ts = P.ts;
-            if (ts.tl > tail + kKllTailSlack) ts = kll_tail_refresh(sh, ts, tail, lane);
-            kll_lds_sort(sh.tb, ts.tl, lane);
+            if (ts.tl > tail + kKllTailSlack || (ts.tl > 2048 && ts.tl > tail)) ts = kll_tail_refresh(sh, ts, tail, lane);
+            if (ts.tl <= 2048) kll_tail_sort(sh.tb, ts.tl, lane);
+            else kll_lds_sort(sh.tb, ts.tl, lane);
             tl_out = ts.tl < tail ? ts.tl : tail;
             for (uint32_t i = lane; i < tl_out; i += kWave) row[kKllHdr + budget + i] = sh.tb[ts.tl - tl_out + i];
             __syncthreads();

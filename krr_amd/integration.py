@@ -106,32 +106,31 @@ async def gather_objects_recommendations(runner: Any, objects: Sequence[Any]) ->
     settings = runner._strategy.settings
     batched = BatchedRunner(strategy, runner.config.cpu_min_value, runner.config.memory_min_value)
     loader = _options(runner)["loader"]
+    ref = dict(model=RefResourceAllocations, resource_type=RefResourceType)
     if loader == "bodies":
         cpu_bodies, mem_bodies = await fetch_pod_bodies(runner, objects, settings)
-        # native packer + one fleet-wide kernel pass + native rounding, off the event loop
-        results = await asyncio.to_thread(batched.recommend_from_bodies, cpu_bodies, mem_bodies, 0,
-                                          _options(runner).get("parser", "device"))
-    elif loader == "grouped":
+        # native packer + one fleet-wide kernel pass + native rounding + bulk models, off the event loop
+        parser = _options(runner).get("parser", "device")
+
+        def run():
+            return batched.allocations_packed(batched.pack_from_bodies(cpu_bodies, mem_bodies, 0, parser), **ref)
+
+        return await asyncio.to_thread(run)
+    if loader == "grouped":
         fleet = await fetch_grouped_fleet(runner, objects, settings, _options(runner).get("parser", "device"),
                                           batched)
-        results = await asyncio.to_thread(batched.recommend_packed, fleet)
-    else:
-        async def history(obj):  # runner.py:88-102, with the reference's own loaders
-            lo = runner._get_prometheus_loader(obj.cluster)
-            data = await asyncio.gather(*[
-                lo.gather_data(obj, rt, settings.history_timedelta, timeframe=settings.timeframe_timedelta)
-                for rt in RefResourceType])
-            return {HipResourceType(rt.value): d for rt, d in zip(RefResourceType, data)}
+        return await asyncio.to_thread(batched.allocations_packed, fleet, **ref)
 
-        histories = await asyncio.gather(*[history(o) for o in objects])
-        # one fleet-wide kernel pass, off the event loop like the reference's to_thread (runner.py:106)
-        results = await asyncio.to_thread(batched.recommend, list(objects), histories)
-    out = []
-    for r in results:
-        out.append(RefResourceAllocations(
-            requests={rt: r[HipResourceType(rt.value)].request for rt in RefResourceType},
-            limits={rt: r[HipResourceType(rt.value)].limit for rt in RefResourceType}))
-    return out
+    async def history(obj):  # runner.py:88-102, with the reference's own loaders
+        lo = runner._get_prometheus_loader(obj.cluster)
+        data = await asyncio.gather(*[
+            lo.gather_data(obj, rt, settings.history_timedelta, timeframe=settings.timeframe_timedelta)
+            for rt in RefResourceType])
+        return {HipResourceType(rt.value): d for rt, d in zip(RefResourceType, data)}
+
+    histories = await asyncio.gather(*[history(o) for o in objects])
+    # one fleet-wide kernel pass, off the event loop like the reference's to_thread (runner.py:106)
+    return await asyncio.to_thread(batched.allocations_packed, strategy.pack(histories), **ref)
 
 
 # ---- body-level loaders -------------------------------------------------------------------------

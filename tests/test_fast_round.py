@@ -97,3 +97,51 @@ def test_huge_values_fall_back_exactly():
     for g, w in zip(got, want):
         for rt in ResourceType:
             assert _same(g[rt].request, w[rt].request)
+
+
+@pytest.mark.parametrize("path", ["cli", "default", "cli7"])
+def test_allocations_batch_equals_validated_models(path):
+    """allocations_batch (bulk, no per-object validation walk) == the reference's list
+    [ResourceAllocations(requests=..., limits=...)] (runner.py:113-120) built through the
+    model's validator from the rounded RunResults: same values, same exponents, same JSON."""
+    from krr_amd.core.fast_round import allocations_batch
+    from krr_amd.core.runner import to_allocations
+
+    st = _settings(path)
+    raw = _raw(7 + len(path), n=5000)
+    want = [to_allocations(r) for r in format_simple_batch(raw, st)]
+    got = allocations_batch(raw, st)
+    assert len(got) == len(want)
+    nq = 0
+    for g, w in zip(got, want):
+        assert type(g) is type(w) and g == w and g.json() == w.json()
+        for part in ("requests", "limits"):
+            gd, wd = getattr(g, part), getattr(w, part)
+            assert list(gd) == list(wd)
+            for k in gd:
+                assert type(gd[k]) is type(wd[k]) and str(gd[k]) == str(wd[k])
+                nq += gd[k] == "?"
+    assert nq > 0  # empty series became "?"
+
+
+def test_allocations_batch_reference_model_types():
+    """With the reference's classes passed in (krr_amd.integration does), the models and
+    their dict keys are those classes' instances."""
+    import enum
+
+    import pydantic.v1 as pd
+
+    from krr_amd.core.fast_round import allocations_batch
+
+    class RT(str, enum.Enum):
+        CPU = "cpu"
+        Memory = "memory"
+
+    class RA(pd.BaseModel):
+        requests: dict
+        limits: dict
+
+    raw = _raw(11, n=50)
+    got = allocations_batch(raw, _settings("cli"), model=RA, resource_type=RT)
+    assert all(type(g) is RA and list(g.requests) == [RT.CPU, RT.Memory] for g in got)
+    assert got[0].dict()["limits"][RT.CPU] is None
