@@ -114,12 +114,15 @@ class BatchedRunner:
         from krr_amd.core.packing import PackedFleet
         from krr_amd.core.prom_native import pack_query_range_bodies
 
-        if parser not in ("device", "host"):
-            raise ValueError("parser must be 'device' or 'host'")
+        if parser not in ("device", "host", "hybrid"):
+            raise ValueError("parser must be 'device', 'host' or 'hybrid'")
         # ONE device for the pack and the kernel pass: this rank's GPU (LOCAL_RANK) unless
         # the caller names one — the packer's own default (settings.device) is GPU 0
         dev = local_device() if device is None else int(device)
-        if parser == "device":
+        if parser == "hybrid":
+            parts = self.pack_hybrid(cpu_bodies, mem_bodies, threads=threads, device=dev)
+            fleet = parts[0] if len(parts) == 1 else _concat_fleets(parts, dev)
+        elif parser == "device":
             fleet = self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=dev)
         else:
             fleet = PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads),
@@ -174,8 +177,13 @@ class BatchedRunner:
 
         if len(cpu_bodies) != len(mem_bodies):
             raise ValueError("cpu and memory bodies need one entry per object each")
-        if parser not in ("device", "host"):
-            raise ValueError("parser must be 'device' or 'host'")
+        if parser not in ("device", "host", "hybrid"):
+            raise ValueError("parser must be 'device', 'host' or 'hybrid'")
+        if parser == "hybrid":
+            parts = self.pack_hybrid(cpu_bodies, mem_bodies, threads=threads)
+            if len(parts) == 1:
+                return parts[0]
+            return _concat_fleets(parts, self.strategy.settings.device)
         if parser == "device":
             return self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads)
         alloc = _pinned_alloc_or_none()
@@ -189,9 +197,88 @@ class BatchedRunner:
         as PrometheusLoader.gather_data would fetch them (prometheus.py:118-143).
         ``parser="device"`` (default): the bodies cross PCIe raw and the MI355X parses them
         (krr_amd.core.device_pack; a batch with bodies outside Prometheus' canonical form
-        goes to the host packer); ``"host"``: the native host packer (libkrr_host.so).
-        No Decimal lists either way; one kernel pass, native rounding."""
+        goes to the host packer); ``"host"``: the native host packer (libkrr_host.so);
+        ``"hybrid"``: both at once on disjoint object ranges (``pack_hybrid``), one kernel
+        pass per range.  No Decimal lists either way; native rounding."""
+        self._require_packed()
+        if parser == "hybrid":
+            parts = self.pack_hybrid(cpu_bodies, mem_bodies, threads=threads)
+            raw = _concat_raw([self.strategy.settings.run_fleet(f) for f in parts])
+            return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
+
+    # parser="hybrid": the share of the JSON bytes the host packer takes, re-estimated after
+    # every call from the rates both sides reached while running together
+    hybrid_share = 0.2
+    hybrid_last: Optional[dict] = None
+
+    def pack_hybrid(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None) -> list:
+        """Raw bodies -> PackedFleets of consecutive object ranges, in object order: the LAST
+        ``hybrid_share`` of the JSON bytes parsed by the host packer (libkrr_host.so, on a
+        worker thread, most of the threads) WHILE the first part crosses PCIe raw and is
+        parsed on the device (krr_amd.core.device_pack, the staging copy on the remaining
+        threads).  Each part equals what its parser gives for that range alone, so the
+        concatenation equals either parser on the whole batch; a body either parser rejects
+        sends the whole batch to the host packer (its result, or its error naming the
+        first bad body).  The share then moves toward r_host / (r_host + r_device)."""
+        import os
+        import threading
+        import time
+
+        import numpy as np
+
+        from krr_amd.core.packing import PackedFleet
+        from krr_amd.core.prom_native import PrometheusResponseError, pack_query_range_bodies
+
+        if len(cpu_bodies) != len(mem_bodies):
+            raise ValueError("cpu and memory bodies need one entry per object each")
+        n = len(cpu_bodies)
+        T = int(threads) or len(os.sched_getaffinity(0))
+        nb = np.fromiter((sum(len(b) for b in cb) + sum(len(b) for b in mb)
+                          for cb, mb in zip(cpu_bodies, mem_bodies)), dtype=np.int64, count=n)
+        cum = np.cumsum(nb)
+        total = int(cum[-1]) if n else 0
+        share = min(max(float(self.hybrid_share), 0.02), 0.8)
+        k = int(np.searchsorted(cum, (1.0 - share) * total, side="left")) + 1 if n else 0
+        k = min(max(k, 1), n)
+        if T < 3 or k >= n or n < 2:
+            return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)]
+        t_dev = max(1, T // 4)  # staging memcpy threads; the host parser gets the rest
+        t_host = max(1, T - t_dev)
+        host_out: dict = {}
+        alloc = _pinned_alloc_or_none()
+
+        def host_part():
+            t0 = time.perf_counter()
+            try:
+                host_out["fleet"] = PackedFleet(
+                    pack_query_range_bodies(cpu_bodies[k:], threads=t_host, alloc=alloc),
+                    pack_query_range_bodies(mem_bodies[k:], threads=t_host, alloc=alloc))
+            except PrometheusResponseError as e:
+                host_out["error"] = e
+            host_out["s"] = time.perf_counter() - t0
+
+        worker = threading.Thread(target=host_part, name="krr-hybrid-host", daemon=True)
+        worker.start()
+        t0 = time.perf_counter()
+        try:
+            dev_fleet = self.pack_bodies_device(cpu_bodies[:k], mem_bodies[:k], threads=t_dev, device=device)
+            dev_s = time.perf_counter() - t0
+        finally:
+            worker.join()
+        if "error" in host_out or self.last_pack_via != ("device", "device"):
+            # a body one side rejected: the outcome is the host packer's on the whole batch
+            self.last_pack_via = ("host", "host")
+            return [PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
+                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))]
+        b_dev, b_host = int(cum[k - 1]), total - int(cum[k - 1])
+        r_dev, r_host = b_dev / max(dev_s, 1e-9), b_host / max(host_out["s"], 1e-9)
+        self.hybrid_last = {"share": share, "split_object": k, "device_s": dev_s, "host_s": host_out["s"],
+                            "device_GBps": r_dev / 1e9, "host_GBps": r_host / 1e9,
+                            "device_threads": t_dev, "host_threads": t_host}
+        self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
+        self.last_pack_via = ("hybrid", "hybrid")
+        return [dev_fleet, host_out["fleet"]]
 
     @staticmethod
     def body_shard_bounds(objects: Sequence[K8sObjectData], world: int) -> list:
@@ -272,6 +359,39 @@ class BatchedRunner:
         histories = await self.gather_histories(objects, loader)
         # the kernel pass runs off the event loop, like the reference's to_thread (runner.py:106)
         return await asyncio.to_thread(self.allocations, objects, histories)
+
+
+def _concat_raw(raws):
+    """RawResults of consecutive object ranges -> one RawResults."""
+    import numpy as np
+
+    from krr_amd.core.engine import RawResults
+
+    if len(raws) == 1:
+        return raws[0]
+    return RawResults(*(np.concatenate([np.asarray(getattr(r, f)) for r in raws])
+                        for f in ("cpu_value", "cpu_count", "cpu_flags", "mem_value", "mem_count", "mem_flags")))
+
+
+def _concat_fleets(parts, device):
+    """PackedFleets of consecutive object ranges (HBM and/or host) -> one PackedFleet in HBM."""
+    import torch
+
+    from krr_amd.core.packing import PackedFleet, PackedSeries
+
+    dev = torch.device("cuda", int(device))
+
+    def cat(series):
+        vals, offs, base = [], [torch.zeros(1, dtype=torch.int64, device=dev)], 0
+        for ps in series:
+            v = ps.values if isinstance(ps.values, torch.Tensor) else torch.from_numpy(ps.values)
+            o = ps.offsets if isinstance(ps.offsets, torch.Tensor) else torch.from_numpy(ps.offsets)
+            vals.append(v.to(dev))
+            offs.append(o[1:].to(dev) + base)
+            base += int(o[-1])
+        return PackedSeries(torch.cat(vals), torch.cat(offs), max(int(ps.max_len) for ps in series))
+
+    return PackedFleet(cat([p.cpu for p in parts]), cat([p.mem for p in parts]))
 
 
 def _pinned_alloc_or_none():
