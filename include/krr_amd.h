@@ -295,7 +295,11 @@ int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* 
 /* Fold each series' rows_per_series rows (rows[(s * W + w) * row_words], e.g. its W time
  * slices after an all-to-all, in time order) left to right into ONE row out_rows[s * row_words]
  * of the same format: coins keyed by (kp->seed, series_base + s, kp->slice as the epoch, w).
- * LDS (3 row_words + 5 budget) x 8 bytes per series: KRR_E_CAPACITY past the device's LDS. */
+ * LDS per series: (3 row_words + 5 budget) x 8 bytes, whatever rows_per_series is (the fold
+ * is left to right, one row at a time); KRR_E_CAPACITY when that exceeds the device's LDS
+ * (160 KiB on gfx950).  With the query's extra budget bytes, rows that both fold and query
+ * satisfy 24 (16 + budget + tail) + 41 budget <= 163,840: budget 512 with any tail, 1024 with
+ * tail <= 4,037, 2048 with tail <= 1,264; budget 4096 builds but cannot fold. */
 int krr_kll_merge(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
                   const krr_kll_params* kp, int64_t series_base, uint64_t* out_rows, void* stream);
 
@@ -304,7 +308,8 @@ int krr_kll_merge(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const
  * n - r <= tail length: the exact tail key; else the smallest body key whose weighted count
  * of keys <= it exceeds r.  out_flags: KRR_FLAG_EMPTY, KRR_FLAG_NAN (value NaN),
  * KRR_FLAG_CAPACITY (a row overflowed its levels or formats differ; never expected).
- * REF_INDEX -> KRR_E_UNSUPPORTED. */
+ * LDS as krr_kll_merge plus budget bytes (the same KRR_E_CAPACITY rule, independent of
+ * rows_per_series).  REF_INDEX -> KRR_E_UNSUPPORTED. */
 int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,
                   const krr_kll_params* kp, int64_t series_base, const krr_percentile_params* params,
                   double* out_value, int64_t* out_count, uint32_t* out_flags, void* stream);

@@ -240,8 +240,8 @@ class BatchedRunner:
         total = int(cum[-1]) if n else 0
         share = min(max(float(self.hybrid_share), 0.02), 0.8)
         k = int(np.searchsorted(cum, (1.0 - share) * total, side="left")) + 1 if n else 0
-        k = min(max(k, 1), n)
-        if T < 3 or k >= n or n < 2:
+        k = min(max(k, 1), n - 1)
+        if T < 3 or n < 2:
             return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)]
         t_dev = max(1, T // 4)  # staging memcpy threads; the host parser gets the rest
         t_host = max(1, T - t_dev)

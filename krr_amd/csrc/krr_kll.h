@@ -34,6 +34,10 @@
 // compacted from level 0 up until `budget` keys remain, each level exported ascending.
 #pragma once
 
+#ifndef KRR_KLL_STREAM
+#define KRR_KLL_STREAM 0  // streaming loop form (kll_stream): 0 one chunk ahead, 1 ping-pong, 2 two ahead
+#endif
+
 namespace krr {
 
 constexpr int kKllHdr = 16;
@@ -480,7 +484,12 @@ __device__ __forceinline__ void kll_tail_count(const uint64_t* tb, uint32_t m, d
 // and tail + slack keys (> v, plus copies of v to reach `tail` when ties straddle it), all
 // counted exactly.  The first pivot is where 64 strided samples put the cut; a miss jumps by
 // the counted distance.  If no sample does, sort the buffer and keep exactly `tail`.
-__device__ KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
+#ifdef KRR_KLL_X_REFRESH_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__
+#endif
+KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
     const uint32_t m = ts.tl;
     double s = bitsd(sh.tb[(uint32_t)(((uint64_t)(uint32_t)lane * m) >> 6)]);
     s = kll_sort64(s, lane);
@@ -688,8 +697,10 @@ struct KllProc {
     }
 
     // Candidates: keys > tau (every present key until the buffer first fills).  A pair whose
-    // larger key is no candidate has none, so the per-slot tests run for hit pair columns only;
-    // a chunk adds at most 1,024 keys, so the buffer is refreshed first when less room is left.
+    // larger key is no candidate has none, so the per-slot tests run for hit pair columns only.
+    // The chunk's candidates are counted first and the buffer refreshed only when they do not
+    // fit: a refresh leaves <= tail + slack keys, so about 1,024 candidates arrive between two
+    // refreshes (refreshing whenever fewer than 1,024 slots were left made it one per ~64).
     template <bool FULL>
     __device__ __forceinline__ bool cand(double x) const {
         return FULL ? x > ts.tau : x == x;
@@ -703,8 +714,12 @@ struct KllProc {
             any |= pm[u];
         }
         if (!any) return;
-        if (ts.tl + 16u * kWave > tcap) {
-            ts = kll_tail_refresh(sh, ts, tail, lane);  // tau rises: recheck the pairs
+        uint32_t add = 0;  // the chunk's candidates (ballots recomputed below: no masks kept)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (pm[u]) add += popc64(ballot(cand<FULL>(a[u]))) + popc64(ballot(cand<FULL>(b[u])));
+        if (ts.tl + add > tcap) {
+            ts = kll_tail_refresh(sh, ts, tail, lane);  // tau rises: recheck the keys
 #pragma unroll
             for (int u = 0; u < 8; ++u) pm[u] = ballot(hi[u] > ts.tau);
         }
@@ -741,7 +756,9 @@ struct KllProc {
             lo[u] = fmin(a[u], b[u]);  // one NaN: both are the present sample
             hi[u] = fmax(a[u], b[u]);
         }
+#ifndef KRR_KLL_X_NOTAIL
         if (tail) tail_filter(a, b, hi);
+#endif
         double out[8];
         uint32_t c0 = 0;
         if (nanm == 0) {  // every slot present: 8 two-key compactions per lane
@@ -866,7 +883,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
     if (head) hv = vals[beg];
     if (tail) tv = vals[a1];
     const double2* __restrict__ zp = g_zero_chunk + lane;
-    auto fill_u = [&](double2 (&c)[kUnroll], int64_t ci) {
+    auto fill_u = [&](double2 (&c)[kUnroll], int64_t ci) __attribute__((always_inline)) {
         if (ci < nfull) {
             load_chunk(c, p + ci * CH);
         } else {
@@ -892,6 +909,36 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
             }
         }
     };
+#if KRR_KLL_STREAM == 1
+    // two chunks per iteration, ping-pong buffers: chunk ci + 1 in flight while ci is processed,
+    // no register copies (npad is a multiple of 8)
+    double2 A[kUnroll], B[kUnroll];
+    fill_u(A, 0);
+#pragma unroll 1
+    for (int64_t ci = 0; ci < npad; ci += 2) {
+        fill_u(B, ci + 1);
+        proc.chunk(A);
+        fill_u(A, ci + 2);
+        proc.chunk(B);
+    }
+#elif KRR_KLL_STREAM == 2
+    // two chunks in flight: ci + 1 and ci + 2 while ci is processed
+    double2 A[kUnroll], B[kUnroll], C[kUnroll];
+    fill_u(A, 0);
+    fill_u(B, 1);
+#pragma unroll 1
+    for (int64_t ci = 0; ci < npad; ci += 2) {
+        fill_u(C, ci + 2);
+        proc.chunk(A);
+        fill_u(A, ci + 3);
+        proc.chunk(B);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            B[u] = A[u];
+            A[u] = C[u];
+        }
+    }
+#else
     double2 cur[kUnroll], nxt[kUnroll];
     fill_u(nxt, 0);
 #pragma unroll
@@ -907,6 +954,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
     }
+#endif
 }
 
 // Level h's keys after the build (per-lane odd slots below 4: `has` / `kv` of this lane, the
@@ -1010,8 +1058,11 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
         if (tail) {
             KllTail ts = P.ts;
             if (ts.tl > tail + kKllTailSlack || (ts.tl > 2048 && ts.tl > tail)) ts = kll_tail_refresh(sh, ts, tail, lane);
+#ifndef KRR_KLL_X_NOREGSORT
             if (ts.tl <= 2048) kll_tail_sort(sh.tb, ts.tl, lane);
-            else kll_lds_sort(sh.tb, ts.tl, lane);
+            else
+#endif
+                kll_lds_sort(sh.tb, ts.tl, lane);
             tl_out = ts.tl < tail ? ts.tl : tail;
             for (uint32_t i = lane; i < tl_out; i += kWave) row[kKllHdr + budget + i] = sh.tb[ts.tl - tl_out + i];
             __syncthreads();

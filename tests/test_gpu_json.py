@@ -191,6 +191,43 @@ def test_recommend_from_bodies_device_equals_host():
            [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in b]
 
 
+@pytest.mark.parametrize("share", [0.02, 0.3, 0.8])
+def test_recommend_from_bodies_hybrid_equals_host(share):
+    """parser="hybrid": the last share of the objects parsed by the host packer while the
+    first part is parsed on the device (one kernel pass each) equals the host packer's path
+    result for result, at any split; the same through pack_from_bodies (one fleet in HBM);
+    a malformed body in either part gives the host packer's error on the whole batch."""
+    from krr_amd.core.prom_native import PrometheusResponseError
+    from krr_amd.core.runner import BatchedRunner
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    def finite(b):
+        return b.replace(b'"NaN"', b'"1"').replace(b'"+Inf"', b'"2"').replace(b'"-Inf"', b'"3"')
+
+    cpu = [[finite(b) for b in bodies] for bodies in _fleet(17, n_obj=80, max_samples=1500)]
+    mem = [[finite(b) for b in bodies] for bodies in _fleet(18, n_obj=80, max_samples=1500)]
+    runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(cpu_percentile="95", memory_buffer_percentage="7")))
+    want = [{k: (str(v.request), str(v.limit)) for k, v in r.items()}
+            for r in runner.recommend_from_bodies(cpu, mem, parser="host")]
+    runner.hybrid_share = share
+    got = runner.recommend_from_bodies(cpu, mem, parser="hybrid", threads=8)
+    assert runner.last_pack_via == ("hybrid", "hybrid") and 0 < runner.hybrid_last["split_object"] < 80
+    assert [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in got] == want
+    fleet = runner.pack_from_bodies(cpu, mem, threads=8, parser="hybrid")
+    assert fleet.cpu.values.is_cuda and fleet.n_objects == 80
+    got2 = runner.recommend_packed(fleet)
+    assert [{k: (str(v.request), str(v.limit)) for k, v in r.items()} for r in got2] == want
+    for bad_at in (0, 79):  # device part / host part
+        broken = [list(b) for b in cpu]
+        broken[bad_at] = [b'{"status":"error","errorType":"bad_data","error":"boom"}'] + broken[bad_at]
+        with pytest.raises(PrometheusResponseError) as e_h:
+            runner.recommend_from_bodies(broken, mem, parser="host")
+        runner.hybrid_share = share
+        with pytest.raises(PrometheusResponseError) as e_y:
+            runner.recommend_from_bodies(broken, mem, parser="hybrid", threads=8)
+        assert str(e_y.value) == str(e_h.value)
+
+
 # ---- grouped bodies (fleet PromQL batching): krr_json_parse_series + krr_pack_match_grouped ----
 
 def _recompact(b: bytes) -> bytes:

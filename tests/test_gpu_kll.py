@@ -310,3 +310,44 @@ def test_alternating_gaps_drive_odd_slot_cascades(ctx):
     x[::2] = np.nan
     _, got = _rows(ctx, x, offs, True, budget=512, tail=64)
     _check_rows(got, x, offs, True, 512, 64)
+
+
+@pytest.mark.parametrize("budget,tail", [(512, 4096), (1024, 4037), (1024, 4038), (2048, 1264), (2048, 1265),
+                                         (4096, 0)])
+def test_fold_and_query_lds_capacity(ctx, budget, tail):
+    """krr_kll_merge / krr_kll_query need a fixed amount of LDS per series whatever the number
+    of rows folded (include/krr_amd.h): (3 row_words + 5 budget) x 8 B for the fold, + budget
+    B for the query, against gfx950's 163,840 B; past it KRR_E_CAPACITY before any launch,
+    inside it the fold and the query equal the restatement (W = 40 rows per series: no
+    limit in W)."""
+    import torch
+
+    from krr_amd import _native
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    cfg = _cfg(budget, tail)
+    rng = np.random.default_rng(budget + tail)
+    offs, x = _fleet(rng, np.full(40, 3000))
+    ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, False)
+    rows = sketch.kll_build(ctx, ser, cfg)  # 40 slices of one series
+    prm = percentile_params(Decimal("99"), "linear")
+    fold_lds = (3 * (16 + budget + tail) + 5 * budget) * 8
+    r = rows.cpu().numpy().view(np.uint64)
+    if fold_lds > 163_840:
+        with pytest.raises(_native.NativeError) as e:
+            sketch.kll_merge(ctx, rows, 40, cfg)
+        assert e.value.code == _native.KRR_E_CAPACITY
+    else:
+        merged = sketch.kll_merge(ctx, rows, 40, cfg)
+        torch.cuda.synchronize()
+        assert np.array_equal(merged.cpu().numpy().view(np.uint64)[0], R.merge_rows(r, seed=SEED, series=0, epoch=0))
+    if fold_lds + budget > 163_840:
+        with pytest.raises(_native.NativeError) as e:
+            sketch.kll_query(ctx, rows, 40, cfg, prm)
+        assert e.value.code == _native.KRR_E_CAPACITY
+    else:
+        out = sketch.kll_query(ctx, rows, 40, cfg, prm)
+        torch.cuda.synchronize()
+        v, n, f = R.query(r, prm.mode, prm.p_num, prm.p_den, prm.q, seed=SEED, series=0, epoch=0)
+        assert out["value"].cpu().numpy()[0] == v and int(out["count"][0]) == n == 120_000

@@ -426,3 +426,14 @@ def test_bench_config4_strong_scaling_leg(world):
     assert r["config4_kernel_ms_max"] == max(r["config4_per_rank_kernel_ms"])
     if world > 1:
         assert len(r["config4_per_rank_gather_ms"]) == world
+
+
+def test_bench_sharded_host_path_two_ranks():
+    """N > 1 host path (gloo rehearsal): every rank packs ITS objects' query_range bodies on its
+    GPU with the hybrid parser (BatchedRunner.recommend_bodies_shard), rank 0 rounds the whole
+    fleet; the per-rank e2e times are reported and sampled objects of every shard equal the
+    host packer's path."""
+    r = _bench(["--gpus", "2", "--containers", "400", "--steps", "2", "--warmup", "1", "--parity-block", "64",
+                "--c4-containers", "0", "--no-cpu-baseline", "--host-objects", "300"], timeout=300)
+    assert r["e2e_parser"] == "hybrid" and len(r["e2e_per_rank_s"]) == 2 and r["e2e_objects_per_s"] > 0, r
+    assert r["e2e_sharded_equals_host_parse"] is True and r["e2e_parity_objects"] == 2 * 2 * 32
