@@ -428,7 +428,17 @@ struct KllTail {
     uint32_t tl;    // keys in the buffer
     uint32_t full;  // tau is active
     double tau;     // keys <= tau are not candidates
+#ifdef KRR_KLL_X_STATS  // profiling variant: refreshes / counting passes / sort fallbacks -> row word 14
+    uint32_t nref = 0, npass = 0, nfall = 0;
+#endif
 };
+#ifdef KRR_KLL_X_STATS
+#define KLL_STAT_COPY(dst, src) ((dst).nref = (src).nref, (dst).npass = (src).npass, (dst).nfall = (src).nfall)
+#define KLL_STAT_ADD(t, f) ((t).f += 1u)
+#else
+#define KLL_STAT_COPY(dst, src) ((void)0)
+#define KLL_STAT_ADD(t, f) ((void)0)
+#endif
 
 // In-place stable compaction: keep keys > v and the first `eq` copies of v.  Four keys per
 // lane per round, their LDS reads issued together.
@@ -455,7 +465,9 @@ __device__ KllTail kll_tail_keep(KllShared sh, KllTail ts, double v, uint32_t eq
         }
     }
     __syncthreads();
-    return KllTail{out, 1u, v};
+    KllTail r{out, 1u, v};
+    KLL_STAT_COPY(r, ts);
+    return r;
 }
 
 // (#keys > v, #keys >= v) of the tail buffer, eight LDS reads per lane in flight.
@@ -491,6 +503,7 @@ __device__
 #endif
 KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
     const uint32_t m = ts.tl;
+    KLL_STAT_ADD(ts, nref);
     double s = bitsd(sh.tb[(uint32_t)(((uint64_t)(uint32_t)lane * m) >> 6)]);
     s = kll_sort64(s, lane);
     const uint32_t want = tail + kKllTailSlack / 2;
@@ -502,6 +515,7 @@ KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
         const double v = bitsd(lane_bcast64(dbits(s), idx));
         uint32_t gt, ge;
         kll_tail_count(sh.tb, m, v, gt, ge, lane);
+        KLL_STAT_ADD(ts, npass);
         if (gt >= tail && gt <= tail + kKllTailSlack) return kll_tail_keep(sh, ts, v, 0, lane);
         if (gt < tail && ge >= tail) return kll_tail_keep(sh, ts, v, tail - gt, lane);
         // jump by the counted distance (about m / 64 keys between neighbouring samples)
@@ -518,7 +532,10 @@ KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
     kll_lds_sort(sh.tb, m, lane);  // exact fallback
     for (uint32_t i = lane; i < tail; i += kWave) sh.tb[i] = sh.tb[m - tail + i];
     __syncthreads();
-    return KllTail{tail, 1u, bitsd(uni64(sh.tb[0]))};
+    KllTail r{tail, 1u, bitsd(uni64(sh.tb[0]))};
+    KLL_STAT_COPY(r, ts);
+    KLL_STAT_ADD(r, nfall);
+    return r;
 }
 
 // 2,048 keys ascending across the wave in registers (lane l holds positions 32 l .. 32 l + 31):
@@ -1134,7 +1151,11 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
             row[7] = ((uint64_t)budget << 32) | tail;
 #pragma unroll
             for (int w = 0; w < 6; ++w) row[8 + w] = lw[w];
+#ifdef KRR_KLL_X_STATS
+            row[14] = ((uint64_t)P.ts.nfall << 48) | ((uint64_t)P.ts.npass << 24) | P.ts.nref;
+#else
             row[14] = 0;
+#endif
             row[15] = overflow ? kKllRowOverflow : 0ull;
         }
         __syncthreads();

@@ -9,6 +9,8 @@ import ctypes
 import os
 import sys
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -70,6 +72,12 @@ def main():
         print(f"{name}: k_kll_build median {ms:.3f} ms over {a.rounds} rounds, {gbs:.1f} GB/s "
               f"= {gbs / 8000:.3f} of 8 TB/s (S={S}, L={L}, budget={a.budget}, tail={a.tail})",
               flush=True)
+    for name, _, _ in libs:  # a KRR_KLL_X_STATS build: tail refresh statistics in row word 14
+        w = rows[name][:, 14].cpu().numpy().view(np.uint64).astype(np.int64)
+        if w.any():
+            nref, npass, nfall = w & 0xFFFFFF, (w >> 24) & 0xFFFFFF, w >> 48
+            print(f"{name}: per series: {nref.mean():.2f} tail refreshes, {npass.mean():.2f} counting passes, "
+                  f"{nfall.mean():.3f} sort fallbacks (max {nref.max()}, {npass.max()}, {nfall.max()})", flush=True)
     if a.check and len(libs) > 1:
         ref = rows[libs[0][0]]
         for name, _, _ in libs[1:]:
