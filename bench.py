@@ -1403,8 +1403,9 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
             return
         if method == "kll":
+            # events: before the body pass, between it and the tail pass, after the tail pass
             res = sketch.kll_time_sharded(ctx, ser_parts, kcfg, params, stream=stream,
-                                          events=None if ev is None else ev[0:2])
+                                          events=None if ev is None else (ev[0], ev[3], ev[1]))
             state["rows"], state["rows_per_series"] = res["rows"], res["rows_per_series"]
         elif method == "window":
             res = sketch.window_exact_time_sharded(ctx, ser_parts, params, ext_slots=T - Lr, stream=stream,
@@ -1468,6 +1469,12 @@ def run_config5(args, world, rank, local, dev, coll_dev):
         # every slot once + offsets + the exported rows
         kbytes = 8 * N + 8 * (S + 1) + 8 * kcfg.row_words * S
         kernels_ms["exchange_merge_query_ms"] = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+        if kcfg.tail > 0 and not kcfg.one_pass_tail:  # the body pass alone; the tail pass beside it
+            kms = float(np.mean([e[0].elapsed_time(e[3]) for e in evs]))
+            tms = float(np.mean([e[3].elapsed_time(e[1]) for e in evs]))
+            kernels_ms["k_kll_tail"] = tms
+            # every slot once + offsets + each row's header and body read + its tail written
+            tbytes = 8 * N + 8 * (S + 1) + 8 * (16 + kcfg.budget) * S + 8 * kcfg.tail * S
     elif method == "window":
         kname = "k_window_export"
         hdr = state["hdr"]
@@ -1533,6 +1540,17 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                             "alltoall_bytes_sent_per_rank": state["exchanged_bytes"],
                             "misses_per_step": state["misses"] / max(args.steps, 1),
                             "hbm_passes_per_step": 1}
+    if "k_kll_tail" in kernels_ms:
+        # the KLL build in two passes: the body (k_kll_build, above) and the exact tail
+        # (k_kll_tail, candidates above a threshold read from the row's body); both HBM streams
+        tms = kernels_ms["k_kll_tail"]
+        result["roofline_tail"] = {"kernel": "k_kll_tail", "bound": "hbm", "achieved": tbytes / (tms * 1e-3) / 1e9,
+                                   "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": tbytes / (tms * 1e-3) / HBM_PEAK,
+                                   "algorithmic_bytes_per_launch": tbytes}
+        result["kll_build_both_passes"] = {
+            "ms": kms + tms, "series_per_s": S / ((kms + tms) * 1e-3),
+            "frac_of_one_pass": kbytes / ((kms + tms) * 1e-3) / HBM_PEAK,
+            "definition": "body + tail passes together, against the bytes of ONE pass over the slice"}
     if method == "sketch":
         result["roofline_collect"] = {"kernel": "k_sketch_collect", "bound": "hbm",
                                       "achieved": cbytes / (cms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

@@ -279,18 +279,36 @@ typedef struct {
     int32_t slice;    /* build: this slice's index (coin key); merge / query: the fold epoch */
     uint64_t seed;    /* coins: (seed, series, slice or epoch, event) hashed */
     int32_t tail;     /* exact tail keys per row: [0, 4096] */
-    int32_t reserved;
+    int32_t reserved; /* flags: KRR_KLL_ONE_PASS_TAIL (build); 0 otherwise */
 } krr_kll_params;
+
+/* krr_kll_params.reserved: keep the tail inside the build's one pass (a running buffer of
+ * candidates above a rising threshold) instead of the default second pass over the slice
+ * (candidates above a threshold read from the row's own body).  Rows are identical. */
+#define KRR_KLL_ONE_PASS_TAIL 1
+/* Testing: the tail pass's threshold without its rank-bound margin, so the body's estimate
+ * often keeps fewer than `tail` keys and the pass streams the slice again (same rows). */
+#define KRR_KLL_TAIL_NO_MARGIN 2
+/* Build only the body: the tail words stay zero (word 6 = 0) until krr_kll_tail fills them
+ * (callers that time the two passes apart, e.g. bench.py). */
+#define KRR_KLL_BODY_ONLY 4
 
 /* uint64 words per row (16 + budget + tail), or < 0 if invalid. */
 int64_t krr_kll_row_words(const krr_kll_params* kp);
 
 /* rows[S * row_words] (device): one row per segment of `series` (gaps_are_nan respected:
  * NaN gaps are absent; a NaN sample in the compact layout is counted in row word 1).
+ * tail > 0: two launches on `stream` (k_kll_build, then k_kll_tail reading the slice again)
+ * unless KRR_KLL_ONE_PASS_TAIL; the tail pass needs max((tail + 1,152) x 8,
+ * (16 + budget) x 8 + budget) bytes of LDS.
  * seg_base: global index of segment 0 (coins depend on it).  KRR_E_UNSUPPORTED for
  * segments past ~130 M slots (run levels). */
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
                   uint64_t* rows, void* stream);
+
+/* The tail pass alone, on rows krr_kll_build wrote with KRR_KLL_BODY_ONLY (same series, same
+ * params): fills each row's tail words and word 6.  No-op when kp->tail == 0. */
+int krr_kll_tail(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, uint64_t* rows, void* stream);
 
 /* Fold each series' rows_per_series rows (rows[(s * W + w) * row_words], e.g. its W time
  * slices after an all-to-all, in time order) left to right into ONE row out_rows[s * row_words]

@@ -22,6 +22,9 @@ KRR_OK = 0
 KRR_E_INVALID = -1
 KRR_E_HIP = -2
 KRR_E_CAPACITY = -3
+KRR_KLL_ONE_PASS_TAIL = 1  # krr_kll_params.reserved (include/krr_amd.h)
+KRR_KLL_TAIL_NO_MARGIN = 2  # testing: the tail pass's fallback stream
+KRR_KLL_BODY_ONLY = 4  # the build leaves the tail to krr_kll_tail
 KRR_E_UNSUPPORTED = -4
 KRR_E_TIMEOUT = -5
 
@@ -64,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_query",
     "krr_kll_row_words",
     "krr_kll_build",
+    "krr_kll_tail",
     "krr_kll_merge",
     "krr_kll_query",
     "krr_sketch_locate",
@@ -274,6 +278,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_kll_row_words.restype = i64
         lib.krr_kll_build.argtypes = [vp, sp, kkp, i64, vp, vp]
         lib.krr_kll_build.restype = ctypes.c_int
+        lib.krr_kll_tail.argtypes = [vp, sp, kkp, vp, vp]
+        lib.krr_kll_tail.restype = ctypes.c_int
         lib.krr_kll_merge.argtypes = [vp, i64, i32, vp, kkp, i64, vp, vp]
         lib.krr_kll_merge.restype = ctypes.c_int
         lib.krr_kll_query.argtypes = [vp, i64, i32, vp, kkp, i64, pp, vp, vp, vp, vp]
@@ -555,6 +561,13 @@ class Context:
         _check_tensor(rows, "int64", S * self.kll_row_words(kp))
         self._check(self._lib.krr_kll_build(self._h, ctypes.byref(series), ctypes.byref(kp), int(seg_base),
                                             rows.data_ptr(), self._stream(stream)))
+
+    def kll_tail(self, series: KrrSeries, kp: KrrKllParams, rows, stream=None) -> None:
+        """The tail pass on rows built with KRR_KLL_BODY_ONLY (krr_kll_tail)."""
+        S = series.n_segments
+        _check_tensor(rows, "int64", S * self.kll_row_words(kp))
+        self._check(self._lib.krr_kll_tail(self._h, ctypes.byref(series), ctypes.byref(kp), rows.data_ptr(),
+                                           self._stream(stream)))
 
     def kll_merge(self, rows, rows_per_series: int, kp: KrrKllParams, out_rows, series_base: int = 0,
                   stream=None) -> None:

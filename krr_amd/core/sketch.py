@@ -651,9 +651,12 @@ class KllConfig:
     budget: int = 512
     tail: int = 0
     seed: int = 0x4B4C4C5345454431
+    one_pass_tail: bool = False  # KRR_KLL_ONE_PASS_TAIL: the tail inside the build (same rows)
+    tail_flags: int = 0          # further krr_kll_params.reserved bits (testing)
 
     def params(self, slice_id: int = 0) -> _native.KrrKllParams:
-        return _native.KrrKllParams(self.budget, int(slice_id), self.seed & (2 ** 64 - 1), self.tail, 0)
+        flags = self.tail_flags | (_native.KRR_KLL_ONE_PASS_TAIL if self.one_pass_tail else 0)
+        return _native.KrrKllParams(self.budget, int(slice_id), self.seed & (2 ** 64 - 1), self.tail, flags)
 
     @property
     def row_words(self) -> int:
@@ -674,9 +677,12 @@ class KllConfig:
 
 
 def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, seg_base: int = 0,
-              stream=None):
-    """One HBM pass: int64 [S, row_words] rows of this rank's slice of every series.
-    ``series``: a KrrSeries, or (lo, hi, KrrSeries) parts in buffers of their own."""
+              stream=None, events=None):
+    """int64 [S, row_words] rows of this rank's slice of every series: one HBM pass for the
+    body, and (tail > 0) the tail pass over the slice again (krr_kll_tail; one pass in all with
+    ``cfg.one_pass_tail``).  ``series``: a KrrSeries, or (lo, hi, KrrSeries) parts in buffers
+    of their own.  ``events`` (3 HIP events, optional): recorded on ``stream`` before the body
+    launches, between them and the tail launches, and after."""
     import torch
 
     parts = _parts(series)
@@ -685,9 +691,24 @@ def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, s
     S = parts[-1][1]
     dev = parts[0][2]._keep[0].device
     rows = torch.empty((max(S, 1), cfg.row_words), dtype=torch.int64, device=dev)
+    kp = cfg.params(slice_id)
+    split = cfg.tail > 0 and not cfg.one_pass_tail
+    if split:  # every body launch first, then every tail launch (timed apart)
+        kp.reserved |= _native.KRR_KLL_BODY_ONLY
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    if events is not None:
+        events[0].record(st)
     for lo, hi, ser in parts:
         if hi > lo:
-            ctx.kll_build(ser, cfg.params(slice_id), rows[lo:hi], seg_base=seg_base + lo, stream=stream)
+            ctx.kll_build(ser, kp, rows[lo:hi], seg_base=seg_base + lo, stream=st)
+    if events is not None:
+        events[1].record(st)
+    if split:
+        for lo, hi, ser in parts:
+            if hi > lo:
+                ctx.kll_tail(ser, kp, rows[lo:hi], stream=st)
+    if events is not None:
+        events[2].record(st)
     return rows[:S]
 
 
@@ -762,11 +783,8 @@ def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _nati
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     with torch.cuda.stream(st):
-        if events is not None:  # around the build pass (its HBM time), on the launch stream
-            events[0].record(st)
-        rows = kll_build(ctx, series, cfg, slice_id=rank, stream=st)
-        if events is not None:
-            events[1].record(st)
+        # events (optional, 3): before the body pass, between it and the tail pass, after
+        rows = kll_build(ctx, series, cfg, slice_id=rank, stream=st, events=events)
         S = rows.shape[0]
         lo, hi = owner_blocks(S, world)[rank] if world > 1 else (0, S)
         gathered, W = kll_exchange(rows, group)

@@ -3486,7 +3486,9 @@ int krr_create(int device, krr_ctx** out_ctx) {
                               (int)c->max_lds);
     for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
                           (const void*)k_window_export<false>, (const void*)k_window_merge,
-                          (const void*)k_kll_build, (const void*)k_kll_merge, (const void*)k_kll_query})
+                          (const void*)k_kll_build<false>, (const void*)k_kll_build<true>, (const void*)k_kll_tail,
+                          (const void*)k_kll_merge,
+                          (const void*)k_kll_query})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
     *out_ctx = c;
     return KRR_OK;
@@ -3844,9 +3846,15 @@ int64_t krr_kll_row_words(const krr_kll_params* kp) {
 
 // tail buffer keys: a refresh leaves <= tail + slack, a chunk adds <= 1,024; the final
 // compression's workspace (1,024 level keys + 512 carry) reuses it
+// Words of the region after tmp: the tail buffer (room for a chunk's 1,024 candidates past a
+// refresh's tail + slack), at least what the final stage needs beyond tmp's 512 words.
+#ifndef KRR_KLL_TAIL_ROOM
+#define KRR_KLL_TAIL_ROOM 512u
+#endif
 static uint32_t kll_tcap(int32_t tail) {
     const uint32_t t = tail > 0 ? (uint32_t)tail + 1024u + kKllTailSlack : 0u;
-    return t > 1536u ? t : 1536u;
+    const uint32_t fin = kKllFinalWords - 2u * kKllRun;
+    return t > fin ? t : fin;
 }
 
 static size_t kll_build_lds(int nrl, uint32_t tcap) {
@@ -3856,6 +3864,27 @@ static size_t kll_build_lds(int nrl, uint32_t tcap) {
 static size_t kll_merge_lds(const krr_kll_params* kp, bool query) {
     const size_t rw = (size_t)kKllHdr + kp->budget + kp->tail;
     return (3 * rw + 5 * (size_t)kp->budget) * 8 + (query ? (size_t)kp->budget : 0);
+}
+
+// The tail pass's LDS: its buffer (tail + slack + room for KRR_KLL_TAIL_ROOM candidates between
+// refreshes; columns of <= 128 keys go in one by one when a chunk brings more), which before the
+// stream holds the body keys and their levels.
+static void kll_tail_lds(const krr_kll_params* kp, uint32_t* tcap_t, size_t* lds_t) {
+    *tcap_t = (uint32_t)kp->tail + kKllTailSlack + KRR_KLL_TAIL_ROOM;
+    const size_t body_t = ((size_t)kKllHdr + kp->budget) * 8 + (size_t)kp->budget;
+    *lds_t = (size_t)*tcap_t * 8 > body_t ? (size_t)*tcap_t * 8 : body_t;
+}
+
+static int kll_tail_launch(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, uint64_t* rows,
+                           hipStream_t st) {
+    uint32_t tcap_t;
+    size_t lds_t;
+    kll_tail_lds(kp, &tcap_t, &lds_t);
+    const double two_ln = (kp->reserved & KRR_KLL_TAIL_NO_MARGIN) ? 0.0 : 2.0 * log(4.0 / 1e-3);
+    KllTailArgs T{series->values, series->offsets, series->n_segments, kp->budget, kp->tail, tcap_t, two_ln, rows};
+    hipLaunchKernelGGL(k_kll_tail, dim3(grid_for(series->n_segments)), dim3(64), lds_t, st, T);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
 }
 
 int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
@@ -3878,14 +3907,47 @@ int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* 
     if (kKllFirstRun + nrl > kKllLevels - 1)
         return set_err(ctx, KRR_E_UNSUPPORTED, "kll: segments of %s%lld slots need more run levels", "",
                        (long long)maxlen);
-    const uint32_t tcap = kll_tcap(kp->tail);
+    // tail > 0: by default the build leaves the tail to k_kll_tail (a second pass over the
+    // slice, candidates above a threshold read from the row's body; KRR_KLL_BODY_ONLY: the
+    // caller launches it, krr_kll_tail); KRR_KLL_ONE_PASS_TAIL keeps the running tail buffer
+    // inside the build.  The rows are the same either way.
+    const bool one_pass = kp->tail > 0 && (kp->reserved & KRR_KLL_ONE_PASS_TAIL);
+    const bool tail_pass = kp->tail > 0 && !one_pass;
+    const uint32_t tcap = kll_tcap(one_pass ? kp->tail : 0);
     const size_t lds = kll_build_lds(nrl, tcap);
     if (lds > ctx->max_lds) return set_err(ctx, KRR_E_CAPACITY, "kll build needs %s%lld B of LDS", "", (long long)lds);
+    uint32_t tcap_t;
+    size_t lds_t;
+    kll_tail_lds(kp, &tcap_t, &lds_t);
+    if (tail_pass && lds_t > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds_t);
     KllBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, kp->budget, kp->tail, nrl, tcap,
-                   (uint32_t)kp->slice, kp->seed, seg_base, rows};
-    hipLaunchKernelGGL(k_kll_build, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
+                   (uint32_t)kp->slice, kp->seed, seg_base, rows, tail_pass ? 1 : 0};
+    if (one_pass)
+        hipLaunchKernelGGL(k_kll_build<true>, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
+    else
+        hipLaunchKernelGGL(k_kll_build<false>, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
+    if (tail_pass && !(kp->reserved & KRR_KLL_BODY_ONLY)) return kll_tail_launch(ctx, series, kp, rows, (hipStream_t)stream);
     return KRR_OK;
+}
+
+int krr_kll_tail(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, uint64_t* rows, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    if (krr_kll_row_words(kp) < 0)
+        return set_err(ctx, KRR_E_INVALID, "kll: budget in [256, 4096] (a multiple of 64), tail in [0, 4096]%s", "");
+    if (series->n_segments == 0 || kp->tail == 0) return KRR_OK;
+    if (!rows) return set_err(ctx, KRR_E_INVALID, "null rows%s", "");
+    uint32_t tcap_t;
+    size_t lds_t;
+    kll_tail_lds(kp, &tcap_t, &lds_t);
+    if (lds_t > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds_t);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    return kll_tail_launch(ctx, series, kp, rows, (hipStream_t)stream);
 }
 
 static int kll_merge_common(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const uint64_t* rows,

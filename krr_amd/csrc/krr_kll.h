@@ -45,6 +45,8 @@ constexpr int kKllLevels = 24;
 constexpr int kKllRun = 256;
 constexpr int kKllFirstRun = 5;
 constexpr uint32_t kKllTailSlack = 128;  // a refresh leaves <= tail + slack keys in the buffer
+constexpr uint32_t kKllWsWords = 576;     // final stage: one level's keys (<= 513)
+constexpr uint32_t kKllFinalWords = kKllWsWords + 256;  // + the carry (<= 256), from tmp on
 // coin tags (oracle/kll_ref.py T_*)
 constexpr uint32_t kT_L0 = 0x100, kT_L1 = 0x200, kT_L2 = 0x300, kT_L3 = 0x400, kT_LODD = 0x800, kT_WAVE = 0x1000,
                    kT_RUN = 0x1100, kT_WODD = 0x1200, kT_FINAL = 0x1300, kT_FOLD = 0x2000;
@@ -339,6 +341,7 @@ struct KllBuildArgs {
     uint64_t seed;
     int64_t seg_base;
     uint64_t* rows;   // [S][kKllHdr + budget + tail]
+    int32_t tail_pass;  // the tail is left to k_kll_tail (zero tail words, word 6 = 0)
 };
 
 // ---- wave-level pieces, free functions of value arguments (the per-wave state below stays in
@@ -499,10 +502,11 @@ __device__ __forceinline__ void kll_tail_count(const uint64_t* tb, uint32_t m, d
 #ifdef KRR_KLL_X_REFRESH_NOINLINE
 __device__ __attribute__((noinline))
 #else
-__device__
+__device__ __forceinline__
 #endif
 KllTail kll_tail_refresh(KllShared sh, KllTail ts, uint32_t tail, int lane) {
     const uint32_t m = ts.tl;
+    if (m <= tail) return ts;  // nothing to drop (callers refresh a buffer of > tail keys)
     KLL_STAT_ADD(ts, nref);
     double s = bitsd(sh.tb[(uint32_t)(((uint64_t)(uint32_t)lane * m) >> 6)]);
     s = kll_sort64(s, lane);
@@ -611,7 +615,85 @@ __device__ void kll_tail_sort(uint64_t* tb, uint32_t m, int lane) {
     __syncthreads();
 }
 
+// ---- the exact tail's candidate filter (the build's, and the tail pass's) ----
+// Candidates: keys > tau (every present key until the buffer first fills).  A pair whose
+// larger key is no candidate has none, so the per-slot tests run for hit pair columns only.
+// The chunk's candidates are counted first and the buffer refreshed only when they do not
+// fit: a refresh leaves <= tail + slack keys, so about 1,024 candidates arrive between two
+// refreshes (refreshing whenever fewer than 1,024 slots were left made it one per ~64).
+template <bool FULL>
+__device__ __forceinline__ bool kll_cand(const KllTail& ts, double x) {
+    return FULL ? x > ts.tau : x == x;
+}
+template <bool FULL>
+__device__ __forceinline__ void kll_tail_append(KllShared sh, KllTail& ts, uint32_t tail, uint32_t tcap, int lane,
+                                                const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
+    uint64_t pm[8], any = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        pm[u] = ballot(kll_cand<FULL>(ts, hi[u]));
+        any |= pm[u];
+    }
+    if (!any) return;
+    uint32_t add = 0;  // the chunk's candidates (ballots recomputed below: no masks kept)
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        if (pm[u]) add += popc64(ballot(kll_cand<FULL>(ts, a[u]))) + popc64(ballot(kll_cand<FULL>(ts, b[u])));
+    bool column_wise = false;
+    if (ts.tl + add > tcap) {
+        if (ts.tl > tail + kKllTailSlack) {  // a refresh leaves <= tail + slack: only then can it help
+            ts = kll_tail_refresh(sh, ts, tail, lane);  // tau rises: recheck the keys
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pm[u] = ballot(hi[u] > ts.tau);
+        }
+        // a buffer with less room than a whole chunk (the tail pass's): columns of <= 128 keys
+        // one by one, refreshing when one does not fit (the buffer then holds > tail keys)
+        column_wise = tcap < tail + kKllTailSlack + 16u * kWave;
+    }
+    uint32_t tl = ts.tl;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        if (pm[u]) {
+            uint64_t ma = ballot(ts.full ? a[u] > ts.tau : a[u] == a[u]);
+            uint64_t mb = ballot(ts.full ? b[u] > ts.tau : b[u] == b[u]);
+            if (column_wise && tl + popc64(ma) + popc64(mb) > tcap) {  // <= 128 keys: fits after it
+                ts.tl = tl;
+                ts = kll_tail_refresh(sh, ts, tail, lane);
+                tl = ts.tl;
+                ma = ballot(a[u] > ts.tau);
+                mb = ballot(b[u] > ts.tau);
+            }
+            if ((ma >> lane) & 1ull) sh.tb[tl + lane_prefix(ma)] = dbits(a[u] + 0.0);  // -0 -> +0
+            tl += popc64(ma);
+            if ((mb >> lane) & 1ull) sh.tb[tl + lane_prefix(mb)] = dbits(b[u] + 0.0);
+            tl += popc64(mb);
+        }
+    }
+    ts.tl = tl;
+}
+__device__ __forceinline__ void kll_tail_filter(KllShared sh, KllTail& ts, uint32_t tail, uint32_t tcap, int lane,
+                                                const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
+    if (ts.full) kll_tail_append<true>(sh, ts, tail, tcap, lane, a, b, hi);
+    else kll_tail_append<false>(sh, ts, tail, tcap, lane, a, b, hi);
+}
+
+// The buffer's top min(n, tail) keys, ascending, into the row's tail words; returns how many.
+__device__ __forceinline__ uint32_t kll_tail_export(KllShared sh, KllTail ts, uint32_t tail, uint64_t* row_tail, int lane) {
+    if (ts.tl > tail + kKllTailSlack || (ts.tl > 2048 && ts.tl > tail)) ts = kll_tail_refresh(sh, ts, tail, lane);
+#ifndef KRR_KLL_X_NOREGSORT
+    if (ts.tl <= 2048) kll_tail_sort(sh.tb, ts.tl, lane);
+    else
+#endif
+        kll_lds_sort(sh.tb, ts.tl, lane);
+    const uint32_t tl_out = ts.tl < tail ? ts.tl : tail;
+    for (uint32_t i = lane; i < tl_out; i += kWave) row_tail[i] = sh.tb[ts.tl - tl_out + i];
+    for (uint32_t i = tl_out + lane; i < tail; i += kWave) row_tail[i] = 0;  // canonical rows
+    __syncthreads();
+    return tl_out;
+}
+
 // Per-wave build state; one instance per series slice (by value: nothing is address-taken).
+template <bool TAIL>  // TAIL: the one-pass tail buffer is part of this build
 struct KllProc {
     KllShared sh;
     uint64_t base;
@@ -713,50 +795,8 @@ struct KllProc {
         w2u += kll_push(sh, base, nrl, 0, C >> 1, kKllFirstRun, lane);
     }
 
-    // Candidates: keys > tau (every present key until the buffer first fills).  A pair whose
-    // larger key is no candidate has none, so the per-slot tests run for hit pair columns only.
-    // The chunk's candidates are counted first and the buffer refreshed only when they do not
-    // fit: a refresh leaves <= tail + slack keys, so about 1,024 candidates arrive between two
-    // refreshes (refreshing whenever fewer than 1,024 slots were left made it one per ~64).
-    template <bool FULL>
-    __device__ __forceinline__ bool cand(double x) const {
-        return FULL ? x > ts.tau : x == x;
-    }
-    template <bool FULL>
-    __device__ __forceinline__ void tail_append(const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
-        uint64_t pm[8], any = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            pm[u] = ballot(cand<FULL>(hi[u]));
-            any |= pm[u];
-        }
-        if (!any) return;
-        uint32_t add = 0;  // the chunk's candidates (ballots recomputed below: no masks kept)
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (pm[u]) add += popc64(ballot(cand<FULL>(a[u]))) + popc64(ballot(cand<FULL>(b[u])));
-        if (ts.tl + add > tcap) {
-            ts = kll_tail_refresh(sh, ts, tail, lane);  // tau rises: recheck the keys
-#pragma unroll
-            for (int u = 0; u < 8; ++u) pm[u] = ballot(hi[u] > ts.tau);
-        }
-        uint32_t tl = ts.tl;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (pm[u]) {
-                const uint64_t ma = ballot(ts.full ? a[u] > ts.tau : a[u] == a[u]);
-                const uint64_t mb = ballot(ts.full ? b[u] > ts.tau : b[u] == b[u]);
-                if ((ma >> lane) & 1ull) sh.tb[tl + lane_prefix(ma)] = dbits(a[u] + 0.0);  // -0 -> +0
-                tl += popc64(ma);
-                if ((mb >> lane) & 1ull) sh.tb[tl + lane_prefix(mb)] = dbits(b[u] + 0.0);
-                tl += popc64(mb);
-            }
-        }
-        ts.tl = tl;
-    }
     __device__ __forceinline__ void tail_filter(const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
-        if (ts.full) tail_append<true>(a, b, hi);
-        else tail_append<false>(a, b, hi);
+        kll_tail_filter(sh, ts, tail, tcap, lane, a, b, hi);
     }
 
     // ---- one chunk ----
@@ -774,7 +814,9 @@ struct KllProc {
             hi[u] = fmax(a[u], b[u]);
         }
 #ifndef KRR_KLL_X_NOTAIL
-        if (tail) tail_filter(a, b, hi);
+        if constexpr (TAIL) {
+            if (tail) tail_filter(a, b, hi);
+        }
 #endif
         double out[8];
         uint32_t c0 = 0;
@@ -879,7 +921,7 @@ struct KllProc {
 // The streaming loop of stream_segment (ONE_SITE, one chunk in flight), run for npad chunks:
 // chunks past the segment's last are all NaN (the flush), and the head / tail slots ride the
 // last real chunk only.
-template <class Proc>
+template <class Proc, int MODE = KRR_KLL_STREAM>
 __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int64_t beg, int64_t end, int64_t npad,
                                            Proc& proc, int lane) {
     int64_t a0 = (beg + 1) & ~(int64_t)1;
@@ -926,7 +968,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
             }
         }
     };
-#if KRR_KLL_STREAM == 1
+    if constexpr (MODE == 1) {
     // two chunks per iteration, ping-pong buffers: chunk ci + 1 in flight while ci is processed,
     // no register copies (npad is a multiple of 8)
     double2 A[kUnroll], B[kUnroll];
@@ -938,7 +980,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
         fill_u(A, ci + 2);
         proc.chunk(B);
     }
-#elif KRR_KLL_STREAM == 2
+    } else if constexpr (MODE == 2) {
     // two chunks in flight: ci + 1 and ci + 2 while ci is processed
     double2 A[kUnroll], B[kUnroll], C[kUnroll];
     fill_u(A, 0);
@@ -955,7 +997,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
             A[u] = C[u];
         }
     }
-#else
+    } else {
     double2 cur[kUnroll], nxt[kUnroll];
     fill_u(nxt, 0);
 #pragma unroll
@@ -971,7 +1013,7 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) cur[u] = nxt[u];
     }
-#endif
+    }
 }
 
 // Level h's keys after the build (per-lane odd slots below 4: `has` / `kv` of this lane, the
@@ -1010,6 +1052,9 @@ __device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t 
 #ifndef KRR_KLL_WAVES_PER_SIMD
 #define KRR_KLL_WAVES_PER_SIMD 1  // the build's LDS (runs + tail buffer) allows one wave per SIMD anyway
 #endif
+// TAIL = false: no tail (tail == 0) or the tail left to k_kll_tail (A.tail_pass); the build then
+// holds none of the tail buffer's code or state.
+template <bool TAIL>
 __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1037,14 +1082,14 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
         uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t nch = kll_nchunks(beg, end);
         const int64_t npad = (nch + 7) & ~(int64_t)7;
-        KllProc P;
+        KllProc<TAIL> P;
         P.sh = sh;
         P.base = kll_slice_base(A.seed, series, A.slice);
         P.w2u = 0;
         P.ci = 0;
         P.lane = lane;
         P.nrl = A.nrl;
-        P.tail = tail;
+        P.tail = A.tail_pass ? 0u : tail;
         P.tcap = A.tcap;
         P.ts = KllTail{0u, 0u, 0.0};
 #pragma unroll
@@ -1071,24 +1116,20 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
         const uint64_t gmax = dbits(bitsd(lane_bcast64(wave_scan64(dbits(P.kmax), kQuietNaN, OpMaxF64Bits{}), kWave - 1)) + 0.0);
 
         // tail: the min(n, tail) largest present keys, ascending
+        // tail: the min(n, tail) largest present keys, ascending (the tail pass writes them
+        // instead when A.tail_pass: this launch leaves them zero)
         uint32_t tl_out = 0;
-        if (tail) {
-            KllTail ts = P.ts;
-            if (ts.tl > tail + kKllTailSlack || (ts.tl > 2048 && ts.tl > tail)) ts = kll_tail_refresh(sh, ts, tail, lane);
-#ifndef KRR_KLL_X_NOREGSORT
-            if (ts.tl <= 2048) kll_tail_sort(sh.tb, ts.tl, lane);
-            else
-#endif
-                kll_lds_sort(sh.tb, ts.tl, lane);
-            tl_out = ts.tl < tail ? ts.tl : tail;
-            for (uint32_t i = lane; i < tl_out; i += kWave) row[kKllHdr + budget + i] = sh.tb[ts.tl - tl_out + i];
-            __syncthreads();
+        if constexpr (TAIL) {
+            if (tail && !A.tail_pass) tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
         }
 
         // body: from level 0 up, while more than `budget` keys remain, compact each level of
         // >= 2 keys once (odd largest set aside) into the next; export every level ascending
-        uint64_t* ws = sh.tb;                // level keys (<= 256 + carry + 64 + 1)
-        uint64_t* cbuf = sh.tb + 1024;       // carry (<= 512)
+        // level keys: a run (<= 256) + the carry (<= 256) + lane odd slots (<= 64, levels < 4) or
+        // the wave slot (1): <= 513; carry <= 256.  They start at tmp (free after the stream)
+        // and run into the tail buffer (already exported): kKllFinalWords in all.
+        uint64_t* ws = sh.tmp;
+        uint64_t* cbuf = sh.tmp + kKllWsWords;
         uint64_t total = 0;
 #pragma unroll 1
         for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
@@ -1139,7 +1180,8 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
         }
         const bool overflow = uni32(sh.misc[1]) != 0;
         for (uint32_t i = pos + lane; i < budget; i += kWave) row[kKllHdr + i] = 0;  // canonical rows: unused words 0
-        for (uint32_t i = tl_out + lane; i < tail; i += kWave) row[kKllHdr + budget + i] = 0;
+        if (A.tail_pass)
+            for (uint32_t i = lane; i < tail; i += kWave) row[kKllHdr + budget + i] = 0;
         if (lane == 0) {
             row[0] = n_pres;
             row[1] = A.gaps ? 0ull : (uint64_t)(end - beg) - n_pres;
@@ -1410,6 +1452,111 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
             A.out_n[s] = (int64_t)n;
             A.out_f[s] = flags;
         }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The exact tail in a pass of its own (the default when tail > 0): k_kll_build runs without the
+// tail buffer (A.tail_pass: fewer VGPRs live, the LDS of a tail-less build, so more waves per
+// CU), then this pass streams each series slice again and keeps the keys >= a threshold tau0
+// read from the row's own body: the body key at estimated rank q = n - tail - 1 - M, M the
+// row's rank bound sqrt(2 ln(4/delta) sum w^2) at delta = 1e-3.  Every key >= tau0 is a
+// candidate, so the buffer holds at least tail keys unless the body's estimate was off by more
+// than M; then the slice is streamed once more with every present key a candidate.  Refreshes
+// (tau rising, as in the build) keep the buffer within its capacity.  Either way the tail words
+// are the top min(n, tail) present keys, exactly what the one-pass build writes: rows are the
+// same bit for bit (oracle/kll_ref.py does not depend on how the tail is found).
+struct KllTailArgs {
+    const double* vals;
+    const int64_t* offs;
+    int64_t S;
+    int32_t budget;
+    int32_t tail;
+    uint32_t tcap;
+    double two_ln;    // 2 ln(4 / delta)
+    uint64_t* rows;
+};
+
+struct KllTailProc {
+    KllShared sh;
+    KllTail ts;
+    uint32_t tail, tcap;
+    int lane;
+    __device__ __forceinline__ void chunk(const double2 (&c)[kUnroll]) {
+        double a[8], b[8], hi[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a[u] = c[u].x;
+            b[u] = c[u].y;
+            hi[u] = fmax(a[u], b[u]);  // one NaN: the present sample
+        }
+        kll_tail_filter(sh, ts, tail, tcap, lane, a, b, hi);
+    }
+};
+
+#ifndef KRR_KLL_TAIL_MARGIN
+#define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
+#endif
+#ifndef KRR_KLL_TAIL_WAVES_PER_SIMD
+#define KRR_KLL_TAIL_WAVES_PER_SIMD 2
+#endif
+__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(KllTailArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
+    KllShared sh{};
+    sh.tb = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* im = sh.tb;  // body keys at im[kKllHdr + i] (kll_body_select's layout), before the stream
+    uint8_t* lvl = reinterpret_cast<uint8_t*>(im + kKllHdr + budget);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        uint64_t* row = A.rows + (size_t)s * RW;
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        const uint64_t n = uni64(row[0]);
+        const double M = ceil(KRR_KLL_TAIL_MARGIN * sqrt(A.two_ln * (double)uni64(row[4])));
+        const double qd = (double)n - (double)tail - 1.0 - M;
+        bool full0 = false;
+        double tau = 0.0;
+        if (qd >= 0.0) {
+            uint32_t m = 0;
+            for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+                const uint32_t l = kll_len(row, h);
+                for (uint32_t i = lane; i < l; i += kWave) {
+                    lvl[m + i] = (uint8_t)h;
+                    im[kKllHdr + m + i] = row[kKllHdr + m + i];
+                }
+                m += l;
+            }
+            __syncthreads();
+            const double t0 = bitsd(okey_inv(kll_body_select(im, lvl, m, (uint64_t)qd, lane)));
+            __syncthreads();
+            if (t0 > -__builtin_inf()) {  // candidates: keys >= t0 (t0 == -inf: every present key)
+                full0 = true;
+                // the next double below t0 (bit arithmetic: no libm call in the kernel)
+                const uint64_t tb0 = dbits(t0);
+                tau = t0 == 0.0 ? bitsd(0x8000000000000001ull) : bitsd(t0 > 0.0 ? tb0 - 1u : tb0 + 1u);
+            }
+        }
+        const int64_t nch = kll_nchunks(beg, end);
+        const int64_t npad = (nch + 1) & ~(int64_t)1;
+        KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
+        uint32_t restreams = 0;
+#pragma unroll 1
+        for (int pass = 0; pass < 2; ++pass) {
+            kll_stream<KllTailProc, 2>(A.vals, beg, end, npad, P, lane);
+            if (!(full0 && P.ts.tl < tail)) break;
+            full0 = false;  // the estimate missed: once more, every present key a candidate
+            P.ts = KllTail{0u, 0u, 0.0};
+            ++restreams;
+        }
+        (void)restreams;
+        const uint32_t tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
+        if (lane == 0) row[6] = tl_out;
+#ifdef KRR_KLL_X_STATS  // refreshes | counting passes << 24 | (full restreams << 8 | sort fallbacks) << 48
+        if (lane == 0)
+            row[14] = ((uint64_t)((restreams << 8) | P.ts.nfall) << 48) | ((uint64_t)P.ts.npass << 24) | P.ts.nref;
+#endif
         __syncthreads();
     }
 }

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--gaps", action="store_true", help="config-2-style NaN gaps")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--one-pass", action="store_true", help="KRR_KLL_ONE_PASS_TAIL: the tail inside the build")
     a = ap.parse_args()
     import torch
 
@@ -49,7 +50,7 @@ def main():
     else:
         ctx.synth_fill_window(vals, offs, 1000003 * 6, 0, 0, False, 0, L)
     ser = ctx.series(vals, offs, L, a.gaps)
-    kp = _native.KrrKllParams(a.budget, 0, 0x4B4C4C5345454431, a.tail, 0)
+    kp = _native.KrrKllParams(a.budget, 0, 0x4B4C4C5345454431, a.tail, 1 if a.one_pass else 0)
     rw = int(base.krr_kll_row_words(ctypes.byref(kp)))
     rows = {name: torch.empty((S, rw), dtype=torch.int64, device=dev) for name, _, _ in libs}
     st = torch.cuda.current_stream()
@@ -57,7 +58,7 @@ def main():
     for r in range(a.rounds + 1):
         for name, lib, h in libs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
+            e0.record(st)  # both launches when the tail has a pass of its own
             rc = lib.krr_kll_build(h, ctypes.byref(ser), ctypes.byref(kp), 0, rows[name].data_ptr(),
                                    ctypes.c_void_p(st.cuda_stream))
             e1.record(st)
@@ -69,15 +70,16 @@ def main():
     for name, _, _ in libs:
         ms = sorted(times[name])[len(times[name]) // 2]
         gbs = nbytes / (ms * 1e-3) / 1e9
-        print(f"{name}: k_kll_build median {ms:.3f} ms over {a.rounds} rounds, {gbs:.1f} GB/s "
+        print(f"{name}: krr_kll_build{' (one pass)' if a.one_pass else ''} median {ms:.3f} ms over {a.rounds} rounds, {gbs:.1f} GB/s "
               f"= {gbs / 8000:.3f} of 8 TB/s (S={S}, L={L}, budget={a.budget}, tail={a.tail})",
               flush=True)
     for name, _, _ in libs:  # a KRR_KLL_X_STATS build: tail refresh statistics in row word 14
         w = rows[name][:, 14].cpu().numpy().view(np.uint64).astype(np.int64)
         if w.any():
-            nref, npass, nfall = w & 0xFFFFFF, (w >> 24) & 0xFFFFFF, w >> 48
+            nref, npass, nfall, nre = w & 0xFFFFFF, (w >> 24) & 0xFFFFFF, (w >> 48) & 0xFF, w >> 56
             print(f"{name}: per series: {nref.mean():.2f} tail refreshes, {npass.mean():.2f} counting passes, "
-                  f"{nfall.mean():.3f} sort fallbacks (max {nref.max()}, {npass.max()}, {nfall.max()})", flush=True)
+                  f"{nfall.mean():.3f} sort fallbacks, {nre.mean():.4f} tail-pass restreams "
+                  f"(max {nref.max()}, {npass.max()}, {nfall.max()}, {nre.max()})", flush=True)
     if a.check and len(libs) > 1:
         ref = rows[libs[0][0]]
         for name, _, _ in libs[1:]:

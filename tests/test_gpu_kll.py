@@ -53,18 +53,23 @@ LENS = [0, 1, 2, 3, 300, 511, 512, 513, 1023, 1024, 1025, 1026, 2047, 2048, 5000
         43_200]
 
 
-def _cfg(budget=512, tail=0):
+# how the build finds the tail (include/krr_amd.h): the default second pass over the slice, the
+# one-pass running buffer, and the second pass with no margin (its fallback stream taken often)
+TAIL_MODES = {"pass": {}, "one_pass": {"one_pass_tail": True}, "no_margin": {"tail_flags": 2}}
+
+
+def _cfg(budget=512, tail=0, mode="pass"):
     from krr_amd.core import sketch
 
-    return sketch.KllConfig(budget=budget, tail=tail, seed=SEED)
+    return sketch.KllConfig(budget=budget, tail=tail, seed=SEED, **TAIL_MODES[mode])
 
 
-def _rows(ctx, x, offs, gaps, budget=512, tail=0, slice_id=0, seg_base=0):
+def _rows(ctx, x, offs, gaps, budget=512, tail=0, slice_id=0, seg_base=0, mode="pass"):
     import torch
 
     from krr_amd.core import sketch
 
-    cfg = _cfg(budget, tail)
+    cfg = _cfg(budget, tail, mode)
     ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, gaps)
     rows = sketch.kll_build(ctx, ser, cfg, slice_id=slice_id, seg_base=seg_base)
     torch.cuda.synchronize()
@@ -79,30 +84,35 @@ def _check_rows(got, x, offs, gaps, budget, tail, slice_id=0, seg_base=0):
                                               want[:R.HDR].tolist())
 
 
+@pytest.mark.parametrize("mode", list(TAIL_MODES))
 @pytest.mark.parametrize("gaps", [False, True])
 @pytest.mark.parametrize("budget,tail", [(256, 0), (512, 64), (1024, 1792)])
-def test_rows_match_restatement(ctx, gaps, budget, tail):
+def test_rows_match_restatement(ctx, gaps, budget, tail, mode):
+    if tail == 0 and mode != "pass":
+        pytest.skip("no tail: one launch either way")
     rng = np.random.default_rng(budget + gaps + tail)
     lens = rng.permutation(np.array(LENS * 2))
     offs, x = _fleet(rng, lens)
     if gaps:
         x[rng.random(x.size) < 0.15] = np.nan
-    _, got = _rows(ctx, x, offs, gaps, budget=budget, tail=tail, seg_base=17)
+    _, got = _rows(ctx, x, offs, gaps, budget=budget, tail=tail, seg_base=17, mode=mode)
     _check_rows(got, x, offs, gaps, budget, tail, seg_base=17)
 
 
-def test_odd_offsets_heads_and_long_carry(ctx):
+@pytest.mark.parametrize("mode", list(TAIL_MODES))
+def test_odd_offsets_heads_and_long_carry(ctx, mode):
     """Segments starting at odd slots (stream_segment's head/tail slots) and long segments
     whose run counter carries to the top."""
     rng = np.random.default_rng(5)
     lens = np.array([3, 1025, 7, 1027, 1, 172_801, 2049, 70_001])
     offs, x = _fleet(rng, lens)
-    _, got = _rows(ctx, x, offs, False, tail=256)
+    _, got = _rows(ctx, x, offs, False, tail=256, mode=mode)
     _check_rows(got, x, offs, False, 512, 256)
 
 
+@pytest.mark.parametrize("mode", list(TAIL_MODES))
 @pytest.mark.parametrize("shape", ["increasing", "quantized", "decreasing", "runs_of_gaps"])
-def test_tail_refresh_paths_match_restatement(ctx, shape):
+def test_tail_refresh_paths_match_restatement(ctx, shape, mode):
     """Inputs that drive the tail buffer's refresh hard: sorted ascending (every key is a new
     candidate), heavy ties around the cut (the tie-keeping rule), descending (one fill, no
     refresh), and long gap runs."""
@@ -124,7 +134,7 @@ def test_tail_refresh_paths_match_restatement(ctx, shape):
     x = np.concatenate(parts)
     gaps = shape == "runs_of_gaps"
     for tail in (64, 1000, 2048):
-        _, got = _rows(ctx, x, offs, gaps, budget=512, tail=tail)
+        _, got = _rows(ctx, x, offs, gaps, budget=512, tail=tail, mode=mode)
         _check_rows(got, x, offs, gaps, 512, tail)
 
 
@@ -351,3 +361,35 @@ def test_fold_and_query_lds_capacity(ctx, budget, tail):
         torch.cuda.synchronize()
         v, n, f = R.query(r, prm.mode, prm.p_num, prm.p_den, prm.q, seed=SEED, series=0, epoch=0)
         assert out["value"].cpu().numpy()[0] == v and int(out["count"][0]) == n == 120_000
+
+
+def test_combined_launch_equals_split_passes(ctx):
+    """krr_kll_build with tail > 0 and no flags launches the body and the tail pass itself;
+    KRR_KLL_BODY_ONLY + krr_kll_tail (what krr_amd.core.sketch.kll_build does, timing them
+    apart) and KRR_KLL_ONE_PASS_TAIL give the same rows; the body-only rows carry no tail."""
+    import torch
+
+    from krr_amd import _native
+
+    rng = np.random.default_rng(77)
+    lens = np.array([0, 5, 1800, 1900, 4097, 60_000, 172_800])
+    offs, x = _fleet(rng, lens)
+    ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, False)
+    cfg = _cfg(512, 1792)
+    rw = cfg.row_words
+    out = {}
+    for name, flags in (("combined", 0), ("one_pass", _native.KRR_KLL_ONE_PASS_TAIL),
+                        ("body", _native.KRR_KLL_BODY_ONLY)):
+        kp = cfg.params(0)
+        kp.reserved = flags
+        rows = torch.full((lens.size, rw), -1, dtype=torch.int64, device="cuda:0")
+        ctx.kll_build(ser, kp, rows)
+        if name == "body":
+            torch.cuda.synchronize()
+            body = rows.cpu().numpy().view(np.uint64)
+            assert not body[:, 16 + 512:].any() and not body[:, 6].any()
+            ctx.kll_tail(ser, kp, rows)
+        torch.cuda.synchronize()
+        out[name] = rows.cpu().numpy().view(np.uint64)
+    assert np.array_equal(out["combined"], out["one_pass"]) and np.array_equal(out["combined"], out["body"])
+    _check_rows(out["combined"], x, offs, False, 512, 1792)
