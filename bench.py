@@ -1569,6 +1569,11 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                 and int(tr[key].get("slots_per_rank", N)) == N):  # the same slice size per rank
             result["roofline"]["traffic"] = tr[key]["hbm_bytes_per_launch"]
             result["roofline"]["traffic_source"] = tr[key].get("source")
+        tkey = f"config5:{params_mode(args)}:p{args.percentile}:k_kll_tail"
+        if ("roofline_tail" in result and tkey in tr and int(tr[tkey].get("containers_per_rank", -1)) == S
+                and int(tr[tkey].get("slots_per_rank", N)) == N):
+            result["roofline_tail"]["traffic"] = tr[tkey]["hbm_bytes_per_launch"]
+            result["roofline_tail"]["traffic_source"] = tr[tkey].get("source")
     except (OSError, ValueError):
         pass
     # parity / rank error on a sample of series, regathered whole on rank 0
