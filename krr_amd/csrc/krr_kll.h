@@ -635,10 +635,17 @@ __device__ __forceinline__ void kll_tail_append(KllShared sh, KllTail& ts, uint3
         any |= pm[u];
     }
     if (!any) return;
-    uint32_t add = 0;  // the chunk's candidates (ballots recomputed below: no masks kept)
+    // the chunk's candidates: at most two per hit pair; counted exactly (ballots recomputed
+    // below: no masks kept) only when that bound does not fit
+    uint32_t add = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-        if (pm[u]) add += popc64(ballot(kll_cand<FULL>(ts, a[u]))) + popc64(ballot(kll_cand<FULL>(ts, b[u])));
+    for (int u = 0; u < 8; ++u) add += 2u * popc64(pm[u]);
+    if (ts.tl + add > tcap) {
+        add = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (pm[u]) add += popc64(ballot(kll_cand<FULL>(ts, a[u]))) + popc64(ballot(kll_cand<FULL>(ts, b[u])));
+    }
     bool column_wise = false;
     if (ts.tl + add > tcap) {
         if (ts.tl > tail + kKllTailSlack) {  // a refresh leaves <= tail + slack: only then can it help
@@ -979,6 +986,21 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
         proc.chunk(A);
         fill_u(A, ci + 2);
         proc.chunk(B);
+    }
+    } else if constexpr (MODE == 3) {
+    // two chunks in flight, three buffers rotated by unrolling by 3 (no register copies);
+    // npad is a multiple of 3
+    double2 A[kUnroll], B[kUnroll], C[kUnroll];
+    fill_u(A, 0);
+    fill_u(B, 1);
+#pragma unroll 1
+    for (int64_t ci = 0; ci < npad; ci += 3) {
+        fill_u(C, ci + 2);
+        proc.chunk(A);
+        fill_u(A, ci + 3);
+        proc.chunk(B);
+        fill_u(B, ci + 4);
+        proc.chunk(C);
     }
     } else if constexpr (MODE == 2) {
     // two chunks in flight: ci + 1 and ci + 2 while ci is processed
@@ -1495,6 +1517,9 @@ struct KllTailProc {
     }
 };
 
+#ifndef KRR_KLL_TAIL_STREAM
+#define KRR_KLL_TAIL_STREAM 2  // kll_stream form of the tail pass (2: two ahead, copies; 3: unrolled by 3)
+#endif
 #ifndef KRR_KLL_TAIL_MARGIN
 #define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
 #endif
@@ -1539,12 +1564,12 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
             }
         }
         const int64_t nch = kll_nchunks(beg, end);
-        const int64_t npad = (nch + 1) & ~(int64_t)1;
+        const int64_t npad = KRR_KLL_TAIL_STREAM == 3 ? (nch + 2) / 3 * 3 : (nch + 1) & ~(int64_t)1;
         KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
         uint32_t restreams = 0;
 #pragma unroll 1
         for (int pass = 0; pass < 2; ++pass) {
-            kll_stream<KllTailProc, 2>(A.vals, beg, end, npad, P, lane);
+            kll_stream<KllTailProc, KRR_KLL_TAIL_STREAM>(A.vals, beg, end, npad, P, lane);
             if (!(full0 && P.ts.tl < tail)) break;
             full0 = false;  // the estimate missed: once more, every present key a candidate
             P.ts = KllTail{0u, 0u, 0.0};
