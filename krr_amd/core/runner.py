@@ -202,14 +202,30 @@ class BatchedRunner:
         pass per range.  No Decimal lists either way; native rounding."""
         self._require_packed()
         if parser == "hybrid":
-            parts = self.pack_hybrid(cpu_bodies, mem_bodies, threads=threads)
-            raw = _concat_raw([self.strategy.settings.run_fleet(f) for f in parts])
+            import threading
+
+            import torch
+
+            settings = self.strategy.settings
+            lock = threading.Lock()  # one engine context: its passes one at a time
+
+            def host_then(fleet):  # the host part's upload + kernel pass, while the device part packs
+                with lock, torch.cuda.stream(torch.cuda.Stream(device=settings.device)):
+                    return settings.run_fleet(fleet)
+
+            parts, raw_host = self._pack_hybrid(cpu_bodies, mem_bodies, threads=threads, host_then=host_then)
+            with lock:
+                raws = [settings.run_fleet(parts[0])]
+            if len(parts) > 1:
+                raws.append(raw_host)
+            raw = _concat_raw(raws)
             return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
 
     # parser="hybrid": the share of the JSON bytes the host packer takes, re-estimated after
     # every call from the rates both sides reached while running together
     hybrid_share = 0.2
+    hybrid_device_threads = 0
     hybrid_last: Optional[dict] = None
 
     def pack_hybrid(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None) -> list:
@@ -221,6 +237,13 @@ class BatchedRunner:
         concatenation equals either parser on the whole batch; a body either parser rejects
         sends the whole batch to the host packer (its result, or its error naming the
         first bad body).  The share then moves toward r_host / (r_host + r_device)."""
+        return self._pack_hybrid(cpu_bodies, mem_bodies, threads, device)[0]
+
+    def _pack_hybrid(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None,
+                     host_then=None):
+        """pack_hybrid, plus ``host_then(host_fleet)`` run on the worker thread as soon as the
+        host part is packed (e.g. its upload and kernel pass, overlapping the device part's
+        pack); returns (parts, host_then's result or None)."""
         import os
         import threading
         import time
@@ -242,8 +265,9 @@ class BatchedRunner:
         k = int(np.searchsorted(cum, (1.0 - share) * total, side="left")) + 1 if n else 0
         k = min(max(k, 1), n - 1)
         if T < 3 or n < 2:
-            return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)]
-        t_dev = max(1, T // 4)  # staging memcpy threads; the host parser gets the rest
+            return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)], None
+        # staging memcpy threads (hybrid_device_threads, default a quarter); the host parser gets the rest
+        t_dev = max(1, min(T - 1, int(self.hybrid_device_threads or T // 4)))
         t_host = max(1, T - t_dev)
         host_out: dict = {}
         alloc = _pinned_alloc_or_none()
@@ -254,8 +278,12 @@ class BatchedRunner:
                 host_out["fleet"] = PackedFleet(
                     pack_query_range_bodies(cpu_bodies[k:], threads=t_host, alloc=alloc),
                     pack_query_range_bodies(mem_bodies[k:], threads=t_host, alloc=alloc))
+                if host_then is not None:
+                    host_out["then"] = host_then(host_out["fleet"])
             except PrometheusResponseError as e:
                 host_out["error"] = e
+            except BaseException as e:  # noqa: BLE001 - re-raised on the calling thread
+                host_out["exc"] = e
             host_out["s"] = time.perf_counter() - t0
 
         worker = threading.Thread(target=host_part, name="krr-hybrid-host", daemon=True)
@@ -266,11 +294,13 @@ class BatchedRunner:
             dev_s = time.perf_counter() - t0
         finally:
             worker.join()
+        if "exc" in host_out:
+            raise host_out["exc"]
         if "error" in host_out or self.last_pack_via != ("device", "device"):
             # a body one side rejected: the outcome is the host packer's on the whole batch
             self.last_pack_via = ("host", "host")
             return [PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
-                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))]
+                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))], None
         b_dev, b_host = int(cum[k - 1]), total - int(cum[k - 1])
         r_dev, r_host = b_dev / max(dev_s, 1e-9), b_host / max(host_out["s"], 1e-9)
         self.hybrid_last = {"share": share, "split_object": k, "device_s": dev_s, "host_s": host_out["s"],
@@ -278,7 +308,7 @@ class BatchedRunner:
                             "device_threads": t_dev, "host_threads": t_host}
         self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
         self.last_pack_via = ("hybrid", "hybrid")
-        return [dev_fleet, host_out["fleet"]]
+        return [dev_fleet, host_out["fleet"]], host_out.get("then")
 
     @staticmethod
     def body_shard_bounds(objects: Sequence[K8sObjectData], world: int) -> list:
