@@ -256,7 +256,7 @@ class BatchedRunner:
         if len(cpu_bodies) != len(mem_bodies):
             raise ValueError("cpu and memory bodies need one entry per object each")
         n = len(cpu_bodies)
-        T = int(threads) or len(os.sched_getaffinity(0))
+        T = int(threads) or _host_threads()
         nb = np.fromiter((sum(len(b) for b in cb) + sum(len(b) for b in mb)
                           for cb, mb in zip(cpu_bodies, mem_bodies)), dtype=np.int64, count=n)
         cum = np.cumsum(nb)
@@ -389,6 +389,16 @@ class BatchedRunner:
         histories = await self.gather_histories(objects, loader)
         # the kernel pass runs off the event loop, like the reference's to_thread (runner.py:106)
         return await asyncio.to_thread(self.allocations, objects, histories)
+
+
+def _host_threads() -> int:
+    """Host threads this process may use: the affinity set, capped by OMP_NUM_THREADS when set
+    (a GPU box may show every CPU of the machine but lease a few per GPU)."""
+    import os
+
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n)
 
 
 def _concat_raw(raws):
