@@ -129,12 +129,50 @@ __device__ __forceinline__ double kll_xord(double d) {
     }
     return bitsd(((uint64_t)kll_xor32<M>((uint32_t)(x >> 32)) << 32) | kll_xor32<M>((uint32_t)x));
 }
+#ifndef KRR_KLL_X_SLOWCROSS
+// (key of the pair's lower lane, key of its upper lane) in every lane, for the pairs
+// lane ^ 16 and lane ^ 32, by gfx950's v_permlane16_swap / v_permlane32_swap: a VALU row swap
+// of a register with itself — no LDS, no address registers.
+template <int M>
+__device__ __forceinline__ void kll_pair_swap(double x, double& a, double& b) {
+    const uint64_t u = dbits(x);
+    const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    if constexpr (M == 32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        a = bitsd(((uint64_t)h[0] << 32) | l[0]);
+        b = bitsd(((uint64_t)h[1] << 32) | l[1]);
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        a = bitsd(((uint64_t)h[0] << 32) | l[0]);
+        b = bitsd(((uint64_t)h[1] << 32) | l[1]);
+    }
+}
+#endif
 template <int M, int N>
 __device__ __forceinline__ void kll_cross(double (&x)[N], bool take_min) {
+#ifndef KRR_KLL_X_SLOWCROSS
+    if constexpr (M == 16 || M == 32) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double a, b;
+            kll_pair_swap<M>(x[i], a, b);
+            x[i] = ((b < a) != take_min) ? a : b;  // take_min: the smaller of the pair
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const double o = kll_xord<M>(x[i]);
+#ifndef KRR_KLL_X_SLOWCROSS
+        // one compare and a select: keep x when (o < x) differs from take_min (keys hold no NaN
+        // and no -0, so either side of a tie is the same key)
+        x[i] = ((o < x[i]) != take_min) ? x[i] : o;
+#else
         x[i] = take_min ? fmin(x[i], o) : fmax(x[i], o);
+#endif
     }
 }
 
@@ -316,6 +354,48 @@ __device__ void kll_lds_merge(const uint64_t* X, uint32_t nx, const uint64_t* Y,
     for (uint32_t j = lane; j < ny; j += kWave) O[j + kll_bound<false>(X, nx, bitsd(Y[j]))] = Y[j];
 }
 
+// Merge-compaction of two ascending runs (a, t <= 256 keys) in registers: lane l holds merged
+// positions 8l .. 8l + 7 of the bitonic sequence L ascending (+inf padded to 256) followed by T
+// descending (+inf first), cleaned by one bitonic merge (6 cross-lane and 3 in-lane stages);
+// positions p < lim with p = off, off + 2, ... are written to O[(p - off) / 2].  Equal keys have
+// equal bits (no -0: keys are folded where kept), so the order among them is immaterial, and a
+// padding +inf is the same key as a real one: the first a + t positions are the merge.
+__device__ __forceinline__ void kll_reg_merge(const uint64_t* L, uint32_t a, const uint64_t* T, uint32_t t,
+                                              uint32_t off, uint32_t lim, uint64_t* O, int lane) {
+    double x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t p = (uint32_t)lane * 8u + (uint32_t)i;
+        const uint32_t q = 511u - p;
+        const bool inL = p < (uint32_t)kKllRun;
+        const bool have = inL ? p < a : q < t;
+        x[i] = have ? bitsd(inL ? L[p] : T[q]) : __builtin_inf();
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const bool take_min = (lane & m) == 0;
+        switch (m) {
+            case 32: kll_cross<32, 8>(x, take_min); break;
+            case 16: kll_cross<16, 8>(x, take_min); break;
+            case 8: kll_cross<8, 8>(x, take_min); break;
+            case 4: kll_cross<4, 8>(x, take_min); break;
+            case 2: kll_cross<2, 8>(x, take_min); break;
+            default: kll_cross<1, 8>(x, take_min); break;
+        }
+    }
+#pragma unroll
+    for (int j = 4; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (!(i & j)) kll_cxd(x[i], x[i + j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t p = (uint32_t)lane * 8u + (uint32_t)i;
+        if (p < lim && p >= off && ((p - off) & 1u) == 0) O[(p - off) >> 1] = dbits(x[i]);
+    }
+}
+
 // Uniform build state in LDS.
 struct KllShared {
     uint64_t* lv;    // runs, level h at lv + (h - kKllFirstRun) * kKllRun
@@ -410,8 +490,12 @@ __device__ uint64_t kll_push(KllShared sh, uint64_t base, int32_t nrl, uint32_t 
         const uint32_t c = uni32(sh.rcnt[h]);
         const uint32_t off = kll_coin32(base, kT_RUN + h, c) & 1u;
         uint64_t* O = sh.tmp + (size_t)(t_sel ^ 1) * kKllRun;
+#ifdef KRR_KLL_X_REGMERGE  // A/B: the register bitonic merge (same speed, more VGPRs; profiles/r04/s)
+        kll_reg_merge(L, a, T, t, off, lim, O, lane);
+#else  // merge-path: positions by binary searches in LDS
         kll_merge_half<true>(L, a, T, t, off, lim, O, lane);  // the run's keys before T's equal keys
         kll_merge_half<false>(T, t, L, a, off, lim, O, lane);
+#endif
         w2 += 1ull << (2 * h);
         __syncthreads();
         if (lane == 0) {
@@ -799,7 +883,9 @@ struct KllProc {
         }
         if (C >= 2) w2u += 1ull << 8;
         __syncthreads();
+#ifndef KRR_KLL_X_NOPUSH  // profiling variant: no run push (rows are not valid)
         w2u += kll_push(sh, base, nrl, 0, C >> 1, kKllFirstRun, lane);
+#endif
     }
 
     __device__ __forceinline__ void tail_filter(const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
@@ -872,7 +958,13 @@ struct KllProc {
                 for (int u = 0; u < 8; ++u) out[u] = bitsd(kKllInfBits);
             }
         }
+#if defined(KRR_KLL_X_CUT) && KRR_KLL_X_CUT == 1  // profiling variant: level 0 only (rows not valid)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kmax = fmax(kmax, out[u]);
+        if (true) {
+#else
         if ((ci & 1u) == 0) {
+#endif
 #pragma unroll
             for (int u = 0; u < 8; ++u) pend1[u] = out[u];
             cp1 = c0;
@@ -887,7 +979,13 @@ struct KllProc {
             kll_sort16(z);
             lane_level<1>(z, cp1 + c0, kT_L1, ci >> 1, y, cy);
             arrivals();
+#if defined(KRR_KLL_X_CUT) && KRR_KLL_X_CUT == 2  // profiling variant: levels 0-1 only
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kmax = fmax(kmax, y[u]);
+            if (true) {
+#else
             if (((ci >> 1) & 1u) == 0) {
+#endif
 #pragma unroll
                 for (int u = 0; u < 8; ++u) pend2[u] = y[u];
                 cp2 = cy;
@@ -1043,6 +1141,29 @@ __device__ __forceinline__ void kll_stream(const double* __restrict__ vals, int6
 __device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t h, bool has, double kv,
                                      const uint64_t* carry, uint32_t nc, uint64_t* ws, int lane) {
     const uint32_t a = (h >= (uint32_t)kKllFirstRun && (int)h < kKllFirstRun + nrl) ? uni32(sh.lens[h]) : 0u;
+#ifndef KRR_KLL_X_SORTGATHER
+    if (!ballot(has)) {
+        // no lane odd slots: the run, the carry and the wave slot are each ascending — place
+        // every key at its merged position (binary searches) instead of sorting the union
+        const uint64_t* R = sh.lv + (size_t)(h >= (uint32_t)kKllFirstRun ? h - kKllFirstRun : 0u) * kKllRun;
+        const bool wk = (uni32(sh.misc[0]) >> h) & 1u;
+        const uint64_t kb = wk ? uni64(sh.wk[h]) : 0ull;
+        const double k = bitsd(kb);
+#pragma unroll 1
+        for (uint32_t i = lane; i < a; i += kWave) {
+            const double x = bitsd(R[i]);
+            ws[i + kll_bound<true>(carry, nc, x) + (wk && k < x ? 1u : 0u)] = R[i];
+        }
+#pragma unroll 1
+        for (uint32_t j = lane; j < nc; j += kWave) {
+            const double x = bitsd(carry[j]);
+            ws[j + kll_bound<false>(R, a, x) + (wk && k < x ? 1u : 0u)] = carry[j];
+        }
+        if (wk && lane == 0) ws[kll_bound<false>(R, a, k) + kll_bound<false>(carry, nc, k)] = kb;
+        __syncthreads();
+        return a + nc + (wk ? 1u : 0u);
+    }
+#endif
     uint32_t m = 0, sources = 0;
     if (a) {
         const uint64_t* R = sh.lv + (size_t)(h - kKllFirstRun) * kKllRun;
@@ -1071,13 +1192,17 @@ __device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t 
     return m;
 }
 
+#ifndef KRR_KLL_BODY_WAVES_PER_SIMD
+#define KRR_KLL_BODY_WAVES_PER_SIMD 2  // the body-only build: two waves per SIMD (LDS allows 9 per CU)
+#endif
 #ifndef KRR_KLL_WAVES_PER_SIMD
 #define KRR_KLL_WAVES_PER_SIMD 1  // the build's LDS (runs + tail buffer) allows one wave per SIMD anyway
 #endif
 // TAIL = false: no tail (tail == 0) or the tail left to k_kll_tail (A.tail_pass); the build then
 // holds none of the tail buffer's code or state.
 template <bool TAIL>
-__global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBuildArgs A) {
+__global__ __launch_bounds__(64, TAIL ? KRR_KLL_WAVES_PER_SIMD : KRR_KLL_BODY_WAVES_PER_SIMD) void k_kll_build(
+    KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     KllShared sh;
@@ -1165,7 +1290,11 @@ __global__ __launch_bounds__(64, KRR_KLL_WAVES_PER_SIMD) void k_kll_build(KllBui
         uint64_t lw[6] = {0, 0, 0, 0, 0, 0};
         uint64_t weight = 0, w2f = 0;
 #pragma unroll 1
+#ifdef KRR_KLL_X_NOFINAL  // profiling variant: no final compression / export (rows are not valid)
+        for (uint32_t h = 0; h < 0u; ++h) {
+#else
         for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+#endif
             const bool has = h < 4 && ((kmask >> h) & 1u);
             const double kv = h == 0 ? K0[0] : (h == 1 ? K0[1] : (h == 2 ? K0[2] : K0[3]));
             const uint32_t m = kll_gather_level(sh, A.nrl, h, has, kv, cbuf, nc, ws, lane);
