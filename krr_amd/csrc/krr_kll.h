@@ -222,10 +222,21 @@ __device__ __forceinline__ void kll_sort512(double (&y)[8], int lane) {
 #pragma unroll 1
     for (uint32_t k = 16; k <= 512; k <<= 1) {
         const bool asc = k >= 512 || (((uint32_t)lane * 8u) & k) == 0;
+#ifndef KRR_KLL_X_NONEG
+        // a descending block is sorted ascending on negated keys (the sign bit flipped, and
+        // flipped back after the stage): every compare-exchange of the stage is ascending
+        const uint32_t neg = asc ? 0u : 0x80000000u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = bitsd(dbits(y[i]) ^ ((uint64_t)neg << 32));
+#endif
 #pragma unroll 1
         for (uint32_t j = k >> 1; j >= 8; j >>= 1) {
             const int m = (int)(j >> 3);
+#ifndef KRR_KLL_X_NONEG
+            const bool take_min = (lane & m) == 0;
+#else
             const bool take_min = ((lane & m) == 0) == asc;
+#endif
             switch (m) {  // wave-uniform
                 case 1: kll_cross<1, 8>(y, take_min); break;
                 case 2: kll_cross<2, 8>(y, take_min); break;
@@ -240,10 +251,18 @@ __device__ __forceinline__ void kll_sort512(double (&y)[8], int lane) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 if (!(i & j)) {
+#ifndef KRR_KLL_X_NONEG
+                    kll_cxd(y[i], y[i + j]);
+#else
                     if (asc) kll_cxd(y[i], y[i + j]);
                     else kll_cxd(y[i + j], y[i]);
+#endif
                 }
         }
+#ifndef KRR_KLL_X_NONEG
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = bitsd(dbits(y[i]) ^ ((uint64_t)neg << 32));
+#endif
     }
 }
 
