@@ -125,6 +125,8 @@ def parse():
     ap.add_argument("--c4-warmup", type=int, default=1, help="config-4 leg: warmup steps")
     ap.add_argument("--host-objects", type=int, default=2000,
                     help="host path: config-1-shaped objects per rank (3 pods x 10,080 samples x 2 resources)")
+    ap.add_argument("--sharded-host-path", action="store_true",
+                    help="testing: the N > 1 host path (recommend_bodies_shard) at one rank (with --force-dist)")
     ap.add_argument("--host-parser", choices=("hybrid", "device", "host"), default="hybrid",
                     help="N > 1 host path: the parser each rank uses for its shard's bodies")
     ap.add_argument("--no-host-path", action="store_true",
@@ -767,7 +769,7 @@ def main():
     if rank == 0:
         phase("right-size")
         result.update(right_size(args, host_rec[:containers_total].numpy()))
-    if rank == 0 and world == 1 and not args.no_host_path:
+    if rank == 0 and world == 1 and not args.no_host_path and not args.sharded_host_path:
         phase("host path")
         result.update(host_path(args, dev, c_host_sample=parts[0][2], objects=args.host_objects))
     if args.c4_containers > 0 and args.config == 2:
@@ -778,7 +780,7 @@ def main():
                           comm if gather_mode == "stream" else None, params)
         if rank == 0:
             result.update(leg)
-    if world > 1 and not args.no_host_path:
+    if (world > 1 or args.sharded_host_path) and dist_on and not args.no_host_path:
         phase("host path (sharded)")
         hp = host_path_sharded(args, dev, world, rank, coll_dev, objects=args.host_objects)
         if rank == 0:

@@ -437,3 +437,26 @@ def test_bench_sharded_host_path_two_ranks():
                 "--c4-containers", "0", "--no-cpu-baseline", "--host-objects", "300"], timeout=300)
     assert r["e2e_parser"] == "hybrid" and len(r["e2e_per_rank_s"]) == 2 and r["e2e_objects_per_s"] > 0, r
     assert r["e2e_sharded_equals_host_parse"] is True and r["e2e_parity_objects"] == 2 * 2 * 32
+
+
+def test_bench_rccl_one_rank_config4_leg_and_sharded_host_path():
+    """The N > 1 code of the config-4 leg (C-ABI gather on the launch stream, receive buffers
+    forwarded to the host by the next launch) and of the sharded host path
+    (recommend_bodies_shard's records gathered over RCCL) at one RCCL rank (`--force-dist`):
+    every key present, parity true."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), KRR_BENCH_BACKEND="nccl")
+    p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist",
+                        "--containers", "400", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                        "--c4-containers", "5000", "--c4-steps", "2", "--chunk-gib", "0.1", "--sharded-host-path",
+                        "--host-objects", "200"], capture_output=True, text=True, env=env, timeout=270)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["config4_parity_vs_oracle_on_sample"] is True and r["config4_parity_gathered_vs_rank0_kernel"] is True
+    assert r["config4_definition"].find("RCCL gather") >= 0 and r["config4_gather_ms_max"] >= 0
+    assert r["e2e_sharded_equals_host_parse"] is True and len(r["e2e_per_rank_s"]) == 1
