@@ -3,7 +3,8 @@ properties, computed with plain torch ops independent of the kernels:
   SORTED_LOWER:  #(x < v) <= k < #(x <= v)            (v is the k-th order statistic)
   LINEAR:        x_(r0) <= v <= x_(r1)  via  #(x < v) <= r1 and #(x <= v) >= r0 + 1
   max / count:   nan-ignoring max (bits) and #present
-The oracle-level bit-exact checks live in test_gpu_kernels.py at smaller sizes."""
+and, for the bench's own config-2 and config-3 workloads, bit for bit against the C oracle on every
+container (test_config{2,3}_full_size_bit_exact_vs_oracle)."""
 import numpy as np
 import pytest
 
@@ -291,3 +292,92 @@ def test_config3_full_size(ctx):
     assert sel.size == 2000
     del cpu, mem
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("mode,pct", [("linear", "99"), ("sorted_lower", "99"), ("linear", "50"),
+                                      ("ref_index", "99")])
+def test_config2_full_size_bit_exact_vs_oracle(ctx, mode, pct):
+    """The bench's config-2 workload exactly (its seeds, 10,000 containers x 5 pods x 10,080
+    slots, NaN-gapped) through the fused launch, against the C oracle on EVERY container: value
+    bits, counts, memory max and counts (full size was property-only here)."""
+    import torch
+    from decimal import Decimal
+
+    from krr_amd.core.engine import percentile_params
+    from oracle import oracle
+
+    S, L = 10_000, 5 * 10080
+    dev = torch.device("cuda:0")
+    offs = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    cpu = torch.empty(S * L, dtype=torch.float64, device=dev)
+    mem = torch.empty(S * L, dtype=torch.float64, device=dev)
+    seed = 1000003 * 3  # bench.py's config-2 seed
+    ctx.synth_fill(cpu, offs, seed, 0, 10080, True)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, 10080, True)
+    prm = percentile_params(Decimal(pct), mode)
+    out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+           (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+            ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+    ctx.simple_run(ctx.series(cpu, offs, L, True), ctx.series(mem, offs, L, True), prm, out)
+    torch.cuda.synchronize()
+    o = offs.cpu().numpy()
+    c_h, m_h = cpu.cpu().numpy(), mem.cpu().numpy()
+    ov, on, of = oracle.percentile(c_h, o, prm.mode, prm.p_num, prm.p_den, prm.q, True, 16)
+    mv, mn, mf = oracle.seg_max(m_h, o, True, 16)
+    gv = out["cpu_value"].cpu().numpy()
+    same = (gv.view(np.uint64) == ov.view(np.uint64)) | (np.isnan(gv) & np.isnan(ov))
+    if mode == "linear":  # the sign of a zero LINEAR result is unspecified
+        same |= (gv == 0) & (ov == 0)
+    assert same.all(), int((~same).sum())
+    assert np.array_equal(out["cpu_count"].cpu().numpy(), on)
+    assert np.array_equal(out["mem_value"].cpu().numpy(), mv, equal_nan=True)
+    assert np.array_equal(out["mem_count"].cpu().numpy(), mn)
+
+
+@pytest.mark.parametrize("mode,pct", [("linear", "99"), ("sorted_lower", "50")])
+def test_config3_full_size_bit_exact_vs_oracle(ctx, mode, pct):
+    """The bench's config-3 workload (100,000 containers, 1..14 days @1m each, compact CSR,
+    lengths and samples from the global container index) against the C oracle on every
+    container."""
+    import os
+    import sys
+
+    import torch
+    from decimal import Decimal
+
+    from krr_amd.core.engine import percentile_params
+    from oracle import oracle
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import container_lengths
+
+    S = 100_000
+    lens = container_lengths(3, 0, S)
+    offs_np = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    dev = torch.device("cuda:0")
+    offs = torch.from_numpy(offs_np).to(dev)
+    N = int(offs_np[-1])
+    cpu = torch.empty(N, dtype=torch.float64, device=dev)
+    mem = torch.empty(N, dtype=torch.float64, device=dev)
+    seed = 1000003 * 4  # bench.py's config-3 seed
+    ctx.synth_fill(cpu, offs, seed, 0, 0, False)
+    ctx.synth_fill(mem, offs, seed ^ 0x5A5A, 1, 0, False)
+    prm = percentile_params(Decimal(pct), mode)
+    out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
+           (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
+            ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+    ctx.simple_run(ctx.series(cpu, offs, int(lens.max()), False), ctx.series(mem, offs, int(lens.max()), False),
+                   prm, out)
+    torch.cuda.synchronize()
+    c_h, m_h = cpu.cpu().numpy(), mem.cpu().numpy()
+    del cpu, mem
+    ov, on, _ = oracle.percentile(c_h, offs_np, prm.mode, prm.p_num, prm.p_den, prm.q, False, 16)
+    mv, mn, _ = oracle.seg_max(m_h, offs_np, False, 16)
+    gv = out["cpu_value"].cpu().numpy()
+    same = (gv.view(np.uint64) == ov.view(np.uint64)) | (np.isnan(gv) & np.isnan(ov))
+    if mode == "linear":
+        same |= (gv == 0) & (ov == 0)
+    assert same.all(), int((~same).sum())
+    assert np.array_equal(out["cpu_count"].cpu().numpy(), on)
+    assert np.array_equal(out["mem_value"].cpu().numpy(), mv, equal_nan=True)
+    assert np.array_equal(out["mem_count"].cpu().numpy(), mn)
