@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--kll-budget", type=int, default=512, help="config 5 kll: body keys kept per row")
     ap.add_argument("--kll-tail", type=int, default=-1,
                     help="config 5 kll: exact top keys per row (-1: just enough for --percentile of the whole "
-                         "30d@15s series when p >= 90, i.e. p99 answered exactly; 256 below p90)")
+                         "30d@15s series, i.e. p99 answered exactly; none when more than 4,096 would be needed)")
     ap.add_argument("--c5-refine", action="store_true",
                     help="config 5 at N=1: run the time-sharded exact path (--c5-method) instead of the direct "
                          "single-window select (N>1 always uses it)")
@@ -1343,8 +1343,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     direct = exact and world == 1 and not args.c5_refine
     method = "direct" if direct else (args.c5_method if exact else ("kll" if args.sketch_kind == "kll" else
                                                                      "sketch-only"))
-    ktail = args.kll_tail if args.kll_tail >= 0 else (
-        sketch.KllConfig.tail_for(T, args.percentile) if Decimal(args.percentile) >= 90 else 256)
+    # auto: the tail that answers --percentile exactly, or none when no row can hold it (p50)
+    ktail = args.kll_tail if args.kll_tail >= 0 else sketch.KllConfig.tail_for(T, args.percentile)
     kcfg = sketch.KllConfig(budget=args.kll_budget, tail=ktail)
     # the direct pass and the window export run per chunk of series in buffers of their own
     # (as configs 2-4, fleet_chunks); the sketch paths keep one buffer per rank

@@ -665,15 +665,17 @@ class KllConfig:
     @staticmethod
     def tail_for(n_total: int, percentile, mode: str = "linear") -> int:
         """The smallest tail (a multiple of 64) that answers ``percentile`` of an ``n_total``-sample
-        series exactly: it must hold every rank from the asked one (and LINEAR's next) to n - 1."""
+        series exactly: it must hold every rank from the asked one (and LINEAR's next) to n - 1.
+        0 when that is more than a row can hold (4,096): a tail that cannot cover the asked rank
+        would cost its pass for nothing, and the body answers it within its bound."""
         from fractions import Fraction
 
         if n_total <= 0:
             return 0
         p = Fraction(str(percentile))
         r0 = int((n_total - 1) * p / 100)  # floor: SORTED_LOWER's rank, LINEAR's lower one
-        need = n_total - r0
-        return int(min(4096, -(-need // 64) * 64))
+        need = -(-(n_total - r0) // 64) * 64
+        return int(need) if need <= 4096 else 0
 
 
 def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, seg_base: int = 0,

@@ -3991,6 +3991,8 @@ int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const
     size_t lds = 0;
     rc = kll_merge_common(ctx, n_series, rows_per_series, rows, kp, series_base, true, &lds);
     if (rc) return rc;
+    if (rows_per_series == 1)  // nothing to fold: the body staged alone (k_kll_query's direct form)
+        lds = ((size_t)kKllHdr + kp->budget) * 8 + (size_t)kp->budget;
     if (n_series == 0) return KRR_OK;
     if (!out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
     DeviceGuard g(ctx->device);

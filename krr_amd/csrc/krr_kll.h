@@ -1565,9 +1565,15 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
     const int lane = threadIdx.x;
     const uint32_t budget = (uint32_t)A.budget;
     const uint32_t RW = (uint32_t)kKllHdr + budget + (uint32_t)A.tail;
-    uint8_t* lvl = reinterpret_cast<uint8_t*>(reinterpret_cast<uint64_t*>(smem) + 3 * (size_t)RW + 5 * (size_t)budget);
+    // W == 1: nothing to fold — the header and the tail are read from the row itself, and only
+    // a body rank stages the body in LDS (the launch's LDS is then a body, not three rows)
+    const bool direct = A.W == 1;
+    uint64_t* bodyb = reinterpret_cast<uint64_t*>(smem);
+    uint8_t* lvl = direct ? reinterpret_cast<uint8_t*>(bodyb + kKllHdr + budget)
+                          : reinterpret_cast<uint8_t*>(reinterpret_cast<uint64_t*>(smem) + 3 * (size_t)RW +
+                                                       5 * (size_t)budget);
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        const uint64_t* im = kll_fold_rows(A, s, smem, lane);
+        const uint64_t* im = direct ? A.rows + (size_t)s * RW : kll_fold_rows(A, s, smem, lane);
         const uint64_t n = im[0], nan = im[1];
         const uint32_t tl = (uint32_t)im[6];
         uint32_t m = 0;
@@ -1603,6 +1609,7 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
                 }
             }
             double v[2];
+            bool staged = false;
 #pragma unroll 1
             for (int qi = 0; qi < 2; ++qi) {
                 const uint64_t r = (uint64_t)(qi ? r1 : r0);
@@ -1613,7 +1620,15 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
                 if (r == 0) v[qi] = bitsd(im[2]);
                 else if (r == n - 1) v[qi] = bitsd(im[3]);
                 else if (n - r <= tl) v[qi] = bitsd(im[kKllHdr + budget + tl - (n - r)]);
-                else v[qi] = bitsd(okey_inv(kll_body_select(im, lvl, m, r, lane)));
+                else if (!direct) v[qi] = bitsd(okey_inv(kll_body_select(im, lvl, m, r, lane)));
+                else {  // stage the body once (uniform branch: r is the same in every lane)
+                    if (!staged) {
+                        for (uint32_t i = lane; i < m; i += kWave) bodyb[kKllHdr + i] = im[kKllHdr + i];
+                        __syncthreads();
+                        staged = true;
+                    }
+                    v[qi] = bitsd(okey_inv(kll_body_select(bodyb, lvl, m, r, lane)));
+                }
             }
             result = A.mode == KRR_PCT_SORTED_LOWER ? v[0] : np_lerp(v[0], v[1], gamma);
         }
