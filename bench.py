@@ -885,7 +885,7 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     for parser in ("host", "device", "hybrid"):
         runner.recommend_from_bodies(cpu_b[:8], mem_b[:8], threads=threads, parser=parser)  # warm-up
         if parser == "hybrid":  # the host share settles on the rates both sides reach together
-            for _ in range(3):
+            for _ in range(5):
                 runner.recommend_from_bodies(cpu_b, mem_b, threads=threads, parser=parser)
         best_e = float("inf")
         for _ in range(2 if parser == "host" else 3):

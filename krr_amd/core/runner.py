@@ -209,15 +209,28 @@ class BatchedRunner:
             settings = self.strategy.settings
             lock = threading.Lock()  # one engine context: its passes one at a time
 
+            import time
+
+            done = {}
+
             def host_then(fleet):  # the host part's upload + kernel pass, while the device part packs
                 with lock, torch.cuda.stream(torch.cuda.Stream(device=settings.device)):
-                    return settings.run_fleet(fleet)
+                    r = settings.run_fleet(fleet)
+                done["host"] = time.perf_counter()
+                return r
 
+            t0 = time.perf_counter()
+            share = self.hybrid_share
             parts, raw_host = self._pack_hybrid(cpu_bodies, mem_bodies, threads=threads, host_then=host_then)
             with lock:
                 raws = [settings.run_fleet(parts[0])]
             if len(parts) > 1:
                 raws.append(raw_host)
+                # balance the whole critical paths (pack + kernel pass on each side), not the packs
+                h = self.hybrid_last
+                r_dev = h["bytes_device"] / max(time.perf_counter() - t0, 1e-9)
+                r_host = h["bytes_host"] / max(done.get("host", t0) - t0, 1e-9)
+                self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
             raw = _concat_raw(raws)
             return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
@@ -307,6 +320,7 @@ class BatchedRunner:
                             "device_GBps": r_dev / 1e9, "host_GBps": r_host / 1e9,
                             "device_threads": t_dev, "host_threads": t_host}
         self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
+        self.hybrid_last.update(bytes_device=b_dev, bytes_host=b_host)
         self.last_pack_via = ("hybrid", "hybrid")
         return [dev_fleet, host_out["fleet"]], host_out.get("then")
 

@@ -37,7 +37,7 @@ def main():
     for d in [int(x) for x in a.dev_threads.split(",")]:
         runner.hybrid_device_threads = d
         runner.hybrid_share = 0.2
-        for _ in range(3):  # the share settles
+        for _ in range(5):  # the share settles
             runner.recommend_from_bodies(cpu_b, mem_b, threads=a.threads, parser="hybrid")
         th = best("hybrid")
         h = runner.hybrid_last
