@@ -192,7 +192,7 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
         def mk(c, m):
             o = new(model)
             setattr_(o, "__dict__", {"requests": {cpu_k: c, mem_k: m}, "limits": {cpu_k: None, mem_k: m}})
-            setattr_(o, "__fields_set__", fields)
+            setattr_(o, "__fields_set__", set(fields))  # its own: pydantic adds to it on assignment
             return o
 
         return list(map(mk, cpu_col, mem_col))

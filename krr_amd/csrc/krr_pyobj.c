@@ -149,12 +149,15 @@ static PyObject* allocations(PyObject* self, PyObject* args) {
         PyObject* req = two_key_dict(ck, hc, c, mk, hm, m);
         PyObject* lim = req ? two_key_dict(ck, hc, Py_None, mk, hm, m) : NULL;
         PyObject* fd = lim ? PyDict_New() : NULL;
-        PyObject* o = fd ? new_instance((PyTypeObject*)model) : NULL;
+        /* a fields-set of its own per object: pydantic adds to it on attribute assignment */
+        PyObject* fs = fd ? PySet_New(fields_set) : NULL;
+        PyObject* o = fs ? new_instance((PyTypeObject*)model) : NULL;
         int bad = !o || set_known(fd, s_requests, hreq, req) < 0 || set_known(fd, s_limits, hlim, lim) < 0 ||
-                  PyObject_GenericSetAttr(o, s_dict, fd) < 0 || PyObject_GenericSetAttr(o, s_fields, fields_set) < 0;
+                  PyObject_GenericSetAttr(o, s_dict, fd) < 0 || PyObject_GenericSetAttr(o, s_fields, fs) < 0;
         Py_XDECREF(req);
         Py_XDECREF(lim);
         Py_XDECREF(fd);
+        Py_XDECREF(fs);
         if (bad) {
             Py_XDECREF(o);
             goto fail;
