@@ -393,3 +393,47 @@ def test_combined_launch_equals_split_passes(ctx):
         out[name] = rows.cpu().numpy().view(np.uint64)
     assert np.array_equal(out["combined"], out["one_pass"]) and np.array_equal(out["combined"], out["body"])
     _check_rows(out["combined"], x, offs, False, 512, 1792)
+
+
+@pytest.mark.parametrize("shape", ["gamma", "quantized"])
+def test_rank_bound_coverage_over_many_series(ctx, shape):
+    """Evidence independent of the restatement: 4,000 series x 43,200 samples built on the
+    device, body answers at p10 / p25 / p50 / p75 / p90 against exact ranks counted on the
+    device (krr_rank_of over the raw series): the rows' bound at delta = 1% may fail for at
+    most 1% of the answers (Azuma: it should essentially never), and the measured errors sit
+    well inside it."""
+    import torch
+
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    S, T = 4000, 43_200
+    g = torch.Generator(device="cuda:0").manual_seed(17)
+    if shape == "gamma":
+        x = torch.distributions.Gamma(torch.full((S * T,), 2.0, device="cuda:0", dtype=torch.float64),
+                                      torch.full((S * T,), 20.0, device="cuda:0", dtype=torch.float64)).sample()
+    else:
+        vals = torch.tensor([0.1, 0.2, 0.3, 0.5], device="cuda:0", dtype=torch.float64)
+        x = vals[torch.multinomial(torch.tensor([0.5, 0.3, 0.15, 0.05], device="cuda:0"), S * T, replacement=True,
+                                   generator=g)]
+    offs = torch.arange(S + 1, dtype=torch.int64, device="cuda:0") * T
+    ser = ctx.series(x, offs, T, False)
+    cfg = sketch.KllConfig(budget=512, tail=0, seed=SEED)
+    rows = sketch.kll_build(ctx, ser, cfg)
+    bound = sketch.kll_rank_bound(rows, delta=0.01)
+    fails, ratios = 0, []
+    for p in ("10", "25", "50", "75", "90"):
+        prm = percentile_params(Decimal(p), "sorted_lower")
+        v = sketch.kll_query(ctx, rows, 1, cfg, prm)["value"]
+        lt = torch.empty(S, dtype=torch.int64, device="cuda:0")
+        le = torch.empty(S, dtype=torch.int64, device="cuda:0")
+        ctx.rank_of(ser, v.contiguous(), lt, le)
+        torch.cuda.synchronize()
+        k = (T - 1) * int(p) // 100
+        ltn, len_ = lt.cpu().numpy(), le.cpu().numpy()
+        err = np.maximum(0, np.maximum(ltn - k, k - (len_ - 1))) / T
+        fails += int((err > bound).sum())
+        ratios.append(float(err.mean() / bound.mean()))
+    print(f"{shape}: {fails} of {5 * S} answers past the bound, mean error / mean bound per p {ratios}")
+    assert fails <= 0.01 * 5 * S, fails
+    assert max(ratios) < 0.5, ratios  # typical errors: a fraction of the worst-case bound
