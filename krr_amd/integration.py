@@ -205,7 +205,7 @@ async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings, par
         plan = FleetQueryPlan.for_settings([objects[i] for i in idx], settings)
         q = query_range_fn(runner._get_prometheus_loader(cluster).prometheus, start, end, step)
         bodies = await asyncio.to_thread(plan.fetch, q)
-        if parser == "device" and batched is not None:  # parsed on the MI355X, routed by pod label
+        if parser in ("device", "hybrid") and batched is not None:  # parsed on the MI355X, routed by pod label
             fleet = await asyncio.to_thread(batched.pack_grouped, plan, bodies[HipResourceType.CPU],
                                             bodies[HipResourceType.Memory], 0, "device")
         else:
@@ -286,14 +286,16 @@ def install(runner_cls: Any = None, *, loader: str = "reference", scan: str = "r
     histories with ``loader`` (see the module docstring), and with ``scan="fleet"`` also
     ``_collect_result`` through ``collect_result``.  ``parser`` (loader="bodies"): "device"
     parses the raw bodies on the MI355X (krr_amd.core.device_pack), "host" with the native
-    host packer.  Calling it again changes the switches;
+    host packer, "hybrid" both at once on disjoint object ranges
+    (``BatchedRunner.pack_hybrid``; loader="grouped" parses as "device").  Calling it again
+    changes the switches;
     ``uninstall`` restores the reference's methods.  Returns the class."""
     if loader not in LOADERS:
         raise ValueError(f"loader must be one of {LOADERS}")
     if scan not in SCANS:
         raise ValueError(f"scan must be one of {SCANS}")
-    if parser not in ("device", "host"):
-        raise ValueError("parser must be 'device' or 'host'")
+    if parser not in ("device", "host", "hybrid"):
+        raise ValueError("parser must be 'device', 'host' or 'hybrid'")
     if runner_cls is None:
         from robusta_krr.core.runner import Runner as runner_cls  # the reference, in its own process
     if getattr(runner_cls, _ORIGINAL_ATTR, None) is None:
