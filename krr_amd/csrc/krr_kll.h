@@ -1560,6 +1560,96 @@ __device__ uint64_t kll_body_select(const uint64_t* im, const uint8_t* lvl, uint
     return lo;
 }
 
+// A 32-bit value of lane ^ M (M a power of two < 64).
+template <int M>
+__device__ __forceinline__ uint32_t kll_lane_xor(uint32_t v) {
+    if constexpr (M == 32) return (uint32_t)__shfl_xor((int)v, 32, kWave);
+    else return kll_xor32<M>(v);
+}
+template <int M>
+__device__ __forceinline__ void kll_kw_cross(uint64_t (&k)[8], uint32_t (&w)[8], bool take_min) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t ok = ((uint64_t)kll_lane_xor<M>((uint32_t)(k[i] >> 32)) << 32) | kll_lane_xor<M>((uint32_t)k[i]);
+        const uint32_t ow = kll_lane_xor<M>(w[i]);
+        const bool mine = (k[i] < ok) == take_min || k[i] == ok;  // equal keys: either is the key
+        k[i] = mine ? k[i] : ok;
+        w[i] = mine ? w[i] : ow;
+    }
+}
+__device__ __forceinline__ void kll_kw_cx(uint64_t& ka, uint32_t& wa, uint64_t& kb, uint32_t& wb, bool asc) {
+    const bool sw = asc ? kb < ka : ka < kb;
+    const uint64_t k0 = sw ? kb : ka, k1 = sw ? ka : kb;
+    const uint32_t w0 = sw ? wb : wa, w1 = sw ? wa : wb;
+    ka = k0; kb = k1; wa = w0; wb = w1;
+}
+
+// Weighted select over a row's body (m <= 512 keys, im[kKllHdr + i] with level lvl[i]) by ONE
+// sort of (ordered key, weight 2^level) pairs across the wave and one prefix sum: for r0 and r1
+// the smallest key whose weighted count of keys <= it exceeds r (the bisection's answer, bit for
+// bit: inside a run of equal keys any order gives the same key).  Ordered-key space (okey).
+template <int NQ>
+__device__ __forceinline__ void kll_body_select2(const uint64_t* im, const uint8_t* lvl, uint32_t m, uint64_t r0,
+                                                 uint64_t r1, int lane, uint64_t& out0, uint64_t& out1) {
+    uint64_t k[8];
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t p = (uint32_t)lane * 8u + (uint32_t)i;
+        k[i] = p < m ? okey(im[kKllHdr + p]) : ~0ull;
+        w[i] = p < m ? (1u << lvl[p]) : 0u;
+    }
+#pragma unroll
+    for (int kk = 2; kk <= 512; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 8) {
+                const int mm = j >> 3;
+                const bool asc = (((uint32_t)lane * 8u) & (uint32_t)kk) == 0;
+                const bool take_min = ((lane & mm) == 0) == asc;
+                switch (mm) {
+                    case 1: kll_kw_cross<1>(k, w, take_min); break;
+                    case 2: kll_kw_cross<2>(k, w, take_min); break;
+                    case 4: kll_kw_cross<4>(k, w, take_min); break;
+                    case 8: kll_kw_cross<8>(k, w, take_min); break;
+                    case 16: kll_kw_cross<16>(k, w, take_min); break;
+                    default: kll_kw_cross<32>(k, w, take_min); break;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (!(i & j)) {
+                        const bool asc = ((((uint32_t)lane * 8u + (uint32_t)i)) & (uint32_t)kk) == 0;
+                        kll_kw_cx(k[i], w[i], k[i + j], w[i + j], asc);
+                    }
+            }
+        }
+    }
+    uint64_t c[8], acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        acc += w[i];
+        c[i] = acc;
+    }
+    const uint64_t base = wave_scan64(acc, 0ull, OpAdd64{}) - acc;  // exclusive over lanes
+#pragma unroll 1
+    for (int q = 0; q < NQ; ++q) {
+        const uint64_t r = q ? r1 : r0;
+        uint64_t sel = ~0ull;
+        bool hit = false;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            const bool h = base + c[i] > r;
+            sel = h ? k[i] : sel;
+            hit = hit || h;
+        }
+        const uint64_t hm = ballot(hit);
+        const uint64_t key = hm ? lane_bcast64(sel, __ffsll((long long)hm) - 1) : ~0ull;
+        if (q) out1 = key;
+        else out0 = key;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1610,6 +1700,14 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
             }
             double v[2];
             bool staged = false;
+#ifndef KRR_KLL_X_BISECT
+            // both ranks in the body: one sort of the body answers both
+            const bool body0 = r0 != 0 && r0 != (int64_t)n - 1 && n - (uint64_t)r0 > tl;
+            const bool body1 = r1 != 0 && r1 != (int64_t)n - 1 && n - (uint64_t)r1 > tl;
+            uint64_t bk0 = 0, bk1 = 0;
+            if ((body0 || body1) && m <= 512u)
+                kll_body_select2<2>(im, lvl, m, (uint64_t)r0, (uint64_t)r1, lane, bk0, bk1);
+#endif
 #pragma unroll 1
             for (int qi = 0; qi < 2; ++qi) {
                 const uint64_t r = (uint64_t)(qi ? r1 : r0);
@@ -1620,6 +1718,9 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
                 if (r == 0) v[qi] = bitsd(im[2]);
                 else if (r == n - 1) v[qi] = bitsd(im[3]);
                 else if (n - r <= tl) v[qi] = bitsd(im[kKllHdr + budget + tl - (n - r)]);
+#ifndef KRR_KLL_X_BISECT
+                else if (m <= 512u) v[qi] = bitsd(okey_inv(qi ? bk1 : bk0));
+#endif
                 else if (!direct) v[qi] = bitsd(okey_inv(kll_body_select(im, lvl, m, r, lane)));
                 else {  // stage the body once (uniform branch: r is the same in every lane)
                     if (!staged) {
@@ -1717,7 +1818,14 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
                 m += l;
             }
             __syncthreads();
+#ifndef KRR_KLL_X_BISECT
+            uint64_t tk = 0, tk1 = 0;
+            if (m <= 512u) kll_body_select2<1>(im, lvl, m, (uint64_t)qd, 0, lane, tk, tk1);
+            else tk = kll_body_select(im, lvl, m, (uint64_t)qd, lane);
+            const double t0 = bitsd(okey_inv(tk));
+#else
             const double t0 = bitsd(okey_inv(kll_body_select(im, lvl, m, (uint64_t)qd, lane)));
+#endif
             __syncthreads();
             if (t0 > -__builtin_inf()) {  // candidates: keys >= t0 (t0 == -inf: every present key)
                 full0 = true;
