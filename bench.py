@@ -763,6 +763,7 @@ def main():
         # the reference's own CPU path, measured in the build container only (cannot travel):
         result["reference_cpu_measured_in_build_container"] = {
             "value": 492.0, "unit": "container-series/s", "cores": 1, "measured_in_this_run": False,
+            "kind": "carried_constant",
             "source": "carried constant from BASELINE.md (SimpleStrategy.run + _format_result, config 1, "
                       "measured once in the build container; the reference cannot travel to the GPU box)"}
 

@@ -35,7 +35,8 @@ r-th contiguous time slice of every series.
   level by level into at most ``budget`` weighted keys (``krr_kll_build``); the W rows of
   a series reach its owner in one all-to-all and are queried together
   (``krr_kll_query``).  Unlike the histogram its RANK error has a data-independent bound:
-  ``kll_rank_bound`` (Hoeffding over the compactions' coins, from the rows' sum of w^2).
+  ``kll_rank_bound`` (Azuma-Hoeffding over the compactions' coins as martingale
+  differences; the deterministic schedule fixes the rows' sum of w^2 before any coin).
 * REF_INDEX (the reference's rule, ``simple.py:36``) stays exact: all-gather the
   per-slice present counts, the rank whose slice holds global index k selects it
   (``krr_select_present``), one all-gather collects the answers.
