@@ -140,8 +140,10 @@ static PyObject* allocations(PyObject* self, PyObject* args) {
     if (hc == -1 || hm == -1) return NULL;
     PyObject* s_requests = PyUnicode_InternFromString("requests");
     PyObject* s_limits = PyUnicode_InternFromString("limits");
+    PyObject* out = NULL;
+    if (!s_requests || !s_limits) goto fail;
     const Py_hash_t hreq = PyObject_Hash(s_requests), hlim = PyObject_Hash(s_limits);
-    PyObject* out = PyList_New(n);
+    out = PyList_New(n);
     if (!out) goto fail;
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* c = PyList_GET_ITEM(cl, i);
@@ -205,9 +207,11 @@ static PyObject* run_results(PyObject* self, PyObject* args) {
     if (hc == -1 || hm == -1) return NULL;
     PyObject* s_request = PyUnicode_InternFromString("request");
     PyObject* s_limit = PyUnicode_InternFromString("limit");
-    PyObject* keys = PyTuple_Pack(2, s_request, s_limit);
+    PyObject *keys = NULL, *out = NULL;
+    if (!s_request || !s_limit) goto fail;
+    keys = PyTuple_Pack(2, s_request, s_limit);
     const Py_hash_t hr = PyObject_Hash(s_request), hl = PyObject_Hash(s_limit);
-    PyObject* out = PyList_New(n);
+    out = PyList_New(n);
     if (!out || !keys) goto fail;
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* c = PyList_GET_ITEM(cl, i);
