@@ -6,12 +6,16 @@ of piece j can share the CUs with the body of piece j+1.  Rows must be identical
 usage: python scripts/kll_overlap.py [--series 20000] [--pieces 2 4 8 16] [--rounds 5]
 """
 import argparse
+import os
+import sys
 import time
 
 import torch
 
-from krr_amd import _native
-from krr_amd.core.sketch import KllConfig
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from krr_amd import _native  # noqa: E402
+from krr_amd.core.sketch import KllConfig  # noqa: E402
 
 
 def main():
