@@ -75,7 +75,7 @@ def main():
     nbytes = 2 * 8 * S * L  # two passes over the slice
     for name, _ in variants:
         ms = sorted(times[name])[len(times[name]) // 2]
-        print(f"{name}: median {ms:.3f} ms over {a.rounds} rounds ({nbytes / ms / 1e9:.0f} GB/s of the two passes' "
+        print(f"{name}: median {ms:.3f} ms over {a.rounds} rounds ({nbytes / (ms * 1e-3) / 1e9:.0f} GB/s of the two passes' "
               f"reads), rows == sequential: {bool(torch.equal(rows[name], ref))}", flush=True)
 
 
