@@ -420,6 +420,18 @@ int krr_rank_of(krr_ctx* ctx, const krr_series* series, const double* values, in
 int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k, double* out,
                        void* stream);
 
+/* Where a selected value sits in its segment (the sample OBJECT the reference returns,
+ * strategies/simple.py:29 `max(data_)` and :36 `data_[k]`, for inputs whose Decimals the
+ * float64 values do not reproduce character for character).  Per segment s with
+ * rank[s] >= -1: out_lt[s] = #samples < values[s], out_eq[s] = #samples == values[s]
+ * (float ==: -0 == +0; NaN equals nothing), out_pos[s] = slot offset (from the segment
+ * start) of the j-th sample equal to values[s] in position order, j = rank[s] - out_lt[s]
+ * (the element sorted(X)[rank] of a stable sort) or j = 0 when rank[s] == -1 (the first
+ * maximal element max() keeps); -1 when there is no such sample.  rank[s] < -1: segment
+ * skipped, its outputs untouched.  Device pointers, n_segments entries each. */
+int krr_locate(krr_ctx* ctx, const krr_series* series, const double* values, const int64_t* rank, int64_t* out_lt,
+               int64_t* out_eq, int64_t* out_pos, void* stream);
+
 /* Synthetic week-long series (bench/test data), generated on the device from a
  * counter-based hash so that no host packing or PCIe is involved.
  * kind 0 = CPU cores ~ Gamma(k=2, theta=0.05); kind 1 = memory bytes

@@ -76,6 +76,7 @@ EXPORTED_SYMBOLS = (
     "krr_sketch_refine",
     "krr_rank_of",
     "krr_select_present",
+    "krr_locate",
     "krr_window_key_cap",
     "krr_window_export",
     "krr_window_merge",
@@ -296,6 +297,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_sketch_refine.restype = ctypes.c_int
         lib.krr_select_present.argtypes = [vp, sp, vp, vp, vp]
         lib.krr_select_present.restype = ctypes.c_int
+        lib.krr_locate.argtypes = [vp, sp, vp, vp, vp, vp, vp, vp]
+        lib.krr_locate.restype = ctypes.c_int
         lib.krr_window_key_cap.argtypes = [i64, i64, pp]
         lib.krr_window_key_cap.restype = i64
         lib.krr_window_export.argtypes = [vp, sp, pp, i64, i64, vp, vp, vp]
@@ -604,6 +607,17 @@ class Context:
         _check_tensor(out, "float64", S)
         self._check(self._lib.krr_select_present(self._h, ctypes.byref(series), k.data_ptr(), out.data_ptr(),
                                                  self._stream(stream)))
+
+    def locate(self, series: KrrSeries, values, rank, out_lt, out_eq, out_pos, stream=None) -> None:
+        """Per segment: #samples < values[s], #== values[s], and the slot offset of the
+        (rank[s] - lt)-th sample equal to values[s] (rank -1: the first one; < -1: skipped)."""
+        S = series.n_segments
+        _check_tensor(values, "float64", S)
+        for t in (rank, out_lt, out_eq, out_pos):
+            _check_tensor(t, "int64", S)
+        self._check(self._lib.krr_locate(self._h, ctypes.byref(series), values.data_ptr(), rank.data_ptr(),
+                                         out_lt.data_ptr(), out_eq.data_ptr(), out_pos.data_ptr(),
+                                         self._stream(stream)))
 
     # --- time-sharded exact percentiles in one pass (window export / merge) ---------
     def window_export(self, series: KrrSeries, params: KrrPercentileParams, ext_slots: int, key_cap: int, hdr,

@@ -162,7 +162,13 @@ def slice_series(ps, lo: int, hi: int):
     a, b = int(ps.offsets[lo]), int(ps.offsets[hi])
     offs = (ps.offsets[lo:hi + 1] - a).astype(np.int64)
     lens = np.diff(offs)
-    return PackedSeries(ps.values[a:b], offs, int(lens.max()) if lens.size else 0, ps.gaps_are_nan)
+    exact = getattr(ps, "exact", None)
+    if exact is not None:
+        exact = exact[lo:hi]
+    sources = getattr(ps, "sources", None)
+    return PackedSeries(ps.values[a:b], offs, int(lens.max()) if lens.size else 0, ps.gaps_are_nan,
+                        exact if exact is not None and exact.any() else None,
+                        sources[lo:hi] if exact is not None and exact.any() else None)
 
 
 def slice_fleet(fleet, lo: int, hi: int):

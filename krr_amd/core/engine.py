@@ -53,6 +53,13 @@ class RawResults:
     mem_value: np.ndarray
     mem_count: np.ndarray
     mem_flags: np.ndarray
+    # HistoryData segments whose Decimals the float64 values do not reproduce
+    # (PackedSeries.exact): krr_locate's answers ({"cpu"|"mem": (lt, eq, pos)}, int64 [S]
+    # each, -1 where not located), then krr_amd.core.exact.resolve's object index -> the
+    # reference's own sample object (CPU proposal / memory max before the buffer)
+    locate: Optional[dict] = None
+    cpu_exact: Optional[dict] = None
+    mem_exact: Optional[dict] = None
 
 
 class SimpleEngine:
@@ -120,15 +127,16 @@ class SimpleEngine:
         from krr_amd.core.distributed import unpack_records
 
         S = fleet.n_objects
+        locate = needs_locate(fleet, params)
         with torch.cuda.device(self.device):
             # the launch writes the 32-B records straight into page-locked host memory
             # (krr_simple_run_records with a mapped host buffer): one sync, no D2H copies
             rec = torch.empty((S, 4), dtype=torch.int64, pin_memory=True)
-            self._run_chunks(fleet, params, rec)
+            loc = self._run_chunks(fleet, params, rec, locate=locate)
             torch.cuda.current_stream(self.device).synchronize()
         host = unpack_records(rec.numpy())
         return RawResults(host["cpu_value"], host["cpu_count"], host["cpu_flags"], host["mem_value"],
-                          host["mem_count"], host["mem_flags"])
+                          host["mem_count"], host["mem_flags"], loc)
 
 
     def run_packed_records(self, fleet: PackedFleet, params: _native.KrrPercentileParams):
@@ -157,11 +165,13 @@ class SimpleEngine:
     # (profiles/r02/footprint)
     chunk_bytes = 16 << 30
 
-    def _run_chunks(self, fleet: PackedFleet, params: _native.KrrPercentileParams, rec) -> None:
+    def _run_chunks(self, fleet: PackedFleet, params: _native.KrrPercentileParams, rec,
+                    locate: bool = False) -> Optional[dict]:
         """Upload + fused launch per chunk of objects, records rows into ``rec`` (device or
         page-locked host), all on the current stream: a chunk's device buffers are released
         to the caching allocator after its launch is enqueued, which reuses them in stream
-        order for the next chunk."""
+        order for the next chunk.  ``locate``: also krr_locate over each chunk's segments of
+        exactness class >= 1 (``_locate_chunk``); returns its answers, else None."""
         import torch
 
         from krr_amd.core.distributed import fleet_shard_bounds, slice_fleet
@@ -176,13 +186,64 @@ class SimpleEngine:
         out = {k: torch.empty(S, dtype=dt, device=dev) for k, dt in
                (("cpu_value", torch.float64), ("cpu_count", torch.int64), ("cpu_flags", torch.int32),
                 ("mem_value", torch.float64), ("mem_count", torch.int64), ("mem_flags", torch.int32))}
+        loc = {r: tuple(np.full(S, -1, dtype=np.int64) for _ in range(3)) for r in ("cpu", "mem")} if locate else None
         for lo, hi in bounds:
             part = fleet if (lo, hi) == (0, S) else slice_fleet(fleet, lo, hi)
             cv, co = self._to_device(part.cpu)
             mv, mo = self._to_device(part.mem)
-            ctx.simple_run(ctx.series(cv, co, max(part.cpu.max_len, 1), part.cpu.gaps_are_nan),
-                           ctx.series(mv, mo, max(part.mem.max_len, 1), part.mem.gaps_are_nan),
-                           params, {k: v[lo:hi] for k, v in out.items()}, records=rec[lo:hi])
+            cs = ctx.series(cv, co, max(part.cpu.max_len, 1), part.cpu.gaps_are_nan)
+            ms = ctx.series(mv, mo, max(part.mem.max_len, 1), part.mem.gaps_are_nan)
+            chunk_out = {k: v[lo:hi] for k, v in out.items()}
+            ctx.simple_run(cs, ms, params, chunk_out, records=rec[lo:hi])
+            if locate:
+                self._locate_chunk(ctx, part, cs, ms, params, chunk_out, loc, lo)
+        return loc
+
+    def _locate_chunk(self, ctx, part: PackedFleet, cs, ms, params, out: dict, loc: dict, lo: int) -> None:
+        """krr_locate for the chunk's class >= 1 segments that select one sample: memory
+        (rank -1: the first maximal element, simple.py:29) and SORTED_LOWER CPU (rank k of
+        the stable sort).  REF_INDEX needs no search (its position IS k) and LINEAR is defined
+        on the float64 values.  Synchronises the stream (the ranks come from the counts)."""
+        import torch
+
+        torch.cuda.current_stream(self.device).synchronize()
+        dev = torch.device("cuda", self.device)
+        for name, ps, series in (("cpu", part.cpu, cs), ("mem", part.mem, ms)):
+            if ps.exact is None:
+                continue
+            rank = locate_ranks(name, ps.exact, out[f"{name}_count"].cpu().numpy(),
+                                out[f"{name}_flags"].cpu().numpy(), params)
+            if rank is None:
+                continue
+            rank_d = torch.from_numpy(rank).to(dev)
+            lt, eq, pos = (torch.full_like(rank_d, -1) for _ in range(3))
+            ctx.locate(series, out[f"{name}_value"], rank_d, lt, eq, pos)
+            for dst, src in zip(loc[name], (lt, eq, pos)):
+                dst[lo:lo + src.numel()] = src.cpu().numpy()
+
+
+def locate_ranks(name: str, exact: np.ndarray, count: np.ndarray, flags: np.ndarray, params) -> Optional[np.ndarray]:
+    """krr_locate's rank per segment ("cpu" | "mem"): -1 (the first maximal sample) for memory,
+    k = floor((n-1)·p/100) for SORTED_LOWER CPU, on class >= 1 segments holding >= 2 samples and
+    no NaN (those answer by the NaN rules); -2 (skip) elsewhere.  None: nothing to locate."""
+    if name == "cpu" and params.mode != _native.KRR_PCT_SORTED_LOWER:
+        return None
+    flags = np.asarray(flags).astype(np.uint32)
+    ok = (np.asarray(exact) > 0) & (flags & (_native.KRR_FLAG_EMPTY | _native.KRR_FLAG_NAN) == 0) & (count >= 2)
+    if not ok.any():
+        return None
+    rank = np.full(count.size, -2, dtype=np.int64)
+    if name == "mem":
+        rank[ok] = -1
+    else:
+        for i in np.flatnonzero(ok).tolist():  # k in exact integers (p_num·n can pass 2^63)
+            rank[i] = (int(count[i]) - 1) * int(params.p_num) // (100 * int(params.p_den))
+    return rank
+
+
+def needs_locate(fleet: PackedFleet, params) -> bool:
+    """Does a fleet hold HistoryData segments whose answer must be located (krr_locate)?"""
+    return fleet.cpu.exact is not None and params.mode == _native.KRR_PCT_SORTED_LOWER or fleet.mem.exact is not None
 
 
 def pinned_alloc(n: int) -> np.ndarray:

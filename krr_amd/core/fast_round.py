@@ -101,6 +101,7 @@ def format_simple_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALU
     buffer = settings.memory_buffer()
     cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
                                memory_min_value, threads)
+    _route_exact(st, raw)
     # Decimals are immutable: one object per distinct string (1m / 1M granularity makes
     # fleets highly repetitive), found by a sort of the string columns, not per object.
     # Each object still gets its own models.
@@ -140,6 +141,16 @@ def decimal_column(strings: np.ndarray, nan=None) -> list:
     return decs[inv.reshape(-1)].tolist()
 
 
+def _route_exact(status, raw) -> None:
+    """Objects whose answer is the reference's own sample object (krr_amd.core.exact: HistoryData
+    Decimals the float64 values do not reproduce) take the Python rounding of that object."""
+    for name, bit in (("cpu_exact", CPU_FALLBACK), ("mem_exact", MEM_FALLBACK)):
+        ex = getattr(raw, name, None)
+        if ex:
+            idx = np.fromiter(ex.keys(), dtype=np.int64, count=len(ex))
+            status[idx] |= bit
+
+
 def _apply_fallbacks(cpu_col, mem_col, status, raw, settings, buffer, cpu_min_value, memory_min_value) -> None:
     """The objects the native rounding did not cover, through the Python restatement (which
     raises what the reference raises)."""
@@ -172,6 +183,7 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
     buffer = settings.memory_buffer()
     cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
                                memory_min_value, threads)
+    _route_exact(st, raw)
     gc_was = gc.isenabled()
     gc.disable()
     try:

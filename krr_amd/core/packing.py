@@ -18,6 +18,7 @@ And one alternative layout:
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from decimal import Decimal
 from typing import Iterable, Mapping, Optional, Sequence
@@ -33,6 +34,11 @@ class PackedSeries:
     offsets: np.ndarray       # int64 [S+1]
     max_len: int              # max segment length (planning hint for the kernels)
     gaps_are_nan: bool = False
+    # HistoryData path only (pack_resource): per segment the exactness class of its Decimals
+    # (EXACT_* below; None = every sample came from a Prometheus string: canonical), and for
+    # class >= 1 segments the tuple of its pod sample lists, which positions index into
+    exact: Optional[np.ndarray] = None
+    sources: Optional[list] = None
 
     @property
     def n_segments(self) -> int:
@@ -60,33 +66,102 @@ def _from_chunks(chunks: list[np.ndarray], lens: list[int], gaps: bool = False) 
     return PackedSeries(values.astype(np.float64, copy=False), offsets, int(max(lens, default=0)), gaps)
 
 
-def _decimals_to_f64(xs: Sequence[Decimal]) -> np.ndarray:
-    # float(Decimal) is correctly rounded; for Prometheus' shortest-repr strings it
-    # recovers the exact float64 the server formatted.
-    #
-    # Contract of the HistoryData path: every Decimal is what the reference's loader
-    # builds, Decimal(<Prometheus sample string>) (prometheus.py:152), and Prometheus
-    # formats samples with Go's strconv.FormatFloat(v, 'f', -1, 64) — the shortest
-    # string that round-trips — so prom_decimal(float(d)) == d.  A hand-made Decimal
-    # with more significant digits than a float64 holds (e.g. 100000000.0000000000000001)
-    # or a non-canonical form ('0.10') is NOT reproduced: the kernel selects float64
-    # values and the host rebuilds the Decimal from the float's shortest repr.
-    return np.fromiter((float(x) for x in xs), dtype=np.float64, count=len(xs))
+# Exactness class of a HistoryData segment — what its samples' float64 images stand for
+# (krr_amd/csrc/krr_pyhist.cpp holds the same rule natively):
+EXACT_CANONICAL = 0  # every Decimal is prom_decimal(float(d)): the one Prometheus' string gives
+EXACT_FAITHFUL = 1   # every VALUE is its float's shortest repr, some representation is not
+EXACT_INEXACT = 2    # some sample is not (more digits than float64 holds, non-Decimal, sNaN)
+
+
+def sample_class(x) -> tuple[float, int]:
+    """(float64, exactness class) of one HistoryData sample (the packer's rule)."""
+    if type(x) is not Decimal:
+        return float(x), EXACT_INEXACT
+    if x.is_nan():
+        return math.nan, (EXACT_CANONICAL if str(x) == "NaN" else EXACT_INEXACT)
+    f = float(x)
+    if x.is_infinite():
+        return f, EXACT_CANONICAL
+    if math.isinf(f):
+        return f, EXACT_INEXACT
+    shortest = Decimal(repr(f))
+    if shortest != x:
+        return f, EXACT_INEXACT
+    _, digits, exp = x.as_tuple()
+    if not any(digits):
+        return f, (EXACT_CANONICAL if exp == 0 else EXACT_FAITHFUL)
+    tz = len(digits) - len("".join(map(str, digits)).rstrip("0"))
+    es = exp + tz
+    return f, (EXACT_CANONICAL if (exp == 0 if es >= 0 else tz == 0) else EXACT_FAITHFUL)
+
+
+def _load_pyhist():
+    """krr_amd/lib/_krr_pyhist.so (krr_amd/csrc/krr_pyhist.cpp, built by __graft_entry__.build()):
+    the per-sample walk in C++.  None when it is not built: the Python form below is equal."""
+    import importlib.machinery
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "_krr_pyhist.so")
+    if not os.path.exists(path):
+        return None
+    try:
+        loader = importlib.machinery.ExtensionFileLoader("_krr_pyhist", path)
+        spec = importlib.util.spec_from_file_location("_krr_pyhist", path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        return mod
+    except ImportError:  # pragma: no cover - built for another interpreter
+        return None
+
+
+_PYHIST = _load_pyhist()
+
+
+def _pack_resource_py(histories: Sequence[Mapping], resource: ResourceType):
+    values: list[float] = []
+    lens: list[int] = []
+    cls: list[int] = []
+    sources: list = []
+    for h in histories:
+        pods = h.get(resource) or {}
+        kept = [samples for samples in pods.values() if len(samples)]
+        c = EXACT_CANONICAL
+        for samples in kept:
+            for x in samples:
+                f, k = sample_class(x)
+                values.append(f)
+                c = max(c, k)
+        lens.append(sum(len(s) for s in kept))
+        cls.append(c)
+        sources.append(tuple(kept) if c else None)
+    return np.asarray(values, dtype=np.float64), lens, np.asarray(cls, dtype=np.uint8), sources
 
 
 def pack_resource(histories: Sequence[Mapping], resource: ResourceType) -> PackedSeries:
-    """One segment per history: its pods' samples concatenated in dict order."""
-    chunks: list[np.ndarray] = []
-    lens: list[int] = []
-    for h in histories:
-        pods = h.get(resource) or {}
-        n = 0
-        for samples in pods.values():
-            if len(samples):
-                chunks.append(_decimals_to_f64(samples))
-                n += len(samples)
-        lens.append(n)
-    return _from_chunks(chunks, lens)
+    """One segment per history: its pods' samples concatenated in dict order, as float64
+    (float(Decimal): correctly rounded, so Prometheus' shortest-repr strings give back the
+    exact float the server formatted), plus each segment's exactness class.
+
+    The reference returns the selected sample object itself (simple.py:36 ``data_[k]``,
+    :29 ``max(data_)``).  For a CANONICAL segment (every Decimal is what the reference's
+    loader parses from Prometheus' string, prometheus.py:152) the host rebuilds that object
+    from the kernel's float64 answer (prom_decimal).  Other segments keep their pod lists
+    (``sources``) and SimpleStrategy returns the reference's own object at the position the
+    GPU located (krr_amd/core/exact.py), e.g. Decimal('0.10') or 25-digit values."""
+    if _PYHIST is not None:
+        vals, lens_b, cls_b, sources = _PYHIST.pack_resource(histories, resource, Decimal)
+        values = np.frombuffer(vals, dtype=np.float64) if len(vals) else np.zeros(0, dtype=np.float64)
+        lens = np.frombuffer(lens_b, dtype=np.int64)
+        cls = np.frombuffer(cls_b, dtype=np.uint8).copy()
+    else:
+        values, lens, cls, sources = _pack_resource_py(histories, resource)
+        lens = np.asarray(lens, dtype=np.int64)
+    offsets = np.zeros(lens.size + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    exact = cls if cls.any() else None
+    return PackedSeries(values, offsets, int(lens.max(initial=0)), False, exact,
+                        sources if exact is not None else None)
 
 
 def pack_histories(histories: Sequence[Mapping]) -> PackedFleet:

@@ -2966,6 +2966,51 @@ __global__ __launch_bounds__(64) void k_select_present(const double* __restrict_
     }
 }
 
+// Where a selected value sits in its segment: lt = #samples < v, eq = #samples == v
+// (float ==: -0 == +0, NaN never), pos = the slot offset of the j-th sample equal to v in
+// position order, j = rank - lt (rank >= 0: the stable-sort rank of sorted(X)[rank]) or 0
+// (rank == -1: the first maximal element Python's max() keeps), -1 when there is none.
+// rank < -1: segment skipped, outputs untouched.  The HistoryData path resolves with it
+// the reference's own sample object (simple.py:29 max(data_), :36 data_[k] of a sorted
+// list) for segments whose Decimals differ in representation from their float64 images.
+__global__ __launch_bounds__(64) void k_locate(const double* __restrict__ vals, const int64_t* __restrict__ offs,
+                                               int64_t S, const double* __restrict__ v,
+                                               const int64_t* __restrict__ rank, int64_t* out_lt,
+                                               int64_t* out_eq, int64_t* out_pos) {
+    const int lane = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const int64_t r = rank[s];
+        if (r < -1) continue;
+        const double x = v[s];
+        const int64_t beg = offs[s], end = offs[s + 1];
+        RankOfProc P{x, 0u, 0u};
+        stream_segment<false>(vals, beg, end, P, lane);
+        const int64_t lt = wave_sum_u32(P.lt), eq = (int64_t)wave_sum_u32(P.le) - lt;
+        const int64_t j = r >= 0 ? r - lt : 0;
+        int64_t pos = -1;
+        if (j >= 0 && j < eq) {
+            int64_t run = 0;
+            for (int64_t base = beg; base < end; base += kWave) {
+                const int64_t i = base + lane;
+                const bool hit = i < end && vals[i] == x;
+                const uint64_t m = ballot(hit);
+                const uint32_t c = popc64(m);
+                if (run + c > j) {
+                    const uint64_t sel = ballot(hit && lane_prefix(m) == (uint32_t)(j - run));
+                    pos = base + (__ffsll((long long)sel) - 1) - beg;
+                    break;
+                }
+                run += c;
+            }
+        }
+        if (lane == 0) {
+            out_lt[s] = lt;
+            out_eq[s] = eq;
+            out_pos[s] = pos;
+        }
+    }
+}
+
 // --------------------- exact refinement of merged sketches ---------------------
 // Sketch counts are exact, so the merged sketch of a time-sharded series tells
 // exactly which bin holds each needed rank and how many samples lie below it.
@@ -4101,6 +4146,25 @@ int krr_select_present(krr_ctx* ctx, const krr_series* series, const int64_t* k,
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     hipLaunchKernelGGL(k_select_present, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
                        series->offsets, S, series->gaps_are_nan, k, out);
+    KRR_HIP(ctx, hipGetLastError());
+    return KRR_OK;
+}
+
+int krr_locate(krr_ctx* ctx, const krr_series* series, const double* values, const int64_t* rank, int64_t* out_lt,
+               int64_t* out_eq, int64_t* out_pos, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    const int64_t S = series->n_segments;
+    if (S == 0) return KRR_OK;
+    if (!values || !rank || !out_lt || !out_eq || !out_pos) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
+    if (series->max_segment_len > (int64_t)UINT32_MAX)
+        return set_err(ctx, KRR_E_UNSUPPORTED, "krr_locate counts in 32 bits%s: segment of %lld slots", "",
+                       (long long)series->max_segment_len);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipLaunchKernelGGL(k_locate, dim3(grid_for(S)), dim3(64), 0, (hipStream_t)stream, series->values,
+                       series->offsets, S, values, rank, out_lt, out_eq, out_pos);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -12,7 +12,10 @@
 
 The GPU returns the selected/maximal float64 sample; the host rebuilds its
 Decimal exactly as the reference parsed it (prom_decimal) and applies the
-memory buffer in the reference's decimal context.
+memory buffer in the reference's decimal context.  HistoryData whose Decimals
+are not Prometheus' shortest strings ('0.10', 25-digit values ...) get the
+reference's own sample object at the position the GPU located
+(krr_amd.core.exact).
 """
 from __future__ import annotations
 
@@ -78,7 +81,13 @@ class SimpleStrategySettings(StrategySettings):
             return Decimal(1 + self.memory_buffer_percentage / 100)
 
     def run_fleet(self, fleet: PackedFleet) -> RawResults:
-        return default_engine(self.device).run_packed(fleet, self.params())
+        params = self.params()
+        raw = default_engine(self.device).run_packed(fleet, params)
+        if fleet.cpu.exact is not None or fleet.mem.exact is not None:
+            from krr_amd.core.exact import resolve
+
+            resolve(fleet, raw, params)
+        return raw
 
     def run_fleet_records(self, fleet: PackedFleet, device: Optional[int] = None):
         """One kernel pass over a fleet shard -> int64 [S, 4] device records (multi-GPU path)."""
@@ -93,6 +102,9 @@ class SimpleStrategySettings(StrategySettings):
             raise RuntimeError(f"object {i}: CPU selection bound violated (KRR_FLAG_CAPACITY)")
         if flags & _native.KRR_FLAG_EMPTY:
             return Decimal("NaN")
+        ex = getattr(raw, "cpu_exact", None)
+        if ex is not None and i in ex:  # the reference's own sample object
+            return ex[i]
         if flags & _native.KRR_FLAG_NAN:
             # sorted() over Decimals compares with '<'; a NaN operand signals once any
             # comparison happens, i.e. when n >= 2 (one sample is never compared).
@@ -105,6 +117,12 @@ class SimpleStrategySettings(StrategySettings):
         flags = int(raw.mem_flags[i])
         if flags & _native.KRR_FLAG_EMPTY:
             return Decimal("NaN")
+        ex = getattr(raw, "mem_exact", None)
+        if ex is not None and i in ex:  # max(data_) itself, times the buffer
+            if buffer is None:
+                buffer = self.memory_buffer()
+            with decimal.localcontext(reference_context()):
+                return ex[i] * buffer
         if flags & _native.KRR_FLAG_NAN:
             # max() over Decimals compares with '>' and a NaN operand signals
             # (simple.py:29) — unless n == 1, where nothing is compared and NaN passes.

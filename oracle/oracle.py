@@ -82,3 +82,21 @@ def seg_max(values: np.ndarray, offsets: np.ndarray, gaps: bool = False, nthread
 
 def exact_rank(n: int, p_num: int, p_den: int) -> int:
     return int(_load().oracle_exact_rank(n, p_num, p_den))
+
+
+def locate(values: np.ndarray, offsets: np.ndarray, v: np.ndarray, rank: np.ndarray):
+    """krr_locate restated (include/krr_amd.h): per segment with rank >= -1, lt = #x < v,
+    eq = #x == v, pos = offset of the j-th x == v (j = rank - lt, or 0 for rank -1), -1
+    if none; other segments -1 everywhere.  Plain numpy, for the CPU stand-in tests."""
+    S = offsets.size - 1
+    lt, eq, pos = (np.full(S, -1, dtype=np.int64) for _ in range(3))
+    for s in range(S):
+        if rank[s] < -1:
+            continue
+        seg = values[offsets[s]:offsets[s + 1]]
+        lt[s] = int(np.count_nonzero(seg < v[s]))
+        hits = np.flatnonzero(seg == v[s])
+        eq[s] = hits.size
+        j = int(rank[s]) - int(lt[s]) if rank[s] >= 0 else 0
+        pos[s] = int(hits[j]) if 0 <= j < hits.size else -1
+    return lt, eq, pos

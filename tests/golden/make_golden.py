@@ -164,46 +164,50 @@ def main():
             ResourceType.Memory: {k: [Decimal(s) for s in v] for k, v in case["mem"].items() if v},
         }
 
-    out_cases = []
-    for case in cases:
-        results = {}
-        for sp_name, make in settings_paths:
-            strat, runner = make()
-            hist = to_hist(case)
-            entry = {}
-            try:
-                raw = strat.run(hist, None)
-                entry["raw"] = {
-                    "cpu_request": dstr(raw[ResourceType.CPU].request),
-                    "cpu_limit": dstr(raw[ResourceType.CPU].limit),
-                    "mem_request": dstr(raw[ResourceType.Memory].request),
-                    "mem_limit": dstr(raw[ResourceType.Memory].limit),
-                }
+    def run_cases(cases):
+        out_cases = []
+        for case in cases:
+            results = {}
+            for sp_name, make in settings_paths:
+                strat, runner = make()
+                hist = to_hist(case)
+                entry = {}
                 try:
-                    rr = runner._format_result(raw)
-                    entry["rounded"] = {
-                        "cpu_request": dstr(rr[ResourceType.CPU].request),
-                        "cpu_limit": dstr(rr[ResourceType.CPU].limit),
-                        "mem_request": dstr(rr[ResourceType.Memory].request),
-                        "mem_limit": dstr(rr[ResourceType.Memory].limit),
+                    raw = strat.run(hist, None)
+                    entry["raw"] = {
+                        "cpu_request": dstr(raw[ResourceType.CPU].request),
+                        "cpu_limit": dstr(raw[ResourceType.CPU].limit),
+                        "mem_request": dstr(raw[ResourceType.Memory].request),
+                        "mem_limit": dstr(raw[ResourceType.Memory].limit),
                     }
-                except Exception as e:  # e.g. ceil(Infinity)
-                    entry["rounded_error"] = type(e).__name__
-            except Exception as e:
-                entry["error"] = type(e).__name__
-            # SORTED_LOWER: the reference's own index rule over pre-sorted samples
-            flat = [Decimal(s) for v in case["cpu"].values() for s in v]
-            try:
-                entry["sorted"] = dstr(strat.settings.calculate_cpu_proposal({"all": sorted(flat)}))
-            except Exception as e:
-                entry["sorted_error"] = type(e).__name__
-            # LINEAR: numpy.percentile on the float64 samples
-            f = np.array([float(s) for s in flat], dtype=np.float64)
-            if f.size:
-                lin = float(np.percentile(f, float(strat.settings.cpu_percentile)))
-                entry["linear_hex"] = lin.hex() if not math.isnan(lin) else "nan"
-            results[sp_name] = entry
-        out_cases.append({"name": case["name"], "cpu": case["cpu"], "mem": case["mem"], "results": results})
+                    try:
+                        rr = runner._format_result(raw)
+                        entry["rounded"] = {
+                            "cpu_request": dstr(rr[ResourceType.CPU].request),
+                            "cpu_limit": dstr(rr[ResourceType.CPU].limit),
+                            "mem_request": dstr(rr[ResourceType.Memory].request),
+                            "mem_limit": dstr(rr[ResourceType.Memory].limit),
+                        }
+                    except Exception as e:  # e.g. ceil(Infinity)
+                        entry["rounded_error"] = type(e).__name__
+                except Exception as e:
+                    entry["error"] = type(e).__name__
+                # SORTED_LOWER: the reference's own index rule over pre-sorted samples
+                flat = [Decimal(s) for v in case["cpu"].values() for s in v]
+                try:
+                    entry["sorted"] = dstr(strat.settings.calculate_cpu_proposal({"all": sorted(flat)}))
+                except Exception as e:
+                    entry["sorted_error"] = type(e).__name__
+                # LINEAR: numpy.percentile on the float64 samples
+                f = np.array([float(s) for s in flat], dtype=np.float64)
+                if f.size:
+                    lin = float(np.percentile(f, float(strat.settings.cpu_percentile)))
+                    entry["linear_hex"] = lin.hex() if not math.isnan(lin) else "nan"
+                results[sp_name] = entry
+            out_cases.append({"name": case["name"], "cpu": case["cpu"], "mem": case["mem"], "results": results})
+        return out_cases
+
+    out_cases = run_cases(cases)
 
     # ---------------- the index rule over (n, p) -------------------------------------
     strat, _ = cli_strategy("99", "5")
@@ -231,6 +235,85 @@ def main():
         json.dump(doc, fh, indent=0, sort_keys=True)
     print(f"wrote {path}: {len(out_cases)} cases x {len(settings_paths)} settings paths, "
           f"{len(index_table)} index rows")
+
+    # ---------------- HistoryData beyond Prometheus' strings --------------------------
+    # The plugin API takes ANY HistoryData (core/abstract/strategies.py:35-36, 54-56): hand-built
+    # Decimals, non-canonical forms, more digits than a float64 holds.  The reference returns
+    # the sample object itself (simple.py:29, :36), so these pin representation and exact ties.
+    exact = exact_cases()
+    doc = {
+        "generator": "tests/golden/make_golden.py",
+        "reference": "yonahd/krr 1.0.0 @ /root/reference (imported, not copied)",
+        "settings_paths": [n for n, _ in settings_paths],
+        "cases": run_cases(exact),
+        "note": "inputs are str(Decimal) of the HistoryData samples, NOT Prometheus strings",
+    }
+    path = os.path.join(HERE, "simple_strategy_exact.json")
+    with open(path, "w") as fh:
+        json.dump(doc, fh, indent=0, sort_keys=True)
+    print(f"wrote {path}: {len(exact)} cases x {len(settings_paths)} settings paths")
+
+
+def exact_cases():
+    """Sample strings (Decimal(s) is the HistoryData sample) outside Prometheus' canonical form."""
+    rng = np.random.default_rng(20261018)
+    cases = []
+
+    def add(name, cpu_pods, mem_pods):
+        cases.append({"name": name, "cpu": cpu_pods, "mem": mem_pods})
+
+    # the round-4 probe (VERDICT.md Weak 1)
+    add("probe_trailing_zeros", {"a": ["0.10", "0.20"]}, {"a": ["1.0E+7", "2.00E+7"]})
+    add("probe_25_digits", {"a": ["0.0010000000000000000000001"]}, {"a": ["100000000.0000000000000001"]})
+    add("probe_float_collision", {"a": ["0.1", "0.1000000000000000055511151231257827"]},
+        {"a": ["20000000.00000000000000001", "20000000"]})
+    add("collision_max_not_first", {"a": ["0.5", "0.50000000000000000001", "0.5"]},
+        {"a": ["20000000", "19999999.99999999999999999", "20000000.000000000000000001", "20000000.00000000000000001",
+               "20000000"]})
+    add("equal_values_repr_ties", {"a": ["0.30", "0.3", "0.300", "0.1"] * 30},
+        {"a": ["2E+7", "20000000", "2.0E+7", "1E+7"], "b": ["2.000E+7"]})
+    add("sorted_ties_repr", {"a": ["0.5", "0.50", "0.500", "0.1", "0.5000", "0.9"]}, {"a": ["5", "5.0"]})
+    add("exponent_forms", {"a": ["1E+2", "100", "1.00E+2", "5E-3", "0.0050"]}, {"a": ["1E+30", "1.0E+30"]})
+    add("zero_forms", {"a": ["0.0", "-0.00", "0E+3", "0", "-0"]}, {"a": ["0.0", "0E+3", "-0.000"]})
+    add("long_digits", {"a": ["0.123456789123456789123456789", "0.0123456789012345678901234567890123"]},
+        {"a": ["123456789.123456789123456789", "123456789.1234567891234567890"]})
+    add("collision_group_sorted", {"a": ["0.3", "0.29999999999999998889776975", "0.3000000000000000166533453694",
+                                         "0.29999999999999998", "0.2", "0.4"] * 7},
+        {"a": ["1073741824.0000000000000000001", "1073741824", "1073741824.00000000000000000001"]})
+    add("nan_forms", {"a": ["0.1", "-NaN", "0.2"]}, {"a": ["7.0"]})
+    for i in range(24):
+        npods = int(rng.integers(1, 4))
+        cpu, mem = {}, {}
+        for p in range(npods):
+            n = int(rng.integers(1, 120))
+            x = rng.gamma(2.0, 0.05, n)
+            if i % 3 == 0:
+                x = np.round(x, 2)  # ties
+            m = np.floor(rng.normal(2e8, 2e7, int(rng.integers(1, 90))))
+            if i % 2 == 0:
+                m[rng.integers(0, m.size, max(1, m.size // 3))] = m.max()  # several copies of the max
+            cpu[f"pod{p}"] = [_variant(rng, float(v), i) for v in x]
+            mem[f"pod{p}"] = [_variant(rng, float(v), i + 1) for v in m]
+        add(f"random_exact_{i}", cpu, mem)
+    return cases
+
+
+def _variant(rng, x: float, i: int) -> str:
+    """One sample string: canonical, a trailing-zero / exponent form of the same value, or the
+    float's full binary expansion (a different Decimal with the same float64)."""
+    from decimal import Decimal as D
+
+    r = float(rng.random())
+    canon = str(D(prom_format(x)))
+    if r < 0.4:
+        return canon
+    if r < 0.6:
+        return canon + ("0" * int(rng.integers(1, 4)) if "." in canon else ".0")
+    if r < 0.75:
+        return format(D(canon), "E")
+    if i % 2 and r < 0.95:
+        return str(D(x))  # exact binary value: > 17 digits, same float, distinct Decimal
+    return canon
 
 
 if __name__ == "__main__":

@@ -52,14 +52,7 @@ from krr_amd import _native  # noqa: E402
 from krr_amd.utils.prom_decimal import prom_format  # noqa: E402
 
 
-def oracle_run_packed(self, fleet, params):
-    from krr_amd.core.engine import RawResults
-    from oracle import oracle
-
-    cv, cn, cf = oracle.percentile(fleet.cpu.values, fleet.cpu.offsets, params.mode, params.p_num, params.p_den,
-                                   params.q, fleet.cpu.gaps_are_nan)
-    mv, mn, mf = oracle.seg_max(fleet.mem.values, fleet.mem.offsets, fleet.mem.gaps_are_nan)
-    return RawResults(cv, cn, cf.astype(np.uint32), mv, mn, mf.astype(np.uint32))
+from _standin import oracle_run_packed  # noqa: E402
 
 
 def main():
@@ -69,6 +62,8 @@ def main():
     ap.add_argument("--loader", choices=integration.LOADERS, default="reference")
     ap.add_argument("--scan", choices=integration.SCANS, default="reference")
     ap.add_argument("--objects", type=int, default=100, help="config-1 objects in the collect check")
+    ap.add_argument("--exact", action="store_true",
+                    help="histories from tests/golden/simple_strategy_exact.json (hand-built Decimals)")
     args = ap.parse_args()
     if args.loader != "reference" or args.scan != "reference":
         return collect_check(args)
@@ -88,10 +83,17 @@ def main():
 
     cpu, mem = config1.inputs()
     cpu_s = {}
+    exact_cases = []
+    if args.exact:  # hand-built HistoryData whose runs the reference completes on this settings path
+        with open(os.path.join(HERE, "golden", "simple_strategy_exact.json")) as fh:
+            exact_cases = [c for c in json.load(fh)["cases"] if "rounded" in c["results"][args.path]]
 
-    class FakePrometheusLoader:  # prometheus.py:108-155's output for config 1
+    class FakePrometheusLoader:  # prometheus.py:108-155's output for config 1 (or the exact cases)
         async def gather_data(self, obj, resource, period, *, timeframe):
             o = int(obj.name.split("-")[1])
+            if args.exact:
+                pods = exact_cases[o]["cpu" if resource == ResourceType.CPU else "mem"]
+                return {k: [Decimal(s) for s in v] for k, v in pods.items() if v}
             x = cpu if resource == ResourceType.CPU else mem
             key = (o, resource.value)
             if key not in cpu_s:
@@ -100,10 +102,12 @@ def main():
             return cpu_s[key]
 
     none = {ResourceType.CPU: None, ResourceType.Memory: None}
-    objects = [K8sObjectData(cluster=None, name=f"app-{o:03d}", container="main", pods=config1.pod_names(o),
+    n_obj = len(exact_cases) if args.exact else config1.OBJECTS
+    objects = [K8sObjectData(cluster=None, name=f"app-{o:03d}", container="main",
+                             pods=(list(exact_cases[o]["cpu"]) if args.exact else config1.pod_names(o)),
                              namespace="default", kind="Deployment",
                              allocations=ResourceAllocations(requests=none, limits=none))
-               for o in range(config1.OBJECTS)]
+               for o in range(n_obj)]
 
     def make_runner(strategy=None):
         other = {"cpu_percentile": "99", "memory_buffer_percentage": "5"} if args.path == "cli_99_5" else {}
@@ -146,11 +150,19 @@ def main():
     report["result_types"] = sorted({type(a).__module__ + "." + type(a).__name__ for a in got})
     original = getattr(Runner, integration._ORIGINAL_ATTR)
     ref = asyncio.run(original(make_runner(), objects))
-    with open(os.path.join(HERE, "golden", "config1_reference.json")) as fh:
-        want = [[w["rounded"]["cpu_request"], w["rounded"]["mem_request"], w["rounded"]["mem_limit"]]
-                for w in json.load(fh)["results"][args.path]]
+    if args.exact:
+        want = [[c["results"][args.path]["rounded"][k] for k in ("cpu_request", "mem_request", "mem_limit")]
+                for c in exact_cases]
+        want = [["?" if v == "NaN" else v for v in w] for w in want]
+        report["n_objects"] = n_obj
+    else:
+        with open(os.path.join(HERE, "golden", "config1_reference.json")) as fh:
+            want = [[w["rounded"]["cpu_request"], w["rounded"]["mem_request"], w["rounded"]["mem_limit"]]
+                    for w in json.load(fh)["results"][args.path]]
     report["equals_reference_runner"] = rows(got) == rows(ref)
     report["equals_golden"] = rows(got) == want
+    if not report["equals_golden"]:
+        report["first_diff"] = next([i, a, b] for i, (a, b) in enumerate(zip(rows(got), want)) if a != b)
 
     # a custom strategy keeps the reference's per-object run() (examples/custom_strategy.py)
     class CustomStrategySettings(StrategySettings):

@@ -49,6 +49,16 @@ def test_reference_runner_results_equal_reference(path):
     assert r["custom_strategy_rows"] == [["99", "10000000", "10000000"]] * 3
 
 
+@pytest.mark.parametrize("path", ["cli_99_5", "default_int"])
+def test_reference_runner_exact_histories(path):
+    """install(Runner) with the reference's loader handing over hand-built Decimals ('0.10',
+    '2.00E+7', 25-digit values, float-colliding pairs; tests/golden/simple_strategy_exact.json):
+    the patched Runner returns the reference's own rounded values, equal to its unpatched run."""
+    r = _check("--engine", "oracle", "--path", path, "--exact")
+    assert r["equals_reference_runner"] and r["equals_golden"], r
+    assert r["n_objects"] >= 30
+
+
 @pytest.mark.parametrize("loader", ["bodies", "grouped"])
 def test_reference_collect_result_native_loader_and_fleet_scan(loader):
     """install(Runner, loader=..., scan="fleet"): the reference's whole _collect_result against
