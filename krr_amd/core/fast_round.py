@@ -197,6 +197,9 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
             if isinstance(mem_col[i], Decimal) and mem_col[i].is_nan():
                 mem_col[i] = q
         fields = {"requests", "limits"}
+        if not _v1_construct_layout(model):  # e.g. a pydantic v2 model: its own constructor, per object
+            return [model(requests={cpu_k: c, mem_k: m}, limits={cpu_k: None, mem_k: m})
+                    for c, m in zip(cpu_col, mem_col)]
         if _PYOBJ is not None:
             return _PYOBJ.allocations(model, fields, cpu_k, mem_k, cpu_col, mem_col)
         new, setattr_ = object.__new__, object.__setattr__
@@ -211,6 +214,16 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
     finally:
         if gc_was:
             gc.enable()
+
+
+def _v1_construct_layout(model) -> bool:
+    """True when instances of ``model`` are exactly pydantic v1's construct() layout (the field
+    dict + __fields_set__): a pydantic.v1 BaseModel without private attributes, as the
+    reference's models are (pydantic 1.10).  Anything else is built by its own constructor."""
+    import pydantic.v1 as pv1
+
+    return (isinstance(model, type) and issubclass(model, pv1.BaseModel)
+            and not getattr(model, "__private_attributes__", None))
 
 
 _FIELDS = ("request", "limit")

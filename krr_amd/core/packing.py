@@ -67,7 +67,7 @@ def _from_chunks(chunks: list[np.ndarray], lens: list[int], gaps: bool = False) 
 
 
 # Exactness class of a HistoryData segment — what its samples' float64 images stand for
-# (krr_amd/csrc/krr_pyhist.cpp holds the same rule natively):
+# (krr_amd/csrc/krr_pydec.cpp holds the same rule natively):
 EXACT_CANONICAL = 0  # every Decimal is prom_decimal(float(d)): the one Prometheus' string gives
 EXACT_FAITHFUL = 1   # every VALUE is its float's shortest repr, some representation is not
 EXACT_INEXACT = 2    # some sample is not (more digits than float64 holds, non-Decimal, sNaN)
@@ -95,19 +95,19 @@ def sample_class(x) -> tuple[float, int]:
     return f, (EXACT_CANONICAL if (exp == 0 if es >= 0 else tz == 0) else EXACT_FAITHFUL)
 
 
-def _load_pyhist():
-    """krr_amd/lib/_krr_pyhist.so (krr_amd/csrc/krr_pyhist.cpp, built by __graft_entry__.build()):
+def _load_pydec():
+    """krr_amd/lib/_krr_pydec.so (krr_amd/csrc/krr_pydec.cpp, built by __graft_entry__.build()):
     the per-sample walk in C++.  None when it is not built: the Python form below is equal."""
     import importlib.machinery
     import importlib.util
     import os
 
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "_krr_pyhist.so")
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "_krr_pydec.so")
     if not os.path.exists(path):
         return None
     try:
-        loader = importlib.machinery.ExtensionFileLoader("_krr_pyhist", path)
-        spec = importlib.util.spec_from_file_location("_krr_pyhist", path, loader=loader)
+        loader = importlib.machinery.ExtensionFileLoader("_krr_pydec", path)
+        spec = importlib.util.spec_from_file_location("_krr_pydec", path, loader=loader)
         mod = importlib.util.module_from_spec(spec)
         loader.exec_module(mod)
         return mod
@@ -115,7 +115,7 @@ def _load_pyhist():
         return None
 
 
-_PYHIST = _load_pyhist()
+_PYDEC = _load_pydec()
 
 
 def _pack_resource_py(histories: Sequence[Mapping], resource: ResourceType):
@@ -149,8 +149,8 @@ def pack_resource(histories: Sequence[Mapping], resource: ResourceType) -> Packe
     from the kernel's float64 answer (prom_decimal).  Other segments keep their pod lists
     (``sources``) and SimpleStrategy returns the reference's own object at the position the
     GPU located (krr_amd/core/exact.py), e.g. Decimal('0.10') or 25-digit values."""
-    if _PYHIST is not None:
-        vals, lens_b, cls_b, sources = _PYHIST.pack_resource(histories, resource, Decimal)
+    if _PYDEC is not None:
+        vals, lens_b, cls_b, sources = _PYDEC.pack_resource(histories, resource)
         values = np.frombuffer(vals, dtype=np.float64) if len(vals) else np.zeros(0, dtype=np.float64)
         lens = np.frombuffer(lens_b, dtype=np.int64)
         cls = np.frombuffer(cls_b, dtype=np.uint8).copy()

@@ -284,6 +284,9 @@ class BatchedRunner:
         t_host = max(1, T - t_dev)
         host_out: dict = {}
         alloc = _pinned_alloc_or_none()
+        # set once the device side knows the batch goes to the host packer whole: host_then's
+        # pass over the partial host fleet would be discarded, so it is not started after that
+        device_fell_back = threading.Event()
 
         def host_part():
             t0 = time.perf_counter()
@@ -291,7 +294,7 @@ class BatchedRunner:
                 host_out["fleet"] = PackedFleet(
                     pack_query_range_bodies(cpu_bodies[k:], threads=t_host, alloc=alloc),
                     pack_query_range_bodies(mem_bodies[k:], threads=t_host, alloc=alloc))
-                if host_then is not None:
+                if host_then is not None and not device_fell_back.is_set():
                     host_out["then"] = host_then(host_out["fleet"])
             except PrometheusResponseError as e:
                 host_out["error"] = e
@@ -304,6 +307,8 @@ class BatchedRunner:
         t0 = time.perf_counter()
         try:
             dev_fleet = self.pack_bodies_device(cpu_bodies[:k], mem_bodies[:k], threads=t_dev, device=device)
+            if self.last_pack_via != ("device", "device"):
+                device_fell_back.set()
             dev_s = time.perf_counter() - t0
         finally:
             worker.join()

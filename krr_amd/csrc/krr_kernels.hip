@@ -4002,9 +4002,13 @@ static int kll_merge_common(krr_ctx* ctx, int64_t n_series, int32_t rows_per_ser
     if (n_series < 0 || rows_per_series < 1 || series_base < 0)
         return set_err(ctx, KRR_E_INVALID, "bad n_series / rows_per_series / series_base%s", "");
     if (n_series && !rows) return set_err(ctx, KRR_E_INVALID, "null rows%s", "");
-    *lds = kll_merge_lds(kp, query);
+    // a query over one row per series folds nothing: k_kll_query stages the body alone
+    *lds = (query && rows_per_series == 1) ? ((size_t)kKllHdr + kp->budget) * 8 + (size_t)kp->budget
+                                           : kll_merge_lds(kp, query);
     if (*lds > ctx->max_lds)
-        return set_err(ctx, KRR_E_CAPACITY, "kll fold of rows this wide needs %s%lld B of LDS", "", (long long)*lds);
+        return set_err(ctx, KRR_E_CAPACITY, "kll %s needs %lld B of LDS",
+                       (query && rows_per_series == 1) ? "query of one row" : "fold of rows this wide",
+                       (long long)*lds);
     return KRR_OK;
 }
 
@@ -4036,8 +4040,6 @@ int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const
     size_t lds = 0;
     rc = kll_merge_common(ctx, n_series, rows_per_series, rows, kp, series_base, true, &lds);
     if (rc) return rc;
-    if (rows_per_series == 1)  // nothing to fold: the body staged alone (k_kll_query's direct form)
-        lds = ((size_t)kKllHdr + kp->budget) * 8 + (size_t)kp->budget;
     if (n_series == 0) return KRR_OK;
     if (!out_value || !out_count || !out_flags) return set_err(ctx, KRR_E_INVALID, "null pointers%s", "");
     DeviceGuard g(ctx->device);

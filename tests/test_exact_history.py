@@ -176,20 +176,22 @@ def _random_decimals(n, seed):
         else:
             x = Decimal(str(rnd.randint(0, 10 ** rnd.randint(1, 18))) + "." + "0" * rnd.randint(0, 3))
         out.append(-x if rnd.random() < 0.3 else x)
-    return out + [Decimal(s) for s in ("NaN", "-NaN", "sNaN", "Infinity", "-Infinity", "1E+400", "1E-400", "0.0",
+    return out + [Decimal(s) for s in ("NaN", "-NaN", "sNaN", "NaN123", "-sNaN7", "Infinity", "-Infinity", "1E+400", "1E-400", "0.0",
                                        "-0", "0E+5", "5E-324", "4.9406564584124654E-324")]
 
 
 def test_native_classifier_equals_python_rule():
-    """krr_pyhist.cpp's classify (Eisel-Lemire / strtod, Ryu shortest digits) against the
+    """krr_pydec.cpp's classify (Eisel-Lemire / strtod, Ryu shortest digits) against the
     Python restatement packing.sample_class and against float(Decimal)."""
     from krr_amd.core import packing
 
-    if packing._PYHIST is None:
-        pytest.skip("_krr_pyhist.so not built")
+    if packing._PYDEC is None:
+        pytest.skip("_krr_pydec.so not built")
     for x in _random_decimals(40000, 5):
-        v, c = packing._PYHIST.classify(str(x))
+        v, c = packing._PYDEC.classify(str(x))
         pv, pc = packing.sample_class(x)
+        sv, sc = packing._PYDEC.sample(x)  # in place from the decimal object (layout checked at load)
+        assert sc == c and (struct.pack("d", sv) == struct.pack("d", v) or (math.isnan(sv) and math.isnan(v))), str(x)
         try:
             fv = float(x)
         except ValueError:  # sNaN
@@ -216,8 +218,8 @@ def test_native_pack_equals_python_pack():
     from krr_amd.core import packing
     from krr_amd.core.models.allocations import ResourceType
 
-    if packing._PYHIST is None:
-        pytest.skip("_krr_pyhist.so not built")
+    if packing._PYDEC is None:
+        pytest.skip("_krr_pydec.so not built")
     xs = _random_decimals(3000, 7)
     rnd = random.Random(8)
     hs = []

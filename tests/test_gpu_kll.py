@@ -363,6 +363,32 @@ def test_fold_and_query_lds_capacity(ctx, budget, tail):
         assert out["value"].cpu().numpy()[0] == v and int(out["count"][0]) == n == 120_000
 
 
+@pytest.mark.parametrize("budget,tail", [(4096, 0), (1024, 4096), (2048, 1265)])
+def test_one_row_query_needs_no_fold_lds(ctx, budget, tail):
+    """krr_kll_query with rows_per_series == 1 folds nothing: only the direct form's
+    (16 + budget) x 8 + budget B of LDS is checked, so rows whose FOLD would not
+    fit (budget 4096, or wide tails) are still queried, equal to the restatement."""
+    import torch
+
+    from krr_amd.core import sketch
+    from krr_amd.core.engine import percentile_params
+
+    cfg = _cfg(budget, tail)
+    rng = np.random.default_rng(budget * 7 + tail)
+    offs, x = _fleet(rng, np.array([30_000, 9_000, 1, 0]))
+    ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, False)
+    rows = sketch.kll_build(ctx, ser, cfg)
+    r = rows.cpu().numpy().view(np.uint64)
+    for mode, p in (("linear", "99"), ("sorted_lower", "50")):
+        prm = percentile_params(Decimal(p), mode)
+        out = sketch.kll_query(ctx, rows, 1, cfg, prm)
+        torch.cuda.synchronize()
+        for s in range(offs.size - 1):
+            v, n, f = R.query(r[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q, seed=SEED, series=s, epoch=0)
+            got = out["value"].cpu().numpy()[s]
+            assert int(out["count"][s]) == n and (got == v or (np.isnan(got) and np.isnan(v))), (mode, s)
+
+
 def test_combined_launch_equals_split_passes(ctx):
     """krr_kll_build with tail > 0 and no flags launches the body and the tail pass itself;
     KRR_KLL_BODY_ONLY + krr_kll_tail (what krr_amd.core.sketch.kll_build does, timing them
