@@ -131,6 +131,8 @@ def parse():
                     help="N > 1 host path: the parser each rank uses for its shard's bodies")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-path measurements (H2D, native packer, end-to-end from JSON bodies)")
+    ap.add_argument("--no-right-size", action="store_true",
+                    help="config-4 leg: skip right-sizing + scanning the whole fleet on rank 0 after its steps")
     args = ap.parse_args()
     if args.c4_containers < 0:
         args.c4_containers = 1_000_000 if args.containers == 0 else 0
@@ -1118,6 +1120,9 @@ def config4_leg(args, ctx, dev, world, rank, dist_on, backend, coll_dev, comm, p
     if rank == 0:
         res.update({("config4_" + k): v for k, v in parity_gathered(
             args, ctx, dev, world, params, host_rec, False, 0, seed, cfg=4, shards=shards).items()})
+        if not args.no_right_size:
+            phase("c4 right-size")
+            res.update(config4_right_size(args, host_rec.numpy(), shards))
     return res
 
 
@@ -1233,6 +1238,101 @@ def right_size(args, records) -> dict:
                                  f"{threads} threads) -> one ResourceAllocations per container built in bulk; median "
                                  f"of 3; checked equal (values, exponents, JSON) to the per-object reference path on "
                                  f"the first {k}")}
+
+
+def fleet_objects(n: int) -> list:
+    """n synthetic K8sObjectData (untimed set-up of the right-size leg): distinct objects whose
+    current allocations cycle through a pool that puts the recommendations in every severity
+    bucket (None, "?"-free values below, near and far above the usual recommendation)."""
+    from decimal import Decimal
+
+    from krr_amd.core.models.allocations import ResourceAllocations, ResourceType
+    from krr_amd.core.models.objects import K8sObjectData
+
+    cpu_rt, mem_rt = ResourceType.CPU, ResourceType.Memory
+    cpus = [None] + [Decimal(x) for x in ("0.05", "0.1", "0.2", "0.25", "0.5", "1", "2")]
+    mems = [None] + [Decimal(x) for x in ("67108864", "134217728", "209715200", "268435456", "536870912")]
+    pool = []
+    for i in range(64):
+        c, m = cpus[i % len(cpus)], mems[(i * 5) % len(mems)]
+        pool.append(ResourceAllocations.construct(requests={cpu_rt: c, mem_rt: m},
+                                                  limits={cpu_rt: cpus[(i * 3) % len(cpus)], mem_rt: m}))
+    new = K8sObjectData.construct
+    return [new(cluster=None, name=f"app-{i}", container="main", pods=[f"app-{i}-0"], namespace=f"ns-{i % 97}",
+                kind="Deployment", allocations=pool[i % 64]) for i in range(n)]
+
+
+def config4_right_size(args, records: np.ndarray, shards) -> dict:
+    """After the config-4 leg, on rank 0: ALL containers' gathered 32-B records -> the
+    reference's Runner output and Result (runner.py:49-131): native exact-decimal rounding,
+    one ResourceAllocations per container, then Runner._collect_result's ResourceScan per
+    container and the Result score (result.py:33-150), all in bulk
+    (fast_round.allocations_batch, models.result.collect_result).  Timed whole and by phase.
+    Checked on 64-object blocks at both ends of EVERY shard against the per-object path
+    (SimpleStrategy result -> Decimal rounding -> validated ResourceAllocations ->
+    ResourceScan.calculate)."""
+    import gc
+
+    from krr_amd.core.distributed import raw_from_records
+    from krr_amd.core.engine import RawResults
+    from krr_amd.core.fast_round import allocations_batch
+    from krr_amd.core.models.result import ResourceScan, collect_result
+    from krr_amd.core.rounding import format_result
+    from krr_amd.core.runner import to_allocations
+    from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
+
+    n = int(records.shape[0])
+    settings = SimpleStrategySettings(cpu_percentile=str(args.percentile), memory_buffer_percentage="5")
+    threads = args.cpu_threads or cpu_lease()["threads"]
+    t_obj = time.perf_counter()
+    objects = fleet_objects(n)
+    t_obj = time.perf_counter() - t_obj
+    warm = RawResults(*(np.asarray(a)[:1000] for a in raw_from_records(records[:1000]).__dict__.values()
+                        if isinstance(a, np.ndarray)))
+    collect_result(objects[:1000], allocations_batch(warm, settings, threads=threads))  # loads the libraries
+    gc.collect()
+    tm: dict = {}
+    t0 = time.perf_counter()
+    raw = raw_from_records(records)
+    t1 = time.perf_counter()
+    allocs = allocations_batch(raw, settings, threads=threads, timings=tm)
+    t2 = time.perf_counter()
+    result = collect_result(objects, allocs)
+    t3 = time.perf_counter()
+    total = t3 - t0
+    # equality with the per-object path on blocks from every shard
+    same, checked = True, 0
+    for a, b in shards:
+        for lo in sorted({a, max(a, b - 64)}):
+            hi = min(lo + 64, b)
+            sub = RawResults(*(np.asarray(x)[lo:hi] for x in (raw.cpu_value, raw.cpu_count, raw.cpu_flags,
+                                                              raw.mem_value, raw.mem_count, raw.mem_flags)))
+            want = [to_allocations(format_result(r)) for r in SimpleStrategy(settings).results_from_raw(sub)]
+            for i, w in zip(range(lo, hi), want):
+                same &= allocs[i] == w and allocs[i].json() == w.json()
+                ref_scan = ResourceScan.calculate(objects[i], w)
+                same &= result.scans[i] == ref_scan and result.scans[i].severity == ref_scan.severity
+                checked += 1
+    sev = {}
+    for s in result.scans[:: max(1, n // 20000)]:
+        sev[s.severity.value] = sev.get(s.severity.value, 0) + 1
+    del result, allocs, objects
+    gc.collect()
+    return {
+        "config4_right_size_s": total,
+        "config4_right_size_objects_per_s": n / total,
+        "config4_right_size_split_s": {"unpack": t1 - t0, "round": tm.get("round_s"), "decimal": tm.get("decimal_s"),
+                                       "allocations_models": tm.get("models_s"), "scan_and_score": t3 - t2},
+        "config4_scan_objects_per_s": n / (t3 - t2),
+        "config4_right_size_equal_per_object_path": bool(same),
+        "config4_right_size_checked_objects": checked,
+        "config4_right_size_severities_sampled": sev,
+        "config4_right_size_definition": (
+            f"rank 0, all {n} containers' gathered records -> krr_round_simple ({threads} threads) -> one "
+            f"ResourceAllocations per container -> Runner._collect_result's ResourceScan per container + Result "
+            f"score, in bulk; one run after a warm-up on 1000; the {n} K8sObjectData are built beforehand "
+            f"({t_obj:.1f} s, untimed); checked equal to the per-object path on {checked} containers, 64-object "
+            f"blocks at both ends of every shard")}
 
 
 def parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed, cfg=None, shards=None) -> dict:

@@ -31,6 +31,9 @@ typedef struct {
     const char* mem_buffer;   /* str(Decimal(1 + b/100)) as the strategy computes it (e.g. "1.05") */
     const char* cpu_minimal;  /* str() of Runner.__get_resource_minimal(CPU), e.g. "0.005000000000000000104083408559" */
     const char* mem_minimal;  /* str() of the memory minimal, e.g. "10000000" */
+    int32_t fast_path;        /* 1: 128-bit integer arithmetic where the operands fit (same results);
+                                 0: digit strings throughout (the reference restatement, for tests) */
+    int32_t reserved;
 } krr_round_params;
 
 #define KRR_ROUND_CPU_FALLBACK 1u  /* cpu_out[i] not written: use the Python path */

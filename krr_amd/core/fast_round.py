@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import gc
 from decimal import Decimal
+from typing import Optional
 
 import numpy as np
 
@@ -57,22 +58,25 @@ _PYOBJ = _load_pyobj()
 
 
 class _Params:
-    def __init__(self, buffer: Decimal, cpu_min: Decimal, mem_min: Decimal):
+    def __init__(self, buffer: Decimal, cpu_min: Decimal, mem_min: Decimal, fast_path: bool = True):
         import ctypes
 
         class P(ctypes.Structure):
             _fields_ = [("mem_buffer", ctypes.c_char_p), ("cpu_minimal", ctypes.c_char_p),
-                        ("mem_minimal", ctypes.c_char_p)]
+                        ("mem_minimal", ctypes.c_char_p), ("fast_path", ctypes.c_int32),
+                        ("reserved", ctypes.c_int32)]
 
         self._strs = [str(buffer).encode(), str(cpu_min).encode(), str(mem_min).encode()]
-        self.struct = P(*self._strs)
+        self.struct = P(*self._strs, int(bool(fast_path)), 0)
 
 
 def round_strings(cpu_value, cpu_flags, mem_value, mem_flags, buffer: Decimal,
                   cpu_min_value: int = DEFAULT_CPU_MIN_VALUE, memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE,
-                  threads: int = 0):
+                  threads: int = 0, fast_path: bool = True):
     """Columnar form: (cpu strings, memory strings, status) as numpy arrays; str(Decimal)
-    of the rounded CPU request and memory request (= limit) per object."""
+    of the rounded CPU request and memory request (= limit) per object.  ``fast_path``: the
+    native code's 128-bit integer arithmetic where the operands fit (False: its digit-string
+    arithmetic throughout; the results are the same)."""
     import ctypes
 
     lib = load_library()
@@ -85,7 +89,7 @@ def round_strings(cpu_value, cpu_flags, mem_value, mem_flags, buffer: Decimal,
     mem_out = np.zeros(max(n, 1), dtype=f"S{WIDTH}")
     status = np.zeros(max(n, 1), dtype=np.uint8)
     params = _Params(buffer, resource_minimal(ResourceType.CPU, cpu_min_value, memory_min_value),
-                     resource_minimal(ResourceType.Memory, cpu_min_value, memory_min_value))
+                     resource_minimal(ResourceType.Memory, cpu_min_value, memory_min_value), fast_path)
     rc = lib.krr_round_simple(n, _ptr(cv), _ptr(cf), _ptr(mv), _ptr(mf), ctypes.byref(params.struct),
                               _ptr(cpu_out), _ptr(mem_out), WIDTH, _ptr(status), int(threads))
     if rc != 0:
@@ -166,7 +170,7 @@ def _apply_fallbacks(cpu_col, mem_col, status, raw, settings, buffer, cpu_min_va
 
 def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
                       memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE, threads: int = 0, model=None,
-                      resource_type=None) -> list:
+                      resource_type=None, timings: Optional[dict] = None) -> list:
     """Runner._gather_objects_recommendations's list (runner.py:113-120) straight from raw kernel
     results: one ``ResourceAllocations`` per object, equal to
     ``ResourceAllocations(requests={rt: r[rt].request ...}, limits={rt: r[rt].limit ...})`` of the
@@ -174,21 +178,30 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
     (allocations.py:33-51: Decimal unchanged, NaN -> "?", the CPU limit None), so each model is
     made without a per-object validation walk (pydantic v1 ``construct``'s layout: the field
     dict and the fields-set).  ``model`` / ``resource_type``: the reference's own classes
-    (krr_amd.integration) or, by default, this package's mirror."""
+    (krr_amd.integration) or, by default, this package's mirror.  ``timings``: filled with the
+    phases' seconds (round_s: native rounding, decimal_s: one Decimal per distinct string,
+    models_s: the models)."""
     from krr_amd.core.models.allocations import ResourceAllocations
 
     model = model or ResourceAllocations
     rtypes = list(resource_type or ResourceType)
     cpu_k, mem_k = rtypes[0], rtypes[1]
+    import time
+
+    t0 = time.perf_counter()
     buffer = settings.memory_buffer()
     cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
                                memory_min_value, threads)
     _route_exact(st, raw)
+    t1 = time.perf_counter()
     gc_was = gc.isenabled()
     gc.disable()
     try:
         q = "?"
         cpu_col, mem_col = decimal_column(cs, q), decimal_column(ms, q)
+        if timings is not None:
+            timings.update(round_s=t1 - t0, decimal_s=time.perf_counter() - t1)
+            t1 = time.perf_counter()
         fb = np.nonzero(st)[0].tolist()
         _apply_fallbacks(cpu_col, mem_col, st, raw, settings, buffer, cpu_min_value, memory_min_value)
         for i in fb:  # the validator's NaN -> "?" (allocations.py:40-41) for the Python-rounded ones
@@ -200,6 +213,13 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
         if not _v1_construct_layout(model):  # e.g. a pydantic v2 model: its own constructor, per object
             return [model(requests={cpu_k: c, mem_k: m}, limits={cpu_k: None, mem_k: m})
                     for c, m in zip(cpu_col, mem_col)]
+        from krr_amd.core.packing import _PYDEC
+
+        if _PYDEC is not None and tuple(model.__fields__) == ("requests", "limits"):
+            out = _PYDEC.allocations(_model_desc(model), (cpu_k, mem_k), cpu_col, mem_col)
+            if timings is not None:
+                timings["models_s"] = time.perf_counter() - t1
+            return out
         if _PYOBJ is not None:
             return _PYOBJ.allocations(model, fields, cpu_k, mem_k, cpu_col, mem_col)
         new, setattr_ = object.__new__, object.__setattr__
@@ -216,6 +236,21 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
             gc.enable()
 
 
+def _model_desc(model) -> tuple:
+    """(class, field names, fields-set, __fields_set__ slot offset): how the native builders
+    (krr_amd/csrc/krr_pydec.cpp) make pydantic-v1 instances in construct() layout.  Every
+    instance of the class shares the one fields-set: it holds every field, so the add()
+    pydantic's __setattr__ does never changes it (_v1_construct_layout admits only models
+    that forbid other names), as pydantic itself shares one between a model and its
+    validation copy (pydantic/v1/main.py _copy_and_set_values)."""
+    import pydantic.v1 as pv1
+
+    from krr_amd.core.packing import _PYDEC
+
+    names = tuple(model.__fields__)
+    return (model, names, set(names), _PYDEC.slot_offset(pv1.BaseModel.__dict__["__fields_set__"]))
+
+
 def _v1_construct_layout(model) -> bool:
     """True when instances of ``model`` are exactly pydantic v1's construct() layout (the field
     dict + __fields_set__): a pydantic.v1 BaseModel without private attributes, as the
@@ -223,7 +258,8 @@ def _v1_construct_layout(model) -> bool:
     import pydantic.v1 as pv1
 
     return (isinstance(model, type) and issubclass(model, pv1.BaseModel)
-            and not getattr(model, "__private_attributes__", None))
+            and not getattr(model, "__private_attributes__", None)
+            and model.__config__.extra is not pv1.Extra.allow)
 
 
 _FIELDS = ("request", "limit")

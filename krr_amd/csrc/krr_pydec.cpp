@@ -138,6 +138,19 @@ uint8_t classify_finite(bool neg, uint64_t ws, int sig, long long exp, int tz, d
     return (es >= 0 ? exp == 0 : tz == 0) ? kCanonical : kFaithful;
 }
 
+using u128 = unsigned __int128;
+
+struct Pow10 {
+    u128 v[39];
+    Pow10() {
+        v[0] = 1;
+        for (int i = 1; i < 39; ++i) v[i] = v[i - 1] * 10;
+    }
+};
+const Pow10 kPow10;
+
+inline u128 pow10_u128(int e) { return kPow10.v[e]; }
+
 inline double w_pow10(uint64_t w, long long e) {
     if (w == 0) return 0.0;
     if (e <= -100000) return 0.0;
@@ -432,9 +445,19 @@ PyObject* sample_py(PyObject*, PyObject* x) {
 enum : int { kCritical = 0, kWarning = 1, kOk = 2, kGood = 3, kUnknown = 4 };
 constexpr double kMargin = 1e-9;  // krr_amd/core/models/result.py _MARGIN
 
+// The cyclic GC need not traverse the result graphs built here: they are trees (a scan ->
+// its recommendation -> dicts -> Recommendation -> value / severity, and the caller's
+// object), so no reference cycle runs through them as built.  Untracking them keeps the
+// gen-0 collection the next allocation triggers from walking millions of fresh objects (a
+// full traversal, ~3 us per scan, otherwise).  A dict that later receives a container is
+// tracked again by CPython itself; a cycle a caller later builds through an instance is
+// kept alive rather than collected.
+inline void untrack(PyObject* o) {
+    if (PyObject_IS_GC(o)) PyObject_GC_UnTrack(o);
+}
+
 // A model class built in pydantic v1 construct() layout: field names (dict order), one
-// shared fields-set (every field is set, so pydantic's add() on assignment never changes
-// it), and where the __fields_set__ slot lives.
+// fields-set shared by its instances (see make()), and where the __fields_set__ slot lives.
 struct Model {
     PyTypeObject* cls = nullptr;
     PyObject* names[3] = {nullptr, nullptr, nullptr};
@@ -452,11 +475,17 @@ struct Model {
         PyObject* vals[3] = {a, b, c};
         bool bad = !d;
         for (int i = 0; !bad && i < n; ++i) bad = _PyDict_SetItem_KnownHash(d, names[i], vals[i], hashes[i]) < 0;
+        if (!bad) untrack(d);
         Py_XDECREF(d);
         if (bad) {
             Py_DECREF(o);
             return nullptr;
         }
+        untrack(o);
+        // the class's fields-set, shared: it holds every field, so the add() pydantic's
+        // __setattr__ does never changes it (these models forbid other names), and pydantic
+        // itself shares a fields-set between a model and its validation copy
+        // (pydantic/v1/main.py:729 _copy_and_set_values(value.__dict__, value.__fields_set__))
         Py_INCREF(fields_set);
         *reinterpret_cast<PyObject**>(reinterpret_cast<char*>(o) + fs_offset) = fields_set;
         return o;
@@ -482,16 +511,17 @@ bool init_model(Model* m, PyObject* cls, PyObject* names, PyObject* fields_set, 
 
 // x's float64 image when it is a finite decimal.Decimal (kind 0), else the kind:
 // 1 None, 2 str ("?"), 3 other (NaN / Infinity Decimals, subclasses, numbers)
-inline int value_kind(PyObject* x, double* f) {
+inline int value_kind(PyObject* x, double* f, DecView* v) {
+    v->special = 1;  // no one-word view unless set below
     if (x == Py_None) return 1;
     if (PyUnicode_Check(x)) return 2;
-    DecView v;
-    if (dec_view(x, &v)) {
-        if (v.special) return 3;
-        const double m = w_pow10(v.w, v.exp);
-        *f = v.neg ? -m : m;
+    if (dec_view(x, v)) {
+        if (v->special) return 3;
+        const double m = w_pow10(v->w, v->exp);
+        *f = v->neg ? -m : m;
         return 0;
     }
+    v->special = 1;
     if (Py_TYPE(x) == g_dec_type) {  // a coefficient wider than one word
         PyObject* fin = PyObject_CallMethod(x, "is_finite", nullptr);
         const int finite = fin ? PyObject_IsTrue(fin) : -1;
@@ -511,35 +541,59 @@ inline int value_kind(PyObject* x, double* f) {
     return 3;
 }
 
+// c == (1 + t) * r exactly, i.e. 4c == M r with M = 4 (1 + t), for one-word Decimals:
+// 1 yes, 0 no, -1 cannot tell here (the aligned operands pass 37 digits)
+int exact_tie(const DecView& c, const DecView& r, int M) {
+    if (c.w == 0 || r.w == 0) return (c.w == 0 && r.w == 0) ? 1 : 0;
+    if (c.neg != r.neg) return 0;  // M > 0
+    const int64_t e = std::min(c.exp, r.exp);
+    const int64_t da = c.exp - e, db = r.exp - e;
+    if (da + 20 > 37 || db + 20 > 37) return -1;
+    const u128 a = (u128)4 * c.w * pow10_u128((int)da), b = (u128)(unsigned)M * r.w * pow10_u128((int)db);
+    return a == b ? 1 : 0;
+}
+
+inline int bucket(double diff) {
+    if (diff > 1.0 || diff < -0.5) return kCritical;
+    if (diff > 0.5 || diff < -0.25) return kWarning;
+    return kGood;
+}
+
 // Severity.calculate(current, recommended) -> code, or -1 with an error set.  Decided on the
-// float64 images unless a threshold is too close (or an operand is zero, subnormal,
-// non-finite, or not a finite Decimal): then `settle` (the Decimal restatement) decides.
+// float64 images; a diff within the margin of a threshold t is decided exactly when the
+// values tie with it (current == (1 + t) * recommended: the reference's Decimal quotient is
+// then exactly t, its subtraction exact); anything else near a threshold, and operands that
+// are zero, subnormal, non-finite or not finite Decimals, go to `settle` (the Decimal
+// restatement, which also raises what the reference raises).
 int severity_code(PyObject* cur, PyObject* rec, PyObject* settle) {
     double c = 0.0, r = 1.0;
-    const int kc = value_kind(cur, &c), kr = value_kind(rec, &r);
+    DecView cv, rv;
+    const int kc = value_kind(cur, &c, &cv), kr = value_kind(rec, &r, &rv);
     if (kc == 2 || kr == 2) return kUnknown;
     if (kc == 1 && kr == 1) return kOk;
     if (kc == 1 || kr == 1) return kWarning;
     bool exact = kc != 0 || kr != 0;
-    double diff = 0.0;
     if (!exact) {
-        diff = (c - r) / r;
-        const double scale = kMargin * (1.0 + std::fabs(c / r));
         const double tiny = std::numeric_limits<double>::min();
-        exact = !std::isfinite(c) || !std::isfinite(r) || std::fabs(r) < tiny || (c != 0 && std::fabs(c) < tiny) ||
-                !(std::fabs(diff - 1.0) > scale) || !(std::fabs(diff + 0.5) > scale) ||
-                !(std::fabs(diff - 0.5) > scale) || !(std::fabs(diff + 0.25) > scale);
+        exact = !std::isfinite(c) || !std::isfinite(r) || std::fabs(r) < tiny || (c != 0 && std::fabs(c) < tiny);
     }
-    if (exact) {
-        PyObject* code = PyObject_CallFunctionObjArgs(settle, cur, rec, nullptr);
-        if (!code) return -1;
-        const long k = PyLong_AsLong(code);
-        Py_DECREF(code);
-        return (k == -1 && PyErr_Occurred()) ? -1 : (int)k;
+    if (!exact) {
+        const double diff = (c - r) / r;
+        const double scale = kMargin * (1.0 + std::fabs(c / r));
+        static const double kT[4] = {1.0, -0.5, 0.5, -0.25};
+        static const int kM[4] = {8, 2, 6, 3};
+        int near = -1;
+        for (int j = 0; j < 4; ++j)
+            if (!(std::fabs(diff - kT[j]) > scale)) near = j;
+        if (near < 0) return bucket(diff);
+        if (cv.special == 0 && rv.special == 0 && exact_tie(cv, rv, kM[near]) == 1) return bucket(kT[near]);
+        exact = true;
     }
-    if (diff > 1.0 || diff < -0.5) return kCritical;
-    if (diff > 0.5 || diff < -0.25) return kWarning;
-    return kGood;
+    PyObject* code = PyObject_CallFunctionObjArgs(settle, cur, rec, nullptr);
+    if (!code) return -1;
+    const long k = PyLong_AsLong(code);
+    Py_DECREF(code);
+    return (k == -1 && PyErr_Occurred()) ? -1 : (int)k;
 }
 
 // attribute of a pydantic-v1 instance: its __dict__ entry, else the generic lookup (new ref)
@@ -666,6 +720,10 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
                 Py_XDECREF(rv);
             }
         }
+        if (!bad) {
+            untrack(dreq);
+            untrack(dlim);
+        }
         PyObject* rr = bad ? nullptr : M[1].make(dreq, dlim);
         PyObject* scan = rr ? M[2].make(obj, rr, PyTuple_GET_ITEM(sevs, worst)) : nullptr;
         Py_XDECREF(rr);
@@ -695,6 +753,61 @@ done:
     return res;
 }
 
+// allocations(model, rts, cpu_list, mem_list) -> list: per object a ResourceAllocations
+// (runner.py:113-120) in construct() layout — requests {cpu: c, mem: m}, limits
+// {cpu: None, mem: m} — the values already what the model's validator leaves
+// (allocations.py:33-51); model = (cls, field names, fields_set, slot offset).
+PyObject* allocations(PyObject*, PyObject* args) {
+    PyObject *md, *rts, *cl, *ml;
+    if (!PyArg_ParseTuple(args, "O!O!O!O!", &PyTuple_Type, &md, &PyTuple_Type, &rts, &PyList_Type, &cl, &PyList_Type,
+                          &ml))
+        return nullptr;
+    const Py_ssize_t n = PyList_GET_SIZE(cl);
+    if (PyList_GET_SIZE(ml) != n || PyTuple_GET_SIZE(rts) != 2 || PyTuple_GET_SIZE(md) != 4) {
+        PyErr_SetString(PyExc_ValueError, "allocations: two equal columns, two resource types, one model");
+        return nullptr;
+    }
+    Model M;
+    const Py_ssize_t off = PyLong_AsSsize_t(PyTuple_GET_ITEM(md, 3));
+    if (off <= 0 || !init_model(&M, PyTuple_GET_ITEM(md, 0), PyTuple_GET_ITEM(md, 1), PyTuple_GET_ITEM(md, 2), off)) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "allocations: bad slot offset");
+        return nullptr;
+    }
+    PyObject* ck = PyTuple_GET_ITEM(rts, 0);
+    PyObject* mk = PyTuple_GET_ITEM(rts, 1);
+    const Py_hash_t hc = PyObject_Hash(ck), hm = PyObject_Hash(mk);
+    if (hc == -1 || hm == -1) return nullptr;
+    PyObject* tmpl = _PyDict_NewPresized(2);
+    if (!tmpl || _PyDict_SetItem_KnownHash(tmpl, ck, Py_None, hc) < 0 ||
+        _PyDict_SetItem_KnownHash(tmpl, mk, Py_None, hm) < 0) {
+        Py_XDECREF(tmpl);
+        return nullptr;
+    }
+    PyObject* out = PyList_New(n);
+    for (Py_ssize_t i = 0; out && i < n; ++i) {
+        PyObject* c = PyList_GET_ITEM(cl, i);
+        PyObject* m = PyList_GET_ITEM(ml, i);
+        PyObject* req = PyDict_Copy(tmpl);
+        PyObject* lim = req ? PyDict_Copy(tmpl) : nullptr;
+        bool bad = !lim || _PyDict_SetItem_KnownHash(req, ck, c, hc) < 0 || _PyDict_SetItem_KnownHash(req, mk, m, hm) < 0 ||
+                   _PyDict_SetItem_KnownHash(lim, mk, m, hm) < 0;
+        if (!bad) {
+            untrack(req);
+            untrack(lim);
+        }
+        PyObject* o = bad ? nullptr : M.make(req, lim);
+        Py_XDECREF(req);
+        Py_XDECREF(lim);
+        if (!o) {
+            Py_CLEAR(out);
+            break;
+        }
+        PyList_SET_ITEM(out, i, o);
+    }
+    Py_DECREF(tmpl);
+    return out;
+}
+
 // slot_offset(member_descriptor) -> its byte offset in the instance (pydantic v1's
 // BaseModel.__fields_set__ slot)
 PyObject* slot_offset(PyObject*, PyObject* d) {
@@ -718,6 +831,7 @@ PyMethodDef methods[] = {
     {"classify", classify_str, METH_VARARGS, "str(Decimal) -> (float64, exactness class)"},
     {"sample", sample_py, METH_O, "one sample object -> (float64, exactness class), the packer's path"},
     {"scan_fleet", scan_fleet, METH_VARARGS, "ResourceScan per object in construct() layout -> (scans, keys_ok)"},
+    {"allocations", allocations, METH_VARARGS, "ResourceAllocations in construct() layout from value columns"},
     {"slot_offset", slot_offset, METH_O, "byte offset of an object slot (member descriptor)"},
     {"layout_ok", layout_ok, METH_NOARGS, "whether Decimals are read in place (else through str())"},
     {nullptr, nullptr, 0, nullptr}};

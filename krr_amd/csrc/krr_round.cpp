@@ -12,6 +12,8 @@
 #include <atomic>
 #include <charconv>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -265,6 +267,215 @@ bool round_mem(double x, const Dec& buffer, const Dec& minimal, std::string* out
     return true;
 }
 
+// ---- integer fast path ---------------------------------------------------------------
+// The same arithmetic on 128-bit integers for the common case: the sample's shortest digits
+// D (<= 17 of them) and, for memory, a buffer coefficient short enough that D * buffer has
+// <= 28 digits (so the 28-digit context never rounds: the CLI path's Decimal('1.05'); the
+// int-default path's 52-digit Decimal(1.05 float) takes the digit-string path above).
+// Results are identical by construction (tests/test_fast_round.py pins both paths).
+using u128 = unsigned __int128;
+using i128 = __int128;
+
+constexpr int kMaxInt = 38;  // decimal digits an i128 magnitude always holds (10^38 < 2^127)
+
+struct Pow10 {
+    u128 v[kMaxInt + 1];
+    Pow10() {
+        v[0] = 1;
+        for (int i = 1; i <= kMaxInt; ++i) v[i] = v[i - 1] * 10;
+    }
+};
+const Pow10 kPow10;
+
+inline u128 pow10_u128(int e) { return kPow10.v[e]; }
+
+// decimal digits of v (no divisions: compared against the powers of ten)
+inline int ndigits(u128 v) {
+    int n = 1;
+    if (v >> 64 == 0) {
+        const uint64_t w = (uint64_t)v;
+        while (n < 20 && w >= (uint64_t)kPow10.v[n]) ++n;
+        return n;
+    }
+    n = 20;
+    while (n <= kMaxInt && v >= kPow10.v[n]) ++n;
+    return n;
+}
+
+// q = m / 10^e and whether a remainder is left, 64-bit division when the operands fit
+inline u128 div_pow10(u128 m, int e, bool* frac) {
+    if (m >> 64 == 0 && e < 20) {
+        const uint64_t w = (uint64_t)m, p = (uint64_t)kPow10.v[e];
+        const uint64_t q = w / p;
+        *frac = q * p != w;
+        return q;
+    }
+    const u128 p = kPow10.v[e];
+    const u128 q = m / p;
+    *frac = q * p != m;
+    return q;
+}
+
+// x's shortest round-trip digits: |x| = D * 10^E (D without trailing zeros; D = 0 for zero)
+void shortest(double x, uint64_t* D, int* E) {
+    char buf[48];
+    auto res = std::to_chars(buf, buf + sizeof(buf), std::fabs(x), std::chars_format::scientific);
+    *res.ptr = 0;
+    uint64_t d = 0;
+    int nd = 0;
+    const char* p = buf;
+    for (; *p && *p != 'e'; ++p)
+        if (*p >= '0' && *p <= '9') {
+            d = d * 10 + (uint64_t)(*p - '0');
+            ++nd;
+        }
+    int e = (*p == 'e') ? atoi(p + 1) : 0;
+    e -= nd - 1;
+    while (d && d % 10 == 0) {
+        d /= 10;
+        ++e;
+    }
+    *D = d;
+    *E = d ? e : 0;
+}
+
+// ceil((-1)^neg * m * 10^e) as a signed integer; false when it needs more than kMaxInt - 1 digits
+bool ceil_scaled(bool neg, u128 m, int e, i128* out) {
+    if (m == 0) {
+        *out = 0;
+        return true;
+    }
+    u128 q;
+    bool frac = false;
+    if (e >= 0) {
+        if (ndigits(m) + e > kMaxInt - 1) return false;
+        q = m * pow10_u128(e);
+    } else if (-e >= kMaxInt) {
+        q = 0;
+        frac = true;
+    } else {
+        q = div_pow10(m, -e, &frac);
+    }
+    if (!neg && frac) ++q;  // toward +inf: a positive fraction rounds up, a negative one truncates
+    if (ndigits(q) > kMaxInt - 1) return false;
+    *out = neg ? -(i128)q : (i128)q;
+    return true;
+}
+
+// The smallest integer t with k < t <=> k * 10^e < minimal (i.e. t = ceil(minimal * 10^-e))
+bool threshold(const Dec& minimal, int e, i128* t) {
+    if (minimal.d.size() > (size_t)kMaxInt - 1) {  // e.g. the CPU floor 0.0050000000000000001040834...
+        Dec m = minimal;
+        m.exp -= e;
+        const Dec c = ceil_int(m);
+        if (c.d.size() > (size_t)kMaxInt - 2) return false;
+        u128 v = 0;
+        for (char ch : c.d) v = v * 10 + (u128)(ch - '0');
+        *t = c.neg ? -(i128)v : (i128)v;
+        return true;
+    }
+    u128 v = 0;
+    for (char ch : minimal.d) v = v * 10 + (u128)(ch - '0');
+    return ceil_scaled(minimal.neg, v, minimal.exp - e, t);
+}
+
+// str(Decimal) of coefficient k (signed) at exponent exp into dst (NUL-terminated)
+void put_sci(char* dst, i128 k, int exp) {
+    char dig[48];
+    int n = 0;
+    const bool neg = k < 0;
+    u128 v = neg ? (u128)(-k) : (u128)k;
+    while (v >> 64) {
+        dig[n++] = (char)('0' + (int)(v % 10));
+        v /= 10;
+    }
+    uint64_t w = (uint64_t)v;
+    do {
+        dig[n++] = (char)('0' + (int)(w % 10));
+        w /= 10;
+    } while (w);
+    char* o = dst;
+    if (neg) *o++ = '-';
+    const int adjusted = exp + n - 1;
+    if (exp <= 0 && adjusted >= -6) {
+        const int point = n + exp;  // digits before the point
+        if (exp == 0) {
+            for (int i = n; i-- > 0;) *o++ = dig[i];
+        } else if (point > 0) {
+            for (int i = n; i-- > 0;) {
+                *o++ = dig[i];
+                if (i == n - point) *o++ = '.';
+            }
+        } else {
+            *o++ = '0';
+            *o++ = '.';
+            for (int z = 0; z < -point; ++z) *o++ = '0';
+            for (int i = n; i-- > 0;) *o++ = dig[i];
+        }
+    } else {
+        *o++ = dig[n - 1];
+        if (n > 1) {
+            *o++ = '.';
+            for (int i = n - 1; i-- > 0;) *o++ = dig[i];
+        }
+        *o++ = 'E';
+        *o++ = adjusted >= 0 ? '+' : '-';
+        o += sprintf(o, "%d", adjusted >= 0 ? adjusted : -adjusted);
+    }
+    *o = 0;
+}
+
+struct Fast {
+    bool cpu_ok = false, mem_ok = false;
+    i128 cpu_t = 0, mem_t = 0;     // thresholds against the minimal (see threshold())
+    std::string cpu_min_s, mem_min_s;
+    u128 buf_c = 0;                // the memory buffer's coefficient and exponent
+    int buf_e = 0;
+    bool buf_neg = false;
+    int buf_digits = 0;
+};
+
+// Runner._round_value(CPU) of prom_decimal(x); false: not covered here
+bool fast_cpu(double x, const Fast& F, char* out) {
+    uint64_t D;
+    int E;
+    shortest(x, &D, &E);
+    i128 k;  // ceil(v * 10^3)
+    if (!ceil_scaled(std::signbit(x), D, E + 3, &k) || ndigits((u128)(k < 0 ? -k : k)) > kPrec - 1) return false;
+    if (k < F.cpu_t) {
+        memcpy(out, F.cpu_min_s.c_str(), F.cpu_min_s.size() + 1);
+        return true;
+    }
+    // k / 1000 at the ideal exponent 0: trailing zeros stripped up to 3
+    int exp = -3;
+    while (exp < 0 && k != 0 && (int)(k < 0 ? (uint64_t)(-k % 10) : (uint64_t)(k % 10)) == 0) {
+        k /= 10;
+        ++exp;
+    }
+    if (k == 0) exp = 0;
+    put_sci(out, k, exp);
+    return true;
+}
+
+// simple.py:29's max * buffer, then Runner._round_value(Memory); false: not covered here
+bool fast_mem(double x, const Fast& F, char* out) {
+    uint64_t D;
+    int E;
+    shortest(x, &D, &E);
+    if (D && ndigits(D) + F.buf_digits > kPrec) return false;  // the 28-digit context would round
+    const u128 P = (u128)D * F.buf_c;
+    i128 r;  // ceil(raw * 10^-6)
+    if (!ceil_scaled(std::signbit(x) != F.buf_neg && P != 0, P, E + F.buf_e - 6, &r) ||
+        ndigits((u128)(r < 0 ? -r : r)) > kPrec - 1)
+        return false;
+    if (r < F.mem_t) {
+        memcpy(out, F.mem_min_s.c_str(), F.mem_min_s.size() + 1);
+        return true;
+    }
+    put_sci(out, r, 6);  // r * 10^6 at the ideal exponent 6
+    return true;
+}
+
 template <class F>
 void parallel_for(int64_t n, int32_t threads, F f) {
     int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
@@ -301,6 +512,17 @@ extern "C" int krr_round_simple(int64_t n, const double* cpu_value, const uint32
     if (!parse_dec(params->mem_buffer, &buffer) || !parse_dec(params->cpu_minimal, &cpu_min) ||
         !parse_dec(params->mem_minimal, &mem_min))
         return -1;
+    Fast F;
+    F.cpu_min_s = to_sci(cpu_min);
+    F.mem_min_s = to_sci(mem_min);
+    F.cpu_ok = threshold(cpu_min, -3, &F.cpu_t) && params->fast_path != 0;
+    F.mem_ok = buffer.d.size() < (size_t)kPrec && threshold(mem_min, 6, &F.mem_t) && params->fast_path != 0;
+    if (F.mem_ok) {
+        for (char ch : buffer.d) F.buf_c = F.buf_c * 10 + (u128)(ch - '0');
+        F.buf_e = buffer.exp;
+        F.buf_neg = buffer.neg;
+        F.buf_digits = buffer.d == "0" ? 1 : (int)buffer.d.size();
+    }
     parallel_for(n, threads, [&](int64_t i) {
         uint8_t st = 0;
         std::string s;
@@ -309,14 +531,18 @@ extern "C" int krr_round_simple(int64_t n, const double* cpu_value, const uint32
         const uint32_t cf = cpu_flags[i], mf = mem_flags[i];
         if (cf == kFlagEmpty) {
             put(co, width, "NaN");
-        } else if (cf != 0 || !std::isfinite(cpu_value[i]) || !round_cpu(cpu_value[i], cpu_min, &s) ||
-                   !put(co, width, s)) {
+        } else if (cf != 0 || !std::isfinite(cpu_value[i])) {
+            st |= KRR_ROUND_CPU_FALLBACK;
+        } else if (!(F.cpu_ok && fast_cpu(cpu_value[i], F, co)) &&
+                   (!round_cpu(cpu_value[i], cpu_min, &s) || !put(co, width, s))) {
             st |= KRR_ROUND_CPU_FALLBACK;
         }
         if (mf == kFlagEmpty) {
             put(mo, width, "NaN");
-        } else if (mf != 0 || !std::isfinite(mem_value[i]) || !round_mem(mem_value[i], buffer, mem_min, &s) ||
-                   !put(mo, width, s)) {
+        } else if (mf != 0 || !std::isfinite(mem_value[i])) {
+            st |= KRR_ROUND_MEM_FALLBACK;
+        } else if (!(F.mem_ok && fast_mem(mem_value[i], F, mo)) &&
+                   (!round_mem(mem_value[i], buffer, mem_min, &s) || !put(mo, width, s))) {
             st |= KRR_ROUND_MEM_FALLBACK;
         }
         (void)kFlagNan;

@@ -122,8 +122,11 @@ def test_allocations_batch_equals_validated_models(path):
                 assert type(gd[k]) is type(wd[k]) and str(gd[k]) == str(wd[k])
                 nq += gd[k] == "?"
     assert nq > 0  # empty series became "?"
-    got[0].__fields_set__.add("scratch")  # every model owns its fields set (pydantic mutates it)
-    assert "scratch" not in got[1].__fields_set__
+    # construct() layout: every field set; assignment keeps it so, other names are refused
+    got[0].requests = dict(got[0].requests)
+    assert got[0].__fields_set__ == got[1].__fields_set__ == {"requests", "limits"}
+    with pytest.raises(ValueError):
+        got[0].scratch = 1
 
 
 def test_allocations_batch_reference_model_types():
