@@ -17,6 +17,10 @@ from decimal import Decimal
 from typing import Optional
 
 import numpy as np
+try:
+    import pydantic.v1 as pv1
+except ImportError:  # a process that aliased pydantic -> pydantic.v1 (the reference's import recipe)
+    import pydantic as pv1
 
 from krr_amd.core.abstract.strategies import ResourceRecommendation, RunResult
 from krr_amd.core.models.allocations import ResourceType
@@ -243,8 +247,6 @@ def _model_desc(model) -> tuple:
     pydantic's __setattr__ does never changes it (_v1_construct_layout admits only models
     that forbid other names), as pydantic itself shares one between a model and its
     validation copy (pydantic/v1/main.py _copy_and_set_values)."""
-    import pydantic.v1 as pv1
-
     from krr_amd.core.packing import _PYDEC
 
     names = tuple(model.__fields__)
@@ -255,8 +257,6 @@ def _v1_construct_layout(model) -> bool:
     """True when instances of ``model`` are exactly pydantic v1's construct() layout (the field
     dict + __fields_set__): a pydantic.v1 BaseModel without private attributes, as the
     reference's models are (pydantic 1.10).  Anything else is built by its own constructor."""
-    import pydantic.v1 as pv1
-
     return (isinstance(model, type) and issubclass(model, pv1.BaseModel)
             and not getattr(model, "__private_attributes__", None)
             and model.__config__.extra is not pv1.Extra.allow)
