@@ -564,6 +564,16 @@ def main():
                     host_rec[: rec.shape[0]].copy_(rec, non_blocking=True)
                 rec.record_stream(copy_stream)  # the receive buffer outlives the copy
 
+    rccl_info = None
+    if comm is not None:
+        try:
+            n_comm, r_comm = ctx.comm_info(comm)
+            rccl_info = {"ranks": n_comm, "rank0_rank": r_comm, "source": "ncclCommCount/ncclCommUserRank through "
+                         "krr_comm_info on torch.distributed's nccl communicator"}
+        except _native.NativeError as e:
+            rccl_info = {"error": str(e)}
+    elif dist_on and backend == "nccl":
+        rccl_info = {"ranks": None, "note": "torch.distributed's communicator not exposed: torch.distributed.gather"}
     if gather_mode == "stream":
         # first use of the C-ABI gather on torch's communicator: if it fails on any rank
         # (an error return, not a hang), every rank falls back to torch.distributed.gather
@@ -683,6 +693,10 @@ def main():
         result["config"]["gather"] = {"stream": "RCCL send/recv on the launch stream (C ABI krr_gather_results)",
                                       "torch": "torch.distributed.gather, overlapping the next launch",
                                       "blocking": "torch.distributed.gather, waited for each step"}[gather_mode]
+        # what actually carried the records (after any fallback), and how many ranks RCCL saw
+        result["gather_mode_requested"] = args.gather
+        result["gather_mode_used"] = gather_mode
+        result["rccl_comm"] = rccl_info
     if zero_copy or (dist_on and rank == 0 and not args.separate):
         # the host buffer holds exactly what the launch computed (after the last step's sync);
         # N > 1: rank 0's own shard leads the gathered records
@@ -1250,13 +1264,17 @@ def fleet_objects(n: int) -> list:
     from krr_amd.core.models.objects import K8sObjectData
 
     cpu_rt, mem_rt = ResourceType.CPU, ResourceType.Memory
-    cpus = [None] + [Decimal(x) for x in ("0.05", "0.1", "0.2", "0.25", "0.5", "1", "2")]
-    mems = [None] + [Decimal(x) for x in ("67108864", "134217728", "209715200", "268435456", "536870912")]
+    # the synthetic fleet's recommendations sit near 0.35 cores and 3.0e8 B: currents from far
+    # below to far above them, plus unset ones
+    cpus = [None] + [Decimal(x) for x in ("0.1", "0.25", "0.35", "0.4", "0.5", "1", "2")]
+    mems = [None] + [Decimal(x) for x in ("100000000", "250000000", "300000000", "350000000", "536870912",
+                                          "1073741824")]
     pool = []
     for i in range(64):
         c, m = cpus[i % len(cpus)], mems[(i * 5) % len(mems)]
         pool.append(ResourceAllocations.construct(requests={cpu_rt: c, mem_rt: m},
-                                                  limits={cpu_rt: cpus[(i * 3) % len(cpus)], mem_rt: m}))
+                                                  limits={cpu_rt: None if i % 2 else cpus[(i * 3) % len(cpus)],
+                                                          mem_rt: mems[(i * 7) % len(mems)]}))
     new = K8sObjectData.construct
     return [new(cluster=None, name=f"app-{i}", container="main", pods=[f"app-{i}-0"], namespace=f"ns-{i % 97}",
                 kind="Deployment", allocations=pool[i % 64]) for i in range(n)]

@@ -198,6 +198,10 @@ int krr_comm_init_timeout(krr_ctx* ctx, int nranks, const void* unique_id, int r
                           void** out_comm);
 int krr_comm_destroy(krr_ctx* ctx, void* comm);
 
+/* The communicator's rank count and this process's rank in it (ncclCommCount /
+ * ncclCommUserRank): what a multi-GPU run reports to show RCCL carried every rank. */
+int krr_comm_info(krr_ctx* ctx, void* comm, int* nranks, int* rank);
+
 /* Gather every rank's n_local records (device int64[4 * n_local]) to `root`,
  * concatenated in rank order into `out` (device, root only; ignored elsewhere).
  * counts: HOST int64[nranks] with every rank's n_local, read on the root only; NULL

@@ -86,6 +86,7 @@ EXPORTED_SYMBOLS = (
     "krr_comm_init",
     "krr_comm_init_timeout",
     "krr_comm_destroy",
+    "krr_comm_info",
     "krr_gather_results",
 )
 
@@ -265,6 +266,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_comm_init_timeout.restype = ctypes.c_int
         lib.krr_comm_destroy.argtypes = [vp, vp]
         lib.krr_comm_destroy.restype = ctypes.c_int
+        lib.krr_comm_info.argtypes = [vp, vp, vp, vp]
+        lib.krr_comm_info.restype = ctypes.c_int
         lib.krr_gather_results.argtypes = [vp, vp, ctypes.c_int, vp, i64, vp, vp, vp]
         lib.krr_gather_results.restype = ctypes.c_int
         skp = ctypes.POINTER(KrrSketchParams)
@@ -469,6 +472,12 @@ class Context:
 
     def comm_destroy(self, comm: int) -> None:
         self._check(self._lib.krr_comm_destroy(self._h, ctypes.c_void_p(comm)))
+
+    def comm_info(self, comm: int) -> tuple[int, int]:
+        """(ranks in the RCCL communicator, this process's rank in it)."""
+        n, r = ctypes.c_int(0), ctypes.c_int(0)
+        self._check(self._lib.krr_comm_info(self._h, ctypes.c_void_p(comm), ctypes.byref(n), ctypes.byref(r)))
+        return int(n.value), int(r.value)
 
     def gather_results(self, comm: int, root: int, records, counts=None, out=None, stream=None) -> None:
         """records: int64 [n_local, 4] device tensor; on the root, out: int64 [sum(counts), 4]

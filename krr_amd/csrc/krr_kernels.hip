@@ -4547,6 +4547,16 @@ int krr_comm_destroy(krr_ctx* ctx, void* comm) {
     return r == ncclSuccess ? KRR_OK : nccl_err(ctx, "ncclCommDestroy", r);
 }
 
+int krr_comm_info(krr_ctx* ctx, void* comm, int* nranks, int* rank) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!comm || !nranks || !rank) return set_err(ctx, KRR_E_INVALID, "null comm / outputs%s", "");
+    const RcclApi& R = rccl();
+    if (!R.ok) return set_err(ctx, KRR_E_UNSUPPORTED, "librccl.so.1 not loadable%s", "");
+    ncclResult_t r = R.comm_count((ncclComm_t)comm, nranks);
+    if (r == ncclSuccess) r = R.comm_user_rank((ncclComm_t)comm, rank);
+    return r == ncclSuccess ? KRR_OK : nccl_err(ctx, "ncclCommCount/UserRank", r);
+}
+
 int krr_gather_results(krr_ctx* ctx, void* comm, int root, const int64_t* records, int64_t n_local,
                        const int64_t* counts, int64_t* out, void* stream) {
     if (!ctx) return KRR_E_INVALID;
