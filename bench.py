@@ -1254,6 +1254,15 @@ def right_size(args, records) -> dict:
                                  f"the first {k}")}
 
 
+def kll_nchunks_np(beg: np.ndarray, end: np.ndarray) -> np.ndarray:
+    """krr_kll.h kll_nchunks per segment: the 1,024-slot chunks the KLL passes stream."""
+    a0 = np.minimum((beg + 1) & ~1, end)
+    a1 = np.maximum(end & ~1, a0)
+    units = (a1 - a0) >> 1
+    full = units // 512
+    return full + (((units - full * 512) > 0) | (a0 > beg) | (a1 < end)).astype(np.int64)
+
+
 def fleet_objects(n: int) -> list:
     """n synthetic K8sObjectData (untimed set-up of the right-size leg): distinct objects whose
     current allocations cycle through a pool that puts the recommendations in every severity
@@ -1525,9 +1534,11 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             return
         if method == "kll":
             # events: before the body pass, between it and the tail pass, after the tail pass
+            kst: dict = {}
             res = sketch.kll_time_sharded(ctx, ser_parts, kcfg, params, stream=stream,
-                                          events=None if ev is None else (ev[0], ev[3], ev[1]))
+                                          events=None if ev is None else (ev[0], ev[3], ev[1]), stats=kst)
             state["rows"], state["rows_per_series"] = res["rows"], res["rows_per_series"]
+            state["kll_stats"] = kst
         elif method == "window":
             res = sketch.window_exact_time_sharded(ctx, ser_parts, params, ext_slots=T - Lr, stream=stream,
                                                    events=None if ev is None else ev[0:2])
@@ -1582,6 +1593,7 @@ def run_config5(args, world, rank, local, dev, coll_dev):
     kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     N = S * Lr
     kernels_ms = {}
+    kll_sparse = None
     if method == "direct":
         kname = "k_select"
         kbytes = 8 * N + 8 * (S + 1) + 20 * S
@@ -1594,8 +1606,24 @@ def run_config5(args, world, rank, local, dev, coll_dev):
             kms = float(np.mean([e[0].elapsed_time(e[3]) for e in evs]))
             tms = float(np.mean([e[3].elapsed_time(e[1]) for e in evs]))
             kernels_ms["k_kll_tail"] = tms
-            # every slot once + offsets + each row's header and body read + its tail written
-            tbytes = 8 * N + 8 * (S + 1) + 8 * (16 + kcfg.budget) * S + 8 * kcfg.tail * S
+            kst = state.get("kll_stats") or {}
+            if "lines_read" in kst:
+                # sparse tail pass (krr_kll_tail_lines): the body also writes 4 B of line maximum per
+                # 128-B line; the tail pass reads those maxima, the lines that can hold a tail key,
+                # offsets, each row's header and body, and writes its tail
+                seg = np.arange(S + 1, dtype=np.int64) * Lr
+                nch = kll_nchunks_np(seg[:-1], seg[1:])
+                nlines = int(nch.sum()) * 64
+                kbytes += 4 * 64 * int(((nch + 7) & ~7).sum())  # the build streams a multiple of 8 chunks
+                read = int(kst["lines_read"].sum().item())
+                tbytes = 4 * nlines + 128 * read + 8 * (S + 1) + 8 * (16 + kcfg.budget) * S + 8 * kcfg.tail * S
+                kll_sparse = {
+                    "lines_read_frac": read / max(nlines, 1), "lines_read": read, "lines_total": nlines,
+                    "definition": "fraction of the slice's 128-B lines the tail pass read (the rest cannot hold "
+                                  "a key above its threshold: their maxima, recorded by the body pass, are below it)"}
+            else:
+                # every slot once + offsets + each row's header and body read + its tail written
+                tbytes = 8 * N + 8 * (S + 1) + 8 * (16 + kcfg.budget) * S + 8 * kcfg.tail * S
     elif method == "window":
         kname = "k_window_export"
         hdr = state["hdr"]
@@ -1661,6 +1689,8 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                             "alltoall_bytes_sent_per_rank": state["exchanged_bytes"],
                             "misses_per_step": state["misses"] / max(args.steps, 1),
                             "hbm_passes_per_step": 1}
+    if kll_sparse:
+        result["kll_sparse_tail"] = kll_sparse
     if "k_kll_tail" in kernels_ms:
         # the KLL build in two passes: the body (k_kll_build, above) and the exact tail
         # (k_kll_tail, candidates above a threshold read from the row's body); both HBM streams

@@ -68,6 +68,9 @@ EXPORTED_SYMBOLS = (
     "krr_kll_row_words",
     "krr_kll_build",
     "krr_kll_tail",
+    "krr_kll_line_words",
+    "krr_kll_build_lines",
+    "krr_kll_tail_lines",
     "krr_kll_merge",
     "krr_kll_query",
     "krr_sketch_locate",
@@ -284,6 +287,12 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_kll_build.restype = ctypes.c_int
         lib.krr_kll_tail.argtypes = [vp, sp, kkp, vp, vp]
         lib.krr_kll_tail.restype = ctypes.c_int
+        lib.krr_kll_line_words.argtypes = [i64]
+        lib.krr_kll_line_words.restype = i64
+        lib.krr_kll_build_lines.argtypes = [vp, sp, kkp, i64, vp, vp, i64, vp]
+        lib.krr_kll_build_lines.restype = ctypes.c_int
+        lib.krr_kll_tail_lines.argtypes = [vp, sp, kkp, vp, vp, i64, vp, vp]
+        lib.krr_kll_tail_lines.restype = ctypes.c_int
         lib.krr_kll_merge.argtypes = [vp, i64, i32, vp, kkp, i64, vp, vp]
         lib.krr_kll_merge.restype = ctypes.c_int
         lib.krr_kll_query.argtypes = [vp, i64, i32, vp, kkp, i64, pp, vp, vp, vp, vp]
@@ -580,6 +589,34 @@ class Context:
         _check_tensor(rows, "int64", S * self.kll_row_words(kp))
         self._check(self._lib.krr_kll_tail(self._h, ctypes.byref(series), ctypes.byref(kp), rows.data_ptr(),
                                            self._stream(stream)))
+
+    def kll_line_words(self, max_segment_len: int) -> int:
+        """uint32 words per series of the line maxima (krr_kll_line_words)."""
+        return int(self._lib.krr_kll_line_words(int(max_segment_len)))
+
+    def kll_build_lines(self, series: KrrSeries, kp: KrrKllParams, rows, lines, line_stride: int, seg_base: int = 0,
+                        stream=None) -> None:
+        """The body-only build that also writes the line maxima: lines int32 [S * line_stride]."""
+        S = series.n_segments
+        _check_tensor(rows, "int64", S * self.kll_row_words(kp))
+        _check_tensor(lines, "int32", S * int(line_stride))
+        self._check(self._lib.krr_kll_build_lines(self._h, ctypes.byref(series), ctypes.byref(kp), int(seg_base),
+                                                  rows.data_ptr(), lines.data_ptr(), int(line_stride),
+                                                  self._stream(stream)))
+
+    def kll_tail_lines(self, series: KrrSeries, kp: KrrKllParams, rows, lines, line_stride: int,
+                       lines_read=None, stream=None) -> None:
+        """The sparse tail pass (krr_kll_tail_lines) over rows and line maxima from kll_build_lines;
+        lines_read (optional int32 [S]): the 128-B lines it read per series."""
+        S = series.n_segments
+        _check_tensor(rows, "int64", S * self.kll_row_words(kp))
+        _check_tensor(lines, "int32", S * int(line_stride))
+        if lines_read is not None:
+            _check_tensor(lines_read, "int32", S)
+        self._check(self._lib.krr_kll_tail_lines(self._h, ctypes.byref(series), ctypes.byref(kp), rows.data_ptr(),
+                                                 lines.data_ptr(), int(line_stride),
+                                                 None if lines_read is None else lines_read.data_ptr(),
+                                                 self._stream(stream)))
 
     def kll_merge(self, rows, rows_per_series: int, kp: KrrKllParams, out_rows, series_base: int = 0,
                   stream=None) -> None:

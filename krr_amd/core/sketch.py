@@ -654,6 +654,10 @@ class KllConfig:
     seed: int = 0x4B4C4C5345454431
     one_pass_tail: bool = False  # KRR_KLL_ONE_PASS_TAIL: the tail inside the build (same rows)
     tail_flags: int = 0          # further krr_kll_params.reserved bits (testing)
+    # the tail pass reads only the 128-B lines whose maximum (recorded by the body build) can
+    # hold a tail key (krr_kll_build_lines / krr_kll_tail_lines; same rows); False: the tail
+    # pass streams the whole slice again (krr_kll_tail)
+    sparse_tail: bool = True
 
     def params(self, slice_id: int = 0) -> _native.KrrKllParams:
         flags = self.tail_flags | (_native.KRR_KLL_ONE_PASS_TAIL if self.one_pass_tail else 0)
@@ -680,12 +684,14 @@ class KllConfig:
 
 
 def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, seg_base: int = 0,
-              stream=None, events=None):
+              stream=None, events=None, stats: Optional[dict] = None):
     """int64 [S, row_words] rows of this rank's slice of every series: one HBM pass for the
     body, and (tail > 0) the tail pass over the slice again (krr_kll_tail; one pass in all with
     ``cfg.one_pass_tail``).  ``series``: a KrrSeries, or (lo, hi, KrrSeries) parts in buffers
     of their own.  ``events`` (3 HIP events, optional): recorded on ``stream`` before the body
-    launches, between them and the tail launches, and after."""
+    launches, between them and the tail launches, and after.  ``stats`` (optional dict, sparse
+    tail pass): gets ``lines_read`` (int32 [S] device tensor: 128-B lines the tail pass read per
+    series) and ``line_words`` (uint32 words of line maxima written per series)."""
     import torch
 
     parts = _parts(series)
@@ -699,20 +705,46 @@ def kll_build(ctx: _native.Context, series, cfg: KllConfig, slice_id: int = 0, s
     if split:  # every body launch first, then every tail launch (timed apart)
         kp.reserved |= _native.KRR_KLL_BODY_ONLY
     st = stream if stream is not None else torch.cuda.current_stream(dev)
+    sparse = split and cfg.sparse_tail
+    lines = {}
+    if sparse:  # per part: its line maxima, written by the body build, read by the tail pass
+        for lo, hi, ser in parts:
+            if hi > lo:
+                stride = ctx.kll_line_words(_max_len(ser))
+                lines[lo] = (torch.empty((hi - lo) * stride, dtype=torch.int32, device=dev), stride)
     if events is not None:
         events[0].record(st)
     for lo, hi, ser in parts:
         if hi > lo:
-            ctx.kll_build(ser, kp, rows[lo:hi], seg_base=seg_base + lo, stream=st)
+            if sparse:
+                ctx.kll_build_lines(ser, kp, rows[lo:hi], *lines[lo], seg_base=seg_base + lo, stream=st)
+            else:
+                ctx.kll_build(ser, kp, rows[lo:hi], seg_base=seg_base + lo, stream=st)
     if events is not None:
         events[1].record(st)
+    read = torch.zeros(max(S, 1), dtype=torch.int32, device=dev) if (sparse and stats is not None) else None
+    if stats is not None and sparse:
+        stats["lines_read"] = read[:S]
+        stats["line_words"] = {lo: lw[1] for lo, lw in lines.items()}
     if split:
         for lo, hi, ser in parts:
             if hi > lo:
-                ctx.kll_tail(ser, kp, rows[lo:hi], stream=st)
+                if sparse:
+                    ctx.kll_tail_lines(ser, kp, rows[lo:hi], *lines[lo],
+                                       lines_read=None if read is None else read[lo:hi], stream=st)
+                else:
+                    ctx.kll_tail(ser, kp, rows[lo:hi], stream=st)
     if events is not None:
         events[2].record(st)
     return rows[:S]
+
+
+def _max_len(ser) -> int:
+    """A KrrSeries' longest segment (its max_segment_len, or from its offsets)."""
+    if int(ser.max_segment_len) > 0:
+        return int(ser.max_segment_len)
+    offs = ser._keep[1]
+    return int((offs[1:] - offs[:-1]).max().item()) if offs.numel() > 1 else 0
 
 
 def kll_exchange(rows, group=None):
@@ -772,7 +804,7 @@ def kll_query(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig,
 
 
 def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _native.KrrPercentileParams,
-                     group=None, stream=None, events=None) -> dict:
+                     group=None, stream=None, events=None, stats: Optional[dict] = None) -> dict:
     """Sketch-only percentile of every time-sharded series: build (one pass over this
     rank's slices; slice id = rank) -> all-to-all of the rows -> fold each series' rows into
     one (krr_kll_merge) -> query on the owner.  value/count/flags of this rank's owner block,
@@ -787,7 +819,7 @@ def kll_time_sharded(ctx: _native.Context, series, cfg: KllConfig, params: _nati
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     with torch.cuda.stream(st):
         # events (optional, 3): before the body pass, between it and the tail pass, after
-        rows = kll_build(ctx, series, cfg, slice_id=rank, stream=st, events=events)
+        rows = kll_build(ctx, series, cfg, slice_id=rank, stream=st, events=events, stats=stats)
         S = rows.shape[0]
         lo, hi = owner_blocks(S, world)[rank] if world > 1 else (0, S)
         gathered, W = kll_exchange(rows, group)

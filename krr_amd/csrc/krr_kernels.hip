@@ -3532,6 +3532,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
     for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
                           (const void*)k_window_export<false>, (const void*)k_window_merge,
                           (const void*)k_kll_build<false>, (const void*)k_kll_build<true>, (const void*)k_kll_tail,
+                          (const void*)k_kll_build<false, true>, (const void*)k_kll_tail_lines,
                           (const void*)k_kll_merge,
                           (const void*)k_kll_query})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
@@ -3932,8 +3933,8 @@ static int kll_tail_launch(krr_ctx* ctx, const krr_series* series, const krr_kll
     return KRR_OK;
 }
 
-int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
-                  uint64_t* rows, void* stream) {
+static int kll_build_common(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
+                            uint64_t* rows, uint32_t* lines, int64_t line_stride, void* stream) {
     if (!ctx) return KRR_E_INVALID;
     int rc = check_series(ctx, series);
     if (rc) return rc;
@@ -3966,14 +3967,76 @@ int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* 
     kll_tail_lds(kp, &tcap_t, &lds_t);
     if (tail_pass && lds_t > ctx->max_lds)
         return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds_t);
+    if (lines) {  // the body-only build that also writes the line maxima (krr_kll_build_lines)
+        if (!tail_pass) return set_err(ctx, KRR_E_INVALID, "kll line maxima need tail > 0 and the tail pass%s", "");
+        if (line_stride < krr_kll_line_words(maxlen))
+            return set_err(ctx, KRR_E_INVALID, "line_stride below krr_kll_line_words(max_segment_len) = %s%lld", "",
+                           (long long)krr_kll_line_words(maxlen));
+    }
     KllBuildArgs A{series->values, series->offsets, S, series->gaps_are_nan, kp->budget, kp->tail, nrl, tcap,
-                   (uint32_t)kp->slice, kp->seed, seg_base, rows, tail_pass ? 1 : 0};
+                   (uint32_t)kp->slice, kp->seed, seg_base, rows, tail_pass ? 1 : 0, lines, line_stride};
+    if (lines) {
+        hipLaunchKernelGGL((k_kll_build<false, true>), dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
+        KRR_HIP(ctx, hipGetLastError());
+        return KRR_OK;
+    }
     if (one_pass)
         hipLaunchKernelGGL(k_kll_build<true>, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
     else
         hipLaunchKernelGGL(k_kll_build<false>, dim3(grid_for(S)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     if (tail_pass && !(kp->reserved & KRR_KLL_BODY_ONLY)) return kll_tail_launch(ctx, series, kp, rows, (hipStream_t)stream);
+    return KRR_OK;
+}
+
+int krr_kll_build(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
+                  uint64_t* rows, void* stream) {
+    return kll_build_common(ctx, series, kp, seg_base, rows, nullptr, 0, stream);
+}
+
+int64_t krr_kll_line_words(int64_t max_segment_len) {
+    if (max_segment_len < 0) return -1;
+    const int64_t nch = max_segment_len / ((int64_t)kUnroll * kWave * 2) + 2;  // 1,024-slot chunks, head/tail
+    return 64 * ((nch + 7) & ~(int64_t)7);  // the build streams a multiple of 8 chunks
+}
+
+int krr_kll_build_lines(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, int64_t seg_base,
+                        uint64_t* rows, uint32_t* lines, int64_t line_stride, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (!lines) return set_err(ctx, KRR_E_INVALID, "null lines%s", "");
+    return kll_build_common(ctx, series, kp, seg_base, rows, lines, line_stride, stream);
+}
+
+int krr_kll_tail_lines(krr_ctx* ctx, const krr_series* series, const krr_kll_params* kp, uint64_t* rows,
+                       const uint32_t* lines, int64_t line_stride, uint32_t* lines_read, void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    int rc = check_series(ctx, series);
+    if (rc) return rc;
+    if (krr_kll_row_words(kp) < 0)
+        return set_err(ctx, KRR_E_INVALID, "kll: budget in [256, 4096] (a multiple of 64), tail in [0, 4096]%s", "");
+    if (series->n_segments == 0 || kp->tail == 0) return KRR_OK;
+    if (!rows || !lines) return set_err(ctx, KRR_E_INVALID, "null rows / lines%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    int64_t maxlen = 0;
+    rc = resolve_maxlen(ctx, series, (hipStream_t)0, &maxlen);
+    if (rc) return rc;
+    if (line_stride < krr_kll_line_words(maxlen))
+        return set_err(ctx, KRR_E_INVALID, "line_stride below krr_kll_line_words(max_segment_len) = %s%lld", "",
+                       (long long)krr_kll_line_words(maxlen));
+    uint32_t tcap_t;
+    size_t lds_t;
+    kll_tail_lds(kp, &tcap_t, &lds_t);
+    const uint32_t qoff = (uint32_t)((lds_t + 15) & ~(size_t)15);
+    const size_t lds = (size_t)qoff + 128 * sizeof(uint32_t);
+    if (lds > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds);
+    const double two_ln = (kp->reserved & KRR_KLL_TAIL_NO_MARGIN) ? 0.0 : 2.0 * log(4.0 / 1e-3);
+    KllLineTailArgs LA{{series->values, series->offsets, series->n_segments, kp->budget, kp->tail, tcap_t, two_ln, rows,
+                        lines, line_stride},
+                       qoff, lines_read};
+    hipLaunchKernelGGL(k_kll_tail_lines, dim3(grid_for(series->n_segments)), dim3(64), lds, (hipStream_t)stream, LA);
+    KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }
 

@@ -441,7 +441,33 @@ struct KllBuildArgs {
     int64_t seg_base;
     uint64_t* rows;   // [S][kKllHdr + budget + tail]
     int32_t tail_pass;  // the tail is left to k_kll_tail (zero tail words, word 6 = 0)
+    uint32_t* lines;    // LINES builds: per series, per chunk, 64 line maxima (kll_line_key)
+    int64_t line_stride;  // u32 words per series in `lines`
 };
+
+// ---- line maxima: where the exact tail's keys can be (the sparse tail pass) ----
+// A "line" is 16 slots = 128 contiguous bytes = the double2 of 8 consecutive lanes in one row
+// u of a chunk.  Its key: the top 32 bits of the ordered key (okey) of the line's largest
+// present sample, rounded UP (0 when every slot is absent), so a line holding a sample x has
+// key >= okey(x) >> 32 — a line whose key is below okey(tau) >> 32 holds no sample > tau.
+// (-0 and +0 get the same key: okey(-0) = 2^63 - 1 rounds up to okey(+0) >> 32.)
+__device__ __forceinline__ uint32_t kll_line_key(double hi) {
+    const uint64_t b = dbits(hi);
+    const uint32_t h = (uint32_t)(b >> 32), l = (uint32_t)b;
+    const uint32_t m = (uint32_t)((int32_t)h >> 31);
+    const uint32_t oh = h ^ (m | 0x80000000u), ol = l ^ m;
+    const uint32_t k = oh + (ol != 0u ? 1u : 0u);
+    return hi == hi ? k : 0u;
+}
+
+// max over each group of 8 consecutive lanes, in every lane of the group (DPP quad_perm
+// [1,0,3,2], [2,3,0,1], then row_half_mirror: lane i <-> 7 - i within 8)
+__device__ __forceinline__ uint32_t kll_max8(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0xB1, 0xF, 0xF, false));
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x4E, 0xF, 0xF, false));
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x141, 0xF, 0xF, false));
+    return k;
+}
 
 // ---- wave-level pieces, free functions of value arguments (the per-wave state below stays in
 // registers: nothing of it is ever address-taken) ----
@@ -803,9 +829,12 @@ __device__ __forceinline__ uint32_t kll_tail_export(KllShared sh, KllTail ts, ui
 }
 
 // Per-wave build state; one instance per series slice (by value: nothing is address-taken).
-template <bool TAIL>  // TAIL: the one-pass tail buffer is part of this build
+// TAIL: the one-pass tail buffer is part of this build; LINES: the build also writes each
+// chunk's 64 line maxima (kll_line_key) to lm[ci * 64 ...] for the sparse tail pass
+template <bool TAIL, bool LINES = false>
 struct KllProc {
     KllShared sh;
+    uint32_t* lm;      // LINES: this series' line maxima
     uint64_t base;
     uint64_t w2u;      // sum w^2 of the wave-level compactions (uniform)
     uint32_t ci;       // chunk index (uniform)
@@ -924,6 +953,17 @@ struct KllProc {
             nanm |= ballot(__builtin_isunordered(a[u], b[u]));
             lo[u] = fmin(a[u], b[u]);  // one NaN: both are the present sample
             hi[u] = fmax(a[u], b[u]);
+        }
+        if constexpr (LINES) {
+            // lane 8g + j stores line (u = j, g) of this chunk: index u * 8 + g
+            const uint32_t j = (uint32_t)lane & 7u;
+            uint32_t mine = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t k = kll_max8(kll_line_key(hi[u]));
+                mine = j == (uint32_t)u ? k : mine;
+            }
+            lm[(size_t)ci * 64u + j * 8u + ((uint32_t)lane >> 3)] = mine;
         }
 #ifndef KRR_KLL_X_NOTAIL
         if constexpr (TAIL) {
@@ -1219,7 +1259,7 @@ __device__ uint32_t kll_gather_level(const KllShared& sh, int32_t nrl, uint32_t 
 #endif
 // TAIL = false: no tail (tail == 0) or the tail left to k_kll_tail (A.tail_pass); the build then
 // holds none of the tail buffer's code or state.
-template <bool TAIL>
+template <bool TAIL, bool LINES = false>
 __global__ __launch_bounds__(64, TAIL ? KRR_KLL_WAVES_PER_SIMD : KRR_KLL_BODY_WAVES_PER_SIMD) void k_kll_build(
     KllBuildArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1248,8 +1288,9 @@ __global__ __launch_bounds__(64, TAIL ? KRR_KLL_WAVES_PER_SIMD : KRR_KLL_BODY_WA
         uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t nch = kll_nchunks(beg, end);
         const int64_t npad = (nch + 7) & ~(int64_t)7;
-        KllProc<TAIL> P;
+        KllProc<TAIL, LINES> P;
         P.sh = sh;
+        P.lm = LINES ? A.lines + (size_t)s * (size_t)A.line_stride : nullptr;
         P.base = kll_slice_base(A.seed, series, A.slice);
         P.w2u = 0;
         P.ci = 0;
@@ -1753,6 +1794,50 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
 // (tau rising, as in the build) keep the buffer within its capacity.  Either way the tail words
 // are the top min(n, tail) present keys, exactly what the one-pass build writes: rows are the
 // same bit for bit (oracle/kll_ref.py does not depend on how the tail is found).
+#ifndef KRR_KLL_TAIL_MARGIN
+#define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
+#endif
+// The tail pass's threshold from the row's own body: the body key t0 at estimated rank
+// q = n - tail - 1 - M (M = KRR_KLL_TAIL_MARGIN x the rank bound at delta = 1e-3); candidates are
+// the keys > *tau (the next double below t0).  false: no usable threshold (every present key is
+// a candidate).  im / lvl: LDS work space (the body keys and their levels).
+__device__ bool kll_tail_tau(const uint64_t* row, uint32_t budget, uint32_t tail, double two_ln, uint64_t* im,
+                             uint8_t* lvl, int lane, double* tau) {
+    const uint64_t n = uni64(row[0]);
+    const double M = ceil(KRR_KLL_TAIL_MARGIN * sqrt(two_ln * (double)uni64(row[4])));
+    const double qd = (double)n - (double)tail - 1.0 - M;
+    bool full0 = false;
+    *tau = 0.0;
+    if (qd >= 0.0) {
+        uint32_t m = 0;
+        for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
+            const uint32_t l = kll_len(row, h);
+            for (uint32_t i = lane; i < l; i += kWave) {
+                lvl[m + i] = (uint8_t)h;
+                im[kKllHdr + m + i] = row[kKllHdr + m + i];
+            }
+            m += l;
+        }
+        __syncthreads();
+#ifndef KRR_KLL_X_BISECT
+        uint64_t tk = 0, tk1 = 0;
+        if (m <= 512u) kll_body_select2<1>(im, lvl, m, (uint64_t)qd, 0, lane, tk, tk1);
+        else tk = kll_body_select(im, lvl, m, (uint64_t)qd, lane);
+        const double t0 = bitsd(okey_inv(tk));
+#else
+        const double t0 = bitsd(okey_inv(kll_body_select(im, lvl, m, (uint64_t)qd, lane)));
+#endif
+        __syncthreads();
+        if (t0 > -__builtin_inf()) {  // candidates: keys >= t0 (t0 == -inf: every present key)
+            full0 = true;
+            // the next double below t0 (bit arithmetic: no libm call in the kernel)
+            const uint64_t tb0 = dbits(t0);
+            *tau = t0 == 0.0 ? bitsd(0x8000000000000001ull) : bitsd(t0 > 0.0 ? tb0 - 1u : tb0 + 1u);
+        }
+    }
+    return full0;
+}
+
 struct KllTailArgs {
     const double* vals;
     const int64_t* offs;
@@ -1762,6 +1847,8 @@ struct KllTailArgs {
     uint32_t tcap;
     double two_ln;    // 2 ln(4 / delta)
     uint64_t* rows;
+    const uint32_t* lines;  // k_kll_tail_lines: the body build's line maxima
+    int64_t line_stride;
 };
 
 struct KllTailProc {
@@ -1784,9 +1871,6 @@ struct KllTailProc {
 #ifndef KRR_KLL_TAIL_STREAM
 #define KRR_KLL_TAIL_STREAM 2  // kll_stream form of the tail pass (2: two ahead, copies; 3: unrolled by 3)
 #endif
-#ifndef KRR_KLL_TAIL_MARGIN
-#define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
-#endif
 #ifndef KRR_KLL_TAIL_WAVES_PER_SIMD
 #define KRR_KLL_TAIL_WAVES_PER_SIMD 2
 #endif
@@ -1802,38 +1886,8 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
         uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
-        const uint64_t n = uni64(row[0]);
-        const double M = ceil(KRR_KLL_TAIL_MARGIN * sqrt(A.two_ln * (double)uni64(row[4])));
-        const double qd = (double)n - (double)tail - 1.0 - M;
-        bool full0 = false;
         double tau = 0.0;
-        if (qd >= 0.0) {
-            uint32_t m = 0;
-            for (uint32_t h = 0; h < (uint32_t)kKllLevels; ++h) {
-                const uint32_t l = kll_len(row, h);
-                for (uint32_t i = lane; i < l; i += kWave) {
-                    lvl[m + i] = (uint8_t)h;
-                    im[kKllHdr + m + i] = row[kKllHdr + m + i];
-                }
-                m += l;
-            }
-            __syncthreads();
-#ifndef KRR_KLL_X_BISECT
-            uint64_t tk = 0, tk1 = 0;
-            if (m <= 512u) kll_body_select2<1>(im, lvl, m, (uint64_t)qd, 0, lane, tk, tk1);
-            else tk = kll_body_select(im, lvl, m, (uint64_t)qd, lane);
-            const double t0 = bitsd(okey_inv(tk));
-#else
-            const double t0 = bitsd(okey_inv(kll_body_select(im, lvl, m, (uint64_t)qd, lane)));
-#endif
-            __syncthreads();
-            if (t0 > -__builtin_inf()) {  // candidates: keys >= t0 (t0 == -inf: every present key)
-                full0 = true;
-                // the next double below t0 (bit arithmetic: no libm call in the kernel)
-                const uint64_t tb0 = dbits(t0);
-                tau = t0 == 0.0 ? bitsd(0x8000000000000001ull) : bitsd(t0 > 0.0 ? tb0 - 1u : tb0 + 1u);
-            }
-        }
+        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau);
         const int64_t nch = kll_nchunks(beg, end);
         const int64_t npad = KRR_KLL_TAIL_STREAM == 3 ? (nch + 2) / 3 * 3 : (nch + 1) & ~(int64_t)1;
         KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
@@ -1853,6 +1907,120 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
         if (lane == 0)
             row[14] = ((uint64_t)((restreams << 8) | P.ts.nfall) << 48) | ((uint64_t)P.ts.npass << 24) | P.ts.nref;
 #endif
+        __syncthreads();
+    }
+}
+
+}  // namespace krr
+namespace krr {
+
+// ---------------------------------------------------------------------------------------------
+// The sparse tail pass (round 5): candidates are the keys > tau, and a line (16 slots, 128 B)
+// whose maximum from the body build (k_kll_build<false, true>: kll_line_key per line) is below
+// tau holds none — so only the lines that can hold a candidate are read.  Their ids queue in
+// LDS (64 per virtual chunk: row r of the virtual chunk = 8 queued lines, 8 lanes each) and
+// each virtual chunk goes through the same candidate filter as a streamed chunk.  The tail is a
+// set (the top min(n, tail) present keys, exported sorted), so the order lines arrive in does
+// not change it: the rows equal k_kll_tail's bit for bit.  If the threshold missed (fewer than
+// `tail` candidates) the slice is streamed whole with every present key a candidate, as there.
+// Reads: the line maxima (1/32 of the slice) + the flagged lines (~20% at p99 of 30d@15s).
+struct KllLineTailArgs {
+    KllTailArgs T;
+    uint32_t queue_off;     // byte offset of the 128-entry line queue in LDS
+    uint32_t* lines_read;   // optional: per series, the lines this pass read (its bytes / 128)
+};
+
+__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_lines(KllLineTailArgs LA) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const KllTailArgs& A = LA.T;
+    const int lane = threadIdx.x;
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
+    KllShared sh{};
+    sh.tb = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* im = sh.tb;
+    uint8_t* lvl = reinterpret_cast<uint8_t*>(im + kKllHdr + budget);
+    uint32_t* q = reinterpret_cast<uint32_t*>(smem + LA.queue_off);
+    const double2* __restrict__ v2 = reinterpret_cast<const double2*>(A.vals);
+    const double qnan = __builtin_nan("");
+    constexpr int64_t CH = (int64_t)kUnroll * kWave;
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        uint64_t* row = A.rows + (size_t)s * RW;
+        const int64_t beg = A.offs[s], end = A.offs[s + 1];
+        double tau = 0.0;
+        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau);
+        const int64_t nch = kll_nchunks(beg, end);
+        KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
+        bool dense = !full0;
+        uint32_t nread = 0;  // lines read (uniform)
+        if (full0 && nch > 0) {
+            // kll_stream's layout of this slice
+            int64_t a0 = (beg + 1) & ~(int64_t)1;
+            if (a0 > end) a0 = end;
+            int64_t a1 = end & ~(int64_t)1;
+            if (a1 < a0) a1 = a0;
+            const int64_t i0 = a0 >> 1, nunits = (a1 >> 1) - i0, nfull = nunits / CH;
+            const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
+            const uint32_t t32 = (uint32_t)(okey(dbits(tau)) >> 32);
+            const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
+            auto process = [&](uint32_t cnt) __attribute__((always_inline)) {
+                double2 c[kUnroll];
+#pragma unroll
+                for (int r = 0; r < kUnroll; ++r) {
+                    const uint32_t slot = (uint32_t)r * 8u + ((uint32_t)lane >> 3);
+                    const uint32_t id = slot < cnt ? q[slot] : 0xFFFFFFFFu;
+                    c[r] = make_double2(qnan, qnan);
+                    if (id != 0xFFFFFFFFu) {
+                        const int64_t ci = id >> 6;
+                        const uint32_t u = (id >> 3) & 7u, ln = (id & 7u) * 8u + ((uint32_t)lane & 7u);
+                        const int64_t j = ci * CH + (int64_t)u * kWave + ln;
+                        if (ci < nfull || j < nunits) c[r] = load16(v2 + i0 + j);
+                        if (ci >= nfull && ci == nch - 1 && u == (uint32_t)kUnroll - 1 && ln == (uint32_t)kWave - 1)
+                            c[r] = make_double2(hv, tv);  // the head / tail slots ride the last chunk
+                    }
+                }
+                __syncthreads();  // the queue entries are read: the caller may shift it
+                P.chunk(c);
+            };
+            uint32_t qn = 0;  // queued lines (uniform)
+#pragma unroll 1
+            for (int64_t cb = 0; cb < nch; cb += 8) {
+                uint32_t lk[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) lk[c] = cb + c < nch ? L[(size_t)(cb + c) * 64u + lane] : 0u;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint64_t m = ballot(cb + c < nch && lk[c] >= t32);
+                    if (!m) continue;
+                    if ((m >> lane) & 1ull) q[qn + lane_prefix(m)] = (uint32_t)((cb + c) * 64 + lane);
+                    qn += popc64(m);
+                    nread += popc64(m);
+                    __syncthreads();
+                    if (qn >= 64u) {
+                        process(64u);
+                        const uint32_t rest = qn - 64u;  // < 64
+                        const uint32_t v = (uint32_t)lane < rest ? q[64 + lane] : 0u;
+                        __syncthreads();
+                        if ((uint32_t)lane < rest) q[lane] = v;
+                        __syncthreads();
+                        qn = rest;
+                    }
+                }
+            }
+            if (qn) process(qn);
+            dense = P.ts.tl < tail;  // the estimate missed: stream whole, every present key a candidate
+            if (dense) P.ts = KllTail{0u, 0u, 0.0};
+        }
+        if (dense) {
+            const int64_t npad = KRR_KLL_TAIL_STREAM == 3 ? (nch + 2) / 3 * 3 : (nch + 1) & ~(int64_t)1;
+            kll_stream<KllTailProc, KRR_KLL_TAIL_STREAM>(A.vals, beg, end, npad, P, lane);
+            nread += (uint32_t)nch * 64u;
+        }
+        const uint32_t tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
+        if (lane == 0) {
+            row[6] = tl_out;
+            if (LA.lines_read) LA.lines_read[s] = nread;
+        }
         __syncthreads();
     }
 }

@@ -53,9 +53,12 @@ LENS = [0, 1, 2, 3, 300, 511, 512, 513, 1023, 1024, 1025, 1026, 2047, 2048, 5000
         43_200]
 
 
-# how the build finds the tail (include/krr_amd.h): the default second pass over the slice, the
-# one-pass running buffer, and the second pass with no margin (its fallback stream taken often)
-TAIL_MODES = {"pass": {}, "one_pass": {"one_pass_tail": True}, "no_margin": {"tail_flags": 2}}
+# how the build finds the tail (include/krr_amd.h): the default second pass reading only the
+# lines whose maximum can hold a tail key (krr_kll_build_lines / krr_kll_tail_lines), the second
+# pass over the whole slice, the one-pass running buffer, and the sparse pass with no margin
+# (its fallback stream taken often)
+TAIL_MODES = {"pass": {}, "dense": {"sparse_tail": False}, "one_pass": {"one_pass_tail": True},
+              "no_margin": {"tail_flags": 2}}
 
 
 def _cfg(budget=512, tail=0, mode="pass"):
@@ -387,6 +390,48 @@ def test_one_row_query_needs_no_fold_lds(ctx, budget, tail):
             v, n, f = R.query(r[s:s + 1], prm.mode, prm.p_num, prm.p_den, prm.q, seed=SEED, series=s, epoch=0)
             got = out["value"].cpu().numpy()[s]
             assert int(out["count"][s]) == n and (got == v or (np.isnan(got) and np.isnan(v))), (mode, s)
+
+
+@pytest.mark.parametrize("shape", ["gamma", "ascending", "descending", "quantised", "one_spike"])
+def test_sparse_tail_rows_equal_dense_at_config5_length(ctx, shape):
+    """The sparse tail pass (line maxima from the body build) against the dense one at 30d@15s
+    length, on shapes that put the tail keys everywhere (gamma), in the last lines (ascending),
+    the first (descending), in huge tie groups (quantised) or in one line (one_spike); odd
+    segment starts so lines straddle cache lines; rows bit-identical, and to the restatement
+    on a few series."""
+    import torch
+
+    from krr_amd.core import sketch
+
+    rng = np.random.default_rng(31)
+    L, S = 172_800, 24
+    lens = np.full(S, L)
+    lens[1::3] = L - 1  # odd starts after these
+    offs = np.concatenate([[3], 3 + np.cumsum(lens)]).astype(np.int64)
+    x = np.full(int(offs[-1]), np.nan)
+    for s in range(S):
+        a, b = int(offs[s]), int(offs[s + 1])
+        v = rng.gamma(2.0, 0.05, b - a)
+        if shape == "ascending":
+            v.sort()
+        elif shape == "descending":
+            v[::-1].sort()
+        elif shape == "quantised":
+            v = np.round(v, 2)
+        elif shape == "one_spike":
+            v = np.round(v, 1) * 0 + 0.1
+            v[rng.integers(0, b - a, 3)] = 7.0
+        x[a:b] = v
+    ser = ctx.series(_dev(x), _dev(offs, np.int64), 0, False)
+    for tail in (1792, 64):
+        sp = sketch.kll_build(ctx, ser, sketch.KllConfig(budget=512, tail=tail, seed=SEED))
+        de = sketch.kll_build(ctx, ser, sketch.KllConfig(budget=512, tail=tail, seed=SEED, sparse_tail=False))
+        torch.cuda.synchronize()
+        assert torch.equal(sp, de), (shape, tail)
+    got = sp.cpu().numpy().view(np.uint64)
+    for s in (0, 1, S - 1):
+        want = R.build_row(x, int(offs[s]), int(offs[s + 1]), budget=512, tail=64, seed=SEED, series=s)
+        assert np.array_equal(got[s], want), s
 
 
 def test_combined_launch_equals_split_passes(ctx):
