@@ -1847,8 +1847,9 @@ struct KllTailArgs {
     uint32_t tcap;
     double two_ln;    // 2 ln(4 / delta)
     uint64_t* rows;
-    const uint32_t* lines;  // k_kll_tail_lines: the body build's line maxima
+    const uint32_t* lines;  // the sparse pass: the body build's line maxima
     int64_t line_stride;
+    const uint32_t* mask;   // optional: only series with mask[s] != 0 (the sparse pass's leftovers)
 };
 
 struct KllTailProc {
@@ -1884,6 +1885,7 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
     uint64_t* im = sh.tb;  // body keys at im[kKllHdr + i] (kll_body_select's layout), before the stream
     uint8_t* lvl = reinterpret_cast<uint8_t*>(im + kKllHdr + budget);
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        if (A.mask && !A.mask[s]) continue;
         uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         double tau = 0.0;
@@ -1915,60 +1917,102 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
 namespace krr {
 
 // ---------------------------------------------------------------------------------------------
-// The sparse tail pass (round 5): candidates are the keys > tau, and a line (16 slots, 128 B)
+// The sparse tail pass (round 5).  Candidates are the keys > tau, and a line (16 slots, 128 B)
 // whose maximum from the body build (k_kll_build<false, true>: kll_line_key per line) is below
-// tau holds none — so only the lines that can hold a candidate are read.  Their ids queue in
-// LDS (64 per virtual chunk: row r of the virtual chunk = 8 queued lines, 8 lanes each) and
-// each virtual chunk goes through the same candidate filter as a streamed chunk.  The tail is a
-// set (the top min(n, tail) present keys, exported sorted), so the order lines arrive in does
-// not change it: the rows equal k_kll_tail's bit for bit.  If the threshold missed (fewer than
-// `tail` candidates) the slice is streamed whole with every present key a candidate, as there.
-// Reads: the line maxima (1/32 of the slice) + the flagged lines (~20% at p99 of 30d@15s).
-struct KllLineTailArgs {
+// tau holds none — so only the lines that can hold a candidate are read.  Three light launches
+// instead of one heavy one (the candidate filter's refresh / sort code held k_kll_tail at two
+// waves per SIMD, too few to hide the latency of sparse reads):
+//   k_kll_tail_tau     per series, tau from the row's own body (kll_tail_tau) at the margin and
+//                      at KRR_KLL_TAIL_RETRY times it;
+//   k_kll_tail_gather  per series, the flagged lines queued in LDS and read 64 at a time (row r
+//                      of a virtual chunk = 8 queued lines, 8 lanes each), every key > tau
+//                      appended to the series' candidate list in HBM (count kept past the
+//                      list's capacity); a miss (fewer than min(n, tail) keys > tau) retries at
+//                      the wider margin;
+//   k_kll_tail_finish  per series, the list into LDS and the tail exported from it exactly as the
+//                      filter's buffer is (kll_tail_export: refresh if long, sort, top
+//                      min(n, tail)); a list past its capacity or still short is left to
+//                      k_kll_tail (mask[s] = 1: the whole slice, the filter).
+// The tail is a set (the top min(n, tail) present keys, exported sorted): the order lines
+// arrive in does not change it, so rows equal k_kll_tail's bit for bit.
+#ifndef KRR_KLL_TAIL_RETRY
+#define KRR_KLL_TAIL_RETRY 4.0  // the gather's second attempt: this many margins
+#endif
+
+struct KllSparseArgs {
     KllTailArgs T;
-    uint32_t queue_off;     // byte offset of the 128-entry line queue in LDS
-    uint32_t* lines_read;   // optional: per series, the lines this pass read (its bytes / 128)
+    double* tau;           // [S][2]: tau at the margin and at the retry margin; NaN: none (every key)
+    uint64_t* cand;        // [S][cap] candidate keys (bits, -0 folded)
+    uint32_t* count;       // [S]: keys > tau found (may exceed cap); 0xFFFFFFFF: no usable threshold
+    uint32_t cap;
+    uint32_t* mask;        // [S]: 1 = left to k_kll_tail (written by finish)
+    uint32_t* lines_read;  // optional [S]
 };
 
-__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_lines(KllLineTailArgs LA) {
+__global__ __launch_bounds__(64) void k_kll_tail_tau(KllSparseArgs X) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const KllTailArgs& A = LA.T;
+    const KllTailArgs& A = X.T;
     const int lane = threadIdx.x;
     const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
     const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
-    KllShared sh{};
-    sh.tb = reinterpret_cast<uint64_t*>(smem);
-    uint64_t* im = sh.tb;
+    uint64_t* im = reinterpret_cast<uint64_t*>(smem);
     uint8_t* lvl = reinterpret_cast<uint8_t*>(im + kKllHdr + budget);
-    uint32_t* q = reinterpret_cast<uint32_t*>(smem + LA.queue_off);
+    const double qnan = __builtin_nan("");
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        const uint64_t* row = A.rows + (size_t)s * RW;
+        double t0 = 0.0, t1 = 0.0;
+        const bool f0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &t0);
+        __syncthreads();
+        const bool f1 = f0 && kll_tail_tau(row, budget, tail, A.two_ln * (KRR_KLL_TAIL_RETRY * KRR_KLL_TAIL_RETRY), im,
+                                           lvl, lane, &t1);
+        if (lane == 0) {
+            X.tau[2 * s] = f0 ? t0 : qnan;
+            X.tau[2 * s + 1] = f1 ? t1 : qnan;
+        }
+        __syncthreads();
+    }
+}
+
+#ifndef KRR_KLL_GATHER_WAVES_PER_SIMD
+#define KRR_KLL_GATHER_WAVES_PER_SIMD 6
+#endif
+__global__ __launch_bounds__(64, KRR_KLL_GATHER_WAVES_PER_SIMD) void k_kll_tail_gather(KllSparseArgs X) {
+    __shared__ uint32_t q[128];
+    const KllTailArgs& A = X.T;
+    const int lane = threadIdx.x;
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
     const double2* __restrict__ v2 = reinterpret_cast<const double2*>(A.vals);
     const double qnan = __builtin_nan("");
     constexpr int64_t CH = (int64_t)kUnroll * kWave;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
-        double tau = 0.0;
-        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau);
         const int64_t nch = kll_nchunks(beg, end);
-        KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
-        bool dense = !full0;
-        uint32_t nread = 0;  // lines read (uniform)
-        if (full0 && nch > 0) {
-            // kll_stream's layout of this slice
-            int64_t a0 = (beg + 1) & ~(int64_t)1;
-            if (a0 > end) a0 = end;
-            int64_t a1 = end & ~(int64_t)1;
-            if (a1 < a0) a1 = a0;
-            const int64_t i0 = a0 >> 1, nunits = (a1 >> 1) - i0, nfull = nunits / CH;
-            const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
+        const uint64_t n = uni64(A.rows[(size_t)s * RW]);
+        const uint32_t need = n < tail ? (uint32_t)n : tail;
+        int64_t a0 = (beg + 1) & ~(int64_t)1;
+        if (a0 > end) a0 = end;
+        int64_t a1 = end & ~(int64_t)1;
+        if (a1 < a0) a1 = a0;
+        const int64_t i0 = a0 >> 1, nunits = (a1 >> 1) - i0, nfull = nunits / CH;
+        const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
+        const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
+        uint64_t* C = X.cand + (size_t)s * X.cap;
+        uint32_t cnt = 0, nread = 0;
+        bool usable = false;
+#pragma unroll 1
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            const double tau = X.tau[2 * s + attempt];
+            if (tau != tau) break;  // no usable threshold: left to k_kll_tail
+            usable = true;
+            cnt = 0;
             const uint32_t t32 = (uint32_t)(okey(dbits(tau)) >> 32);
-            const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
-            auto process = [&](uint32_t cnt) __attribute__((always_inline)) {
+            auto take = [&](uint32_t nq) __attribute__((always_inline)) {
                 double2 c[kUnroll];
 #pragma unroll
                 for (int r = 0; r < kUnroll; ++r) {
                     const uint32_t slot = (uint32_t)r * 8u + ((uint32_t)lane >> 3);
-                    const uint32_t id = slot < cnt ? q[slot] : 0xFFFFFFFFu;
+                    const uint32_t id = slot < nq ? q[slot] : 0xFFFFFFFFu;
                     c[r] = make_double2(qnan, qnan);
                     if (id != 0xFFFFFFFFu) {
                         const int64_t ci = id >> 6;
@@ -1980,7 +2024,15 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     }
                 }
                 __syncthreads();  // the queue entries are read: the caller may shift it
-                P.chunk(c);
+#pragma unroll
+                for (int r = 0; r < kUnroll; ++r) {
+                    const bool ka = c[r].x > tau, kb = c[r].y > tau;  // false for NaN (absent)
+                    const uint64_t ma = ballot(ka), mb = ballot(kb);
+                    if (ka && cnt + lane_prefix(ma) < X.cap) C[cnt + lane_prefix(ma)] = dbits(c[r].x + 0.0);
+                    cnt += popc64(ma);
+                    if (kb && cnt + lane_prefix(mb) < X.cap) C[cnt + lane_prefix(mb)] = dbits(c[r].y + 0.0);
+                    cnt += popc64(mb);
+                }
             };
             uint32_t qn = 0;  // queued lines (uniform)
 #pragma unroll 1
@@ -1997,7 +2049,7 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     nread += popc64(m);
                     __syncthreads();
                     if (qn >= 64u) {
-                        process(64u);
+                        take(64u);
                         const uint32_t rest = qn - 64u;  // < 64
                         const uint32_t v = (uint32_t)lane < rest ? q[64 + lane] : 0u;
                         __syncthreads();
@@ -2007,20 +2059,39 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     }
                 }
             }
-            if (qn) process(qn);
-            dense = P.ts.tl < tail;  // the estimate missed: stream whole, every present key a candidate
-            if (dense) P.ts = KllTail{0u, 0u, 0.0};
+            if (qn) take(qn);
+            __syncthreads();
+            if (cnt >= need) break;  // else: missed; once more at the wider margin
         }
-        if (dense) {
-            const int64_t npad = KRR_KLL_TAIL_STREAM == 3 ? (nch + 2) / 3 * 3 : (nch + 1) & ~(int64_t)1;
-            kll_stream<KllTailProc, KRR_KLL_TAIL_STREAM>(A.vals, beg, end, npad, P, lane);
-            nread += (uint32_t)nch * 64u;
-        }
-        const uint32_t tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
         if (lane == 0) {
-            row[6] = tl_out;
-            if (LA.lines_read) LA.lines_read[s] = nread;
+            X.count[s] = usable ? cnt : 0xFFFFFFFFu;
+            if (X.lines_read) X.lines_read[s] = nread;
         }
+    }
+}
+
+__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_finish(KllSparseArgs X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const KllTailArgs& A = X.T;
+    const int lane = threadIdx.x;
+    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
+    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
+    KllShared sh{};
+    sh.tb = reinterpret_cast<uint64_t*>(smem);
+    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        uint64_t* row = A.rows + (size_t)s * RW;
+        const uint32_t cnt = X.count[s];
+        const uint64_t n = uni64(row[0]);
+        const uint32_t need = n < tail ? (uint32_t)n : tail;
+        const bool ok = cnt != 0xFFFFFFFFu && cnt <= X.cap && cnt >= need;
+        if (lane == 0) X.mask[s] = ok ? 0u : 1u;
+        if (!ok) continue;  // uniform
+        const uint64_t* C = X.cand + (size_t)s * X.cap;
+        for (uint32_t i = lane; i < cnt; i += kWave) sh.tb[i] = C[i];
+        __syncthreads();
+        const double tau = X.tau[2 * s] == X.tau[2 * s] ? X.tau[2 * s] : 0.0;
+        const uint32_t tl_out = kll_tail_export(sh, KllTail{cnt, 1u, tau}, tail, row + kKllHdr + budget, lane);
+        if (lane == 0) row[6] = tl_out;
         __syncthreads();
     }
 }
