@@ -448,16 +448,15 @@ struct KllBuildArgs {
 // ---- line maxima: where the exact tail's keys can be (the sparse tail pass) ----
 // A "line" is 16 slots = 128 contiguous bytes = the double2 of 8 consecutive lanes in one row
 // u of a chunk.  Its key: the top 32 bits of the ordered key (okey) of the line's largest
-// present sample, rounded UP (0 when every slot is absent), so a line holding a sample x has
-// key >= okey(x) >> 32 — a line whose key is below okey(tau) >> 32 holds no sample > tau.
-// (-0 and +0 get the same key: okey(-0) = 2^63 - 1 rounds up to okey(+0) >> 32.)
+// sample, plus one — an upper bound of okey(x) >> 32 for every x in the line, in 5 VALU (no
+// rounding test, no NaN test: a NaN slot only makes its line's key large, so the tail pass
+// reads that line and finds no candidate in the NaN).  A line whose key is below
+// okey(tau) >> 32 holds no sample > tau.  (+1 wraps to 0 only for NaN bit patterns, and a
+// wrapped lane never lowers its line's maximum below a real sample's key.)
 __device__ __forceinline__ uint32_t kll_line_key(double hi) {
-    const uint64_t b = dbits(hi);
-    const uint32_t h = (uint32_t)(b >> 32), l = (uint32_t)b;
+    const uint32_t h = (uint32_t)(dbits(hi) >> 32);
     const uint32_t m = (uint32_t)((int32_t)h >> 31);
-    const uint32_t oh = h ^ (m | 0x80000000u), ol = l ^ m;
-    const uint32_t k = oh + (ol != 0u ? 1u : 0u);
-    return hi == hi ? k : 0u;
+    return (h ^ (m | 0x80000000u)) + 1u;
 }
 
 // max over each group of 8 consecutive lanes, in every lane of the group (DPP quad_perm
