@@ -3329,8 +3329,6 @@ struct krr_ctx {
     hipStream_t fail_stream;
     bool fail_ev_valid;
     char* d_label;                // krr_json_parse_segments: the routing label key (device copy)
-    char* d_kll_scratch;          // krr_kll_tail_lines: thresholds, candidate lists, masks (grown on demand)
-    size_t kll_scratch_bytes;
     char err[512];
 };
 
@@ -3508,8 +3506,6 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->fail_stream = nullptr;
     c->fail_ev_valid = false;
     c->d_label = nullptr;
-    c->d_kll_scratch = nullptr;
-    c->kll_scratch_bytes = 0;
     if (hipEventCreateWithFlags(&c->fail_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return KRR_E_HIP;
@@ -3536,8 +3532,7 @@ int krr_create(int device, krr_ctx** out_ctx) {
     for (const void* f : {(const void*)k_hselect_list, (const void*)k_window_export<true>,
                           (const void*)k_window_export<false>, (const void*)k_window_merge,
                           (const void*)k_kll_build<false>, (const void*)k_kll_build<true>, (const void*)k_kll_tail,
-                          (const void*)k_kll_build<false, true>, (const void*)k_kll_tail_tau,
-                          (const void*)k_kll_tail_finish,
+                          (const void*)k_kll_build<false, true>, (const void*)k_kll_tail_lines,
                           (const void*)k_kll_merge,
                           (const void*)k_kll_query})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->max_lds);
@@ -3552,7 +3547,6 @@ int krr_destroy(krr_ctx* ctx) {
     if (ctx->d_fail_count) (void)hipFree(ctx->d_fail_count);
     if (ctx->d_fail_list) (void)hipFree(ctx->d_fail_list);
     if (ctx->d_label) (void)hipFree(ctx->d_label);
-    if (ctx->d_kll_scratch) (void)hipFree(ctx->d_kll_scratch);
     if (ctx->fail_ev) (void)hipEventDestroy(ctx->fail_ev);
     delete ctx;
     return KRR_OK;
@@ -4021,14 +4015,12 @@ int krr_kll_tail_lines(krr_ctx* ctx, const krr_series* series, const krr_kll_par
     if (rc) return rc;
     if (krr_kll_row_words(kp) < 0)
         return set_err(ctx, KRR_E_INVALID, "kll: budget in [256, 4096] (a multiple of 64), tail in [0, 4096]%s", "");
-    const int64_t S = series->n_segments;
-    if (S == 0 || kp->tail == 0) return KRR_OK;
+    if (series->n_segments == 0 || kp->tail == 0) return KRR_OK;
     if (!rows || !lines) return set_err(ctx, KRR_E_INVALID, "null rows / lines%s", "");
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
-    hipStream_t st = (hipStream_t)stream;
     int64_t maxlen = 0;
-    rc = resolve_maxlen(ctx, series, st, &maxlen);
+    rc = resolve_maxlen(ctx, series, (hipStream_t)stream, &maxlen);
     if (rc) return rc;
     if (line_stride < krr_kll_line_words(maxlen))
         return set_err(ctx, KRR_E_INVALID, "line_stride below krr_kll_line_words(max_segment_len) = %s%lld", "",
@@ -4036,44 +4028,15 @@ int krr_kll_tail_lines(krr_ctx* ctx, const krr_series* series, const krr_kll_par
     uint32_t tcap_t;
     size_t lds_t;
     kll_tail_lds(kp, &tcap_t, &lds_t);
-    // a series' candidate list: room for twice the tail (+512) keys; longer lists (ties at the
-    // threshold) and misses go to k_kll_tail
-    uint32_t cap = (uint32_t)((2 * kp->tail + 512 + 63) & ~63);
-    if (cap > 8192) cap = 8192;
-    const size_t lds_fin = (size_t)cap * 8 > lds_t ? (size_t)cap * 8 : lds_t;
-    const size_t lds_tau = ((size_t)kKllHdr + kp->budget) * 8 + (size_t)kp->budget;
-    if (lds_fin > ctx->max_lds || lds_t > ctx->max_lds)
-        return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds_fin);
-    // scratch (the ctx's, grown on demand): tau[S][2], count[S], mask[S], cand[S][cap]
-    const size_t need = (size_t)S * (16 + 4 + 4) + (size_t)S * cap * 8 + 256;
-    if (ctx->kll_scratch_bytes < need) {
-        if (ctx->d_kll_scratch) {
-            KRR_HIP(ctx, hipStreamSynchronize(st));
-            (void)hipFree(ctx->d_kll_scratch);
-            ctx->d_kll_scratch = nullptr;
-            ctx->kll_scratch_bytes = 0;
-        }
-        KRR_HIP(ctx, hipMalloc(&ctx->d_kll_scratch, need));
-        ctx->kll_scratch_bytes = need;
-    }
-    char* base = ctx->d_kll_scratch;
-    double* tau = reinterpret_cast<double*>(base);
-    uint64_t* cand = reinterpret_cast<uint64_t*>(base + (size_t)S * 16);
-    uint32_t* count = reinterpret_cast<uint32_t*>(base + (size_t)S * 16 + (size_t)S * cap * 8);
-    uint32_t* mask = count + S;
+    const uint32_t qoff = (uint32_t)((lds_t + 15) & ~(size_t)15);
+    const size_t lds = (size_t)qoff + 128 * sizeof(uint32_t);
+    if (lds > ctx->max_lds)
+        return set_err(ctx, KRR_E_CAPACITY, "kll tail pass needs %s%lld B of LDS", "", (long long)lds);
     const double two_ln = (kp->reserved & KRR_KLL_TAIL_NO_MARGIN) ? 0.0 : 2.0 * log(4.0 / 1e-3);
-    KllTailArgs T{series->values, series->offsets, S, kp->budget, kp->tail, tcap_t, two_ln, rows, lines, line_stride,
-                  nullptr};
-    KllSparseArgs X{T, tau, cand, count, cap, mask, lines_read};
-    const dim3 grid(grid_for(S)), blk(64);
-    hipLaunchKernelGGL(k_kll_tail_tau, grid, blk, lds_tau, st, X);
-    KRR_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_kll_tail_gather, grid, blk, 0, st, X);
-    KRR_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_kll_tail_finish, grid, blk, lds_fin, st, X);
-    KRR_HIP(ctx, hipGetLastError());
-    T.mask = mask;  // the leftovers: the whole slice through the candidate filter
-    hipLaunchKernelGGL(k_kll_tail, grid, blk, lds_t, st, T);
+    KllLineTailArgs LA{{series->values, series->offsets, series->n_segments, kp->budget, kp->tail, tcap_t, two_ln, rows,
+                        lines, line_stride, nullptr},
+                       qoff, lines_read};
+    hipLaunchKernelGGL(k_kll_tail_lines, dim3(grid_for(series->n_segments)), dim3(64), lds, (hipStream_t)stream, LA);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
 }

@@ -1794,7 +1794,7 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
 // are the top min(n, tail) present keys, exactly what the one-pass build writes: rows are the
 // same bit for bit (oracle/kll_ref.py does not depend on how the tail is found).
 #ifndef KRR_KLL_TAIL_MARGIN
-#define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
+#define KRR_KLL_TAIL_MARGIN 0.125  // the threshold's margin, in units of the rank bound at delta = 1e-3 (r05: 0.5 -> 0.125 with the sparse pass's retry)
 #endif
 // The tail pass's threshold from the row's own body: the body key t0 at estimated rank
 // q = n - tail - 1 - M (M = KRR_KLL_TAIL_MARGIN x the rank bound at delta = 1e-3); candidates are
@@ -1916,102 +1916,74 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail(Kl
 namespace krr {
 
 // ---------------------------------------------------------------------------------------------
-// The sparse tail pass (round 5).  Candidates are the keys > tau, and a line (16 slots, 128 B)
+// The sparse tail pass (round 5): candidates are the keys > tau, and a line (16 slots, 128 B)
 // whose maximum from the body build (k_kll_build<false, true>: kll_line_key per line) is below
-// tau holds none — so only the lines that can hold a candidate are read.  Three light launches
-// instead of one heavy one (the candidate filter's refresh / sort code held k_kll_tail at two
-// waves per SIMD, too few to hide the latency of sparse reads):
-//   k_kll_tail_tau     per series, tau from the row's own body (kll_tail_tau) at the margin and
-//                      at KRR_KLL_TAIL_RETRY times it;
-//   k_kll_tail_gather  per series, the flagged lines queued in LDS and read 64 at a time (row r
-//                      of a virtual chunk = 8 queued lines, 8 lanes each), every key > tau
-//                      appended to the series' candidate list in HBM (count kept past the
-//                      list's capacity); a miss (fewer than min(n, tail) keys > tau) retries at
-//                      the wider margin;
-//   k_kll_tail_finish  per series, the list into LDS and the tail exported from it exactly as the
-//                      filter's buffer is (kll_tail_export: refresh if long, sort, top
-//                      min(n, tail)); a list past its capacity or still short is left to
-//                      k_kll_tail (mask[s] = 1: the whole slice, the filter).
-// The tail is a set (the top min(n, tail) present keys, exported sorted): the order lines
-// arrive in does not change it, so rows equal k_kll_tail's bit for bit.
+// tau holds none — so only the lines that can hold a candidate are read.  Their ids queue in
+// LDS (64 per virtual chunk: row r of the virtual chunk = 8 queued lines, 8 lanes each) and
+// each virtual chunk goes through the same candidate filter as a streamed chunk.  The tail is a
+// set (the top min(n, tail) present keys, exported sorted), so the order lines arrive in does
+// not change it: the rows equal k_kll_tail's bit for bit.  If the threshold missed (fewer than
+// `tail` candidates) the slice is streamed whole with every present key a candidate, as there.
+// Reads: the line maxima (1/32 of the slice) + the flagged lines (~20% at p99 of 30d@15s).
 #ifndef KRR_KLL_TAIL_RETRY
-#define KRR_KLL_TAIL_RETRY 4.0  // the gather's second attempt: this many margins
+#define KRR_KLL_TAIL_RETRY 4.0  // a sparse attempt that missed is retried at this many margins
 #endif
-
-struct KllSparseArgs {
+struct KllLineTailArgs {
     KllTailArgs T;
-    double* tau;           // [S][2]: tau at the margin and at the retry margin; NaN: none (every key)
-    uint64_t* cand;        // [S][cap] candidate keys (bits, -0 folded)
-    uint32_t* count;       // [S]: keys > tau found (may exceed cap); 0xFFFFFFFF: no usable threshold
-    uint32_t cap;
-    uint32_t* mask;        // [S]: 1 = left to k_kll_tail (written by finish)
-    uint32_t* lines_read;  // optional [S]
+    uint32_t queue_off;     // byte offset of the 128-entry line queue in LDS
+    uint32_t* lines_read;   // optional: per series, the lines this pass read (its bytes / 128)
 };
 
-__global__ __launch_bounds__(64) void k_kll_tail_tau(KllSparseArgs X) {
+__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_lines(KllLineTailArgs LA) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const KllTailArgs& A = X.T;
+    const KllTailArgs& A = LA.T;
     const int lane = threadIdx.x;
     const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
     const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
-    uint64_t* im = reinterpret_cast<uint64_t*>(smem);
+    KllShared sh{};
+    sh.tb = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* im = sh.tb;
     uint8_t* lvl = reinterpret_cast<uint8_t*>(im + kKllHdr + budget);
-    const double qnan = __builtin_nan("");
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        const uint64_t* row = A.rows + (size_t)s * RW;
-        double t0 = 0.0, t1 = 0.0;
-        const bool f0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &t0);
-        __syncthreads();
-        const bool f1 = f0 && kll_tail_tau(row, budget, tail, A.two_ln * (KRR_KLL_TAIL_RETRY * KRR_KLL_TAIL_RETRY), im,
-                                           lvl, lane, &t1);
-        if (lane == 0) {
-            X.tau[2 * s] = f0 ? t0 : qnan;
-            X.tau[2 * s + 1] = f1 ? t1 : qnan;
-        }
-        __syncthreads();
-    }
-}
-
-#ifndef KRR_KLL_GATHER_WAVES_PER_SIMD
-#define KRR_KLL_GATHER_WAVES_PER_SIMD 6
-#endif
-__global__ __launch_bounds__(64, KRR_KLL_GATHER_WAVES_PER_SIMD) void k_kll_tail_gather(KllSparseArgs X) {
-    __shared__ uint32_t q[128];
-    const KllTailArgs& A = X.T;
-    const int lane = threadIdx.x;
-    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
-    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
+    uint32_t* q = reinterpret_cast<uint32_t*>(smem + LA.queue_off);
     const double2* __restrict__ v2 = reinterpret_cast<const double2*>(A.vals);
     const double qnan = __builtin_nan("");
     constexpr int64_t CH = (int64_t)kUnroll * kWave;
     for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
+        uint64_t* row = A.rows + (size_t)s * RW;
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t nch = kll_nchunks(beg, end);
-        const uint64_t n = uni64(A.rows[(size_t)s * RW]);
-        const uint32_t need = n < tail ? (uint32_t)n : tail;
-        int64_t a0 = (beg + 1) & ~(int64_t)1;
-        if (a0 > end) a0 = end;
-        int64_t a1 = end & ~(int64_t)1;
-        if (a1 < a0) a1 = a0;
-        const int64_t i0 = a0 >> 1, nunits = (a1 >> 1) - i0, nfull = nunits / CH;
-        const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
-        const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
-        uint64_t* C = X.cand + (size_t)s * X.cap;
-        uint32_t cnt = 0, nread = 0;
-        bool usable = false;
+        double tau = 0.0;
+        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau);
+        KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
+        bool dense = !full0;
+        uint32_t nread = 0;  // lines read (uniform)
+        // sparse attempts: the threshold at the margin, then (a miss: fewer than `tail` keys above
+        // it) at KRR_KLL_TAIL_RETRY margins; then the whole slice, every present key a candidate
 #pragma unroll 1
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            const double tau = X.tau[2 * s + attempt];
-            if (tau != tau) break;  // no usable threshold: left to k_kll_tail
-            usable = true;
-            cnt = 0;
+        for (int attempt = 0; attempt < 2 && full0 && nch > 0; ++attempt) {
+            if (attempt == 1) {
+                __syncthreads();
+                full0 = kll_tail_tau(row, budget, tail, A.two_ln * (KRR_KLL_TAIL_RETRY * KRR_KLL_TAIL_RETRY), im, lvl,
+                                     lane, &tau);
+                __syncthreads();
+                P.ts = KllTail{0u, full0 ? 1u : 0u, tau};
+                if (!full0) break;
+            }
+            // kll_stream's layout of this slice
+            int64_t a0 = (beg + 1) & ~(int64_t)1;
+            if (a0 > end) a0 = end;
+            int64_t a1 = end & ~(int64_t)1;
+            if (a1 < a0) a1 = a0;
+            const int64_t i0 = a0 >> 1, nunits = (a1 >> 1) - i0, nfull = nunits / CH;
+            const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
             const uint32_t t32 = (uint32_t)(okey(dbits(tau)) >> 32);
-            auto take = [&](uint32_t nq) __attribute__((always_inline)) {
+            const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
+            auto process = [&](uint32_t cnt) __attribute__((always_inline)) {
                 double2 c[kUnroll];
 #pragma unroll
                 for (int r = 0; r < kUnroll; ++r) {
                     const uint32_t slot = (uint32_t)r * 8u + ((uint32_t)lane >> 3);
-                    const uint32_t id = slot < nq ? q[slot] : 0xFFFFFFFFu;
+                    const uint32_t id = slot < cnt ? q[slot] : 0xFFFFFFFFu;
                     c[r] = make_double2(qnan, qnan);
                     if (id != 0xFFFFFFFFu) {
                         const int64_t ci = id >> 6;
@@ -2023,22 +1995,20 @@ __global__ __launch_bounds__(64, KRR_KLL_GATHER_WAVES_PER_SIMD) void k_kll_tail_
                     }
                 }
                 __syncthreads();  // the queue entries are read: the caller may shift it
-#pragma unroll
-                for (int r = 0; r < kUnroll; ++r) {
-                    const bool ka = c[r].x > tau, kb = c[r].y > tau;  // false for NaN (absent)
-                    const uint64_t ma = ballot(ka), mb = ballot(kb);
-                    if (ka && cnt + lane_prefix(ma) < X.cap) C[cnt + lane_prefix(ma)] = dbits(c[r].x + 0.0);
-                    cnt += popc64(ma);
-                    if (kb && cnt + lane_prefix(mb) < X.cap) C[cnt + lane_prefix(mb)] = dbits(c[r].y + 0.0);
-                    cnt += popc64(mb);
-                }
+                P.chunk(c);
             };
             uint32_t qn = 0;  // queued lines (uniform)
+            // the line maxima of 8 chunks at a time, the next 8 in flight while these are queued
+            uint32_t nk[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) nk[c] = c < nch ? L[(size_t)c * 64u + lane] : 0u;
 #pragma unroll 1
             for (int64_t cb = 0; cb < nch; cb += 8) {
                 uint32_t lk[8];
 #pragma unroll
-                for (int c = 0; c < 8; ++c) lk[c] = cb + c < nch ? L[(size_t)(cb + c) * 64u + lane] : 0u;
+                for (int c = 0; c < 8; ++c) lk[c] = nk[c];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) nk[c] = cb + 8 + c < nch ? L[(size_t)(cb + 8 + c) * 64u + lane] : 0u;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
                     const uint64_t m = ballot(cb + c < nch && lk[c] >= t32);
@@ -2048,7 +2018,7 @@ __global__ __launch_bounds__(64, KRR_KLL_GATHER_WAVES_PER_SIMD) void k_kll_tail_
                     nread += popc64(m);
                     __syncthreads();
                     if (qn >= 64u) {
-                        take(64u);
+                        process(64u);
                         const uint32_t rest = qn - 64u;  // < 64
                         const uint32_t v = (uint32_t)lane < rest ? q[64 + lane] : 0u;
                         __syncthreads();
@@ -2058,39 +2028,21 @@ __global__ __launch_bounds__(64, KRR_KLL_GATHER_WAVES_PER_SIMD) void k_kll_tail_
                     }
                 }
             }
-            if (qn) take(qn);
-            __syncthreads();
-            if (cnt >= need) break;  // else: missed; once more at the wider margin
+            if (qn) process(qn);
+            dense = P.ts.tl < tail;  // a miss
+            if (!dense) break;
         }
+        if (dense) P.ts = KllTail{0u, 0u, 0.0};  // the whole slice, every present key a candidate
+        if (dense) {
+            const int64_t npad = KRR_KLL_TAIL_STREAM == 3 ? (nch + 2) / 3 * 3 : (nch + 1) & ~(int64_t)1;
+            kll_stream<KllTailProc, KRR_KLL_TAIL_STREAM>(A.vals, beg, end, npad, P, lane);
+            nread += (uint32_t)nch * 64u;
+        }
+        const uint32_t tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
         if (lane == 0) {
-            X.count[s] = usable ? cnt : 0xFFFFFFFFu;
-            if (X.lines_read) X.lines_read[s] = nread;
+            row[6] = tl_out;
+            if (LA.lines_read) LA.lines_read[s] = nread;
         }
-    }
-}
-
-__global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_finish(KllSparseArgs X) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const KllTailArgs& A = X.T;
-    const int lane = threadIdx.x;
-    const uint32_t budget = (uint32_t)A.budget, tail = (uint32_t)A.tail;
-    const uint32_t RW = (uint32_t)kKllHdr + budget + tail;
-    KllShared sh{};
-    sh.tb = reinterpret_cast<uint64_t*>(smem);
-    for (int64_t s = blockIdx.x; s < A.S; s += gridDim.x) {
-        uint64_t* row = A.rows + (size_t)s * RW;
-        const uint32_t cnt = X.count[s];
-        const uint64_t n = uni64(row[0]);
-        const uint32_t need = n < tail ? (uint32_t)n : tail;
-        const bool ok = cnt != 0xFFFFFFFFu && cnt <= X.cap && cnt >= need;
-        if (lane == 0) X.mask[s] = ok ? 0u : 1u;
-        if (!ok) continue;  // uniform
-        const uint64_t* C = X.cand + (size_t)s * X.cap;
-        for (uint32_t i = lane; i < cnt; i += kWave) sh.tb[i] = C[i];
-        __syncthreads();
-        const double tau = X.tau[2 * s] == X.tau[2 * s] ? X.tau[2 * s] : 0.0;
-        const uint32_t tl_out = kll_tail_export(sh, KllTail{cnt, 1u, tau}, tail, row + kKllHdr + budget, lane);
-        if (lane == 0) row[6] = tl_out;
         __syncthreads();
     }
 }
