@@ -1794,16 +1794,19 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
 // are the top min(n, tail) present keys, exactly what the one-pass build writes: rows are the
 // same bit for bit (oracle/kll_ref.py does not depend on how the tail is found).
 #ifndef KRR_KLL_TAIL_MARGIN
-#define KRR_KLL_TAIL_MARGIN 0.125  // the threshold's margin, in units of the rank bound at delta = 1e-3 (r05: 0.5 -> 0.125 with the sparse pass's retry)
+#define KRR_KLL_TAIL_MARGIN 0.5  // the threshold's margin, in units of the rank bound at delta = 1e-3
+#endif
+#ifndef KRR_KLL_SPARSE_MARGIN
+#define KRR_KLL_SPARSE_MARGIN 0.125  // the sparse pass's first margin (a miss retries at KRR_KLL_TAIL_RETRY x)
 #endif
 // The tail pass's threshold from the row's own body: the body key t0 at estimated rank
 // q = n - tail - 1 - M (M = KRR_KLL_TAIL_MARGIN x the rank bound at delta = 1e-3); candidates are
 // the keys > *tau (the next double below t0).  false: no usable threshold (every present key is
 // a candidate).  im / lvl: LDS work space (the body keys and their levels).
 __device__ bool kll_tail_tau(const uint64_t* row, uint32_t budget, uint32_t tail, double two_ln, uint64_t* im,
-                             uint8_t* lvl, int lane, double* tau) {
+                             uint8_t* lvl, int lane, double* tau, double margin = KRR_KLL_TAIL_MARGIN) {
     const uint64_t n = uni64(row[0]);
-    const double M = ceil(KRR_KLL_TAIL_MARGIN * sqrt(two_ln * (double)uni64(row[4])));
+    const double M = ceil(margin * sqrt(two_ln * (double)uni64(row[4])));
     const double qd = (double)n - (double)tail - 1.0 - M;
     bool full0 = false;
     *tau = 0.0;
@@ -1953,7 +1956,7 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t nch = kll_nchunks(beg, end);
         double tau = 0.0;
-        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau);
+        bool full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau, KRR_KLL_SPARSE_MARGIN);
         KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
         bool dense = !full0;
         uint32_t nread = 0;  // lines read (uniform)
@@ -1963,8 +1966,8 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
         for (int attempt = 0; attempt < 2 && full0 && nch > 0; ++attempt) {
             if (attempt == 1) {
                 __syncthreads();
-                full0 = kll_tail_tau(row, budget, tail, A.two_ln * (KRR_KLL_TAIL_RETRY * KRR_KLL_TAIL_RETRY), im, lvl,
-                                     lane, &tau);
+                full0 = kll_tail_tau(row, budget, tail, A.two_ln, im, lvl, lane, &tau,
+                                     KRR_KLL_TAIL_RETRY * KRR_KLL_SPARSE_MARGIN);
                 __syncthreads();
                 P.ts = KllTail{0u, full0 ? 1u : 0u, tau};
                 if (!full0) break;
