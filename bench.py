@@ -1327,19 +1327,25 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
     result = collect_result(objects, allocs)
     t3 = time.perf_counter()
     total = t3 - t0
-    # equality with the per-object path on blocks from every shard
-    same, checked = True, 0
+    # equality with the per-object path: 64-object blocks at both ends of every shard plus a
+    # stride over the whole fleet (every pool entry of fleet_objects, so every severity bucket)
+    idx = set(range(0, n, max(1, n // 4096)))
     for a, b in shards:
         for lo in sorted({a, max(a, b - 64)}):
-            hi = min(lo + 64, b)
-            sub = RawResults(*(np.asarray(x)[lo:hi] for x in (raw.cpu_value, raw.cpu_count, raw.cpu_flags,
-                                                              raw.mem_value, raw.mem_count, raw.mem_flags)))
-            want = [to_allocations(format_result(r)) for r in SimpleStrategy(settings).results_from_raw(sub)]
-            for i, w in zip(range(lo, hi), want):
-                same &= allocs[i] == w and allocs[i].json() == w.json()
-                ref_scan = ResourceScan.calculate(objects[i], w)
-                same &= result.scans[i] == ref_scan and result.scans[i].severity == ref_scan.severity
-                checked += 1
+            idx.update(range(lo, min(lo + 64, b)))
+    idx = np.array(sorted(idx), dtype=np.int64)
+    sub = RawResults(*(np.asarray(x)[idx] for x in (raw.cpu_value, raw.cpu_count, raw.cpu_flags,
+                                                    raw.mem_value, raw.mem_count, raw.mem_flags)))
+    want = [to_allocations(format_result(r)) for r in SimpleStrategy(settings).results_from_raw(sub)]
+    same, checked, pair_sev = True, 0, {}
+    for i, w in zip(idx.tolist(), want):
+        same &= allocs[i] == w and allocs[i].json() == w.json()
+        ref_scan = ResourceScan.calculate(objects[i], w)
+        same &= result.scans[i] == ref_scan and result.scans[i].severity == ref_scan.severity
+        for sel in (ref_scan.recommended.requests, ref_scan.recommended.limits):
+            for r in sel.values():
+                pair_sev[r.severity.value] = pair_sev.get(r.severity.value, 0) + 1
+        checked += 1
     sev = {}
     for s in result.scans[:: max(1, n // 20000)]:
         sev[s.severity.value] = sev.get(s.severity.value, 0) + 1
@@ -1354,12 +1360,14 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
         "config4_right_size_equal_per_object_path": bool(same),
         "config4_right_size_checked_objects": checked,
         "config4_right_size_severities_sampled": sev,
+        "config4_right_size_checked_pair_severities": pair_sev,
         "config4_right_size_definition": (
             f"rank 0, all {n} containers' gathered records -> krr_round_simple ({threads} threads) -> one "
             f"ResourceAllocations per container -> Runner._collect_result's ResourceScan per container + Result "
             f"score, in bulk; one run after a warm-up on 1000; the {n} K8sObjectData are built beforehand "
-            f"({t_obj:.1f} s, untimed); checked equal to the per-object path on {checked} containers, 64-object "
-            f"blocks at both ends of every shard")}
+            f"({t_obj:.1f} s, untimed); checked equal to the per-object path on {checked} containers (64-object "
+            f"blocks at both ends of every shard and a stride over the fleet; per (resource, selector) "
+            f"severities of the checked ones in _checked_pair_severities)")}
 
 
 def parity_gathered(args, ctx, dev, world, params, host_rec, gaps, pod_len, seed, cfg=None, shards=None) -> dict:
@@ -1691,6 +1699,15 @@ def run_config5(args, world, rank, local, dev, coll_dev):
                             "hbm_passes_per_step": 1}
     if kll_sparse:
         result["kll_sparse_tail"] = kll_sparse
+    if method == "kll":
+        # what one slice of one series puts on the all-to-all (a rank sends (N-1)/N of its
+        # rows), beside the exact window path's row for the same slicing (krr_window_key_cap)
+        l8 = -(-T // 8)
+        result["exchange_bytes_per_series_slice"] = {
+            "kll_row": 8 * kcfg.row_words,
+            "window_row": 8 * (_native.HDR_WORDS + _native.window_key_cap(max(Lr, 1), T - Lr, params)),
+            "window_row_at_n8": 8 * (_native.HDR_WORDS + _native.window_key_cap(l8, T - l8, params)),
+            "n": world}
     if "k_kll_tail" in kernels_ms:
         # the KLL build in two passes: the body (k_kll_build, above) and the exact tail
         # (k_kll_tail, candidates above a threshold read from the row's body); both HBM streams
