@@ -921,6 +921,10 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     out["e2e_device_equals_host"] = e2e["device"][1] == e2e["host"][1]
     out["e2e_hybrid_equals_host"] = e2e["hybrid"][1] == e2e["host"][1]
     out["e2e_hybrid_split"] = runner.hybrid_last
+    from krr_amd.core.device_pack import default_packer as _dp
+
+    # the device side's last staging: JSON bytes vs bytes over PCIe (timestamps cut, krr_strip.h)
+    out["e2e_device_upload"] = _dp(dev.index or 0).last_upload
     # the device packer alone: staging copy -> H2D -> parse -> CSR in HBM, both resources
     from krr_amd.core.device_pack import default_packer
 

@@ -107,6 +107,25 @@ int krr_pack_parse_grouped(const char* const* bodies, const int64_t* body_lens, 
 int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
                     const int64_t* dst_offsets, char* dst, int32_t threads);
 
+/* The same staging with each sample timestamp cut to its first digit (krr_amd/csrc/krr_strip.h:
+ * `[1700000000.25,"0.3"]` -> `[1,"0.3"]`; the reference drops timestamps,
+ * robusta_krr/core/integrations/prometheus.py:152).  A body outside the strippable form
+ * (whitespace or a backslash in its values array, a timestamp other than
+ * (0|[1-9][0-9]*)(.[0-9]+)?, a CPU without AVX-512 VBMI2) is copied unchanged.  Bodies are cut
+ * into at most `max_runs` contiguous runs (by bytes); run r = bodies [run_first[r],
+ * run_first[r + 1]) is written back to back from dst[dst_offsets[run_first[r]] - dst_offsets[0]],
+ * inside the run's own unstripped extent.  new_lens[b] = bytes written for body b; *n_runs = the
+ * runs used (run_first holds n_runs + 1 entries, run_first[n_runs] == n_bodies).
+ * Neither the device parser nor the host packer reads a timestamp's value without
+ * want_timestamps, so a stripped body packs to the same CSR as the original. */
+int krr_pack_concat_strip(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                          const int64_t* dst_offsets, char* dst, int32_t threads, int32_t max_runs,
+                          int64_t* new_lens, int64_t* run_first, int32_t* n_runs);
+
+/* One body stripped as above into out (body_len bytes of room): the bytes written, or -1
+ * when it is not strippable.  (Tests and probes.) */
+int64_t krr_pack_strip_body(const char* body, int64_t body_len, char* out);
+
 /* Routing for the device packer's grouped bodies (include/krr_amd.h krr_json_find_series /
  * krr_json_parse_segments).  `bodies` is the staged host copy of the device buffer (same
  * offsets).  Per body: the envelope is walked up to data.result's first series, the

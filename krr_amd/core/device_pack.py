@@ -51,10 +51,16 @@ class DevicePacker:
     ones smaller, doubling from 16 MiB, so the copy engine starts early), each parsed as
     soon as it is in HBM."""
 
-    def __init__(self, ctx: _native.Context, chunk_bytes: int = 256 << 20, threads: int = 0):
+    def __init__(self, ctx: _native.Context, chunk_bytes: int = 256 << 20, threads: int = 0, strip: Optional[bool] = None):
+        import os
+
         import torch
 
         self.ctx = ctx
+        # per-pod bodies are staged with their sample timestamps cut to one digit
+        # (krr_pack_concat_strip, krr_amd/csrc/krr_strip.h): fewer bytes over PCIe, same CSR
+        self.strip = (os.environ.get("KRR_PACK_STRIP", "1") != "0") if strip is None else bool(strip)
+        self.last_upload: Optional[dict] = None
         self.device = torch.device("cuda", ctx.device)
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
@@ -92,10 +98,11 @@ class DevicePacker:
 
         return torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
 
-    def _upload(self, flat, want_ts, st, launch):
+    def _upload(self, flat, want_ts, st, launch, strip: bool = False):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
         copy stream and call ``launch(jb, a, b, tmp_v, tmp_t, lo, hi)`` on ``st`` for bodies
-        [a, b) = bytes [lo, hi) once the chunk is there."""
+        [a, b) = bytes [lo, hi) once the chunk is there.  ``strip``: the bodies' timestamps
+        are cut while staging (``_upload_stripped``; lo / hi are then meaningless)."""
         import torch
 
         dev = self.device
@@ -106,6 +113,8 @@ class DevicePacker:
         total = int(boffs[-1])
         stage = self._staging(total + 128)
         d_bodies = torch.empty(total + 128, dtype=torch.uint8, device=dev)
+        if strip and not want_ts and nb:
+            return self._upload_stripped(flat, lens, boffs, total, stage, d_bodies, st, launch)
         d_boffs = torch.from_numpy(boffs).to(dev)
         slots = total // 8 + 1
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
@@ -135,7 +144,69 @@ class DevicePacker:
             launch(jb, a, b, tmp_v, tmp_t, lo, hi)
             a = b
         self._last = (d_bodies, stage)
+        self.last_upload = {"bytes": total, "bytes_sent": total, "bodies": nb, "bodies_stripped": 0}
         return lens, boffs, total, jb, tmp_v, tmp_t
+
+    def _upload_stripped(self, flat, lens, boffs, total, stage, d_bodies, st, launch):
+        """_upload with the timestamps cut while staging (krr_pack_concat_strip): each chunk's
+        bodies are stripped by the host threads in runs, run r back to back inside its own
+        unstripped extent of the staging buffer; the runs go to HBM back to back, so the device
+        offsets are the prefix sums of the stripped lengths (uploaded per chunk before its
+        parse).  The scratch is sized for the unstripped bytes (an upper bound)."""
+        import os
+
+        import torch
+
+        dev = self.device
+        nb = len(flat)
+        T = self.threads or len(os.sched_getaffinity(0))
+        max_runs = max(1, 2 * T)
+        new_lens = np.empty(nb, dtype=np.int64)
+        runs = np.empty(max_runs + 1, dtype=np.int64)
+        n_runs = ctypes.c_int32(0)
+        new_offs = torch.zeros(nb + 1, dtype=torch.int64, pin_memory=True)
+        no = new_offs.numpy()
+        d_boffs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+        slots = total // 8 + 1
+        tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
+        jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
+        ptrs = (ctypes.c_char_p * nb)(*flat)
+        host = load_library()
+        cs = self._copy_stream
+        cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        a = 0
+        step = min(self.chunk_bytes, 16 << 20)  # small first chunks: the DMA starts early
+        while a < nb:
+            b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
+            step = min(2 * step, self.chunk_bytes)
+            b = min(max(b, a + 1), nb)
+            lo = int(boffs[a])
+            rc = host.krr_pack_concat_strip(ctypes.addressof(ptrs) + a * ctypes.sizeof(ctypes.c_char_p),
+                                            lens[a:].ctypes.data, b - a, boffs[a:].ctypes.data,
+                                            stage.data_ptr() + lo, self.threads, max_runs,
+                                            new_lens[a:].ctypes.data, runs.ctypes.data, ctypes.byref(n_runs))
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_concat_strip failed")
+            np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
+            no[a + 1:b + 1] += no[a]
+            with torch.cuda.stream(cs):
+                for r in range(n_runs.value):
+                    b0, b1 = a + int(runs[r]), a + int(runs[r + 1])
+                    d0, d1 = int(no[b0]), int(no[b1])
+                    if d1 > d0:
+                        s0 = int(boffs[b0])
+                        d_bodies[d0:d1].copy_(stage[s0:s0 + (d1 - d0)], non_blocking=True)
+                d_boffs[a:b + 1].copy_(new_offs[a:b + 1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            st.wait_event(ev)
+            launch(jb, a, b, tmp_v, None, lo, int(boffs[b]))
+            a = b
+        self._last = (d_bodies, stage, new_offs)
+        sent = int(no[nb])
+        self.last_upload = {"bytes": total, "bytes_sent": sent, "bodies": nb,
+                            "bodies_stripped": int((new_lens < lens).sum())}
+        return lens, boffs, total, jb, tmp_v, None
 
     def pack_grouped(self, plan, bodies: Sequence[bytes], *, want_timestamps: bool = False,
                      return_pod_counts: bool = False, stream=None, label: str = "pod") -> DevicePacked:
@@ -285,7 +356,7 @@ class DevicePacker:
         def launch(jb, a, b, tmp_v, tmp_t, lo, hi):
             self.ctx.json_parse(jb, a, b - a, want_ts, tmp_v, tmp_t, counts, status, stream=st)
 
-        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
+        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch, strip=self.strip)
         R = len(resources)
         with torch.cuda.stream(st):
             obj_t = torch.from_numpy(np.asarray(obj, dtype=np.int64)).to(dev, non_blocking=False)

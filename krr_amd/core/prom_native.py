@@ -32,7 +32,8 @@ KRR_PACK_E_VALUE = -4
 EXPORTED_SYMBOLS = ("krr_pack_abi_version", "krr_pack_parse", "krr_pack_n_values", "krr_pack_max_len",
                     "krr_pack_copy", "krr_pack_error", "krr_pack_free", "krr_pack_parse_series", "krr_series_count",
                     "krr_series_label", "krr_series_len", "krr_series_copy", "krr_series_error", "krr_series_free",
-                    "krr_pack_parse_grouped", "krr_round_simple", "krr_pack_concat", "krr_pack_route_grouped")
+                    "krr_pack_parse_grouped", "krr_round_simple", "krr_pack_concat", "krr_pack_route_grouped",
+                    "krr_pack_concat_strip", "krr_pack_strip_body")
 
 
 class PackerUnavailable(RuntimeError):
@@ -100,6 +101,10 @@ def load_library() -> ctypes.CDLL:
         lib.krr_round_simple.restype = ctypes.c_int
         lib.krr_pack_concat.argtypes = [vp, vp, i64, vp, vp, i32]
         lib.krr_pack_concat.restype = ctypes.c_int
+        lib.krr_pack_concat_strip.argtypes = [vp, vp, i64, vp, vp, i32, i32, vp, vp, ctypes.POINTER(i32)]
+        lib.krr_pack_concat_strip.restype = ctypes.c_int
+        lib.krr_pack_strip_body.argtypes = [ctypes.c_char_p, i64, vp]
+        lib.krr_pack_strip_body.restype = i64
         lib.krr_pack_route_grouped.argtypes = [vp, vp, i64, ctypes.c_char_p, vp, i64, vp, ctypes.c_char_p, vp, i64,
                                                vp, vp, vp, i32]
         lib.krr_pack_route_grouped.restype = ctypes.c_int
@@ -107,6 +112,15 @@ def load_library() -> ctypes.CDLL:
             raise PackerUnavailable("libkrr_host.so packer ABI version mismatch")
         _lib = lib
         return lib
+
+
+def strip_body(body: bytes) -> Optional[bytes]:
+    """``body`` with every number outside strings cut to its first digit (the device
+    packer's staging form, krr_amd/csrc/krr_strip.h), or None when it is not strippable."""
+    lib = load_library()
+    out = ctypes.create_string_buffer(max(len(body), 1))
+    n = lib.krr_pack_strip_body(body, len(body), ctypes.addressof(out))
+    return None if n < 0 else out.raw[:n]
 
 
 def _ptr(a: np.ndarray):

@@ -10,6 +10,7 @@
 // parallel, then the kept samples are copied into one CSR buffer.
 #include "krr_pack.h"
 #include "krr_json_parse.h"
+#include "krr_strip.h"
 
 #include <algorithm>
 #include <atomic>
@@ -735,6 +736,51 @@ int krr_pack_concat(const char* const* bodies, const int64_t* body_lens, int64_t
         if (body_lens[b]) memcpy(dst + (dst_offsets[b] - base), bodies[b], (size_t)body_lens[b]);
     });
     return KRR_PACK_OK;
+}
+
+int krr_pack_concat_strip(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                          const int64_t* dst_offsets, char* dst, int32_t threads, int32_t max_runs,
+                          int64_t* new_lens, int64_t* run_first, int32_t* n_runs) {
+    if (n_bodies < 0 || max_runs < 1 || !run_first || !n_runs ||
+        (n_bodies > 0 && (!bodies || !body_lens || !dst_offsets || !dst || !new_lens)))
+        return KRR_PACK_E_INVALID;
+    for (int64_t b = 0; b < n_bodies; ++b)
+        if (body_lens[b] < 0 || (body_lens[b] > 0 && !bodies[b]) ||
+            dst_offsets[b + 1] - dst_offsets[b] != body_lens[b])
+            return KRR_PACK_E_INVALID;
+    const int64_t base = n_bodies > 0 ? dst_offsets[0] : 0;
+    const int64_t total = n_bodies > 0 ? dst_offsets[n_bodies] - base : 0;
+    // runs of about equal bytes, each ending on a body boundary (a body never splits)
+    int32_t R = 0;
+    run_first[0] = 0;
+    for (int64_t b = 0; b < n_bodies;) {
+        const int64_t target = base + (total * (int64_t)(R + 1)) / max_runs;
+        int64_t e = (int64_t)(std::lower_bound(dst_offsets + b + 1, dst_offsets + n_bodies + 1, target) - dst_offsets);
+        e = std::min<int64_t>(std::max<int64_t>(e, b + 1), n_bodies);
+        if (R + 1 == max_runs) e = n_bodies;
+        run_first[++R] = e;
+        b = e;
+    }
+    *n_runs = R;
+    parallel_for(R, threads, [&](int64_t r) {
+        char* o = dst + (dst_offsets[run_first[r]] - base);
+        for (int64_t b = run_first[r]; b < run_first[r + 1]; ++b) {
+            const int64_t n = body_lens[b];
+            int64_t w = n ? krr::strip::strip_body(bodies[b], n, o) : 0;
+            if (w < 0) {  // not strippable: unchanged (o never passes the body's own extent)
+                memmove(o, bodies[b], (size_t)n);
+                w = n;
+            }
+            new_lens[b] = w;
+            o += w;
+        }
+    });
+    return KRR_PACK_OK;
+}
+
+int64_t krr_pack_strip_body(const char* body, int64_t body_len, char* out) {
+    if (body_len < 0 || (body_len > 0 && (!body || !out))) return -1;
+    return krr::strip::strip_body(body, body_len, out);
 }
 
 int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int64_t n_bodies, const char* label,

@@ -1,0 +1,113 @@
+// krr_strip.h — the device packer's staging copy with the sample timestamps cut (round 5).
+//
+// The reference drops every sample's timestamp (robusta_krr/core/integrations/prometheus.py:152,
+// `[Decimal(value) for _, value in ...]`), yet ~30-40% of a query_range body's bytes are
+// timestamps, and the device packer's end-to-end rate is bound by the bytes crossing PCIe
+// (DESIGN.md §9).  While staging a body this copy writes `[1700000000.25,"0.3"]` as
+// `[1,"0.3"]`: the timestamp cut to its first digit — still a JSON number, so the device
+// parser (krr_json.h) and the host packer read the stripped body unchanged, and neither reads
+// a timestamp's value unless timestamps were asked for (then nothing is stripped).
+//
+// Contract.  Every maximal run of digits and '.' outside strings is cut to its first byte,
+// and a body is stripped only when every such run is a whole JSON number token of the form
+// (0|[1-9][0-9]*)(\.[0-9]+)? — no sign or exponent next to it (no e E + - ) / before it, no
+// e E after it) — and the body holds no backslash (so the quotes delimit the strings
+// exactly); anything else is copied unchanged.  Cutting a valid number token to one digit keeps every
+// token of the body in place and every string byte for byte, so the host reader and the
+// device parser walk the same structure, read the same value strings, and accept or reject
+// the same bodies; the only numbers outside strings in a query_range body are the sample
+// timestamps, whose values nobody reads unless timestamps were asked for (then nothing is
+// stripped).  When the device rejects a stripped body its batch goes to the host packer,
+// which parses the ORIGINAL bodies (krr_amd/core/device_pack.py).
+//
+// 64 bytes at a time (AVX-512BW masks + VBMI2 compress): the string mask by a carry-less
+// prefix XOR of the quotes, runs by "preceded by" relations (bit 63 carried to the next
+// block), the fraction digits by one 64-bit addition whose carry runs past them (the byte
+// after them must not be a second '.'), the kept bytes by a masked compress store.  Without
+// AVX-512 VBMI2 nothing is stripped.
+#pragma once
+
+#include <immintrin.h>
+#include <stdint.h>
+#include <string.h>
+
+namespace krr {
+namespace strip {
+
+#define KRR_STRIP_TARGET __attribute__((target("avx512f,avx512bw,avx512vbmi2,bmi,bmi2,pclmul,popcnt")))
+
+inline bool supported() {
+    static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                           __builtin_cpu_supports("avx512vbmi2") && __builtin_cpu_supports("bmi2") &&
+                           __builtin_cpu_supports("pclmul");
+    return ok;
+}
+
+KRR_STRIP_TARGET inline uint64_t prefix_xor(uint64_t x) {
+    const __m128i v = _mm_clmulepi64_si128(_mm_set_epi64x(0, (long long)x), _mm_set1_epi8((char)0xFF), 0);
+    return (uint64_t)_mm_cvtsi128_si64(v);
+}
+
+// One body [s, s + n) stripped into out (n bytes of room): bytes written, or -1 when the
+// body is not strippable (the caller copies it unchanged).
+KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out) {
+    // bit 63 of each class mask of the previous block ("preceded by" across the boundary)
+    uint64_t in_str = 0, cT = 0, cZ = 0, cDt = 0, cX = 0;
+    unsigned char cadd = 0;
+    char* o = out;
+    const __m512i kq = _mm512_set1_epi8('"'), kbs = _mm512_set1_epi8('\\'), kdt = _mm512_set1_epi8('.');
+    const __m512i k0 = _mm512_set1_epi8('0'), k9 = _mm512_set1_epi8(9);
+    const __m512i k20 = _mm512_set1_epi8(0x20), ke = _mm512_set1_epi8('e');
+    const __m512i k06 = _mm512_set1_epi8(0x06), k2f = _mm512_set1_epi8(0x2F);
+    while (p < e) {
+        const int64_t left = e - p;
+        const uint64_t valid = left >= 64 ? ~0ull : _bzhi_u64(~0ull, (unsigned)left);
+        const __m512i x = _mm512_maskz_loadu_epi8(valid, p);  // no read past the body
+        if (_mm512_mask_cmpeq_epi8_mask(valid, x, kbs)) return -1;
+        const uint64_t qt = _mm512_mask_cmpeq_epi8_mask(valid, x, kq);
+        const uint64_t dt = _mm512_mask_cmpeq_epi8_mask(valid, x, kdt);
+        const uint64_t zr = _mm512_mask_cmpeq_epi8_mask(valid, x, k0);
+        const uint64_t dg = _mm512_mask_cmple_epu8_mask(valid, _mm512_sub_epi8(x, k0), k9);
+        // exponent letters e / E, and + - (with ) / : x | 6 == '/')
+        const uint64_t ee = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k20), ke);
+        const uint64_t pm = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k06), k2f);
+        // strings: from an opening quote (set) to its closing quote (clear)
+        const uint64_t instr = prefix_xor(qt) ^ in_str;
+        const uint64_t outside = ~instr & ~qt;
+        const uint64_t D = dg & outside, Dt = dt & outside, T = D | Dt;
+        const uint64_t sT = (T << 1) | cT;
+        const uint64_t first = T & ~sT;              // each run's first byte: kept
+        const uint64_t Z = first & zr;
+        const uint64_t sDt = (Dt << 1) | cDt;
+        const uint64_t X = (ee | pm) & outside;
+        unsigned long long run;                       // fraction digits: the carry runs past them
+        const unsigned char cout = _addcarry_u64(cadd, D, sDt & D, &run);
+        uint64_t bad = first & ~D;                    // a run starts with a digit,
+        bad |= ((Z << 1) | cZ) & D;                   // no leading zero,
+        bad |= sDt & ~D;                              // '.' then a digit,
+        bad |= run & ~D & Dt;                         // and one '.' at most;
+        bad |= first & ((X << 1) | cX);               // a whole token: no sign or exponent before
+        bad |= ee & outside & sT;                     // nor an exponent after
+        if (bad & (valid | (valid + 1))) return -1;  // (+ the byte after a partial block)
+        const uint64_t keep = valid & ~(T & sT);      // a run's bytes after its first
+        const __m512i y = _mm512_maskz_compress_epi8(keep, x);
+        const unsigned cnt = (unsigned)_mm_popcnt_u64(keep);
+        _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), y);
+        o += cnt;
+        in_str = 0ull - (instr >> 63);
+        cT = T >> 63, cZ = Z >> 63, cDt = Dt >> 63, cX = X >> 63;
+        cadd = cout;
+        p += 64;
+    }
+    // a run that ends the body: its last checks had no byte after it to look at
+    if (cDt) return -1;
+    return o - out;
+}
+
+inline int64_t strip_body(const char* s, int64_t n, char* out) {
+    if (!supported() || n <= 0) return -1;
+    return strip_span(s, s + n, out);
+}
+
+}  // namespace strip
+}  // namespace krr

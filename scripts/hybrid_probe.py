@@ -1,7 +1,9 @@
 """Hybrid parse A/B (GPU): BatchedRunner.recommend_from_bodies on bench.py's host-path fleet
 (2,000 config-1-shaped objects) with parser='device' and parser='hybrid' at several staging
 thread counts; best of 3 after the share settles.
-usage: python scripts/hybrid_probe.py [--objects 2000] [--threads 16] [--dev-threads 2,3,4,6]"""
+With --strip 0,1 the sweep runs with the device packer's staging copy plain and with the
+timestamps cut (krr_amd/csrc/krr_strip.h).
+usage: python scripts/hybrid_probe.py [--objects 2000] [--threads 16] [--dev-threads 2,3,4,6] [--strip 0,1]"""
 import argparse
 import os
 import sys
@@ -15,6 +17,7 @@ def main():
     ap.add_argument("--objects", type=int, default=2000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dev-threads", default="2,3,4,6")
+    ap.add_argument("--strip", default="1")
     a = ap.parse_args()
     from bench import body_fleet
     from krr_amd.core.runner import BatchedRunner
@@ -32,19 +35,25 @@ def main():
             t = min(t, time.perf_counter() - t0)
         return t
 
-    td = best("device")
-    print(f"device: {a.objects / td:.0f} objects/s ({td * 1e3:.1f} ms)", flush=True)
-    for d in [int(x) for x in a.dev_threads.split(",")]:
-        runner.hybrid_device_threads = d
-        runner.hybrid_share = 0.2
-        for _ in range(5):  # the share settles
-            runner.recommend_from_bodies(cpu_b, mem_b, threads=a.threads, parser="hybrid")
-        th = best("hybrid")
-        h = runner.hybrid_last
-        print(f"hybrid dev_threads={d}: {a.objects / th:.0f} objects/s ({th * 1e3:.1f} ms, +{td / th - 1:.1%}), "
-              f"share {h['share']:.3f}, device {h['device_s'] * 1e3:.1f} ms {h['device_GBps']:.1f} GB/s, "
-              f"host {h['host_s'] * 1e3:.1f} ms {h['host_GBps']:.1f} GB/s", flush=True)
+    from krr_amd.core.device_pack import default_packer
 
+    packer = default_packer(0)
+    for strip in [int(x) for x in a.strip.split(",")]:
+        packer.strip = bool(strip)
+        td = best("device")
+        up = packer.last_upload or {}
+        print(f"strip={strip} device: {a.objects / td:.0f} objects/s ({td * 1e3:.1f} ms), link bytes "
+              f"{up.get('bytes_sent', 0) / max(up.get('bytes', 1), 1):.3f} of the JSON", flush=True)
+        for d in [int(x) for x in a.dev_threads.split(",")]:
+            runner.hybrid_device_threads = d
+            runner.hybrid_share = 0.2
+            for _ in range(5):  # the share settles
+                runner.recommend_from_bodies(cpu_b, mem_b, threads=a.threads, parser="hybrid")
+            th = best("hybrid")
+            h = runner.hybrid_last
+            print(f"strip={strip} hybrid dev_threads={d}: {a.objects / th:.0f} objects/s ({th * 1e3:.1f} ms, "
+                  f"+{td / th - 1:.1%}), share {h['share']:.3f}, device {h['device_s'] * 1e3:.1f} ms "
+                  f"{h['device_GBps']:.1f} GB/s, host {h['host_s'] * 1e3:.1f} ms {h['host_GBps']:.1f} GB/s", flush=True)
 
 if __name__ == "__main__":
     main()

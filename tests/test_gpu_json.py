@@ -34,7 +34,10 @@ def _host(per_obj, want_ts=True):
 
 
 def _same(dp, per_obj, want_ts=True):
-    ps, ts, counts = _host(per_obj, want_ts)
+    if want_ts:
+        ps, ts, counts = _host(per_obj, want_ts)
+    else:
+        ps, counts = _host(per_obj, want_ts)
     got = dp.series
     v = got.values.cpu().numpy() if hasattr(got.values, "cpu") else got.values
     o = got.offsets.cpu().numpy() if hasattr(got.offsets, "cpu") else got.offsets
@@ -341,3 +344,68 @@ def test_grouped_many_and_small_chunks(packer):
             assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
             assert np.array_equal(dp.timestamps.cpu().numpy().view(np.uint64), want_ts.view(np.uint64))
             assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+def _stripped_cases():
+    import json as _json
+
+    from test_prom_native import _fleet as pn_fleet
+
+    compacted = [[_json.dumps(_json.loads(b), separators=(",", ":")).encode() for b in bodies]
+                 for bodies in pn_fleet(1)]
+    mixed = _fleet(6, n_obj=30)
+    # bodies the strip leaves whole, beside stripped ones: an escape, an exponent and a
+    # leading-zero timestamp (the device then parses the original bytes of those)
+    mixed[3] = mixed[3] + [b'{"status":"success","data":{"resultType":"matrix","result":[{"metric":{"pod":"a\\"b"},'
+                           b'"values":[[1700000000.5,"0.5"],[1700000060,"0.75"]]}]}}']
+    mixed[7] = mixed[7] + [b'{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},'
+                           b'"values":[[1.7e9,"1"],[1.70000006e9,"2"]]}]}}']
+    mixed[9] = mixed[9] + [b'{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},'
+                           b'"values":[[0.5,"3"],[10,"4"]]}]}}']
+    return {"fleet1": _fleet(1), "fleet2": _fleet(2), "prom_native_compacted": compacted,
+            "prom_native_as_is": pn_fleet(1), "mixed": mixed}
+
+
+@pytest.mark.parametrize("case", ["fleet1", "fleet2", "prom_native_compacted", "prom_native_as_is", "mixed"])
+@pytest.mark.parametrize("chunk", [1 << 20, 4096])
+def test_stripped_staging_equals_host(packer, case, chunk):
+    """Without timestamps the bodies are staged with their timestamps cut (krr_strip.h): fewer
+    bytes cross PCIe and the CSR, the pod drops and the device/host decision are unchanged."""
+    from krr_amd.core.device_pack import DevicePacker
+
+    per_obj = _stripped_cases()[case]
+    p = DevicePacker(packer.ctx, chunk_bytes=chunk)
+    assert p.strip
+    dp = p.pack(per_obj, want_timestamps=False, return_pod_counts=True)
+    assert dp.via == "device"
+    _same(dp, per_obj, want_ts=False)
+    up = p.last_upload
+    if case.startswith("prom_native"):  # escaped label values in every body: none stripped
+        assert up["bodies_stripped"] == 0 and up["bytes_sent"] == up["bytes"]
+    else:
+        assert up["bodies_stripped"] > 0 and up["bytes_sent"] < 0.8 * up["bytes"]
+    q = DevicePacker(packer.ctx, chunk_bytes=chunk, strip=False)
+    dq = q.pack(per_obj, want_timestamps=False, return_pod_counts=True)
+    assert q.last_upload["bytes_sent"] == q.last_upload["bytes"]
+    assert np.array_equal(dq.series.values.cpu().numpy().view(np.uint64), dp.series.values.cpu().numpy().view(np.uint64))
+
+
+def test_stripped_staging_error_and_host_batches(packer):
+    """A batch the device hands to the host, and one with an error body, behave as without
+    the strip: the host packer's result or error on the ORIGINAL bodies."""
+    from krr_amd.core.prom_native import PrometheusResponseError
+
+    per_obj = _fleet(4, n_obj=12)
+    per_obj[5] = per_obj[5] + [_compact({"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {}, "values": [[1, "2"]]}]}}).replace(b'"status"', b'"st\\u0061tus"')]
+    dp = packer.pack(per_obj, want_timestamps=False, return_pod_counts=True)
+    assert dp.via == "host" and dp.host_bodies == 1
+    _same(dp, per_obj, want_ts=False)
+    bad = _fleet(3, n_obj=10)
+    bad[4] = bad[4] + [b'{"status":"success","data":{"resultType":"matrix","result":[{"metric":{},'
+                       b'"values":[[1700000000,"1"],[1700000015,2]]}]}}']  # an unquoted value
+    with pytest.raises(PrometheusResponseError) as dev_err:
+        packer.pack(bad)
+    with pytest.raises(PrometheusResponseError) as host_err:
+        _host(bad)
+    assert str(dev_err.value) == str(host_err.value) and dev_err.value.code == host_err.value.code

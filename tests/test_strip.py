@@ -1,0 +1,177 @@
+"""The device packer's stripped staging (krr_amd/csrc/krr_strip.h, krr_pack_concat_strip):
+every number outside strings cut to its first digit while the bodies are staged, so fewer
+bytes cross PCIe.  The reference drops the timestamps (robusta_krr/core/integrations/
+prometheus.py:152); what must hold is that the host packer (the parity restatement of that
+loader) reads a stripped body exactly as the original: same values, same pod drops, or the
+same error.  CPU only: the device parser's side is tests/test_gpu_json.py."""
+import ctypes
+import random
+import re
+
+import numpy as np
+import pytest
+
+from krr_amd.core import prom_native
+from krr_amd.core.prom_native import PrometheusResponseError, pack_query_range_bodies, strip_body
+
+HEAD = '{"status":"success","data":{"resultType":"matrix","result":['
+_NUM = re.compile(rb"[0-9.]+")
+_OK_RUN = re.compile(rb"(0|[1-9][0-9]*)(\.[0-9]+)?")
+
+
+def _restated(body: bytes):
+    """The strip restated in Python: None unless every run of digits / '.' outside strings
+    is a whole number token (0|[1-9][0-9]*)(\\.[0-9]+)? (no e E + - ) / before it, no e E
+    after it) and no backslash occurs; else each run cut to one byte."""
+    if b"\\" in body:
+        return None
+    parts = body.split(b'"')
+    for i in range(0, len(parts), 2):  # outside strings
+        part = parts[i]
+        for m in _NUM.finditer(part):
+            if not _OK_RUN.fullmatch(m.group()):
+                return None
+            if m.start() > 0 and part[m.start() - 1:m.start()] in (b"e", b"E", b"+", b"-", b")", b"/"):
+                return None                      # a sign or exponent before the run
+            if part[m.end():m.end() + 1] in (b"e", b"E"):
+                return None                      # an exponent after it
+        parts[i] = _NUM.sub(lambda m: m.group()[:1], parts[i])
+    return b'"'.join(parts)
+
+
+def _body(values, ts=None, pod="p", extra=""):
+    ts = ts if ts is not None else [f"{1.7e9 + 15 * i!r}" for i in range(len(values))]
+    items = ",".join(f'[{t},"{v}"]' for t, v in zip(ts, values))
+    return (HEAD + f'{{"metric":{{"pod":"{pod}"}},"values":[{items}]{extra}}}]}}}}').encode()
+
+
+def _packed(bodies):
+    try:
+        ps, counts = pack_query_range_bodies([[b] for b in bodies], threads=2, return_pod_counts=True)
+    except PrometheusResponseError as e:
+        return ("error", e.code)
+    return (np.asarray(ps.values).view(np.int64).tolist(), np.asarray(ps.offsets).tolist(),
+            np.asarray(counts).tolist())
+
+
+def _same_outcome(orig: bytes, stripped: bytes):
+    return _packed([orig]) == _packed([stripped])
+
+
+def test_bench_shaped_bodies_strip_to_a_third_less():
+    rng = np.random.default_rng(1)
+    for vals in ([repr(x) for x in rng.gamma(2.0, 0.05, 3000).tolist()],
+                 [repr(x) for x in np.floor(rng.normal(2e8, 2e7, 3000)).tolist()]):
+        b = _body(vals)
+        s = strip_body(b)
+        assert s is not None and s == _restated(b)
+        assert len(s) < 0.72 * len(b)
+        assert b'[1,"' in s and b"1700000" not in s
+        assert _same_outcome(b, s)
+
+
+TIMESTAMPS = ["1700000000", "1700000000.5", "1700000000.123", "0", "0.5", "7"]
+NOT_STRIPPED = ["01700000000", "1700000000.", ".5", "1.2.3", "1e9", "1.7E9", "-5", "1700000000.5.5"]
+
+
+@pytest.mark.parametrize("t", TIMESTAMPS + NOT_STRIPPED)
+def test_timestamp_forms(t):
+    b = _body(["0.25", "1", "NaN"], ts=[t, t, t])
+    s = strip_body(b)
+    assert s == _restated(b)
+    if t in NOT_STRIPPED:
+        assert s is None
+    if s is not None:
+        assert _same_outcome(b, s)
+
+
+@pytest.mark.parametrize("body", [
+    _body(["0.1"] * 5, pod='p\\"q'),                                   # a backslash: not stripped
+    _body(["0.1", "0.2"]).replace(b",", b" , "),                        # whitespace between tokens
+    (HEAD + "]}}").encode(),                                            # an empty result: dropped pod
+    b'{"status":"error","errorType":"bad_data","error":"x 12.5"}',     # an error body
+    _body(["0.1", "2"], extra=',"x":[1.25,2.5e3]'),                     # other numbers in result[0]
+    _body(["0.1", "0.2"]).replace(b'"0.2"', b"0.2"),                    # an unquoted value
+    _body(["1.5", "2"], pod="pod-123.45"),                              # digits inside strings stay
+    _body([]),
+])
+def test_odd_bodies_keep_their_outcome(body):
+    s = strip_body(body)
+    assert s == _restated(body)
+    if s is not None:
+        assert _same_outcome(body, s)
+
+
+def test_fuzzed_bodies_keep_their_outcome():
+    """Byte mutations of a small body: whenever it strips, the host packer's outcome on the
+    stripped body (values, drops, or error code) is the original's."""
+    rng = random.Random(7)
+    base = _body(["0.25", "1e-3", "NaN", "+Inf", "12"], ts=["1700000000", "1700000015.5", "0", "3", "99.25"])
+    alphabet = b'0123456789.,[]{}"-+eE :\\ a'
+    stripped = 0
+    for _ in range(20000):
+        b = bytearray(base)
+        for _ in range(rng.randint(1, 3)):
+            i = rng.randrange(len(b))
+            op = rng.random()
+            if op < 0.4:
+                b[i] = rng.choice(alphabet)
+            elif op < 0.7:
+                b.insert(i, rng.choice(alphabet))
+            else:
+                del b[i]
+        b = bytes(b)
+        s = strip_body(b)
+        assert s == _restated(b), b
+        if s is not None:
+            stripped += 1
+            assert _same_outcome(b, s), b
+    assert stripped > 5000
+
+
+def test_block_boundaries():
+    """Runs and strings crossing the 64-byte blocks, at every alignment."""
+    for pad in range(0, 70):
+        b = _body(["0.5", "17", "3.25"], ts=["1700000000.125", "1700000015", "1700000030.5"], pod="x" * pad)
+        s = strip_body(b)
+        assert s == _restated(b)
+        assert _same_outcome(b, s)
+        bad = _body(["0.5"], ts=["1700000000.1.5"], pod="x" * pad)
+        assert strip_body(bad) is None
+        bad = _body(["0.5"], ts=["1700000000."], pod="x" * pad)
+        assert strip_body(bad) is None
+
+
+def test_concat_strip_runs_lay_out_the_stripped_bodies():
+    lib = prom_native.load_library()
+    rng = np.random.default_rng(3)
+    bodies = []
+    for k in range(37):
+        n = int(rng.integers(0, 400))
+        b = _body([repr(x) for x in rng.gamma(2.0, 0.05, n).tolist()])
+        if k % 9 == 4:
+            b = b.replace(b'"metric":{', b'"metric":{"a":"\\"",')   # not strippable
+        bodies.append(b)
+    lens = np.array([len(b) for b in bodies], dtype=np.int64)
+    offs = np.zeros(len(bodies) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    dst = ctypes.create_string_buffer(int(offs[-1]) + 64)
+    new_lens = np.zeros(len(bodies), dtype=np.int64)
+    for max_runs in (1, 3, 8, 64):
+        runs = np.zeros(max_runs + 1, dtype=np.int64)
+        nr = ctypes.c_int32()
+        ptrs = (ctypes.c_char_p * len(bodies))(*bodies)
+        rc = lib.krr_pack_concat_strip(ctypes.addressof(ptrs), lens.ctypes.data, len(bodies), offs.ctypes.data,
+                                       ctypes.addressof(dst), 4, max_runs, new_lens.ctypes.data, runs.ctypes.data,
+                                       ctypes.byref(nr))
+        assert rc == 0 and 1 <= nr.value <= max_runs and runs[0] == 0 and runs[nr.value] == len(bodies)
+        raw = dst.raw
+        for r in range(nr.value):
+            pos = int(offs[runs[r]])
+            for i in range(int(runs[r]), int(runs[r + 1])):
+                want = strip_body(bodies[i]) if bodies[i] else b""
+                want = bodies[i] if want is None else want
+                assert new_lens[i] == len(want)
+                assert raw[pos:pos + len(want)] == want
+                pos += len(want)
+            assert pos <= offs[runs[r + 1]]
