@@ -61,6 +61,7 @@ class DevicePacker:
         # (krr_pack_concat_strip, krr_amd/csrc/krr_strip.h): fewer bytes over PCIe, same CSR
         self.strip = (os.environ.get("KRR_PACK_STRIP", "1") != "0") if strip is None else bool(strip)
         self.last_upload: Optional[dict] = None
+        self.strip_runs_per_thread = 2  # runs per staging thread (each run = one H2D copy)
         self.device = torch.device("cuda", ctx.device)
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
@@ -160,7 +161,7 @@ class DevicePacker:
         dev = self.device
         nb = len(flat)
         T = self.threads or len(os.sched_getaffinity(0))
-        max_runs = max(1, 2 * T)
+        max_runs = max(1, self.strip_runs_per_thread * T)
         new_lens = np.empty(nb, dtype=np.int64)
         runs = np.empty(max_runs + 1, dtype=np.int64)
         n_runs = ctypes.c_int32(0)

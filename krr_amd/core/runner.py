@@ -227,17 +227,16 @@ class BatchedRunner:
             if len(parts) > 1:
                 raws.append(raw_host)
                 # balance the whole critical paths (pack + kernel pass on each side), not the packs
-                h = self.hybrid_last
-                r_dev = h["bytes_device"] / max(time.perf_counter() - t0, 1e-9)
-                r_host = h["bytes_host"] / max(done.get("host", t0) - t0, 1e-9)
-                self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
+                self.hybrid_share = _rebalance(share, time.perf_counter() - t0, done.get("host", t0) - t0)
             raw = _concat_raw(raws)
             return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
 
-    # parser="hybrid": the share of the JSON bytes the host packer takes, re-estimated after
-    # every call from the rates both sides reached while running together
-    hybrid_share = 0.2
+    # parser="hybrid": the share of the JSON bytes the host packer takes, moved after every
+    # call toward equal finishing times of the two sides (_rebalance)
+    hybrid_share = 0.14
+    # staging threads of the device side (0: half the threads when the device packer strips
+    # timestamps while staging, a quarter for a plain copy; the host parser gets the rest)
     hybrid_device_threads = 0
     hybrid_last: Optional[dict] = None
 
@@ -279,8 +278,11 @@ class BatchedRunner:
         k = min(max(k, 1), n - 1)
         if T < 3 or n < 2:
             return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)], None
-        # staging memcpy threads (hybrid_device_threads, default a quarter); the host parser gets the rest
-        t_dev = max(1, min(T - 1, int(self.hybrid_device_threads or T // 4)))
+        # staging threads (hybrid_device_threads); the host parser gets the rest.  A stripping
+        # staging thread moves ~8x the JSON bytes per second of a host parser thread and keeps
+        # fewer bytes on the link, so it gets half the threads (a plain copy: a quarter)
+        strips = self._device_packer(threads, device).strip
+        t_dev = max(1, min(T - 1, int(self.hybrid_device_threads or (T // 2 if strips else T // 4))))
         t_host = max(1, T - t_dev)
         host_out: dict = {}
         alloc = _pinned_alloc_or_none()
@@ -323,8 +325,9 @@ class BatchedRunner:
         r_dev, r_host = b_dev / max(dev_s, 1e-9), b_host / max(host_out["s"], 1e-9)
         self.hybrid_last = {"share": share, "split_object": k, "device_s": dev_s, "host_s": host_out["s"],
                             "device_GBps": r_dev / 1e9, "host_GBps": r_host / 1e9,
-                            "device_threads": t_dev, "host_threads": t_host}
-        self.hybrid_share = 0.5 * share + 0.5 * r_host / (r_host + r_dev)
+                            "device_threads": t_dev, "host_threads": t_host,
+                            "device_upload": self._device_packer(threads, device).last_upload}
+        self.hybrid_share = _rebalance(share, dev_s, host_out["s"])
         self.hybrid_last.update(bytes_device=b_dev, bytes_host=b_host)
         self.last_pack_via = ("hybrid", "hybrid")
         return [dev_fleet, host_out["fleet"]], host_out.get("then")
@@ -408,6 +411,14 @@ class BatchedRunner:
         histories = await self.gather_histories(objects, loader)
         # the kernel pass runs off the event loop, like the reference's to_thread (runner.py:106)
         return await asyncio.to_thread(self.allocations, objects, histories)
+
+
+def _rebalance(share: float, t_device: float, t_host: float) -> float:
+    """The hybrid parser's next host share: moved toward equal finishing times by the square
+    root of their ratio, at most 25% per call, within [0.02, 0.8].  (Balancing the two sides'
+    RATES instead runs away on a shared host: each side's rate depends on the other's load.)"""
+    r = (max(t_device, 1e-9) / max(t_host, 1e-9)) ** 0.5
+    return min(max(share * min(max(r, 0.8), 1.25), 0.02), 0.8)
 
 
 def _host_threads() -> int:

@@ -1931,6 +1931,9 @@ namespace krr {
 #ifndef KRR_KLL_TAIL_RETRY
 #define KRR_KLL_TAIL_RETRY 4.0  // a sparse attempt that missed is retried at this many margins
 #endif
+#ifndef KRR_KLL_SPARSE_PIPE
+#define KRR_KLL_SPARSE_PIPE 1  // one batch of flagged lines in flight while the previous one is filtered
+#endif
 struct KllLineTailArgs {
     KllTailArgs T;
     uint32_t queue_off;     // byte offset of the 128-entry line queue in LDS
@@ -1981,8 +1984,8 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
             const double hv = a0 > beg ? A.vals[beg] : qnan, tv = a1 < end ? A.vals[a1] : qnan;
             const uint32_t t32 = (uint32_t)(okey(dbits(tau)) >> 32);
             const uint32_t* L = A.lines + (size_t)s * (size_t)A.line_stride;
-            auto process = [&](uint32_t cnt) __attribute__((always_inline)) {
-                double2 c[kUnroll];
+            // the lines of queue slots [0, cnt) loaded into c (row r = slots 8r .. 8r + 7)
+            auto load_batch = [&](uint32_t cnt, double2 (&c)[kUnroll]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int r = 0; r < kUnroll; ++r) {
                     const uint32_t slot = (uint32_t)r * 8u + ((uint32_t)lane >> 3);
@@ -1998,9 +2001,15 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     }
                 }
                 __syncthreads();  // the queue entries are read: the caller may shift it
-                P.chunk(c);
             };
             uint32_t qn = 0;  // queued lines (uniform)
+#if KRR_KLL_SPARSE_PIPE
+            // one batch in flight: a full batch's lines are loaded when it fills and filtered
+            // when the next one fills (or at the end), so the loads overlap the scan of the
+            // maxima and the previous batch's filter; the batches keep their order
+            double2 cp[kUnroll];
+            bool pend = false;
+#endif
             // the line maxima of 8 chunks at a time, the next 8 in flight while these are queued
             uint32_t nk[8];
 #pragma unroll
@@ -2021,7 +2030,18 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     nread += popc64(m);
                     __syncthreads();
                     if (qn >= 64u) {
-                        process(64u);
+#if KRR_KLL_SPARSE_PIPE
+                        double2 cn[kUnroll];
+                        load_batch(64u, cn);
+                        if (pend) P.chunk(cp);
+#pragma unroll
+                        for (int r = 0; r < kUnroll; ++r) cp[r] = cn[r];
+                        pend = true;
+#else
+                        double2 cn[kUnroll];
+                        load_batch(64u, cn);
+                        P.chunk(cn);
+#endif
                         const uint32_t rest = qn - 64u;  // < 64
                         const uint32_t v = (uint32_t)lane < rest ? q[64 + lane] : 0u;
                         __syncthreads();
@@ -2031,7 +2051,14 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                     }
                 }
             }
-            if (qn) process(qn);
+#if KRR_KLL_SPARSE_PIPE
+            if (pend) P.chunk(cp);
+#endif
+            if (qn) {
+                double2 cn[kUnroll];
+                load_batch(qn, cn);
+                P.chunk(cn);
+            }
             dense = P.ts.tl < tail;  // a miss
             if (!dense) break;
         }

@@ -48,59 +48,91 @@ KRR_STRIP_TARGET inline uint64_t prefix_xor(uint64_t x) {
     return (uint64_t)_mm_cvtsi128_si64(v);
 }
 
-// One body [s, s + n) stripped into out (n bytes of room): bytes written, or -1 when the
-// body is not strippable (the caller copies it unchanged).
-KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out) {
-    // bit 63 of each class mask of the previous block ("preceded by" across the boundary)
+// Carried from one 64-byte block to the next: inside a string, and bit 63 of the class
+// masks the "preceded by" relations look back at.
+#ifndef KRR_STRIP_MASKED_STORES
+#define KRR_STRIP_MASKED_STORES 0  // 1: whole blocks stored with a byte mask too (scripts/strip_bench.cpp:
+                                    // plain stores 8-26% faster on the EPYC 9575F host, masked faster on SPR)
+#endif
+struct StripState {
     uint64_t in_str = 0, cT = 0, cZ = 0, cDt = 0, cX = 0;
     unsigned char cadd = 0;
-    char* o = out;
+};
+
+// One block x (bytes `valid`): false when a run breaks the contract, else *keep = the bytes
+// the stripped copy keeps.
+KRR_STRIP_TARGET __attribute__((always_inline)) inline bool strip_block(StripState& st, __m512i x, uint64_t valid,
+                                                                        uint64_t* keep) {
     const __m512i kq = _mm512_set1_epi8('"'), kbs = _mm512_set1_epi8('\\'), kdt = _mm512_set1_epi8('.');
     const __m512i k0 = _mm512_set1_epi8('0'), k9 = _mm512_set1_epi8(9);
     const __m512i k20 = _mm512_set1_epi8(0x20), ke = _mm512_set1_epi8('e');
     const __m512i k06 = _mm512_set1_epi8(0x06), k2f = _mm512_set1_epi8(0x2F);
-    while (p < e) {
-        const int64_t left = e - p;
-        const uint64_t valid = left >= 64 ? ~0ull : _bzhi_u64(~0ull, (unsigned)left);
-        const __m512i x = _mm512_maskz_loadu_epi8(valid, p);  // no read past the body
-        if (_mm512_mask_cmpeq_epi8_mask(valid, x, kbs)) return -1;
-        const uint64_t qt = _mm512_mask_cmpeq_epi8_mask(valid, x, kq);
-        const uint64_t dt = _mm512_mask_cmpeq_epi8_mask(valid, x, kdt);
-        const uint64_t zr = _mm512_mask_cmpeq_epi8_mask(valid, x, k0);
-        const uint64_t dg = _mm512_mask_cmple_epu8_mask(valid, _mm512_sub_epi8(x, k0), k9);
-        // exponent letters e / E, and + - (with ) / : x | 6 == '/')
-        const uint64_t ee = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k20), ke);
-        const uint64_t pm = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k06), k2f);
-        // strings: from an opening quote (set) to its closing quote (clear)
-        const uint64_t instr = prefix_xor(qt) ^ in_str;
-        const uint64_t outside = ~instr & ~qt;
-        const uint64_t D = dg & outside, Dt = dt & outside, T = D | Dt;
-        const uint64_t sT = (T << 1) | cT;
-        const uint64_t first = T & ~sT;              // each run's first byte: kept
-        const uint64_t Z = first & zr;
-        const uint64_t sDt = (Dt << 1) | cDt;
-        const uint64_t X = (ee | pm) & outside;
-        unsigned long long run;                       // fraction digits: the carry runs past them
-        const unsigned char cout = _addcarry_u64(cadd, D, sDt & D, &run);
-        uint64_t bad = first & ~D;                    // a run starts with a digit,
-        bad |= ((Z << 1) | cZ) & D;                   // no leading zero,
-        bad |= sDt & ~D;                              // '.' then a digit,
-        bad |= run & ~D & Dt;                         // and one '.' at most;
-        bad |= first & ((X << 1) | cX);               // a whole token: no sign or exponent before
-        bad |= ee & outside & sT;                     // nor an exponent after
-        if (bad & (valid | (valid + 1))) return -1;  // (+ the byte after a partial block)
-        const uint64_t keep = valid & ~(T & sT);      // a run's bytes after its first
-        const __m512i y = _mm512_maskz_compress_epi8(keep, x);
+    if (_mm512_mask_cmpeq_epi8_mask(valid, x, kbs)) return false;
+    const uint64_t qt = _mm512_mask_cmpeq_epi8_mask(valid, x, kq);
+    const uint64_t dt = _mm512_mask_cmpeq_epi8_mask(valid, x, kdt);
+    const uint64_t zr = _mm512_mask_cmpeq_epi8_mask(valid, x, k0);
+    const uint64_t dg = _mm512_mask_cmple_epu8_mask(valid, _mm512_sub_epi8(x, k0), k9);
+    // exponent letters e / E, and + - (with ) / : x | 6 == '/')
+    const uint64_t ee = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k20), ke);
+    const uint64_t pm = _mm512_mask_cmpeq_epi8_mask(valid, _mm512_or_si512(x, k06), k2f);
+    // strings: from an opening quote (set) to its closing quote (clear)
+    const uint64_t instr = prefix_xor(qt) ^ st.in_str;
+    const uint64_t outside = ~instr & ~qt;
+    const uint64_t D = dg & outside, Dt = dt & outside, T = D | Dt;
+    const uint64_t sT = (T << 1) | st.cT;
+    const uint64_t first = T & ~sT;              // each run's first byte: kept
+    const uint64_t Z = first & zr;
+    const uint64_t sDt = (Dt << 1) | st.cDt;
+    const uint64_t X = (ee | pm) & outside;
+    unsigned long long run;                       // fraction digits: the carry runs past them
+    const unsigned char cout = _addcarry_u64(st.cadd, D, sDt & D, &run);
+    uint64_t bad = first & ~D;                    // a run starts with a digit,
+    bad |= ((Z << 1) | st.cZ) & D;                // no leading zero,
+    bad |= sDt & ~D;                              // '.' then a digit,
+    bad |= run & ~D & Dt;                         // and one '.' at most;
+    bad |= first & ((X << 1) | st.cX);            // a whole token: no sign or exponent before
+    bad |= ee & outside & sT;                     // nor an exponent after
+    if (bad & (valid | (valid + 1))) return false;  // (+ the byte after a partial block)
+    *keep = valid & ~(T & sT);                    // a run's bytes after its first
+    st.in_str = 0ull - (instr >> 63);
+    st.cT = T >> 63, st.cZ = Z >> 63, st.cDt = Dt >> 63, st.cX = X >> 63;
+    st.cadd = cout;
+    return true;
+}
+
+// The span [p, e) stripped into out (e - p bytes of room): bytes written, or -1 when it is
+// not strippable (out then holds garbage).  Whole blocks by plain loads and stores (the
+// stripped copy never runs ahead of the input, so a 64-byte store stays inside out); the
+// last partial block by a masked load and store (nothing read past e or written past the
+// stripped end).
+KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out) {
+    StripState st;
+    char* o = out;
+    while (e - p >= 64) {
+        const __m512i x = _mm512_loadu_si512(p);
+        uint64_t keep;
+        if (!strip_block(st, x, ~0ull, &keep)) return -1;
+#if KRR_STRIP_MASKED_STORES
         const unsigned cnt = (unsigned)_mm_popcnt_u64(keep);
-        _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), y);
+        _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), _mm512_maskz_compress_epi8(keep, x));
         o += cnt;
-        in_str = 0ull - (instr >> 63);
-        cT = T >> 63, cZ = Z >> 63, cDt = Dt >> 63, cX = X >> 63;
-        cadd = cout;
+#else
+        _mm512_storeu_si512(o, _mm512_maskz_compress_epi8(keep, x));
+        o += _mm_popcnt_u64(keep);
+#endif
         p += 64;
     }
-    // a run that ends the body: its last checks had no byte after it to look at
-    if (cDt) return -1;
+    if (p < e) {
+        const uint64_t valid = _bzhi_u64(~0ull, (unsigned)(e - p));
+        const __m512i x = _mm512_maskz_loadu_epi8(valid, p);
+        uint64_t keep;
+        if (!strip_block(st, x, valid, &keep)) return -1;
+        const unsigned cnt = (unsigned)_mm_popcnt_u64(keep);
+        _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), _mm512_maskz_compress_epi8(keep, x));
+        o += cnt;
+    } else if (st.cDt) {
+        return -1;  // a '.' ends the body: nothing after it to look at
+    }
     return o - out;
 }
 

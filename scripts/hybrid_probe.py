@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dev-threads", default="2,3,4,6")
     ap.add_argument("--strip", default="1")
+    ap.add_argument("--fixed-shares", default="", help="e.g. 0.05,0.1: time these host shares as set, no settling")
     a = ap.parse_args()
     from bench import body_fleet
     from krr_amd.core.runner import BatchedRunner
@@ -44,6 +45,21 @@ def main():
         up = packer.last_upload or {}
         print(f"strip={strip} device: {a.objects / td:.0f} objects/s ({td * 1e3:.1f} ms), link bytes "
               f"{up.get('bytes_sent', 0) / max(up.get('bytes', 1), 1):.3f} of the JSON", flush=True)
+        if a.fixed_shares:
+            for d in [int(x) for x in a.dev_threads.split(",")]:
+                runner.hybrid_device_threads = d
+                for sh in [float(x) for x in a.fixed_shares.split(",")]:
+                    t = float("inf")
+                    for _ in range(4):
+                        runner.hybrid_share = sh
+                        t0 = time.perf_counter()
+                        runner.recommend_from_bodies(cpu_b, mem_b, threads=a.threads, parser="hybrid")
+                        t = min(t, time.perf_counter() - t0)
+                    h = runner.hybrid_last
+                    print(f"strip={strip} fixed share {sh:.2f} dev_threads={d}: {a.objects / t:.0f} objects/s "
+                          f"({t * 1e3:.1f} ms), device {h['device_s'] * 1e3:.1f} ms {h['device_GBps']:.1f} GB/s, "
+                          f"host {h['host_s'] * 1e3:.1f} ms {h['host_GBps']:.1f} GB/s", flush=True)
+            continue
         for d in [int(x) for x in a.dev_threads.split(",")]:
             runner.hybrid_device_threads = d
             runner.hybrid_share = 0.2
