@@ -61,7 +61,7 @@ class DevicePacker:
         # (krr_pack_concat_strip, krr_amd/csrc/krr_strip.h): fewer bytes over PCIe, same CSR
         self.strip = (os.environ.get("KRR_PACK_STRIP", "1") != "0") if strip is None else bool(strip)
         self.last_upload: Optional[dict] = None
-        self.strip_runs_per_thread = 2  # runs per staging thread (each run = one H2D copy)
+        self.strip_runs_per_thread = 1  # runs per staging thread (each run = one H2D copy)
         self.device = torch.device("cuda", ctx.device)
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
@@ -100,6 +100,15 @@ class DevicePacker:
         return torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
 
     def _upload(self, flat, want_ts, st, launch, strip: bool = False):
+        """``flat``: the bodies (bytes), or a body table (int64 buffer addresses, int64
+        lengths) from ``_body_table``."""
+        if isinstance(flat, tuple):
+            return self._upload_table(int(flat[0].ctypes.data), flat[1], want_ts, st, launch, strip)
+        lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=len(flat))
+        ptrs = (ctypes.c_char_p * len(flat))(*flat)  # alive while the staging below runs
+        return self._upload_table(ctypes.addressof(ptrs), lens, want_ts, st, launch, strip)
+
+    def _upload_table(self, ptr_addr, lens, want_ts, st, launch, strip: bool = False):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
         copy stream and call ``launch(jb, a, b, tmp_v, tmp_t, lo, hi)`` on ``st`` for bodies
         [a, b) = bytes [lo, hi) once the chunk is there.  ``strip``: the bodies' timestamps
@@ -107,21 +116,19 @@ class DevicePacker:
         import torch
 
         dev = self.device
-        nb = len(flat)
-        lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=nb)
+        nb = len(lens)
         boffs = np.zeros(nb + 1, dtype=np.int64)
         np.cumsum(lens, out=boffs[1:])
         total = int(boffs[-1])
         stage = self._staging(total + 128)
         d_bodies = torch.empty(total + 128, dtype=torch.uint8, device=dev)
         if strip and not want_ts and nb:
-            return self._upload_stripped(flat, lens, boffs, total, stage, d_bodies, st, launch)
+            return self._upload_stripped(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch)
         d_boffs = torch.from_numpy(boffs).to(dev)
         slots = total // 8 + 1
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
         tmp_t = torch.empty(slots, dtype=torch.float64, device=dev) if want_ts else None
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
-        ptrs = (ctypes.c_char_p * nb)(*flat)
         host = load_library()
         cs = self._copy_stream
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
@@ -132,7 +139,7 @@ class DevicePacker:
             step = min(2 * step, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
             lo, hi = int(boffs[a]), int(boffs[b])
-            rc = host.krr_pack_concat(ctypes.addressof(ptrs) + a * ctypes.sizeof(ctypes.c_char_p),
+            rc = host.krr_pack_concat(ptr_addr + a * 8,
                                       lens[a:].ctypes.data, b - a, boffs[a:].ctypes.data,
                                       stage.data_ptr() + lo, self.threads)
             if rc != KRR_PACK_OK:
@@ -148,7 +155,7 @@ class DevicePacker:
         self.last_upload = {"bytes": total, "bytes_sent": total, "bodies": nb, "bodies_stripped": 0}
         return lens, boffs, total, jb, tmp_v, tmp_t
 
-    def _upload_stripped(self, flat, lens, boffs, total, stage, d_bodies, st, launch):
+    def _upload_stripped(self, ptr_addr, lens, boffs, total, stage, d_bodies, st, launch):
         """_upload with the timestamps cut while staging (krr_pack_concat_strip): each chunk's
         bodies are stripped by the host threads in runs, run r back to back inside its own
         unstripped extent of the staging buffer; the runs go to HBM back to back, so the device
@@ -159,7 +166,7 @@ class DevicePacker:
         import torch
 
         dev = self.device
-        nb = len(flat)
+        nb = len(lens)
         T = self.threads or len(os.sched_getaffinity(0))
         max_runs = max(1, self.strip_runs_per_thread * T)
         new_lens = np.empty(nb, dtype=np.int64)
@@ -171,7 +178,6 @@ class DevicePacker:
         slots = total // 8 + 1
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
-        ptrs = (ctypes.c_char_p * nb)(*flat)
         host = load_library()
         cs = self._copy_stream
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
@@ -182,7 +188,7 @@ class DevicePacker:
             step = min(2 * step, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
             lo = int(boffs[a])
-            rc = host.krr_pack_concat_strip(ctypes.addressof(ptrs) + a * ctypes.sizeof(ctypes.c_char_p),
+            rc = host.krr_pack_concat_strip(ptr_addr + a * 8,
                                             lens[a:].ctypes.data, b - a, boffs[a:].ctypes.data,
                                             stage.data_ptr() + lo, self.threads, max_runs,
                                             new_lens[a:].ctypes.data, runs.ctypes.data, ctypes.byref(n_runs))
@@ -328,18 +334,27 @@ class DevicePacker:
     def _pack_multi(self, resources, want_ts, want_counts, stream) -> list:
         import torch
 
-        flat: list = []
-        obj: list = []      # global object index (objects of resource r after those of r - 1)
-        body0, obj0 = [0], [0]
+        obj0 = [0]
         for per_object_bodies in resources:
-            base = obj0[-1]
-            for o, bodies in enumerate(per_object_bodies):
-                for b in bodies:
-                    flat.append(b if isinstance(b, bytes) else bytes(b))  # c_char_p takes bytes only
-                    obj.append(base + o)
-            body0.append(len(flat))
-            obj0.append(base + len(per_object_bodies))
-        n_obj, nb = obj0[-1], len(flat)
+            obj0.append(obj0[-1] + len(per_object_bodies))
+        table = _body_table(resources)
+        if table is not None:  # one native pass over the bodies (krr_pydec.cpp body_table)
+            ptr_col, lens_col, obj_col = table[:3]
+            flat = (ptr_col, lens_col)
+            obj = obj_col
+            body0 = np.searchsorted(obj_col, obj0, side="left").tolist()
+        else:
+            fl: list = []
+            ob: list = []      # global object index (objects of resource r after those of r - 1)
+            body0 = [0]
+            for r, per_object_bodies in enumerate(resources):
+                for o, bodies in enumerate(per_object_bodies):
+                    for b in bodies:
+                        fl.append(b if isinstance(b, bytes) else bytes(b))  # c_char_p takes bytes only
+                        ob.append(obj0[r] + o)
+                body0.append(len(fl))
+            flat, obj = fl, ob
+        n_obj, nb = obj0[-1], body0[-1]
         dev = self.device
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         if nb == 0:
@@ -400,6 +415,20 @@ class DevicePacker:
         # the staging buffer is reused by the next call: its copies are done (the parse
         # launches waited for them before the summary synchronised)
         return out
+
+
+def _body_table(resources):
+    """(buffer addresses, lengths, object ids, bytes per object) int64 arrays of the bodies of
+    resources[r][o][i] from the native extension (one pass, no per-body Python), or None
+    (extension missing, or a body that is not bytes)."""
+    from krr_amd.core.packing import _PYDEC
+
+    if _PYDEC is None or not hasattr(_PYDEC, "body_table"):
+        return None
+    t = _PYDEC.body_table(resources)
+    if t is None:
+        return None
+    return tuple(np.frombuffer(c, dtype=np.int64).copy() for c in t)
 
 
 _packers: dict = {}

@@ -223,11 +223,15 @@ class BatchedRunner:
             share = self.hybrid_share
             parts, raw_host = self._pack_hybrid(cpu_bodies, mem_bodies, threads=threads, host_then=host_then)
             with lock:
+                tp = time.perf_counter()
                 raws = [settings.run_fleet(parts[0])]
+                tp = time.perf_counter() - tp
             if len(parts) > 1:
                 raws.append(raw_host)
-                # balance the whole critical paths (pack + kernel pass on each side), not the packs
-                self.hybrid_share = _rebalance(share, time.perf_counter() - t0, done.get("host", t0) - t0)
+                # balance the whole critical paths (pack + kernel pass on each side), not the packs:
+                # the device side's pass starts only after the host side is joined, so its own
+                # duration is added to the device pack's, not read off the wall clock
+                self.hybrid_share = _rebalance(share, self.hybrid_last["device_s"] + tp, done.get("host", t0) - t0)
             raw = _concat_raw(raws)
             return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
@@ -269,8 +273,14 @@ class BatchedRunner:
             raise ValueError("cpu and memory bodies need one entry per object each")
         n = len(cpu_bodies)
         T = int(threads) or _host_threads()
-        nb = np.fromiter((sum(len(b) for b in cb) + sum(len(b) for b in mb)
-                          for cb, mb in zip(cpu_bodies, mem_bodies)), dtype=np.int64, count=n)
+        from krr_amd.core.device_pack import _body_table
+
+        table = _body_table([cpu_bodies, mem_bodies])
+        if table is not None:  # bytes per object from one native pass
+            nb = table[3][:n] + table[3][n:]
+        else:
+            nb = np.fromiter((sum(len(b) for b in cb) + sum(len(b) for b in mb)
+                              for cb, mb in zip(cpu_bodies, mem_bodies)), dtype=np.int64, count=n)
         cum = np.cumsum(nb)
         total = int(cum[-1]) if n else 0
         share = min(max(float(self.hybrid_share), 0.02), 0.8)

@@ -825,6 +825,63 @@ PyObject* slot_offset(PyObject*, PyObject* d) {
 
 PyObject* layout_ok(PyObject*, PyObject*) { return PyBool_FromLong(g_layout_ok); }
 
+// body_table(resources) -> (ptrs, lens, obj, obj_bytes): the device packer's flat body table in
+// one pass over resources[r][o][i] (bytes bodies, objects of resource r numbered after those of
+// r - 1): ptrs / lens / obj as int64 columns packed in bytes objects (the bodies' buffer
+// addresses — valid while the caller holds `resources` — lengths and object ids), obj_bytes
+// per object.  None when a body is not exactly bytes (the caller's Python path converts it).
+PyObject* body_table(PyObject*, PyObject* resources) {
+    PyObject* rs = PySequence_Fast(resources, "resources must be a sequence");
+    if (!rs) return nullptr;
+    std::vector<int64_t> ptrs, lens, obj, obj_bytes;
+    bool ok = true, plain = true;
+    int64_t base = 0;
+    for (Py_ssize_t r = 0; ok && plain && r < PySequence_Fast_GET_SIZE(rs); ++r) {
+        PyObject* objs = PySequence_Fast(PySequence_Fast_GET_ITEM(rs, r), "a resource must be a sequence");
+        if (!objs) {
+            ok = false;
+            break;
+        }
+        const Py_ssize_t n = PySequence_Fast_GET_SIZE(objs);
+        for (Py_ssize_t o = 0; ok && plain && o < n; ++o) {
+            PyObject* bodies = PySequence_Fast(PySequence_Fast_GET_ITEM(objs, o), "an object's bodies must be a sequence");
+            if (!bodies) {
+                ok = false;
+                break;
+            }
+            int64_t tot = 0;
+            for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(bodies); ++i) {
+                PyObject* b = PySequence_Fast_GET_ITEM(bodies, i);
+                if (!PyBytes_CheckExact(b)) {
+                    plain = false;
+                    break;
+                }
+                ptrs.push_back((int64_t)(intptr_t)PyBytes_AS_STRING(b));
+                lens.push_back((int64_t)PyBytes_GET_SIZE(b));
+                obj.push_back(base + o);
+                tot += (int64_t)PyBytes_GET_SIZE(b);
+            }
+            Py_DECREF(bodies);
+            obj_bytes.push_back(tot);
+        }
+        base += n;
+        Py_DECREF(objs);
+    }
+    Py_DECREF(rs);
+    if (!ok) return nullptr;
+    if (!plain) Py_RETURN_NONE;
+    auto col = [](const std::vector<int64_t>& v) {
+        return PyBytes_FromStringAndSize(reinterpret_cast<const char*>(v.data()), (Py_ssize_t)(v.size() * 8));
+    };
+    PyObject *a = col(ptrs), *l = col(lens), *ob = col(obj), *ob2 = col(obj_bytes);
+    PyObject* res = (a && l && ob && ob2) ? PyTuple_Pack(4, a, l, ob, ob2) : nullptr;
+    Py_XDECREF(a);
+    Py_XDECREF(l);
+    Py_XDECREF(ob);
+    Py_XDECREF(ob2);
+    return res;
+}
+
 PyMethodDef methods[] = {
     {"pack_resource", pack_resource, METH_VARARGS,
      "HistoryData list -> (float64 CSR values, lens, exactness class, pod lists) for one resource"},
@@ -834,6 +891,7 @@ PyMethodDef methods[] = {
     {"allocations", allocations, METH_VARARGS, "ResourceAllocations in construct() layout from value columns"},
     {"slot_offset", slot_offset, METH_O, "byte offset of an object slot (member descriptor)"},
     {"layout_ok", layout_ok, METH_NOARGS, "whether Decimals are read in place (else through str())"},
+    {"body_table", body_table, METH_O, "resources[r][o][i] bytes -> (ptrs, lens, obj, obj_bytes) int64 columns"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_krr_pydec", nullptr, -1, methods, nullptr, nullptr, nullptr, nullptr};

@@ -175,3 +175,22 @@ def test_concat_strip_runs_lay_out_the_stripped_bodies():
                 assert raw[pos:pos + len(want)] == want
                 pos += len(want)
             assert pos <= offs[runs[r + 1]]
+
+
+def test_body_table_matches_the_python_walk():
+    """krr_pydec.cpp body_table (the device packer's flat table in one native pass) against the
+    Python walk it replaces; None when a body is not bytes (the Python path converts those)."""
+    from krr_amd.core.device_pack import _body_table
+    from krr_amd.core.packing import _PYDEC
+
+    if _PYDEC is None:
+        pytest.skip("_krr_pydec.so not built")
+    res = [[[b"ab", b"c"], [], [b"defg"]], [[b"", b"hi"], [b"j"], []]]
+    ptrs, lens, obj, ob = _body_table(res)
+    flat = [(b, r * 3 + o) for r, objs in enumerate(res) for o, bodies in enumerate(objs) for b in bodies]
+    assert lens.tolist() == [len(b) for b, _ in flat]
+    assert obj.tolist() == [o for _, o in flat]
+    assert ob.tolist() == [sum(map(len, bodies)) for objs in res for bodies in objs]
+    assert [ctypes.string_at(int(p), int(n)) for p, n in zip(ptrs, lens)] == [b for b, _ in flat]
+    assert _body_table([[[b"x", bytearray(b"y")]]]) is None
+    assert _body_table([]) is not None and len(_body_table([])[0]) == 0
