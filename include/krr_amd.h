@@ -515,6 +515,12 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
                      const double* scratch_ts, const int64_t* counts, const int32_t* status,
                      const int64_t* out_pos, double* values, double* timestamps, void* stream);
 
+/* n host -> device copies enqueued on `stream` in order (dst[i] <- src[i], bytes[i] bytes;
+ * src page-locked for an asynchronous copy): the device packer's staged runs and body
+ * offsets, one call per chunk instead of one runtime call per run from Python. */
+int krr_copy_h2d_batch(krr_ctx* ctx, int64_t n, void* const* dst, const void* const* src, const int64_t* bytes,
+                       void* stream);
+
 /* Grouped bodies (`sum by (pod) (...)`, one series per pod: the host packer's
  * krr_pack_parse_grouped, include/krr_pack.h), one wave per SERIES:
  *   krr_json_find_series    every `[{"metric":` / `,{"metric":` starting in [begin, end) whose

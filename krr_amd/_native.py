@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "krr_abi_version",
     "krr_json_parse",
     "krr_json_compact",
+    "krr_copy_h2d_batch",
     "krr_json_find_series",
     "krr_json_parse_segments",
     "krr_json_gather",
@@ -322,6 +323,8 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse.restype = ctypes.c_int
         lib.krr_json_compact.argtypes = [vp, jb, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_compact.restype = ctypes.c_int
+        lib.krr_copy_h2d_batch.argtypes = [vp, i64, vp, vp, vp, vp]
+        lib.krr_copy_h2d_batch.restype = ctypes.c_int
         lib.krr_json_find_series.argtypes = [vp, jb, i64, i64, i64, vp, i64, vp, vp]
         lib.krr_json_find_series.restype = ctypes.c_int
         lib.krr_json_parse_segments.argtypes = [vp, jb, vp, vp, i64, ctypes.c_char_p, i32, vp, vp, vp, vp]
@@ -741,6 +744,18 @@ class Context:
             scratch_ts.data_ptr() if timestamps is not None else None, counts.data_ptr(), status.data_ptr(),
             out_pos.data_ptr(), values.data_ptr(), timestamps.data_ptr() if timestamps is not None else None,
             self._stream(stream)))
+
+    def copy_h2d_batch(self, dst, src, nbytes, stream=None) -> None:
+        """int64 arrays (numpy) of device destinations, host sources (page-locked) and byte
+        counts: one asynchronous copy each, in order, on ``stream`` (krr_copy_h2d_batch)."""
+        import numpy as np
+
+        dst, src, nbytes = (np.ascontiguousarray(a, dtype=np.int64) for a in (dst, src, nbytes))
+        n = len(nbytes)
+        if len(dst) != n or len(src) != n:
+            raise ValueError("copy_h2d_batch: dst / src / nbytes differ in length")
+        self._check(self._lib.krr_copy_h2d_batch(self._h, n, dst.ctypes.data, src.ctypes.data, nbytes.ctypes.data,
+                                                 self._stream(stream)))
 
     def json_find_series(self, jb: KrrJsonBodies, candidates, n_candidates, begin: int = 0, end: Optional[int] = None,
                          limit: Optional[int] = None, stream=None) -> None:

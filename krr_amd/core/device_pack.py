@@ -181,11 +181,15 @@ class DevicePacker:
         host = load_library()
         cs = self._copy_stream
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
+        o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
         a = 0
         step = min(self.chunk_bytes, 16 << 20)  # small first chunks: the DMA starts early
         while a < nb:
             b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
-            step = min(2 * step, self.chunk_bytes)
+            # x1.5 per chunk: staging (~130 GB/s of JSON on 16 threads) stays ahead of the
+            # link (~85 GB/s of JSON once stripped) while the chunks grow
+            step = min(step * 3 // 2, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
             lo = int(boffs[a])
             rc = host.krr_pack_concat_strip(ptr_addr + a * 8,
@@ -196,14 +200,18 @@ class DevicePacker:
                 raise PrometheusResponseError(rc, "krr_pack_concat_strip failed")
             np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
             no[a + 1:b + 1] += no[a]
+            # every run of the chunk, then its body offsets: one native call of async copies
+            nr = n_runs.value
+            b0 = a + runs[:nr]
+            dst = np.empty(nr + 1, dtype=np.int64)
+            src = np.empty(nr + 1, dtype=np.int64)
+            nby = np.empty(nr + 1, dtype=np.int64)
+            dst[:nr] = d_base + no[b0]
+            src[:nr] = s_base + boffs[b0]
+            nby[:nr] = no[a + runs[1:nr + 1]] - no[b0]
+            dst[nr], src[nr], nby[nr] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
+            self.ctx.copy_h2d_batch(dst, src, nby, stream=cs)
             with torch.cuda.stream(cs):
-                for r in range(n_runs.value):
-                    b0, b1 = a + int(runs[r]), a + int(runs[r + 1])
-                    d0, d1 = int(no[b0]), int(no[b1])
-                    if d1 > d0:
-                        s0 = int(boffs[b0])
-                        d_bodies[d0:d1].copy_(stage[s0:s0 + (d1 - d0)], non_blocking=True)
-                d_boffs[a:b + 1].copy_(new_offs[a:b + 1], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(cs)
             st.wait_event(ev)

@@ -4383,6 +4383,21 @@ int krr_json_compact(krr_ctx* ctx, const krr_json_bodies* b, const double* scrat
     return KRR_OK;
 }
 
+int krr_copy_h2d_batch(krr_ctx* ctx, int64_t n, void* const* dst, const void* const* src, const int64_t* bytes,
+                       void* stream) {
+    if (!ctx) return KRR_E_INVALID;
+    if (n < 0 || (n > 0 && (!dst || !src || !bytes))) return set_err(ctx, KRR_E_INVALID, "copy: bad batch%s", "");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    for (int64_t i = 0; i < n; ++i) {
+        if (bytes[i] < 0 || (bytes[i] > 0 && (!dst[i] || !src[i])))
+            return set_err(ctx, KRR_E_INVALID, "copy: bad entry %s%lld", "", (long long)i);
+        if (bytes[i] == 0) continue;
+        KRR_HIP(ctx, hipMemcpyAsync(dst[i], src[i], (size_t)bytes[i], hipMemcpyHostToDevice, (hipStream_t)stream));
+    }
+    return KRR_OK;
+}
+
 int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t begin, int64_t end, int64_t limit,
                          int64_t* candidates, int64_t cap, uint64_t* n_candidates, void* stream) {
     if (!ctx) return KRR_E_INVALID;

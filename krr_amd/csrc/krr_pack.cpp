@@ -14,6 +14,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -460,6 +465,68 @@ int pool_size(int32_t threads, int64_t work) {
     return t;
 }
 
+// Worker threads kept for the life of the process: the device packer stages a batch in ~20
+// chunks, one parallel call each, and spawning 15 threads per call cost ~0.3 ms of the
+// caller's time per chunk, with the link idle behind it.  A call hands `helpers` tickets of
+// one job to the pool (spawning workers only when too few are idle) and works on the job
+// itself; jobs of concurrent callers (the hybrid parser's two sides) queue side by side.
+class WorkerPool {
+  public:
+    void run(int helpers, const std::function<void()>& work) {
+        auto job = std::make_shared<Job>();
+        job->work = &work;
+        job->pending = helpers;
+        {
+            std::lock_guard<std::mutex> l(m_);
+            for (int k = 0; k < helpers; ++k) queue_.push_back(job);
+            for (int k = idle_; k < (int)queue_.size(); ++k) {
+                std::thread(&WorkerPool::loop, this).detach();  // lives as long as the process
+                ++idle_;
+            }
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> l(job->m);
+        job->done.wait(l, [&] { return job->pending == 0; });
+    }
+
+  private:
+    struct Job {
+        const std::function<void()>* work = nullptr;
+        int pending = 0;
+        std::mutex m;
+        std::condition_variable done;
+    };
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Job> job;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [&] { return !queue_.empty(); });
+                job = queue_.front();
+                queue_.pop_front();
+                --idle_;
+            }
+            (*job->work)();
+            {
+                std::lock_guard<std::mutex> l(job->m);
+                if (--job->pending == 0) job->done.notify_all();
+            }
+            std::lock_guard<std::mutex> l(m_);
+            ++idle_;
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Job>> queue_;
+    int idle_ = 0;
+};
+
+WorkerPool& worker_pool() {
+    static WorkerPool* pool = new WorkerPool();  // never destroyed: its threads outlive static destructors
+    return *pool;
+}
+
 template <class F>
 void parallel_for(int64_t n, int32_t threads, F f) {
     const int t = pool_size(threads, n);
@@ -471,7 +538,7 @@ void parallel_for(int64_t n, int32_t threads, F f) {
     // items (grouped bodies) still spread over the pool
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(8, n / ((int64_t)t * 4)));
     std::atomic<int64_t> next{0};
-    auto worker = [&]() {
+    const std::function<void()> worker = [&]() {
         for (;;) {
             const int64_t b = next.fetch_add(chunk);
             if (b >= n) return;
@@ -479,11 +546,7 @@ void parallel_for(int64_t n, int32_t threads, F f) {
             for (int64_t i = b; i < e; ++i) f(i);
         }
     };
-    std::vector<std::thread> pool;
-    pool.reserve((size_t)t - 1);
-    for (int k = 1; k < t; ++k) pool.emplace_back(worker);
-    worker();
-    for (auto& th : pool) th.join();
+    worker_pool().run(t - 1, worker);
 }
 
 }  // namespace
