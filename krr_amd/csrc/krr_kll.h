@@ -1963,6 +1963,15 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
         KllTailProc P{sh, KllTail{0u, full0 ? 1u : 0u, tau}, tail, A.tcap, lane};
         bool dense = !full0;
         uint32_t nread = 0;  // lines read (uniform)
+#ifdef KRR_KLL_X_SPARSE_NOFILTER  // profiling variant: the lines are loaded, not filtered (rows not valid)
+        double xsink = 0.0;
+#define KLL_SPARSE_CHUNK(c)                                                  \
+    do {                                                                     \
+        _Pragma("unroll") for (int r_ = 0; r_ < kUnroll; ++r_) xsink = fmax(xsink, fmax((c)[r_].x, (c)[r_].y)); \
+    } while (0)
+#else
+#define KLL_SPARSE_CHUNK(c) P.chunk(c)
+#endif
         // sparse attempts: the threshold at the margin, then (a miss: fewer than `tail` keys above
         // it) at KRR_KLL_TAIL_RETRY margins; then the whole slice, every present key a candidate
 #pragma unroll 1
@@ -2023,7 +2032,11 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                 for (int c = 0; c < 8; ++c) nk[c] = cb + 8 + c < nch ? L[(size_t)(cb + 8 + c) * 64u + lane] : 0u;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
+#ifndef KRR_KLL_X_SPARSE_NOLOAD
                     const uint64_t m = ballot(cb + c < nch && lk[c] >= t32);
+#else  // profiling variant: the maxima are scanned, no line is read (rows not valid)
+                    const uint64_t m = ballot(cb + c < nch && lk[c] >= t32 && t32 == 0xFFFFFFFFu);
+#endif
                     if (!m) continue;
                     if ((m >> lane) & 1ull) q[qn + lane_prefix(m)] = (uint32_t)((cb + c) * 64 + lane);
                     qn += popc64(m);
@@ -2033,14 +2046,14 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
 #if KRR_KLL_SPARSE_PIPE
                         double2 cn[kUnroll];
                         load_batch(64u, cn);
-                        if (pend) P.chunk(cp);
+                        if (pend) KLL_SPARSE_CHUNK(cp);
 #pragma unroll
                         for (int r = 0; r < kUnroll; ++r) cp[r] = cn[r];
                         pend = true;
 #else
                         double2 cn[kUnroll];
                         load_batch(64u, cn);
-                        P.chunk(cn);
+                        KLL_SPARSE_CHUNK(cn);
 #endif
                         const uint32_t rest = qn - 64u;  // < 64
                         const uint32_t v = (uint32_t)lane < rest ? q[64 + lane] : 0u;
@@ -2052,14 +2065,17 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
                 }
             }
 #if KRR_KLL_SPARSE_PIPE
-            if (pend) P.chunk(cp);
+            if (pend) KLL_SPARSE_CHUNK(cp);
 #endif
             if (qn) {
                 double2 cn[kUnroll];
                 load_batch(qn, cn);
-                P.chunk(cn);
+                KLL_SPARSE_CHUNK(cn);
             }
             dense = P.ts.tl < tail;  // a miss
+#if defined(KRR_KLL_X_SPARSE_NOFILTER) || defined(KRR_KLL_X_SPARSE_NOLOAD)
+            dense = false;  // profiling variants: no retry, no restream
+#endif
             if (!dense) break;
         }
         if (dense) P.ts = KllTail{0u, 0u, 0.0};  // the whole slice, every present key a candidate
@@ -2068,11 +2084,18 @@ __global__ __launch_bounds__(64, KRR_KLL_TAIL_WAVES_PER_SIMD) void k_kll_tail_li
             kll_stream<KllTailProc, KRR_KLL_TAIL_STREAM>(A.vals, beg, end, npad, P, lane);
             nread += (uint32_t)nch * 64u;
         }
+#ifndef KRR_KLL_X_SPARSE_NOEXPORT
         const uint32_t tl_out = kll_tail_export(sh, P.ts, tail, row + kKllHdr + budget, lane);
+#else  // profiling variant: no sort / export (rows not valid)
+        const uint32_t tl_out = P.ts.tl;
+#endif
         if (lane == 0) {
             row[6] = tl_out;
             if (LA.lines_read) LA.lines_read[s] = nread;
         }
+#ifdef KRR_KLL_X_SPARSE_NOFILTER
+        if (lane == 0) row[15] = dbits(xsink);
+#endif
         __syncthreads();
     }
 }

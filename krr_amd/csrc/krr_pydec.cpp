@@ -465,17 +465,18 @@ struct Model {
     int n = 0;
     PyObject* fields_set = nullptr;
     Py_ssize_t fs_offset = 0;
+    bool skip_dict = false;  // profiling variant KRR_X_NODICT only: instances without a dict
 
     PyObject* make(PyObject* a, PyObject* b, PyObject* c = nullptr) const {
         PyObject* o = cls->tp_alloc(cls, 0);
         if (!o) return nullptr;
         // the instance dict as attribute assignment would create it: a split table sharing the
         // class's cached keys (the fields, in order), about half the size and time of a new dict
-        PyObject* d = PyObject_GenericGetDict(o, nullptr);
+        PyObject* d = skip_dict ? nullptr : PyObject_GenericGetDict(o, nullptr);
         PyObject* vals[3] = {a, b, c};
-        bool bad = !d;
-        for (int i = 0; !bad && i < n; ++i) bad = _PyDict_SetItem_KnownHash(d, names[i], vals[i], hashes[i]) < 0;
-        if (!bad) untrack(d);
+        bool bad = !d && !skip_dict;
+        for (int i = 0; !bad && d && i < n; ++i) bad = _PyDict_SetItem_KnownHash(d, names[i], vals[i], hashes[i]) < 0;
+        if (!bad && d) untrack(d);
         Py_XDECREF(d);
         if (bad) {
             Py_DECREF(o);
@@ -659,6 +660,9 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
             return nullptr;
         }
     }
+#ifdef KRR_X_NODICT  // profiling variant: the scan's models without instance dicts (not valid)
+    for (int i = 0; i < 3; ++i) M[i].skip_dict = true;
+#endif
     PyObject* ob = PySequence_Fast(objects, "objects must be a sequence");
     if (!ob) return nullptr;
     PyObject* rb = PySequence_Fast(recs, "recommendations must be a sequence");
@@ -710,7 +714,11 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
                 bool pc = false, pr = false;
                 PyObject* cv = dict_get(sel_cur[j], rt, h_rt[k], &pc);
                 PyObject* rv = cv ? dict_get(sel_rec[j], rt, h_rt[k], &pr) : nullptr;
+#ifndef KRR_X_NOSEV
                 const int code = rv ? severity_code(cv, rv, settle) : -1;
+#else  // profiling variant: no severity decided (scans not valid)
+                const int code = rv ? kOk : -1;
+#endif
                 PyObject* r = code >= 0 ? M[0].make(rv, PyTuple_GET_ITEM(sevs, code)) : nullptr;
                 bad = !r || _PyDict_SetItem_KnownHash(sel_out[j], rt, r, h_rt[k]) < 0;
                 keys_ok = keys_ok && pc;  // Result's score indexes the current allocations (result.py:137-143)
