@@ -186,6 +186,9 @@ class DevicePacker:
         a = 0
         step = min(self.chunk_bytes, 16 << 20)  # small first chunks: the DMA starts early
         while a < nb:
+            left = total - int(boffs[a])
+            if left <= step + step // 2:  # the end: a small last chunk, whose parse is the tail
+                step = max(left * 3 // 4, 16 << 20)
             b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
             # x1.5 per chunk: staging (~130 GB/s of JSON on 16 threads) stays ahead of the
             # link (~85 GB/s of JSON once stripped) while the chunks grow

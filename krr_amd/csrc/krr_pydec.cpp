@@ -466,8 +466,62 @@ struct Model {
     PyObject* fields_set = nullptr;
     Py_ssize_t fs_offset = 0;
     bool skip_dict = false;  // profiling variant KRR_X_NODICT only: instances without a dict
+    // A prototype instance dict (split table, field k's value at ma_values[k]): each new
+    // instance's dict is PyDict_Copy of it (for a split table: the shared keys and a copy of
+    // the values array) with the values then replaced in place — no key lookups.  Null when
+    // the class's dicts are not laid out so (the SetItem path below is used).
+    PyObject* proto = nullptr;
+
+    ~Model() { Py_XDECREF(proto); }
+
+    // Build `proto` from one instance made the slow way with the field names as sentinel
+    // values, if its dict is a split table holding field k at value slot k.
+    void init_proto() {
+        PyObject* o = make_slow(names[0], names[1], n > 2 ? names[2] : nullptr);
+        if (!o) {
+            PyErr_Clear();
+            return;
+        }
+        PyObject** dp = _PyObject_GetDictPtr(o);
+        PyObject* d = dp ? *dp : nullptr;
+        bool ok = d && PyDict_CheckExact(d) && reinterpret_cast<PyDictObject*>(d)->ma_values != nullptr &&
+                  PyDict_GET_SIZE(d) == n;
+        for (int k = 0; ok && k < n; ++k) ok = reinterpret_cast<PyDictObject*>(d)->ma_values[k] == names[k];
+        if (ok) {
+            Py_INCREF(d);
+            proto = d;
+        }
+        Py_DECREF(o);
+    }
 
     PyObject* make(PyObject* a, PyObject* b, PyObject* c = nullptr) const {
+        if (!proto) return make_slow(a, b, c);
+        PyObject* o = cls->tp_alloc(cls, 0);
+        if (!o) return nullptr;
+        PyObject** dp = _PyObject_GetDictPtr(o);
+        PyObject* d = dp ? PyDict_Copy(proto) : nullptr;
+        if (!d || reinterpret_cast<PyDictObject*>(d)->ma_values == nullptr) {  // (a combined copy: never)
+            Py_XDECREF(d);
+            Py_DECREF(o);
+            return dp ? nullptr : make_slow(a, b, c);
+        }
+        PyObject** v = reinterpret_cast<PyDictObject*>(d)->ma_values;
+        PyObject* vals[3] = {a, b, c};
+        for (int k = 0; k < n; ++k) {
+            PyObject* old = v[k];
+            Py_INCREF(vals[k]);
+            v[k] = vals[k];
+            Py_DECREF(old);
+        }
+        untrack(d);
+        *dp = d;
+        untrack(o);
+        Py_INCREF(fields_set);
+        *reinterpret_cast<PyObject**>(reinterpret_cast<char*>(o) + fs_offset) = fields_set;
+        return o;
+    }
+
+    PyObject* make_slow(PyObject* a, PyObject* b, PyObject* c = nullptr) const {
         PyObject* o = cls->tp_alloc(cls, 0);
         if (!o) return nullptr;
         // the instance dict as attribute assignment would create it: a split table sharing the
@@ -507,6 +561,9 @@ bool init_model(Model* m, PyObject* cls, PyObject* names, PyObject* fields_set, 
     }
     m->fields_set = fields_set;
     m->fs_offset = fs_offset;
+#ifndef KRR_X_NOPROTO
+    m->init_proto();
+#endif
     return true;
 }
 
