@@ -219,19 +219,23 @@ class BatchedRunner:
                 done["host"] = time.perf_counter()
                 return r
 
+            def device_then(fleet):  # the device part's kernel pass, before the host side is joined
+                with lock:
+                    r = settings.run_fleet(fleet)
+                done["device"] = time.perf_counter()
+                return r
+
             t0 = time.perf_counter()
             share = self.hybrid_share
-            parts, raw_host = self._pack_hybrid(cpu_bodies, mem_bodies, threads=threads, host_then=host_then)
-            with lock:
-                tp = time.perf_counter()
-                raws = [settings.run_fleet(parts[0])]
-                tp = time.perf_counter() - tp
+            parts, (raw_host, raw_dev) = self._pack_hybrid(cpu_bodies, mem_bodies, threads=threads,
+                                                           host_then=host_then, device_then=device_then)
             if len(parts) > 1:
-                raws.append(raw_host)
-                # balance the whole critical paths (pack + kernel pass on each side), not the packs:
-                # the device side's pass starts only after the host side is joined, so its own
-                # duration is added to the device pack's, not read off the wall clock
-                self.hybrid_share = _rebalance(share, self.hybrid_last["device_s"] + tp, done.get("host", t0) - t0)
+                raws = [raw_dev, raw_host]
+                # balance the whole critical paths (pack + kernel pass on each side), not the packs
+                self.hybrid_share = _rebalance(share, done["device"] - t0, done.get("host", t0) - t0)
+            else:
+                with lock:
+                    raws = [settings.run_fleet(parts[0])]
             raw = _concat_raw(raws)
             return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
         return self.recommend_packed(self.pack_from_bodies(cpu_bodies, mem_bodies, threads, parser))
@@ -256,10 +260,12 @@ class BatchedRunner:
         return self._pack_hybrid(cpu_bodies, mem_bodies, threads, device)[0]
 
     def _pack_hybrid(self, cpu_bodies, mem_bodies, threads: int = 0, device: Optional[int] = None,
-                     host_then=None):
+                     host_then=None, device_then=None):
         """pack_hybrid, plus ``host_then(host_fleet)`` run on the worker thread as soon as the
         host part is packed (e.g. its upload and kernel pass, overlapping the device part's
-        pack); returns (parts, host_then's result or None)."""
+        pack) and ``device_then(device_fleet)`` on the calling thread as soon as the device part
+        is packed (before the host side is joined); returns (parts, (host_then's result,
+        device_then's result)), None for a callback not run or whose part was discarded."""
         import os
         import threading
         import time
@@ -287,7 +293,7 @@ class BatchedRunner:
         k = int(np.searchsorted(cum, (1.0 - share) * total, side="left")) + 1 if n else 0
         k = min(max(k, 1), n - 1)
         if T < 3 or n < 2:
-            return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)], None
+            return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)], (None, None)
         # staging threads (hybrid_device_threads); the host parser gets the rest.  A stripping
         # staging thread moves ~8x the JSON bytes per second of a host parser thread and keeps
         # fewer bytes on the link, so it gets half the threads (a plain copy: a quarter)
@@ -317,11 +323,16 @@ class BatchedRunner:
         worker = threading.Thread(target=host_part, name="krr-hybrid-host", daemon=True)
         worker.start()
         t0 = time.perf_counter()
+        dev_then = None
         try:
             dev_fleet = self.pack_bodies_device(cpu_bodies[:k], mem_bodies[:k], threads=t_dev, device=device)
-            if self.last_pack_via != ("device", "device"):
+            dev_via = self.last_pack_via
+            if dev_via != ("device", "device"):
                 device_fell_back.set()
             dev_s = time.perf_counter() - t0
+            if device_then is not None and dev_via == ("device", "device"):
+                dev_then = device_then(dev_fleet)
+            self.last_pack_via = dev_via
         finally:
             worker.join()
         if "exc" in host_out:
@@ -330,7 +341,7 @@ class BatchedRunner:
             # a body one side rejected: the outcome is the host packer's on the whole batch
             self.last_pack_via = ("host", "host")
             return [PackedFleet(pack_query_range_bodies(cpu_bodies, threads=threads, alloc=alloc),
-                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))], None
+                                pack_query_range_bodies(mem_bodies, threads=threads, alloc=alloc))], (None, None)
         b_dev, b_host = int(cum[k - 1]), total - int(cum[k - 1])
         r_dev, r_host = b_dev / max(dev_s, 1e-9), b_host / max(host_out["s"], 1e-9)
         self.hybrid_last = {"share": share, "split_object": k, "device_s": dev_s, "host_s": host_out["s"],
@@ -340,7 +351,7 @@ class BatchedRunner:
         self.hybrid_share = _rebalance(share, dev_s, host_out["s"])
         self.hybrid_last.update(bytes_device=b_dev, bytes_host=b_host)
         self.last_pack_via = ("hybrid", "hybrid")
-        return [dev_fleet, host_out["fleet"]], host_out.get("then")
+        return [dev_fleet, host_out["fleet"]], (host_out.get("then"), dev_then)
 
     @staticmethod
     def body_shard_bounds(objects: Sequence[K8sObjectData], world: int) -> list:
