@@ -131,6 +131,8 @@ def parse():
                     help="N > 1 host path: the parser each rank uses for its shard's bodies")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-path measurements (H2D, native packer, end-to-end from JSON bodies)")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="leave the process on every CPU it may use (default: the GPU-local NUMA node's)")
     ap.add_argument("--no-right-size", action="store_true",
                     help="config-4 leg: skip right-sizing + scanning the whole fleet on rank 0 after its steps")
     args = ap.parse_args()
@@ -140,6 +142,9 @@ def parse():
 
 
 _LAST_PHASE = ["started"]
+
+
+_NUMA: Optional[dict] = None  # this rank's NUMA binding (main), reported in the host-path keys
 
 
 def phase(name: str) -> None:
@@ -375,6 +380,14 @@ def main():
                  f"per rank (KRR_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # the host side (staging, host packer, DMA sources) next to this rank's GPU: threads created
+    # and pages first touched from here on stay on its NUMA node (krr_amd.utils.numa)
+    global _NUMA
+    if not args.no_numa_bind:
+        from krr_amd.utils.numa import bind_local, gpu_numa_node
+
+        cpus = bind_local(local)
+        _NUMA = {"gpu_node": gpu_numa_node(local), "bound_cpus": len(cpus) if cpus else None}
     # RCCL ("nccl") over xGMI in production; KRR_BENCH_BACKEND=gloo rehearses the
     # N>1 path with several ranks on ONE GPU (RCCL refuses duplicate devices).
     backend = os.environ.get("KRR_BENCH_BACKEND", "nccl")
@@ -921,6 +934,7 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     out["e2e_device_equals_host"] = e2e["device"][1] == e2e["host"][1]
     out["e2e_hybrid_equals_host"] = e2e["hybrid"][1] == e2e["host"][1]
     out["e2e_hybrid_split"] = runner.hybrid_last
+    out["host_numa"] = _NUMA
     from krr_amd.core.device_pack import default_packer as _dp
 
     # the device side's last staging: JSON bytes vs bytes over PCIe (timestamps cut, krr_strip.h)

@@ -1,0 +1,67 @@
+"""NUMA placement of the host side next to the GPU it feeds.
+
+The host path (staging bodies into page-locked memory, the host packer, the H2D DMA) moves
+several GB per fleet through host memory; on a two-socket host, threads and pages on the far
+socket send every byte over the inter-socket link.  ``gpu_local_cpus(device)`` reads the GPU's
+NUMA node from sysfs (its PCI address from the HIP runtime); ``bind_local(device)`` restricts
+this process (and every thread it creates afterwards, the host runtime's worker pool included)
+to that node's CPUs, within the CPUs the process may already use.  Pages are placed by first
+touch, so bind before allocating the bodies and staging buffers."""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+
+def _parse_cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def gpu_numa_node(device: int = 0) -> Optional[int]:
+    """The NUMA node of HIP device ``device`` (None when sysfs does not say)."""
+    import torch
+
+    try:
+        bus = torch.cuda.get_device_properties(device).pci_bus_id
+        dom = getattr(torch.cuda.get_device_properties(device), "pci_domain_id", 0)
+        dev = getattr(torch.cuda.get_device_properties(device), "pci_device_id", 0)
+        addr = f"{dom:04x}:{bus:02x}:{dev:02x}.0"
+        with open(f"/sys/bus/pci/devices/{addr}/numa_node") as fh:
+            node = int(fh.read().strip())
+        return node if node >= 0 else None
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return None
+
+
+def gpu_local_cpus(device: int = 0) -> Optional[set]:
+    """CPUs of the GPU's NUMA node that this process may use, or None."""
+    node = gpu_numa_node(device)
+    if node is None:
+        return None
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as fh:
+            local = _parse_cpulist(fh.read())
+    except OSError:
+        return None
+    mine = local & os.sched_getaffinity(0)
+    return mine or None
+
+
+def bind_local(device: int = 0) -> Optional[set]:
+    """Restrict this process to the GPU-local CPUs (returns them), or leave it (None)."""
+    cpus = gpu_local_cpus(device)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+__all__ = ["bind_local", "gpu_local_cpus", "gpu_numa_node"]
