@@ -42,8 +42,23 @@ def gpu_numa_node(device: int = 0) -> Optional[int]:
         return None
 
 
-def gpu_local_cpus(device: int = 0) -> Optional[set]:
-    """CPUs of the GPU's NUMA node that this process may use, or None."""
+def _one_per_core(cpus: set) -> set:
+    """The lowest-numbered hardware thread of each core in ``cpus`` (SMT siblings dropped)."""
+    out = set()
+    for c in sorted(cpus):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as fh:
+                sib = _parse_cpulist(fh.read())
+        except OSError:
+            sib = {c}
+        if min(sib & cpus or {c}) == c:
+            out.add(c)
+    return out
+
+
+def gpu_local_cpus(device: int = 0, one_per_core: bool = False) -> Optional[set]:
+    """CPUs of the GPU's NUMA node that this process may use (one hardware thread per core
+    with ``one_per_core``: two busy threads of ours never share a core), or None."""
     node = gpu_numa_node(device)
     if node is None:
         return None
@@ -53,12 +68,14 @@ def gpu_local_cpus(device: int = 0) -> Optional[set]:
     except OSError:
         return None
     mine = local & os.sched_getaffinity(0)
+    if one_per_core and mine:
+        mine = _one_per_core(mine)
     return mine or None
 
 
-def bind_local(device: int = 0) -> Optional[set]:
+def bind_local(device: int = 0, one_per_core: bool = False) -> Optional[set]:
     """Restrict this process to the GPU-local CPUs (returns them), or leave it (None)."""
-    cpus = gpu_local_cpus(device)
+    cpus = gpu_local_cpus(device, one_per_core)
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus

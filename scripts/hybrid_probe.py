@@ -18,13 +18,14 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dev-threads", default="2,3,4,6")
     ap.add_argument("--strip", default="1")
+    ap.add_argument("--cores", action="store_true", help="with --numa: one hardware thread per core")
     ap.add_argument("--numa", action="store_true", help="bind to the GPU-local NUMA node first (krr_amd.utils.numa)")
     ap.add_argument("--fixed-shares", default="", help="e.g. 0.05,0.1: time these host shares as set, no settling")
     a = ap.parse_args()
     if a.numa:
         from krr_amd.utils.numa import bind_local, gpu_numa_node
 
-        cpus = bind_local(0)
+        cpus = bind_local(0, one_per_core=a.cores)
         print(f"numa: GPU 0 on node {gpu_numa_node(0)}, bound to {len(cpus) if cpus else 0} CPUs", flush=True)
     from bench import body_fleet
     from krr_amd.core.runner import BatchedRunner

@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--objects", type=int, default=2000)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--cores", action="store_true", help="with --numa: one hardware thread per core")
     ap.add_argument("--numa", action="store_true")
     ap.add_argument("--only", default="", help="strip,chunk_mib,runs_per_thread: one configuration (for traces)")
     a = ap.parse_args()
@@ -22,7 +23,7 @@ def main():
     if a.numa:
         from krr_amd.utils.numa import bind_local, gpu_numa_node
 
-        cpus = bind_local(0)
+        cpus = bind_local(0, one_per_core=a.cores)
         print(f"numa: GPU 0 on node {gpu_numa_node(0)}, bound to {len(cpus) if cpus else 0} CPUs", flush=True)
     from bench import body_fleet
     from krr_amd import _native
