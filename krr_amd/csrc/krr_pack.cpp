@@ -19,6 +19,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <pthread.h>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -522,9 +523,20 @@ class WorkerPool {
     int idle_ = 0;
 };
 
+// Never destroyed: its threads outlive static destructors.  A child forked while the pool has
+// workers (multiprocessing's fork start method) gets the pool's memory but none of its threads,
+// and maybe a mutex another thread held: the child starts a fresh pool (the old one leaks).
+WorkerPool* g_pool = nullptr;
+std::once_flag g_pool_once;
+
+void pool_after_fork_in_child() { g_pool = new WorkerPool(); }
+
 WorkerPool& worker_pool() {
-    static WorkerPool* pool = new WorkerPool();  // never destroyed: its threads outlive static destructors
-    return *pool;
+    std::call_once(g_pool_once, [] {
+        g_pool = new WorkerPool();
+        pthread_atfork(nullptr, nullptr, pool_after_fork_in_child);
+    });
+    return *g_pool;
 }
 
 template <class F>
