@@ -176,6 +176,24 @@ __device__ __forceinline__ void kll_cross(double (&x)[N], bool take_min) {
     }
 }
 
+#ifndef KRR_KLL_BATCHER
+#define KRR_KLL_BATCHER 1  // Batcher's odd-even networks (63 / 25 compare-exchanges) instead of bitonic (80 / 32)
+#endif
+#if KRR_KLL_BATCHER
+// Batcher's odd-even merge sort of 16 and odd-even merge of two sorted 8-runs, as (i, j)
+// compare-exchange pairs (scripts-free: both checked on all 2^16 0-1 inputs, the 0-1 principle).
+// Any sorting network leaves the same ascending keys (no NaN, -0 folded), so rows do not change.
+constexpr int kKllSort16[126] = {0, 1, 2, 3, 0, 2, 1, 3, 1, 2, 4, 5, 6, 7, 4, 6, 5, 7, 5, 6, 0, 4, 2, 6, 2, 4, 1, 5, 3, 7, 3, 5, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 8, 10, 9, 11, 9, 10, 12, 13, 14, 15, 12, 14, 13, 15, 13, 14, 8, 12, 10, 14, 10, 12, 9, 13, 11, 15, 11, 13, 9, 10, 11, 12, 13, 14, 0, 8, 4, 12, 4, 8, 2, 10, 6, 14, 6, 10, 2, 4, 6, 8, 10, 12, 1, 9, 5, 13, 5, 9, 3, 11, 7, 15, 7, 11, 3, 5, 7, 9, 11, 13, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14};
+constexpr int kKllMerge16[50] = {0, 8, 4, 12, 4, 8, 2, 10, 6, 14, 6, 10, 2, 4, 6, 8, 10, 12, 1, 9, 5, 13, 5, 9, 3, 11, 7, 15, 7, 11, 3, 5, 7, 9, 11, 13, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14};
+__device__ __forceinline__ void kll_sort16(double (&x)[16]) {
+#pragma unroll
+    for (int c = 0; c < 63; ++c) kll_cxd(x[kKllSort16[2 * c]], x[kKllSort16[2 * c + 1]]);
+}
+__device__ __forceinline__ void kll_merge16(double (&z)[16]) {
+#pragma unroll
+    for (int c = 0; c < 25; ++c) kll_cxd(z[kKllMerge16[2 * c]], z[kKllMerge16[2 * c + 1]]);
+}
+#else
 // The lane's 16 keys ascending (a full bitonic sort in registers).
 __device__ __forceinline__ void kll_sort16(double (&x)[16]) {
 #pragma unroll
@@ -207,6 +225,7 @@ __device__ __forceinline__ void kll_merge16(double (&z)[16]) {
             if (!(i & j)) kll_cxd(z[i], z[i + j]);
     }
 }
+#endif
 
 // 512 keys ascending across the wave: lane l holds positions 8l .. 8l+7, each lane's 8
 // already ascending (odd lanes' runs are reversed first, so stage 16 starts bitonic).
@@ -753,9 +772,38 @@ template <bool FULL>
 __device__ __forceinline__ bool kll_cand(const KllTail& ts, double x) {
     return FULL ? x > ts.tau : x == x;
 }
+#ifndef KRR_KLL_LANE_APPEND
+#define KRR_KLL_LANE_APPEND 1  // candidates that fit go in lane-major by one wave scan (else column by column)
+#endif
 template <bool FULL>
 __device__ __forceinline__ void kll_tail_append(KllShared sh, KllTail& ts, uint32_t tail, uint32_t tcap, int lane,
                                                 const double (&a)[8], const double (&b)[8], const double (&hi)[8]) {
+#if KRR_KLL_LANE_APPEND
+    {
+        // the lane's candidates counted, one wave scan places them: when they all fit, each lane
+        // writes its own after the keys of the lanes below it (the buffer is a set: the export
+        // sorts it and a refresh keeps every key above its pivot, so the order is free)
+        uint32_t mine = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool ca = kll_cand<FULL>(ts, a[u]), cb = kll_cand<FULL>(ts, b[u]);
+            mine += (ca ? 1u : 0u) + (cb ? 1u : 0u);
+        }
+        const uint32_t incl = wave_scan32(mine, 0u, OpAdd32{});
+        const uint32_t total = lane_bcast32(incl, kWave - 1);
+        if (total == 0) return;
+        if (ts.tl + total <= tcap) {
+            uint32_t pos = ts.tl + incl - mine;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (kll_cand<FULL>(ts, a[u])) sh.tb[pos++] = dbits(a[u] + 0.0);  // -0 -> +0
+                if (kll_cand<FULL>(ts, b[u])) sh.tb[pos++] = dbits(b[u] + 0.0);
+            }
+            ts.tl += total;
+            return;
+        }
+    }
+#endif
     uint64_t pm[8], any = 0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -814,7 +862,13 @@ __device__ __forceinline__ void kll_tail_filter(KllShared sh, KllTail& ts, uint3
 
 // The buffer's top min(n, tail) keys, ascending, into the row's tail words; returns how many.
 __device__ __forceinline__ uint32_t kll_tail_export(KllShared sh, KllTail ts, uint32_t tail, uint64_t* row_tail, int lane) {
+    // a buffer the register sort holds (<= 2,048 keys) is sorted as it is: the top `tail` of it are
+    // the same keys a refresh would have kept
+#ifdef KRR_KLL_X_OLDEXPORT
     if (ts.tl > tail + kKllTailSlack || (ts.tl > 2048 && ts.tl > tail)) ts = kll_tail_refresh(sh, ts, tail, lane);
+#else
+    if (ts.tl > 2048 && ts.tl > tail) ts = kll_tail_refresh(sh, ts, tail, lane);
+#endif
 #ifndef KRR_KLL_X_NOREGSORT
     if (ts.tl <= 2048) kll_tail_sort(sh.tb, ts.tl, lane);
     else
