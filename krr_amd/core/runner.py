@@ -242,9 +242,9 @@ class BatchedRunner:
 
     # parser="hybrid": the share of the JSON bytes the host packer takes, moved after every
     # call toward equal finishing times of the two sides (_rebalance)
-    hybrid_share = 0.14
-    # staging threads of the device side (0: half the threads when the device packer strips
-    # timestamps while staging, a quarter for a plain copy; the host parser gets the rest)
+    hybrid_share = 0.08
+    # staging threads of the device side (0: three quarters of the threads when the device packer
+    # strips timestamps while staging, a quarter for a plain copy; the host parser gets the rest)
     hybrid_device_threads = 0
     hybrid_last: Optional[dict] = None
 
@@ -295,10 +295,11 @@ class BatchedRunner:
         if T < 3 or n < 2:
             return [self.pack_bodies_device(cpu_bodies, mem_bodies, threads=threads, device=device)], (None, None)
         # staging threads (hybrid_device_threads); the host parser gets the rest.  A stripping
-        # staging thread moves ~8x the JSON bytes per second of a host parser thread and keeps
-        # fewer bytes on the link, so it gets half the threads (a plain copy: a quarter)
+        # staging thread moves 5-9x the JSON bytes per second of a host parser thread and keeps
+        # fewer bytes on the link, so it gets three quarters of the threads — enough to keep
+        # the link busy on a host whose cores strip only ~7 GB/s each (a plain copy: a quarter)
         strips = self._device_packer(threads, device).strip
-        t_dev = max(1, min(T - 1, int(self.hybrid_device_threads or (T // 2 if strips else T // 4))))
+        t_dev = max(1, min(T - 1, int(self.hybrid_device_threads or (3 * T // 4 if strips else T // 4))))
         t_host = max(1, T - t_dev)
         host_out: dict = {}
         alloc = _pinned_alloc_or_none()
