@@ -1320,8 +1320,8 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
 
     from krr_amd.core.distributed import raw_from_records
     from krr_amd.core.engine import RawResults
-    from krr_amd.core.fast_round import allocations_batch
-    from krr_amd.core.models.result import ResourceScan, collect_result
+    from krr_amd.core.fast_round import result_batch
+    from krr_amd.core.models.result import ResourceScan
     from krr_amd.core.rounding import format_result
     from krr_amd.core.runner import to_allocations
     from krr_amd.strategies.simple import SimpleStrategy, SimpleStrategySettings
@@ -1334,16 +1334,17 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
     t_obj = time.perf_counter() - t_obj
     warm = RawResults(*(np.asarray(a)[:1000] for a in raw_from_records(records[:1000]).__dict__.values()
                         if isinstance(a, np.ndarray)))
-    collect_result(objects[:1000], allocations_batch(warm, settings, threads=threads))  # loads the libraries
+    result_batch(objects[:1000], warm, settings, threads=threads)  # loads the libraries
     gc.collect()
     tm: dict = {}
     t0 = time.perf_counter()
     raw = raw_from_records(records)
     t1 = time.perf_counter()
-    allocs = allocations_batch(raw, settings, threads=threads, timings=tm)
-    t2 = time.perf_counter()
-    result = collect_result(objects, allocs)
+    # rounding -> value columns -> ResourceScan per container + score, one native pass (the
+    # ResourceAllocations the reference builds in between are read by its scan only)
+    result = result_batch(objects, raw, settings, threads=threads, timings=tm)
     t3 = time.perf_counter()
+    t2 = t3 - tm.get("scan_s", 0.0)
     total = t3 - t0
     # equality with the per-object path: 64-object blocks at both ends of every shard plus a
     # stride over the whole fleet (every pool entry of fleet_objects, so every severity bucket)
@@ -1357,9 +1358,9 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
     want = [to_allocations(format_result(r)) for r in SimpleStrategy(settings).results_from_raw(sub)]
     same, checked, pair_sev = True, 0, {}
     for i, w in zip(idx.tolist(), want):
-        same &= allocs[i] == w and allocs[i].json() == w.json()
         ref_scan = ResourceScan.calculate(objects[i], w)
-        same &= result.scans[i] == ref_scan and result.scans[i].severity == ref_scan.severity
+        same &= (result.scans[i] == ref_scan and result.scans[i].severity == ref_scan.severity
+                 and result.scans[i].json() == ref_scan.json())
         for sel in (ref_scan.recommended.requests, ref_scan.recommended.limits):
             for r in sel.values():
                 pair_sev[r.severity.value] = pair_sev.get(r.severity.value, 0) + 1
@@ -1367,22 +1368,24 @@ def config4_right_size(args, records: np.ndarray, shards) -> dict:
     sev = {}
     for s in result.scans[:: max(1, n // 20000)]:
         sev[s.severity.value] = sev.get(s.severity.value, 0) + 1
-    del result, allocs, objects
+    del result, objects
     gc.collect()
     return {
         "config4_right_size_s": total,
         "config4_right_size_objects_per_s": n / total,
         "config4_right_size_split_s": {"unpack": t1 - t0, "round": tm.get("round_s"), "decimal": tm.get("decimal_s"),
-                                       "allocations_models": tm.get("models_s"), "scan_and_score": t3 - t2},
+                                       "scan_and_score": t3 - t2},
         "config4_scan_objects_per_s": n / (t3 - t2),
         "config4_right_size_equal_per_object_path": bool(same),
         "config4_right_size_checked_objects": checked,
         "config4_right_size_severities_sampled": sev,
         "config4_right_size_checked_pair_severities": pair_sev,
         "config4_right_size_definition": (
-            f"rank 0, all {n} containers' gathered records -> krr_round_simple ({threads} threads) -> one "
-            f"ResourceAllocations per container -> Runner._collect_result's ResourceScan per container + Result "
-            f"score, in bulk; one run after a warm-up on 1000; the {n} K8sObjectData are built beforehand "
+            f"rank 0, all {n} containers' gathered records -> krr_round_simple ({threads} threads) -> the rounded "
+            f"value columns -> Runner._collect_result's ResourceScan per container + Result score, in one native "
+            f"pass (fast_round.result_batch; the ResourceAllocations the reference builds between them are only "
+            f"read by its scan, so they are not materialised); one run after a warm-up on 1000; the {n} "
+            f"K8sObjectData are built beforehand "
             f"({t_obj:.1f} s, untimed); checked equal to the per-object path on {checked} containers (64-object "
             f"blocks at both ends of every shard and a stride over the fleet; per (resource, selector) "
             f"severities of the checked ones in _checked_pair_severities)")}

@@ -52,7 +52,8 @@
 extern "C" {
 #endif
 
-#define KRR_ABI_VERSION 2  /* 2: krr_kll_params gained `tail`; krr_kll_merge; krr_kll_query takes series_base */
+#define KRR_ABI_VERSION 3  /* 3: krr_percentile_params gained k_table / k_table_len;
+                              2: krr_kll_params gained `tail`; krr_kll_merge; krr_kll_query takes series_base */
 
 typedef enum {
     KRR_OK = 0,
@@ -64,9 +65,14 @@ typedef enum {
 } krr_status;
 
 /* Percentile rule for the CPU recommendation.  All rules share n = number of
- * present samples and, for the exact rules, k = floor((n-1) * p / 100)
- * computed in exact rational arithmetic (reference simple.py:36 evaluates
- * int((n-1) * p / 100) in Decimal, which is exact for p with <= 15 digits). */
+ * present samples and, for the exact rules, the index k(n).  The reference
+ * evaluates k = int((n-1) * p / 100) (simple.py:36) in Decimal (prec 28, CLI path)
+ * or in int arithmetic (the default int 99).  That equals the exact floor
+ * floor((n-1) * p_num / p_den / 100), which the kernels compute in 128-bit
+ * integers, whenever (n-1) * p has at most 28 significant digits; past that the
+ * product is ROUNDED before the floor (p = 99.99999999999999999999999999 gives
+ * k(3) = 2, not 1).  For such p the caller evaluates the reference's expression
+ * per n and passes it as krr_percentile_params.k_table. */
 typedef enum {
     KRR_PCT_REF_INDEX = 0,    /* X[k] of the UNSORTED pod-ordered concatenation (the
                                  reference's actual rule, simple.py:36) */
@@ -101,8 +107,17 @@ typedef struct {
     int32_t mode;            /* krr_percentile_mode */
     int32_t reserved;
     int64_t p_num;           /* percentile p = p_num / p_den exactly, 0 < p <= 100 */
-    int64_t p_den;           /* positive; p_den <= 1e15 */
+    int64_t p_den;           /* positive; p_den <= 1e15 (with k_table: a rational within 1e-15
+                                of p, used only to size selection buffers) */
     double q;                /* float64(p) / 100.0 as numpy computes it (LINEAR only) */
+    /* Optional index table (REF_INDEX / SORTED_LOWER; LINEAR ignores it): k(n) =
+     * k_table[n] for 1 <= n < k_table_len, device-accessible (HBM or page-locked host
+     * memory).  NULL: k(n) = the exact floor above.  Entries outside [0, n-1] are clamped
+     * into it.  k_table_len must exceed the longest segment's slots (checked, KRR_E_INVALID)
+     * or, for sketch / KLL / window queries, every merged present count (a series past the
+     * table is flagged KRR_FLAG_CAPACITY). */
+    const int64_t* k_table;
+    int64_t k_table_len;
 } krr_percentile_params;
 
 typedef struct krr_ctx krr_ctx;

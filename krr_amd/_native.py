@@ -124,7 +124,32 @@ class KrrPercentileParams(ctypes.Structure):
         ("p_num", ctypes.c_int64),
         ("p_den", ctypes.c_int64),
         ("q", ctypes.c_double),
+        ("k_table", ctypes.c_void_p),
+        ("k_table_len", ctypes.c_int64),
     ]
+
+
+def bind_index_table(params: KrrPercentileParams, max_n: Optional[int], device: int) -> KrrPercentileParams:
+    """params with krr_percentile_params.k_table set when its index rule needs one for counts of
+    up to max_n samples (``params.rule``: krr_amd.core.index_rule.IndexRule, attached by
+    krr_amd.core.engine.percentile_params; the reference's int((n-1) * p / 100) for p whose
+    product Decimal rounds).  Unchanged for LINEAR, an explicit table, or no rule."""
+    rule = getattr(params, "rule", None)
+    if rule is None or params.k_table or params.mode == KRR_PCT_LINEAR:
+        return params
+    if max_n is None:
+        if not rule.needs_table(1 << 62):
+            return params
+        raise ValueError(f"cpu_percentile {rule.percentile!r} needs the reference's index table here: "
+                         "pass the largest present count (max_n)")
+    if not rule.needs_table(max_n):
+        return params
+    tab = rule.device_table(max_n, device)
+    out = KrrPercentileParams(params.mode, params.reserved, params.p_num, params.p_den, params.q, tab.data_ptr(),
+                              tab.numel())
+    out.rule = rule
+    out._keep = tab
+    return out
 
 
 class KrrSketchParams(ctypes.Structure):
@@ -331,7 +356,7 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_parse_segments.restype = ctypes.c_int
         lib.krr_json_gather.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_gather.restype = ctypes.c_int
-        if lib.krr_abi_version() != 2:
+        if lib.krr_abi_version() != 3:
             raise NativeUnavailable("libkrr_amd.so ABI version mismatch")
         _lib = lib
         return lib
@@ -378,6 +403,14 @@ class Context:
             stream = torch.cuda.current_stream()
         return ctypes.c_void_p(stream.cuda_stream)
 
+    def _bound(self, params: KrrPercentileParams, *series: KrrSeries, max_n: Optional[int] = None):
+        """params with the index table its rule needs for these series (or max_n samples)."""
+        if getattr(params, "rule", None) is None or params.mode == KRR_PCT_LINEAR:
+            return params
+        if max_n is None and series:
+            max_n = max(_series_max_len(s) for s in series)
+        return bind_index_table(params, max_n, self.device)
+
     def series(self, values, offsets, max_segment_len: int = 0, gaps_are_nan: bool = False) -> KrrSeries:
         """Describe device tensors as a krr_series.  The struct keeps references to
         both tensors, so their memory cannot be freed and reused while it is alive.
@@ -397,6 +430,7 @@ class Context:
                              out_flags, stream=None) -> None:
         for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
             _check_tensor(t, dt, series.n_segments)
+        params = self._bound(params, series)
         self._check(self._lib.krr_segmented_percentile(
             self._h, ctypes.byref(series), ctypes.byref(params), out_value.data_ptr(), out_count.data_ptr(),
             out_flags.data_ptr(), self._stream(stream)))
@@ -431,6 +465,7 @@ class Context:
             if dst.numel() * 8 < fbytes:
                 raise ValueError(f"forward destination holds {dst.numel() * 8} bytes, need {fbytes}")
             fsrc, fdst = src.data_ptr(), dst.data_ptr()
+        params = self._bound(params, cpu)
         self._check(self._lib.krr_simple_run_forward(
             self._h, ctypes.byref(cpu), ctypes.byref(mem), ctypes.byref(params),
             out["cpu_value"].data_ptr(), out["cpu_count"].data_ptr(), out["cpu_flags"].data_ptr(),
@@ -526,8 +561,11 @@ class Context:
             flags.data_ptr(), self._stream(stream)))
 
     def sketch_query(self, counts, vmin, vmax, sp: KrrSketchParams, params: KrrPercentileParams, out_value,
-                     out_count, out_flags, stream=None) -> None:
+                     out_count, out_flags, stream=None, max_n: Optional[int] = None) -> None:
+        """max_n: the largest merged present count (needed when the percentile's index rule
+        takes a table, krr_amd.core.index_rule)."""
         S = vmin.numel()
+        params = self._bound(params, max_n=max_n)
         _check_tensor(counts, "int32", S * self.sketch_width(sp))
         for t, dt in ((vmax, "float64"), (out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
             _check_tensor(t, dt, S)
@@ -536,9 +574,10 @@ class Context:
             out_value.data_ptr(), out_count.data_ptr(), out_flags.data_ptr(), self._stream(stream)))
 
     def sketch_locate(self, counts, sp: KrrSketchParams, params: KrrPercentileParams, out_loc,
-                      stream=None) -> None:
-        """out_loc: int64 [S, LOC_WORDS] (krr_sketch_loc per series)."""
+                      stream=None, max_n: Optional[int] = None) -> None:
+        """out_loc: int64 [S, LOC_WORDS] (krr_sketch_loc per series); max_n as sketch_query."""
         S = out_loc.shape[0]
+        params = self._bound(params, max_n=max_n)
         _check_tensor(counts, "int32", S * self.sketch_width(sp))
         _check_tensor(out_loc, "int64", S * LOC_WORDS)
         self._check(self._lib.krr_sketch_locate(self._h, S, counts.data_ptr(), ctypes.byref(sp), ctypes.byref(params),
@@ -632,9 +671,10 @@ class Context:
                                             int(series_base), out_rows.data_ptr(), self._stream(stream)))
 
     def kll_query(self, rows, rows_per_series: int, kp: KrrKllParams, params: KrrPercentileParams, out_value,
-                  out_count, out_flags, series_base: int = 0, stream=None) -> None:
-        """rows: int64 [S * rows_per_series, kll_row_words], series-major."""
+                  out_count, out_flags, series_base: int = 0, stream=None, max_n: Optional[int] = None) -> None:
+        """rows: int64 [S * rows_per_series, kll_row_words], series-major; max_n as sketch_query."""
         S = out_value.numel()
+        params = self._bound(params, max_n=max_n)
         _check_tensor(rows, "int64", S * int(rows_per_series) * self.kll_row_words(kp))
         for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
             _check_tensor(t, dt, S)
@@ -680,9 +720,11 @@ class Context:
 
     def window_merge(self, n_series: int, n_slices: int, slice_stride: int, hdr, keys, key_cap: int,
                      params: KrrPercentileParams, out_value, out_count, out_flags, miss_count=None,
-                     stream=None) -> None:
+                     stream=None, max_n: Optional[int] = None) -> None:
         """Slice j of series i: hdr[j * slice_stride + i], keys row j * slice_stride + i.
-        miss_count: optional int32 [1] device tensor (zeroed, then counts the misses)."""
+        miss_count: optional int32 [1] device tensor (zeroed, then counts the misses); max_n as
+        sketch_query."""
+        params = self._bound(params, max_n=max_n)
         _check_tensor(hdr, "int64", ((n_slices - 1) * slice_stride + n_series) * HDR_WORDS if n_series else 0)
         _check_tensor(keys, "int64", ((n_slices - 1) * slice_stride + n_series) * int(key_cap) if n_series else 0)
         for t, dt in ((out_value, "float64"), (out_count, "int64"), (out_flags, "int32")):
@@ -803,6 +845,12 @@ def select_plan(max_segment_len: int, params: KrrPercentileParams) -> KrrSelectP
     LINEAR (host only: no device needed).  Raises NativeError for REF_INDEX."""
     lib = load_library()
     info = KrrSelectPlanInfo()
+    rule = getattr(params, "rule", None)
+    if rule is not None and not params.k_table and params.mode != KRR_PCT_LINEAR and rule.needs_table(max_segment_len):
+        # the plan only needs to know a table is there (its wider margins); it reads no entry
+        tab = rule.table(max(int(max_segment_len), 1))
+        params = KrrPercentileParams(params.mode, params.reserved, params.p_num, params.p_den, params.q,
+                                     tab.ctypes.data, tab.size)
     rc = lib.krr_select_plan(int(max_segment_len), ctypes.byref(params), ctypes.byref(info))
     if rc != KRR_OK:
         raise NativeError(rc, "krr_select_plan")
@@ -816,6 +864,16 @@ def window_key_cap(max_slice_len: int, ext_slots: int, params: KrrPercentilePara
     if k <= 0:
         raise NativeError(KRR_E_INVALID, "krr_window_key_cap: REF_INDEX or invalid arguments")
     return k
+
+
+def _series_max_len(series: KrrSeries) -> int:
+    """The longest segment's slots: max_segment_len, or from the offsets (synchronises)."""
+    if series.max_segment_len > 0:
+        return int(series.max_segment_len)
+    offs = series._keep[1]
+    if offs.numel() < 2:
+        return 0
+    return int((offs[1:] - offs[:-1]).max().item())
 
 
 def _check_tensor(t, dtype: str, numel: Optional[int] = None, host_pinned_ok: bool = False) -> None:

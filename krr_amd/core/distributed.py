@@ -57,6 +57,16 @@ def pack_records(out: dict):
     return torch.stack([cv, mv, cc, mc], dim=1).contiguous()
 
 
+def records_from_raw(raw, device):
+    """Host RawResults -> the int64 [S, 4] records on ``device`` (pack_records' layout)."""
+    import torch
+
+    cols = {k: torch.from_numpy(np.ascontiguousarray(getattr(raw, k))) for k in ("cpu_value", "mem_value")}
+    for k in ("cpu_count", "mem_count", "cpu_flags", "mem_flags"):
+        cols[k] = torch.from_numpy(np.ascontiguousarray(getattr(raw, k), dtype=np.int64))
+    return pack_records(cols).to(device)
+
+
 def unpack_records(rec) -> dict:
     """int64 [S, 4] (tensor or array) -> host numpy arrays of the six result fields."""
     a = rec.cpu().numpy() if hasattr(rec, "cpu") else np.asarray(rec)

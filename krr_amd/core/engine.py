@@ -10,8 +10,6 @@ from __future__ import annotations
 
 import threading
 from dataclasses import dataclass
-from decimal import Decimal
-from fractions import Fraction
 from typing import Optional
 
 import numpy as np
@@ -21,27 +19,27 @@ from krr_amd.core.packing import PackedFleet, PackedSeries
 
 MODE_CODES = {"ref_index": _native.KRR_PCT_REF_INDEX, "sorted_lower": _native.KRR_PCT_SORTED_LOWER,
               "linear": _native.KRR_PCT_LINEAR}
-P_DEN_MAX = 10**15
 
 
 def percentile_params(percentile, mode: str) -> _native.KrrPercentileParams:
-    """Exact rational p for the index rule, float64 q = p/100 for numpy's LINEAR rule.
+    """The kernels' percentile parameters for any ``cpu_percentile`` the reference accepts.
 
-    The reference evaluates int((n-1) * p / 100) in Decimal (CLI path, p a Decimal)
-    or int/float arithmetic (default path, p the int 99); both equal the exact
-    floor for p with <= 15 significant digits, which the kernel computes in
-    128-bit integers.
+    The index rule k(n) (REF_INDEX, SORTED_LOWER) is the reference's int((n-1) * p / 100)
+    (simple.py:36) evaluated as it evaluates it (krr_amd.core.index_rule): the kernels'
+    128-bit exact floor of p_num / p_den where that provably agrees, else a table of k(n)
+    that ``_native`` binds at launch time (``params.rule``, sized by the launch's longest
+    segment).  q = float(p) / 100 is numpy's LINEAR rule.
     """
+    from krr_amd.core.index_rule import IndexRule
+
     if mode not in MODE_CODES:
         raise ValueError(f"unknown percentile mode {mode!r}; expected one of {sorted(MODE_CODES)}")
-    frac = Fraction(Decimal(percentile)) if not isinstance(percentile, Fraction) else percentile
-    if not (0 < frac <= 100):
-        raise ValueError(f"percentile must be in (0, 100], got {percentile}")
-    if frac.denominator > P_DEN_MAX or frac.numerator > 100 * P_DEN_MAX:
-        raise ValueError(f"percentile {percentile} needs more than 15 significant digits; "
-                         "the batched exact index rule supports p_den <= 1e15")
+    rule = IndexRule.of(percentile)
+    p_num, p_den = rule.approx()
     q = float(percentile) / 100.0
-    return _native.KrrPercentileParams(MODE_CODES[mode], 0, frac.numerator, frac.denominator, q)
+    params = _native.KrrPercentileParams(MODE_CODES[mode], 0, p_num, p_den, q)
+    params.rule = rule
+    return params
 
 
 @dataclass
@@ -236,9 +234,20 @@ def locate_ranks(name: str, exact: np.ndarray, count: np.ndarray, flags: np.ndar
     if name == "mem":
         rank[ok] = -1
     else:
-        for i in np.flatnonzero(ok).tolist():  # k in exact integers (p_num·n can pass 2^63)
-            rank[i] = (int(count[i]) - 1) * int(params.p_num) // (100 * int(params.p_den))
+        rank[ok] = index_rule_of(params).ks(np.asarray(count)[ok])
     return rank
+
+
+def index_rule_of(params):
+    """The IndexRule a params struct carries (percentile_params), or the exact p_num / p_den one."""
+    rule = getattr(params, "rule", None)
+    if rule is None:
+        from fractions import Fraction
+
+        from krr_amd.core.index_rule import IndexRule
+
+        rule = IndexRule.of(Fraction(int(params.p_num), int(params.p_den)))
+    return rule
 
 
 def needs_locate(fleet: PackedFleet, params) -> bool:

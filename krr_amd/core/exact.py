@@ -43,7 +43,9 @@ def sample_at(pods: Sequence[Sequence], pos: int):
 
 
 def _index_k(n: int, params) -> int:
-    return (n - 1) * int(params.p_num) // (100 * int(params.p_den))
+    from krr_amd.core.engine import index_rule_of
+
+    return index_rule_of(params).k(n)
 
 
 def resolve(fleet: PackedFleet, raw, params) -> None:

@@ -192,27 +192,11 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
     cpu_k, mem_k = rtypes[0], rtypes[1]
     import time
 
-    t0 = time.perf_counter()
-    buffer = settings.memory_buffer()
-    cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
-                               memory_min_value, threads)
-    _route_exact(st, raw)
-    t1 = time.perf_counter()
     gc_was = gc.isenabled()
     gc.disable()
     try:
-        q = "?"
-        cpu_col, mem_col = decimal_column(cs, q), decimal_column(ms, q)
-        if timings is not None:
-            timings.update(round_s=t1 - t0, decimal_s=time.perf_counter() - t1)
-            t1 = time.perf_counter()
-        fb = np.nonzero(st)[0].tolist()
-        _apply_fallbacks(cpu_col, mem_col, st, raw, settings, buffer, cpu_min_value, memory_min_value)
-        for i in fb:  # the validator's NaN -> "?" (allocations.py:40-41) for the Python-rounded ones
-            if isinstance(cpu_col[i], Decimal) and cpu_col[i].is_nan():
-                cpu_col[i] = q
-            if isinstance(mem_col[i], Decimal) and mem_col[i].is_nan():
-                mem_col[i] = q
+        cpu_col, mem_col = rounded_columns(raw, settings, cpu_min_value, memory_min_value, threads, timings)
+        t1 = time.perf_counter()
         fields = {"requests", "limits"}
         if not _v1_construct_layout(model):  # e.g. a pydantic v2 model: its own constructor, per object
             return [model(requests={cpu_k: c, mem_k: m}, limits={cpu_k: None, mem_k: m})
@@ -235,6 +219,64 @@ def allocations_batch(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
             return o
 
         return list(map(mk, cpu_col, mem_col))
+    finally:
+        if gc_was:
+            gc.enable()
+
+
+def rounded_columns(raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
+                    memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE, threads: int = 0,
+                    timings: Optional[dict] = None) -> tuple[list, list]:
+    """The rounded CPU request and memory request / limit of every object as the
+    ResourceAllocations validator leaves them (a Decimal, or "?" for NaN; allocations.py:33-51):
+    Runner._format_result's values (runner.py:49-86) from raw kernel results, by the native
+    rounding, with the reference's own arithmetic for what it does not cover.  ``timings``:
+    round_s (native rounding), decimal_s (one Decimal per distinct string)."""
+    import time
+
+    t0 = time.perf_counter()
+    buffer = settings.memory_buffer()
+    cs, ms, st = round_strings(raw.cpu_value, raw.cpu_flags, raw.mem_value, raw.mem_flags, buffer, cpu_min_value,
+                               memory_min_value, threads)
+    _route_exact(st, raw)
+    t1 = time.perf_counter()
+    q = "?"
+    cpu_col, mem_col = decimal_column(cs, q), decimal_column(ms, q)
+    if timings is not None:
+        timings.update(round_s=t1 - t0, decimal_s=time.perf_counter() - t1)
+    fb = np.nonzero(st)[0].tolist()
+    _apply_fallbacks(cpu_col, mem_col, st, raw, settings, buffer, cpu_min_value, memory_min_value)
+    for i in fb:  # the validator's NaN -> "?" (allocations.py:40-41) for the Python-rounded ones
+        if isinstance(cpu_col[i], Decimal) and cpu_col[i].is_nan():
+            cpu_col[i] = q
+        if isinstance(mem_col[i], Decimal) and mem_col[i].is_nan():
+            mem_col[i] = q
+    return cpu_col, mem_col
+
+
+def result_batch(objects, raw, settings, cpu_min_value: int = DEFAULT_CPU_MIN_VALUE,
+                 memory_min_value: int = DEFAULT_MEMORY_MIN_VALUE, threads: int = 0, models=None,
+                 timings: Optional[dict] = None):
+    """Runner._collect_result (runner.py:122-131) from raw kernel results: the rounded values
+    (rounded_columns) scanned straight into the Result — ResourceScan.calculate per object and
+    the score (result.py:33-150) — without the ResourceAllocations list in between, which the
+    reference builds only for the scan to read (runner.py:113-120).  Equal to
+    collect_result(objects, allocations_batch(raw, ...)).  ``models``: the reference's result
+    module (krr_amd.integration) or, by default, this package's mirror.  ``timings``: as
+    rounded_columns, plus scan_s."""
+    import time
+
+    from krr_amd.core.models.result import collect_result_columns
+
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        cpu_col, mem_col = rounded_columns(raw, settings, cpu_min_value, memory_min_value, threads, timings)
+        t0 = time.perf_counter()
+        res = collect_result_columns(objects, cpu_col, mem_col, models)
+        if timings is not None:
+            timings["scan_s"] = time.perf_counter() - t0
+        return res
     finally:
         if gc_was:
             gc.enable()

@@ -89,18 +89,51 @@ class BatchedRunner:
 
         import torch
 
+        import numpy as np
+        import torch.distributed as dist
+
+        from krr_amd.core.distributed import record_counts, records_from_raw
+
         self._require_packed()
         dev = local_device() if device is None else int(device)
-        rec = self.strategy.settings.run_fleet_records(local_fleet, dev)
+        settings = self.strategy.settings
         coll = collective_device(group, dev)
+        objs = None
+        if local_fleet.cpu.exact is not None or local_fleet.mem.exact is not None:
+            # HistoryData whose Decimals the float64 images do not reproduce ('0.10', 25-digit
+            # values ...): this rank locates and resolves its shard's sample objects
+            # (krr_amd.core.exact, as run_fleet does on one GPU) and sends them to dst
+            raw = settings.run_fleet(local_fleet, device=dev)
+            rec = records_from_raw(raw, coll)
+            objs = {"cpu": raw.cpu_exact or {}, "mem": raw.mem_exact or {}}
+        else:
+            rec = settings.run_fleet_records(local_fleet, dev)
         if coll.type == "cuda":
             # this may run on a worker thread (gather_objects_recommendations_sharded):
             # its current device is 0 until set, and RCCL enqueues on the current device
             torch.cuda.set_device(coll)
-        full = gather_records(rec.to(coll), dst=dst, group=group)
+        counts = record_counts(rec.shape[0], coll, group)
+        full = gather_records(rec.to(coll), dst=dst, group=group, counts=counts)
+        # every rank says whether it holds such objects (one all_reduce of an int); only then
+        # do the per-rank dicts travel (gather_object), keyed by global object index
+        flag = torch.tensor([0 if objs is None else 1], dtype=torch.int64, device=coll)
+        dist.all_reduce(flag, group=group)
+        exact = None
+        if int(flag.item()):
+            rank = dist.get_rank(group)
+            gdst = dist.get_global_rank(group, dst) if group is not None else dst
+            got = [None] * dist.get_world_size(group) if rank == dst else None
+            dist.gather_object(objs or {"cpu": {}, "mem": {}}, got, dst=gdst, group=group)
+            if got is not None:
+                base = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+                exact = {name: {int(base[r]) + i: v for r, o in enumerate(got) for i, v in o[name].items()}
+                         for name in ("cpu", "mem")}
         if full is None:
             return None
-        return self.strategy.format_raw(raw_from_records(full), self.cpu_min_value, self.memory_min_value)
+        raw = raw_from_records(full)
+        if exact is not None:
+            raw.cpu_exact, raw.mem_exact = exact["cpu"] or None, exact["mem"] or None
+        return self.strategy.format_raw(raw, self.cpu_min_value, self.memory_min_value)
 
     def recommend_bodies_shard(self, cpu_bodies: Sequence[Sequence[bytes]], mem_bodies: Sequence[Sequence[bytes]],
                                group=None, dst: int = 0, device: Optional[int] = None, parser: str = "device",
@@ -169,6 +202,19 @@ class BatchedRunner:
         raw = self.strategy.settings.run_fleet(fleet)
         return allocations_batch(raw, self.strategy.settings, self.cpu_min_value, self.memory_min_value, model=model,
                                  resource_type=resource_type)
+
+    def result_packed(self, objects: Sequence[K8sObjectData], fleet, models=None, threads: int = 0):
+        """Runner._collect_result's Result (runner.py:122-131) for a PackedFleet: one kernel pass,
+        native rounding, and the ResourceScan per object + score built straight from the rounded
+        values (krr_amd.core.fast_round.result_batch: the ResourceAllocations the reference builds
+        in between are only read by the scan).  ``models``: the reference's result module
+        (default this package's mirror)."""
+        from krr_amd.core.fast_round import result_batch
+
+        self._require_packed()
+        raw = self.strategy.settings.run_fleet(fleet)
+        return result_batch(objects, raw, self.strategy.settings, self.cpu_min_value, self.memory_min_value,
+                            threads=threads, models=models)
 
     def pack_from_bodies(self, cpu_bodies, mem_bodies, threads: int = 0, parser: str = "device"):
         """The PackedFleet of raw per-pod query_range bodies (see recommend_from_bodies)."""

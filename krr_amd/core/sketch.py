@@ -145,6 +145,14 @@ def merge_time_sharded(sk: dict, group=None) -> dict:
             "flags": flags[:n].contiguous(), "block": (lo, hi)}
 
 
+def _needs_table(params) -> bool:
+    """Does the percentile's index rule need a table whatever the counts (krr_amd.core.index_rule)?
+    Only then do the queries below size one from their merged counts (a synchronisation)."""
+    rule = getattr(params, "rule", None)
+    return (rule is not None and params.mode != _native.KRR_PCT_LINEAR and not params.k_table
+            and rule.needs_table(1 << 62))
+
+
 def query(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native.KrrPercentileParams,
           stream=None) -> dict:
     """Percentile of every (merged) sketch.  KRR_FLAG_NAN from the build is carried over."""
@@ -155,8 +163,9 @@ def query(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native
     out = {"value": torch.empty(S, dtype=torch.float64, device=dev),
            "count": torch.empty(S, dtype=torch.int64, device=dev),
            "flags": torch.empty(S, dtype=torch.int32, device=dev)}
+    max_n = int(merged["counts"].sum(dim=1).max().item()) if S and _needs_table(params) else None
     ctx.sketch_query(merged["counts"], merged["vmin"], merged["vmax"], cfg.params(), params, out["value"],
-                     out["count"], out["flags"], stream)
+                     out["count"], out["flags"], stream, max_n=max_n)
     nan = (merged["flags"] & _native.KRR_FLAG_NAN) != 0
     if bool(nan.any()):
         out["flags"] |= merged["flags"] & _native.KRR_FLAG_NAN
@@ -174,7 +183,8 @@ def locate(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _nativ
     S = merged["counts"].shape[0]
     loc = torch.empty((S, _native.LOC_WORDS), dtype=torch.int64, device=merged["counts"].device)
     if S:
-        ctx.sketch_locate(merged["counts"], cfg.params(), params, loc, stream)
+        max_n = int(merged["counts"].sum(dim=1).max().item()) if _needs_table(params) else None
+        ctx.sketch_locate(merged["counts"], cfg.params(), params, loc, stream, max_n=max_n)
     return loc
 
 
@@ -291,8 +301,11 @@ def exact_time_sharded(ctx: _native.Context, series: _native.KrrSeries, local: d
 
 # ----------------------------- exact time-sharded merges ------------------------------
 
-def exact_rank_np(n: np.ndarray, p_num: int, p_den: int) -> np.ndarray:
-    """floor((n-1) * p_num / (100 p_den)) exactly, elementwise (n >= 1)."""
+def exact_rank_np(n: np.ndarray, p_num: int, p_den: int, rule=None) -> np.ndarray:
+    """floor((n-1) * p_num / (100 p_den)) exactly, elementwise (n >= 1); with ``rule``
+    (krr_amd.core.index_rule.IndexRule) the reference's own k(n) instead."""
+    if rule is not None:
+        return rule.ks(n)
     n = np.asarray(n, dtype=np.int64)
     a = n - 1
     den = 100 * int(p_den)
@@ -301,14 +314,14 @@ def exact_rank_np(n: np.ndarray, p_num: int, p_den: int) -> np.ndarray:
     return np.array([(int(x) * int(p_num)) // den for x in a], dtype=np.int64)
 
 
-def refindex_locate(all_n: np.ndarray, p_num: int, p_den: int, rank: int):
+def refindex_locate(all_n: np.ndarray, p_num: int, p_den: int, rank: int, rule=None):
     """Global REF_INDEX position from per-slice present counts all_n[world, S]
     (time order = rank order): n[S], k[S] (-1 if empty), owner[S] = the rank whose
     slice holds k (-1 if empty), and this rank's local index (-1 if not its own)."""
     all_n = np.asarray(all_n, dtype=np.int64)
     n = all_n.sum(axis=0)
     prefix = np.cumsum(all_n, axis=0) - all_n  # samples in earlier slices
-    k = np.where(n > 0, exact_rank_np(np.maximum(n, 1), p_num, p_den), -1)
+    k = np.where(n > 0, exact_rank_np(np.maximum(n, 1), p_num, p_den, rule), -1)
     inside = (k[None, :] >= prefix) & (k[None, :] < prefix + all_n)
     owner = np.where(n > 0, np.argmax(inside, axis=0), -1)
     k_local = np.where(owner == rank, k - prefix[rank], -1).astype(np.int64)
@@ -343,7 +356,7 @@ def refindex_time_sharded(ctx: _native.Context, series: _native.KrrSeries, param
         all_n = torch.stack(g).cpu().numpy()  # [world, S], time order = rank order
     else:
         all_n = local_n.cpu().numpy()[None, :]
-    n, k, owner, k_local = refindex_locate(all_n, params.p_num, params.p_den, rank)
+    n, k, owner, k_local = refindex_locate(all_n, params.p_num, params.p_den, rank, getattr(params, "rule", None))
     mine = owner == rank
     kt = torch.from_numpy(k_local).to(dev)
     found = torch.full((S,), float("nan"), dtype=torch.float64, device=dev)
@@ -549,8 +562,9 @@ def _window_exact_body(ctx, series, params, ext_slots, group, st, events, key_ca
            "count": torch.empty(max(nb, 1), dtype=torch.int64, device=dev)[:nb],
            "flags": torch.empty(max(nb, 1), dtype=torch.int32, device=dev)[:nb]}
     miss = torch.zeros(1, dtype=torch.int32, device=dev)
+    # a series holds at most this rank's longest slice plus the slots elsewhere (ext_slots)
     ctx.window_merge(nb, world, stride, hdr_r, keys_r, kc, params, out["value"], out["count"], out["flags"], miss,
-                     st)
+                     st, max_n=(Lmax + ext_slots) if _needs_table(params) else None)
     nmiss = int(miss.item())
     total = nmiss
     if world > 1:
@@ -798,8 +812,11 @@ def kll_query(ctx: _native.Context, rows, rows_per_series: int, cfg: KllConfig,
            "count": torch.empty(max(n, 1), dtype=torch.int64, device=dev)[:n],
            "flags": torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]}
     if n:
+        max_n = None
+        if _needs_table(params):  # row word 0 = the row's present count (oracle/kll_ref.py)
+            max_n = int(rows.view(n, max(rows_per_series, 1), -1)[:, :, 0].sum(dim=1).max().item())
         ctx.kll_query(rows, rows_per_series, cfg.params(epoch), params, out["value"], out["count"], out["flags"],
-                      series_base=series_base, stream=stream)
+                      series_base=series_base, stream=stream, max_n=max_n)
     return out
 
 

@@ -137,4 +137,19 @@ __device__ __forceinline__ int64_t exact_rank(int64_t n, int64_t p_num, int64_t 
     return (int64_t)k;
 }
 
+// The index rule k(n) of krr_percentile_params: the caller's k_table entry (the
+// reference's own int((n-1) * p / 100) for p whose product it rounds), clamped into
+// [0, n-1], else the exact floor.  n past the table: the table's last entry (the ABI
+// checks the longest segment against the table; queries flag it, rule_covers).
+__device__ __forceinline__ int64_t rule_rank(int64_t n, int64_t p_num, int64_t p_den, const int64_t* tab,
+                                             int64_t tab_len) {
+    if (!tab) return exact_rank(n, p_num, p_den);
+    int64_t k = tab[n < tab_len ? n : tab_len - 1];
+    k = k < 0 ? 0 : k;
+    return k > n - 1 ? n - 1 : k;
+}
+__device__ __forceinline__ bool rule_covers(int64_t n, const int64_t* tab, int64_t tab_len) {
+    return !tab || n < tab_len;
+}
+
 }  // namespace krr

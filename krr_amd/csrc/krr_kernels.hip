@@ -959,6 +959,8 @@ struct SelectArgs {
     int32_t gaps;
     int64_t p_num, p_den;
     double q;
+    const int64_t* ktab;  // krr_percentile_params.k_table (null: the exact floor)
+    int64_t ktab_len;
     uint32_t cap;        // single-pass candidate capacity (keys); longer segments use hselect
     uint32_t wcap;       // window select (wselect) capacity (keys)
     double* out_v;
@@ -992,7 +994,7 @@ __device__ __forceinline__ Ranks ranks_for(const SelectArgs& A, uint64_t n) {
     Ranks R;
     R.gamma = 0.0;
     if (A.mode == KRR_PCT_SORTED_LOWER) {
-        R.r0 = R.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+        R.r0 = R.r1 = rule_rank((int64_t)n, A.p_num, A.p_den, A.ktab, A.ktab_len);
     } else {  // KRR_PCT_LINEAR, numpy method="linear"
         const double vidx = __dmul_rn((double)(n - 1), A.q);
         if (vidx >= (double)(n - 1)) {
@@ -1048,7 +1050,7 @@ __device__ __forceinline__ void select_segment_with(const SelectArgs& A, int64_t
     {
         const int64_t beg = A.offs[s], end = A.offs[s + 1];
         const int64_t L = end - beg;
-        const SidePlan sp = plan_side(L, A.mode, A.p_num, A.p_den, A.q);
+        const SidePlan sp = plan_side(L, A.mode, A.p_num, A.p_den, A.q, A.ktab != nullptr);
         SelectProc P;
         P.buf = reinterpret_cast<uint64_t*>(smem + kSelectLdsFixed);
         P.H = reinterpret_cast<uint32_t*>(smem);
@@ -2327,6 +2329,8 @@ __global__ __launch_bounds__(64) void k_window_merge(WindowMergeArgs M) {
             flags = KRR_FLAG_NAN;  // a NaN sample (compact layout): NaN, as the whole-series select says
         } else if (n == 0) {
             flags = KRR_FLAG_EMPTY;
+        } else if (!rule_covers((int64_t)n, A.ktab, A.ktab_len)) {
+            flags = KRR_FLAG_CAPACITY;  // the caller's k_table stops short of the merged count
         } else if (any_fail || Lk > Hk) {
             miss = true;
         } else {
@@ -2422,6 +2426,8 @@ struct RefArgs {
     const int64_t* offs;
     int64_t S;
     int64_t p_num, p_den;
+    const int64_t* ktab;  // krr_percentile_params.k_table (null: the exact floor)
+    int64_t ktab_len;
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
@@ -2443,7 +2449,7 @@ __device__ __forceinline__ void refindex_gaps_segment(const RefArgs& A, int64_t 
         if (n == 0) {
             flags = KRR_FLAG_EMPTY;
         } else {
-            const uint64_t k = (uint64_t)exact_rank((int64_t)n, A.p_num, A.p_den);
+            const uint64_t k = (uint64_t)rule_rank((int64_t)n, A.p_num, A.p_den, A.ktab, A.ktab_len);
             // walk from the nearer end in blocks of 16 x 64 slots whose loads are all
             // in flight at once (one HBM round trip per 1,024 slots, not per 64)
             const bool back = k >= n / 2;
@@ -2501,7 +2507,7 @@ __global__ __launch_bounds__(256) void k_refindex_dense(RefArgs A) {
         A.out_f[s] = KRR_FLAG_EMPTY;
         return;
     }
-    const int64_t k = exact_rank(n, A.p_num, A.p_den);
+    const int64_t k = rule_rank(n, A.p_num, A.p_den, A.ktab, A.ktab_len);
     A.out_v[s] = A.vals[beg + k];
     A.out_n[s] = n;
     A.out_f[s] = 0;
@@ -2796,6 +2802,8 @@ struct SketchQueryArgs {
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
+    const int64_t* ktab = nullptr;  // krr_percentile_params.k_table
+    int64_t ktab_len = 0;
 };
 
 // Value estimate of ascending rank r inside bin b holding c keys, `before` below.
@@ -2851,7 +2859,8 @@ __global__ __launch_bounds__(64) void k_sketch_query(SketchQueryArgs A) {
             Ranks R;
             R.gamma = 0.0;
             if (A.mode == KRR_PCT_SORTED_LOWER) {
-                R.r0 = R.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+                R.r0 = R.r1 = rule_rank((int64_t)n, A.p_num, A.p_den, A.ktab, A.ktab_len);
+                if (!rule_covers((int64_t)n, A.ktab, A.ktab_len)) flags |= KRR_FLAG_CAPACITY;
             } else {
                 const double vidx = __dmul_rn((double)(n - 1), A.q);
                 if (vidx >= (double)(n - 1)) {
@@ -3048,6 +3057,8 @@ struct SketchLocateArgs {
     int64_t p_num, p_den;
     double q;
     krr_sketch_loc* out;
+    const int64_t* ktab = nullptr;  // krr_percentile_params.k_table
+    int64_t ktab_len = 0;
 };
 
 __global__ __launch_bounds__(64) void k_sketch_locate(SketchLocateArgs A) {
@@ -3074,7 +3085,8 @@ __global__ __launch_bounds__(64) void k_sketch_locate(SketchLocateArgs A) {
             L.flags = KRR_FLAG_EMPTY;
         } else {
             if (A.mode == KRR_PCT_SORTED_LOWER) {
-                L.r0 = L.r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+                L.r0 = L.r1 = rule_rank((int64_t)n, A.p_num, A.p_den, A.ktab, A.ktab_len);
+                if (!rule_covers((int64_t)n, A.ktab, A.ktab_len)) L.flags |= KRR_FLAG_CAPACITY;
             } else {  // numpy method="linear" (ranks_for)
                 const double vidx = __dmul_rn((double)(n - 1), A.q);
                 if (vidx >= (double)(n - 1)) {
@@ -3383,6 +3395,18 @@ int resolve_maxlen(krr_ctx* ctx, const krr_series* s, hipStream_t st, int64_t* o
     return KRR_OK;
 }
 
+// A launch reading krr_percentile_params.k_table: every segment's count must index it.
+int check_table(krr_ctx* ctx, const krr_series* s, const krr_percentile_params* p, hipStream_t st) {
+    if (!p->k_table || p->mode == KRR_PCT_LINEAR) return KRR_OK;
+    int64_t Lmax = 0;
+    int rc = resolve_maxlen(ctx, s, st, &Lmax);
+    if (rc) return rc;
+    if (Lmax >= p->k_table_len)
+        return set_err(ctx, KRR_E_INVALID, "k_table holds %s%lld entries, segments reach more slots", "",
+                       (long long)p->k_table_len);
+    return KRR_OK;
+}
+
 int check_series(krr_ctx* ctx, const krr_series* s) {
     if (!s) return set_err(ctx, KRR_E_INVALID, "null series%s", "");
     if (s->n_segments < 0) return set_err(ctx, KRR_E_INVALID, "negative n_segments%s", "");
@@ -3399,7 +3423,11 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     int64_t Lmax = 0;
     int rc = resolve_maxlen(ctx, series, st, &Lmax);
     if (rc) return rc;
-    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
+    if (params->k_table && params->mode != KRR_PCT_LINEAR && Lmax >= params->k_table_len)
+        return set_err(ctx, KRR_E_INVALID, "k_table holds %s%lld entries, segments reach more slots", "",
+                       (long long)params->k_table_len);
+    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q,
+                                  params->k_table != nullptr);
     const uint32_t need = capacity_for(sp.tkeep);
     const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom, fused);  // every segment through wselect
     const uint32_t cap = hsel ? 0u : need;
@@ -3412,6 +3440,8 @@ int plan_select(krr_ctx* ctx, const krr_series* series, const krr_percentile_par
     A->p_num = params->p_num;
     A->p_den = params->p_den;
     A->q = params->q;
+    A->ktab = params->k_table;
+    A->ktab_len = params->k_table_len;
     A->cap = cap;
     A->out_v = ov;
     A->out_n = on;
@@ -3465,6 +3495,8 @@ int check_params(krr_ctx* ctx, const krr_percentile_params* p) {
         return set_err(ctx, KRR_E_INVALID, "bad percentile mode %s%lld", "", p->mode);
     if (p->p_den <= 0 || p->p_den > 1000000000000000LL || p->p_num <= 0 || p->p_num > 100 * p->p_den)
         return set_err(ctx, KRR_E_INVALID, "percentile must be in (0, 100] with p_den <= 1e15%s", "");
+    if ((p->k_table != nullptr) != (p->k_table_len > 0) || (p->k_table && p->k_table_len < 2))
+        return set_err(ctx, KRR_E_INVALID, "k_table needs k_table_len >= 2 (and a table for a length)%s", "");
     if (p->mode == KRR_PCT_LINEAR && !(p->q > 0.0 && p->q <= 1.0))
         return set_err(ctx, KRR_E_INVALID, "LINEAR needs q = p/100 in (0, 1]%s", "");
     return KRR_OK;
@@ -3569,7 +3601,10 @@ int krr_segmented_percentile(krr_ctx* ctx, const krr_series* series, const krr_p
     hipStream_t st = (hipStream_t)stream;
 
     if (params->mode == KRR_PCT_REF_INDEX) {
-        RefArgs A{series->values, series->offsets, S, params->p_num, params->p_den, out_value, out_count, out_flags};
+        rc = check_table(ctx, series, params, st);
+        if (rc) return rc;
+        RefArgs A{series->values, series->offsets, S, params->p_num, params->p_den, params->k_table,
+                  params->k_table_len, out_value, out_count, out_flags};
         if (series->gaps_are_nan) {
             hipLaunchKernelGGL(k_refindex_gaps, dim3(grid_for(S)), dim3(64), 0, st, A);
         } else {
@@ -3673,10 +3708,13 @@ int krr_simple_run_forward(krr_ctx* ctx, const krr_series* cpu, const krr_series
         M.fwd_items = ((fwd_units + kFwdItemUnits - 1) / kFwdItemUnits + 7) & ~(int64_t)7;
     }
     const int64_t items = M.fwd_items + 2 * S;
-    RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, cpu_value, cpu_count, cpu_flags, records};
+    RefArgs R{cpu->values, cpu->offsets, S, params->p_num, params->p_den, params->k_table, params->k_table_len,
+              cpu_value, cpu_count, cpu_flags, records};
     SelectArgs A{};
     const bool fwd = M.fwd_items > 0;
     if (params->mode == KRR_PCT_REF_INDEX) {
+        rc = check_table(ctx, cpu, params, st);
+        if (rc) return rc;
         if (fwd) hipLaunchKernelGGL((k_simple<CPU_REF_GAPS, true>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
         else hipLaunchKernelGGL((k_simple<CPU_REF_GAPS>), dim3(grid_for(items)), dim3(64), 0, st, A, R, M);
     } else {
@@ -3878,7 +3916,8 @@ int krr_sketch_query(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, c
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     SketchQueryArgs A{n_segments, sketch_geom(*sp), counts, vmin, vmax, params->mode, params->p_num,
-                      params->p_den, params->q, out_value, out_count, out_flags};
+                      params->p_den, params->q, out_value, out_count, out_flags, params->k_table,
+                      params->k_table_len};
     hipLaunchKernelGGL(k_sketch_query, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
@@ -4109,7 +4148,8 @@ int krr_kll_query(krr_ctx* ctx, int64_t n_series, int32_t rows_per_series, const
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     KllMergeArgs A{n_series, rows_per_series, kp->budget, kp->tail, (uint32_t)kp->slice, kp->seed, series_base, rows,
-                   nullptr, params->mode, params->p_num, params->p_den, params->q, out_value, out_count, out_flags};
+                   nullptr, params->mode, params->p_num, params->p_den, params->q, out_value, out_count, out_flags,
+                   params->k_table, params->k_table_len};
     hipLaunchKernelGGL(k_kll_query, dim3(grid_for(n_series)), dim3(64), lds, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
@@ -4129,7 +4169,7 @@ int krr_sketch_locate(krr_ctx* ctx, int64_t n_segments, const uint32_t* counts, 
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
     SketchLocateArgs A{n_segments, sketch_geom(*sp), counts, params->mode, params->p_num, params->p_den, params->q,
-                       out};
+                       out, params->k_table, params->k_table_len};
     hipLaunchKernelGGL(k_sketch_locate, dim3(grid_for(n_segments)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;
@@ -4279,6 +4319,8 @@ int krr_window_export(krr_ctx* ctx, const krr_series* slices, const krr_percenti
     X.A.p_num = params->p_num;
     X.A.p_den = params->p_den;
     X.A.q = params->q;
+    X.A.ktab = params->k_table;
+    X.A.ktab_len = params->k_table_len;
     X.A.wcap = wsel_cap_for(Lmax, slices->gaps_are_nan != 0);
     X.ext = (double)ext_slots;
     X.key_cap = (uint32_t)key_cap;
@@ -4321,6 +4363,8 @@ int krr_window_merge(krr_ctx* ctx, int64_t n_series, int32_t n_slices, int64_t s
     M.A.p_num = params->p_num;
     M.A.p_den = params->p_den;
     M.A.q = params->q;
+    M.A.ktab = params->k_table;
+    M.A.ktab_len = params->k_table_len;
     M.A.out_v = out_value;
     M.A.out_n = out_count;
     M.A.out_f = out_flags;
@@ -4464,7 +4508,8 @@ int krr_select_plan(int64_t max_segment_len, const krr_percentile_params* params
     *out = krr_select_plan_info{};
     if (params->mode == KRR_PCT_REF_INDEX) return KRR_E_UNSUPPORTED;  // no selection: an index walk
     const int64_t Lmax = max_segment_len > 0 ? max_segment_len : 1;
-    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q);
+    const SidePlan sp = plan_side(Lmax, params->mode, params->p_num, params->p_den, params->q,
+                                  params->k_table != nullptr);
     const uint32_t need = capacity_for(sp.tkeep);
     const bool hsel = window_select(need, sp.tkeep, Lmax, sp.bottom, false);
     out->hselect = hsel ? 1 : 0;

@@ -1601,6 +1601,8 @@ struct KllMergeArgs {
     double* out_v;
     int64_t* out_n;
     uint32_t* out_f;
+    const int64_t* ktab = nullptr;  // query: krr_percentile_params.k_table
+    int64_t ktab_len = 0;
 };
 
 // The series' W rows folded left to right into the image returned (LDS).
@@ -1779,7 +1781,8 @@ __global__ __launch_bounds__(64) void k_kll_query(KllMergeArgs A) {
             int64_t r0, r1;
             double gamma = 0.0;
             if (A.mode == KRR_PCT_SORTED_LOWER) {
-                r0 = r1 = exact_rank((int64_t)n, A.p_num, A.p_den);
+                r0 = r1 = rule_rank((int64_t)n, A.p_num, A.p_den, A.ktab, A.ktab_len);
+                if (!rule_covers((int64_t)n, A.ktab, A.ktab_len)) flags |= KRR_FLAG_CAPACITY;
             } else {
                 const double vidx = __dmul_rn((double)(n - 1), A.q);
                 if (vidx >= (double)(n - 1)) {

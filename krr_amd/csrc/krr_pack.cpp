@@ -16,6 +16,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -486,15 +487,25 @@ class WorkerPool {
             }
         }
         cv_.notify_all();
-        work();
+        // `work` lives on this frame: whatever it throws here (e.g. std::bad_alloc from a
+        // parse), the helpers still calling it must finish before the frame unwinds
+        std::exception_ptr mine;
+        try {
+            work();
+        } catch (...) {
+            mine = std::current_exception();
+        }
         std::unique_lock<std::mutex> l(job->m);
         job->done.wait(l, [&] { return job->pending == 0; });
+        if (mine) std::rethrow_exception(mine);
+        if (job->error) std::rethrow_exception(job->error);
     }
 
   private:
     struct Job {
         const std::function<void()>* work = nullptr;
         int pending = 0;
+        std::exception_ptr error;  // the first a helper caught (rethrown by the caller)
         std::mutex m;
         std::condition_variable done;
     };
@@ -508,9 +519,15 @@ class WorkerPool {
                 queue_.pop_front();
                 --idle_;
             }
-            (*job->work)();
+            std::exception_ptr err;
+            try {
+                (*job->work)();
+            } catch (...) {  // a detached thread must not let it escape (std::terminate)
+                err = std::current_exception();
+            }
             {
                 std::lock_guard<std::mutex> l(job->m);
+                if (err && !job->error) job->error = err;
                 if (--job->pending == 0) job->done.notify_all();
             }
             std::lock_guard<std::mutex> l(m_);

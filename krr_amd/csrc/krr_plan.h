@@ -30,13 +30,17 @@ KRR_HD inline int64_t exact_rank_hd(int64_t n, int64_t p_num, int64_t p_den) {
 // The kernel needs ranks r1 (and r1+1 for LINEAR) of the n <= L present samples.
 // Keeping the top T = L - k(L) + 2 keys (or the bottom k(L) + 4) covers every
 // n <= L, because n - k(n) and k(n) are non-decreasing in n; the +2/+4 margins
-// absorb the +-1 floor error of the float64 LINEAR index.
+// absorb the +-1 floor error of the float64 LINEAR index.  `table`: k(n) comes from
+// krr_percentile_params.k_table, which is within [k_exact(n), k_exact(n) + 1] of the exact
+// floor of p while p_num / p_den is within 1e-15 of p: two more keys on each side cover it
+// (n - k(n) may then step down by one, and k(L) may exceed the plan's estimate by two).
 struct SidePlan {
     uint32_t tkeep;
     uint32_t bottom;  // 1: keep the smallest keys (flip the order)
 };
 
-KRR_HD inline SidePlan plan_side(int64_t L, int32_t mode, int64_t p_num, int64_t p_den, double q) {
+KRR_HD inline SidePlan plan_side(int64_t L, int32_t mode, int64_t p_num, int64_t p_den, double q,
+                                 bool table = false) {
     SidePlan sp;
     if (L <= 0) {
         sp.tkeep = 1;
@@ -52,8 +56,9 @@ KRR_HD inline SidePlan plan_side(int64_t L, int32_t mode, int64_t p_num, int64_t
     } else {
         k = exact_rank_hd(L, p_num, p_den);
     }
-    int64_t top = L - k + 2;
-    int64_t bot = k + 4;
+    const int64_t wide = (table && mode != KRR_PCT_LINEAR) ? 2 : 0;
+    int64_t top = L - k + 2 + wide;
+    int64_t bot = k + 4 + wide;
     if (top > L) top = L;
     if (bot > L) bot = L;
     if (top <= bot) {

@@ -689,45 +689,12 @@ inline PyObject* dict_get(PyObject* d, PyObject* k, Py_hash_t h, bool* present) 
     return v;
 }
 
-// scan_fleet(objects, recommendations, rts, severities, settle, rec_model, rr_model, scan_model)
-//   rts: tuple of ResourceType members; severities: the 5 Severity members in code order;
-//   settle(current, recommended) -> code; *_model: (cls, field names, fields_set, slot offset)
-// -> (scans, all_keys_present)
-PyObject* scan_fleet(PyObject*, PyObject* args) {
-    bool keys_ok = true;
-    PyObject *objects, *recs, *rts, *sevs, *settle, *md_rec, *md_rr, *md_scan;
-    if (!PyArg_ParseTuple(args, "OOO!O!OO!O!O!", &objects, &recs, &PyTuple_Type, &rts, &PyTuple_Type, &sevs, &settle,
-                          &PyTuple_Type, &md_rec, &PyTuple_Type, &md_rr, &PyTuple_Type, &md_scan))
-        return nullptr;
-    if (PyTuple_GET_SIZE(sevs) != 5 || PyTuple_GET_SIZE(rts) < 1 || PyTuple_GET_SIZE(rts) > 8) {
-        PyErr_SetString(PyExc_ValueError, "scan_fleet: 5 severities and 1..8 resource types");
-        return nullptr;
-    }
-    Model M[3];
-    PyObject* mds[3] = {md_rec, md_rr, md_scan};
-    for (int i = 0; i < 3; ++i) {
-        PyObject* t = mds[i];
-        if (PyTuple_GET_SIZE(t) != 4) {
-            PyErr_SetString(PyExc_ValueError, "scan_fleet: model = (cls, names, fields_set, offset)");
-            return nullptr;
-        }
-        const Py_ssize_t off = PyLong_AsSsize_t(PyTuple_GET_ITEM(t, 3));
-        if (off <= 0 || !init_model(&M[i], PyTuple_GET_ITEM(t, 0), PyTuple_GET_ITEM(t, 1), PyTuple_GET_ITEM(t, 2), off)) {
-            if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "scan_fleet: bad slot offset");
-            return nullptr;
-        }
-    }
-#ifdef KRR_X_NODICT  // profiling variant: the scan's models without instance dicts (not valid)
-    for (int i = 0; i < 3; ++i) M[i].skip_dict = true;
-#endif
-    PyObject* ob = PySequence_Fast(objects, "objects must be a sequence");
-    if (!ob) return nullptr;
-    PyObject* rb = PySequence_Fast(recs, "recommendations must be a sequence");
-    if (!rb) {
-        Py_DECREF(ob);
-        return nullptr;
-    }
-    const Py_ssize_t n = PySequence_Fast_GET_SIZE(ob);
+// The scan loop shared by scan_fleet and scan_columns.  `recommended(i, alloc_k, sel, rv_out)`
+// gives object i's recommended value for resource type k under selector sel (0 requests,
+// 1 limits) as a new reference and whether the key is present, or returns false with an error.
+template <class RecOf>
+PyObject* scan_loop(PyObject* ob, Py_ssize_t n, PyObject* rts, PyObject* sevs, PyObject* settle, Model* M,
+                    RecOf recommended, bool* keys_ok) {
     const Py_ssize_t R = PyTuple_GET_SIZE(rts);
     PyObject* out = nullptr;
     PyObject* tmpl = nullptr;
@@ -740,10 +707,6 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
     bool ok = s_alloc && s_req && s_lim && h_alloc != -1 && h_req != -1 && h_lim != -1;
     for (Py_ssize_t k = 0; ok && k < R; ++k) ok = (h_rt[k] = PyObject_Hash(PyTuple_GET_ITEM(rts, k))) != -1;
     if (!ok) goto done;
-    if (PySequence_Fast_GET_SIZE(rb) != n) {
-        PyErr_SetString(PyExc_ValueError, "one recommendation per object");
-        goto done;
-    }
     tmpl = _PyDict_NewPresized(R);
     for (Py_ssize_t k = 0; tmpl && k < R; ++k)
         if (_PyDict_SetItem_KnownHash(tmpl, PyTuple_GET_ITEM(rts, k), Py_None, h_rt[k]) < 0) Py_CLEAR(tmpl);
@@ -752,25 +715,22 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
     if (!out) goto done;
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* obj = PySequence_Fast_GET_ITEM(ob, i);
-        PyObject* rec = PySequence_Fast_GET_ITEM(rb, i);
         PyObject* alloc = field(obj, s_alloc, h_alloc);
         PyObject* creq = alloc ? field(alloc, s_req, h_req) : nullptr;
         PyObject* clim = creq ? field(alloc, s_lim, h_lim) : nullptr;
-        PyObject* rreq = clim ? field(rec, s_req, h_req) : nullptr;
-        PyObject* rlim = rreq ? field(rec, s_lim, h_lim) : nullptr;
-        PyObject* dreq = rlim ? PyDict_Copy(tmpl) : nullptr;  // {rt: None ...}: values replaced below
+        PyObject* dreq = clim ? PyDict_Copy(tmpl) : nullptr;  // {rt: None ...}: values replaced below
         PyObject* dlim = dreq ? PyDict_Copy(tmpl) : nullptr;
         bool bad = !dlim;
         int worst = kUnknown;
         for (Py_ssize_t k = 0; !bad && k < R; ++k) {
             PyObject* rt = PyTuple_GET_ITEM(rts, k);
             PyObject* sel_cur[2] = {creq, clim};
-            PyObject* sel_rec[2] = {rreq, rlim};
             PyObject* sel_out[2] = {dreq, dlim};
             for (int j = 0; !bad && j < 2; ++j) {
                 bool pc = false, pr = false;
                 PyObject* cv = dict_get(sel_cur[j], rt, h_rt[k], &pc);
-                PyObject* rv = cv ? dict_get(sel_rec[j], rt, h_rt[k], &pr) : nullptr;
+                PyObject* rv = nullptr;
+                if (cv && !recommended(i, k, j, h_rt[k], &rv, &pr)) rv = nullptr;
 #ifndef KRR_X_NOSEV
                 const int code = rv ? severity_code(cv, rv, settle) : -1;
 #else  // profiling variant: no severity decided (scans not valid)
@@ -778,7 +738,7 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
 #endif
                 PyObject* r = code >= 0 ? M[0].make(rv, PyTuple_GET_ITEM(sevs, code)) : nullptr;
                 bad = !r || _PyDict_SetItem_KnownHash(sel_out[j], rt, r, h_rt[k]) < 0;
-                keys_ok = keys_ok && pc;  // Result's score indexes the current allocations (result.py:137-143)
+                *keys_ok = *keys_ok && pc;  // Result's score indexes the current allocations (result.py:137-143)
                 if (code >= 0 && code < worst) worst = code;
                 Py_XDECREF(r);
                 Py_XDECREF(cv);
@@ -797,8 +757,6 @@ PyObject* scan_fleet(PyObject*, PyObject* args) {
         Py_XDECREF(alloc);
         Py_XDECREF(creq);
         Py_XDECREF(clim);
-        Py_XDECREF(rreq);
-        Py_XDECREF(rlim);
         if (!scan) {
             Py_CLEAR(out);
             goto done;
@@ -810,12 +768,132 @@ done:
     Py_XDECREF(s_alloc);
     Py_XDECREF(s_req);
     Py_XDECREF(s_lim);
-    Py_DECREF(ob);
-    Py_DECREF(rb);
+    return out;
+}
+
+// The three models of a scan: (cls, field names, fields_set, slot offset) each.
+bool init_scan_models(Model* M, PyObject* md_rec, PyObject* md_rr, PyObject* md_scan) {
+    PyObject* mds[3] = {md_rec, md_rr, md_scan};
+    for (int i = 0; i < 3; ++i) {
+        PyObject* t = mds[i];
+        if (PyTuple_GET_SIZE(t) != 4) {
+            PyErr_SetString(PyExc_ValueError, "scan: model = (cls, names, fields_set, offset)");
+            return false;
+        }
+        const Py_ssize_t off = PyLong_AsSsize_t(PyTuple_GET_ITEM(t, 3));
+        if (off <= 0 || !init_model(&M[i], PyTuple_GET_ITEM(t, 0), PyTuple_GET_ITEM(t, 1), PyTuple_GET_ITEM(t, 2), off)) {
+            if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "scan: bad slot offset");
+            return false;
+        }
+    }
+#ifdef KRR_X_NODICT  // profiling variant: the scan's models without instance dicts (not valid)
+    for (int i = 0; i < 3; ++i) M[i].skip_dict = true;
+#endif
+    return true;
+}
+
+PyObject* scan_result(PyObject* out, bool keys_ok) {
     if (!out) return nullptr;
     PyObject* res = Py_BuildValue("(OO)", out, keys_ok ? Py_True : Py_False);
     Py_DECREF(out);
     return res;
+}
+
+// scan_fleet(objects, recommendations, rts, severities, settle, rec_model, rr_model, scan_model)
+//   rts: tuple of ResourceType members; severities: the 5 Severity members in code order;
+//   settle(current, recommended) -> code; *_model: (cls, field names, fields_set, slot offset)
+// -> (scans, all_keys_present)
+PyObject* scan_fleet(PyObject*, PyObject* args) {
+    bool keys_ok = true;
+    PyObject *objects, *recs, *rts, *sevs, *settle, *md_rec, *md_rr, *md_scan;
+    if (!PyArg_ParseTuple(args, "OOO!O!OO!O!O!", &objects, &recs, &PyTuple_Type, &rts, &PyTuple_Type, &sevs, &settle,
+                          &PyTuple_Type, &md_rec, &PyTuple_Type, &md_rr, &PyTuple_Type, &md_scan))
+        return nullptr;
+    if (PyTuple_GET_SIZE(sevs) != 5 || PyTuple_GET_SIZE(rts) < 1 || PyTuple_GET_SIZE(rts) > 8) {
+        PyErr_SetString(PyExc_ValueError, "scan_fleet: 5 severities and 1..8 resource types");
+        return nullptr;
+    }
+    Model M[3];
+    if (!init_scan_models(M, md_rec, md_rr, md_scan)) return nullptr;
+    PyObject* ob = PySequence_Fast(objects, "objects must be a sequence");
+    if (!ob) return nullptr;
+    PyObject* rb = PySequence_Fast(recs, "recommendations must be a sequence");
+    if (!rb) {
+        Py_DECREF(ob);
+        return nullptr;
+    }
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(ob);
+    PyObject* out = nullptr;
+    if (PySequence_Fast_GET_SIZE(rb) != n) {
+        PyErr_SetString(PyExc_ValueError, "one recommendation per object");
+    } else {
+        PyObject* s_req = PyUnicode_InternFromString("requests");
+        PyObject* s_lim = PyUnicode_InternFromString("limits");
+        const Py_hash_t h_req = s_req ? PyObject_Hash(s_req) : -1, h_lim = s_lim ? PyObject_Hash(s_lim) : -1;
+        if (h_req != -1 && h_lim != -1) {
+            // the recommendation's selector dicts of the object in hand (fetched once per object)
+            Py_ssize_t cur = -1;
+            PyObject* sel[2] = {nullptr, nullptr};
+            auto rec_of = [&](Py_ssize_t i, Py_ssize_t k, int j, Py_hash_t h, PyObject** rv, bool* present) {
+                if (i != cur) {
+                    Py_CLEAR(sel[0]);
+                    Py_CLEAR(sel[1]);
+                    cur = i;
+                    PyObject* rec = PySequence_Fast_GET_ITEM(rb, i);
+                    sel[0] = field(rec, s_req, h_req);
+                    sel[1] = sel[0] ? field(rec, s_lim, h_lim) : nullptr;
+                }
+                if (!sel[1]) return false;
+                *rv = dict_get(sel[j], PyTuple_GET_ITEM(rts, k), h, present);
+                return *rv != nullptr;
+            };
+            out = scan_loop(ob, n, rts, sevs, settle, M, rec_of, &keys_ok);
+            Py_XDECREF(sel[0]);
+            Py_XDECREF(sel[1]);
+        }
+        Py_XDECREF(s_req);
+        Py_XDECREF(s_lim);
+    }
+    Py_DECREF(ob);
+    Py_DECREF(rb);
+    return scan_result(out, keys_ok);
+}
+
+// scan_columns(objects, cpu_col, mem_col, rts, severities, settle, rec_model, rr_model, scan_model)
+// -> (scans, all_keys_present): scan_fleet of the ResourceAllocations allocations() would build
+// from the same columns (requests {cpu: c, mem: m}, limits {cpu: None, mem: m}; runner.py:113-120)
+// without building them — Runner._collect_result only reads them (runner.py:122-131).
+PyObject* scan_columns(PyObject*, PyObject* args) {
+    bool keys_ok = true;
+    PyObject *objects, *cl, *ml, *rts, *sevs, *settle, *md_rec, *md_rr, *md_scan;
+    if (!PyArg_ParseTuple(args, "OO!O!O!O!OO!O!O!", &objects, &PyList_Type, &cl, &PyList_Type, &ml, &PyTuple_Type,
+                          &rts, &PyTuple_Type, &sevs, &settle, &PyTuple_Type, &md_rec, &PyTuple_Type, &md_rr,
+                          &PyTuple_Type, &md_scan))
+        return nullptr;
+    if (PyTuple_GET_SIZE(sevs) != 5 || PyTuple_GET_SIZE(rts) != 2) {
+        PyErr_SetString(PyExc_ValueError, "scan_columns: 5 severities and the 2 resource types (CPU, Memory)");
+        return nullptr;
+    }
+    Model M[3];
+    if (!init_scan_models(M, md_rec, md_rr, md_scan)) return nullptr;
+    PyObject* ob = PySequence_Fast(objects, "objects must be a sequence");
+    if (!ob) return nullptr;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(ob);
+    PyObject* out = nullptr;
+    if (PyList_GET_SIZE(cl) != n || PyList_GET_SIZE(ml) != n) {
+        PyErr_SetString(PyExc_ValueError, "one recommendation per object");
+    } else {
+        auto rec_of = [&](Py_ssize_t i, Py_ssize_t k, int j, Py_hash_t, PyObject** rv, bool* present) {
+            PyObject* v = k == 0 ? (j == 0 ? PyList_GET_ITEM(cl, i) : Py_None) : PyList_GET_ITEM(ml, i);
+            Py_INCREF(v);
+            *rv = v;
+            *present = true;
+            return true;
+        };
+        out = scan_loop(ob, n, rts, sevs, settle, M, rec_of, &keys_ok);
+    }
+    Py_DECREF(ob);
+    return scan_result(out, keys_ok);
 }
 
 // allocations(model, rts, cpu_list, mem_list) -> list: per object a ResourceAllocations
@@ -953,6 +1031,8 @@ PyMethodDef methods[] = {
     {"classify", classify_str, METH_VARARGS, "str(Decimal) -> (float64, exactness class)"},
     {"sample", sample_py, METH_O, "one sample object -> (float64, exactness class), the packer's path"},
     {"scan_fleet", scan_fleet, METH_VARARGS, "ResourceScan per object in construct() layout -> (scans, keys_ok)"},
+    {"scan_columns", scan_columns, METH_VARARGS,
+     "scan_fleet of the ResourceAllocations two value columns describe, without building them"},
     {"allocations", allocations, METH_VARARGS, "ResourceAllocations in construct() layout from value columns"},
     {"slot_offset", slot_offset, METH_O, "byte offset of an object slot (member descriptor)"},
     {"layout_ok", layout_ok, METH_NOARGS, "whether Decimals are read in place (else through str())"},

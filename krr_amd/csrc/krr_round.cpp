@@ -435,17 +435,23 @@ struct Fast {
     int buf_digits = 0;
 };
 
-// Runner._round_value(CPU) of prom_decimal(x); false: not covered here
-bool fast_cpu(double x, const Fast& F, char* out) {
+// put_sci writes at most this many bytes (sign, 27 digits, point, "E+", exponent, NUL) for the
+// coefficients the fast paths produce (< 10^27): any width >= 64 holds it
+constexpr int32_t kFastMaxBytes = 40;
+
+// Runner._round_value(CPU) of prom_decimal(x) into out (width bytes); false: not covered here
+bool fast_cpu(double x, const Fast& F, char* out, int32_t width) {
     uint64_t D;
     int E;
     shortest(x, &D, &E);
     i128 k;  // ceil(v * 10^3)
     if (!ceil_scaled(std::signbit(x), D, E + 3, &k) || ndigits((u128)(k < 0 ? -k : k)) > kPrec - 1) return false;
     if (k < F.cpu_t) {
+        if ((int32_t)F.cpu_min_s.size() + 1 > width) return false;
         memcpy(out, F.cpu_min_s.c_str(), F.cpu_min_s.size() + 1);
         return true;
     }
+    if (width < kFastMaxBytes) return false;
     // k / 1000 at the ideal exponent 0: trailing zeros stripped up to 3
     int exp = -3;
     while (exp < 0 && k != 0 && (int)(k < 0 ? (uint64_t)(-k % 10) : (uint64_t)(k % 10)) == 0) {
@@ -458,7 +464,7 @@ bool fast_cpu(double x, const Fast& F, char* out) {
 }
 
 // simple.py:29's max * buffer, then Runner._round_value(Memory); false: not covered here
-bool fast_mem(double x, const Fast& F, char* out) {
+bool fast_mem(double x, const Fast& F, char* out, int32_t width) {
     uint64_t D;
     int E;
     shortest(x, &D, &E);
@@ -469,9 +475,11 @@ bool fast_mem(double x, const Fast& F, char* out) {
         ndigits((u128)(r < 0 ? -r : r)) > kPrec - 1)
         return false;
     if (r < F.mem_t) {
+        if ((int32_t)F.mem_min_s.size() + 1 > width) return false;
         memcpy(out, F.mem_min_s.c_str(), F.mem_min_s.size() + 1);
         return true;
     }
+    if (width < kFastMaxBytes) return false;
     put_sci(out, r, 6);  // r * 10^6 at the ideal exponent 6
     return true;
 }
@@ -533,7 +541,7 @@ extern "C" int krr_round_simple(int64_t n, const double* cpu_value, const uint32
             put(co, width, "NaN");
         } else if (cf != 0 || !std::isfinite(cpu_value[i])) {
             st |= KRR_ROUND_CPU_FALLBACK;
-        } else if (!(F.cpu_ok && fast_cpu(cpu_value[i], F, co)) &&
+        } else if (!(F.cpu_ok && fast_cpu(cpu_value[i], F, co, width)) &&
                    (!round_cpu(cpu_value[i], cpu_min, &s) || !put(co, width, s))) {
             st |= KRR_ROUND_CPU_FALLBACK;
         }
@@ -541,7 +549,7 @@ extern "C" int krr_round_simple(int64_t n, const double* cpu_value, const uint32
             put(mo, width, "NaN");
         } else if (mf != 0 || !std::isfinite(mem_value[i])) {
             st |= KRR_ROUND_MEM_FALLBACK;
-        } else if (!(F.mem_ok && fast_mem(mem_value[i], F, mo)) &&
+        } else if (!(F.mem_ok && fast_mem(mem_value[i], F, mo, width)) &&
                    (!round_mem(mem_value[i], buffer, mem_min, &s) || !put(mo, width, s))) {
             st |= KRR_ROUND_MEM_FALLBACK;
         }

@@ -59,6 +59,7 @@ REFERENCE_SIMPLE = ("robusta_krr.strategies.simple", "SimpleStrategy")
 _ORIGINAL_ATTR = "_krr_amd_original_gather"
 _ORIGINAL_COLLECT_ATTR = "_krr_amd_original_collect"
 _OPTIONS_ATTR = "_krr_amd_options"
+_PATCHED_ATTR = "_krr_amd_gather"  # marks install()'s _gather_objects_recommendations
 LOADERS = ("reference", "bodies", "grouped")
 SCANS = ("reference", "fleet")
 
@@ -103,23 +104,27 @@ async def gather_objects_recommendations(runner: Any, objects: Sequence[Any]) ->
         return [RefResourceAllocations(requests={rt: r[rt].request for rt in RefResourceType},
                                        limits={rt: r[rt].limit for rt in RefResourceType}) for r in recs]
 
-    settings = runner._strategy.settings
     batched = BatchedRunner(strategy, runner.config.cpu_min_value, runner.config.memory_min_value)
-    loader = _options(runner)["loader"]
+    fleet = await packed_fleet(runner, objects, strategy, batched)
     ref = dict(model=RefResourceAllocations, resource_type=RefResourceType)
+    # one fleet-wide kernel pass + native rounding + bulk models, off the event loop like the
+    # reference's to_thread (runner.py:106)
+    return await asyncio.to_thread(batched.allocations_packed, fleet, **ref)
+
+
+async def packed_fleet(runner: Any, objects: Sequence[Any], strategy: SimpleStrategy, batched: BatchedRunner):
+    """The fleet's PackedFleet through the installed loader: the reference's own per-object
+    gather_data (runner.py:88-102), per-pod bodies, or grouped bodies."""
+    RefResourceType, _ = _reference_types(runner)
+    settings = runner._strategy.settings
+    loader = _options(runner)["loader"]
     if loader == "bodies":
         cpu_bodies, mem_bodies = await fetch_pod_bodies(runner, objects, settings)
-        # native packer + one fleet-wide kernel pass + native rounding + bulk models, off the event loop
+        # native packer (device by default), off the event loop
         parser = _options(runner).get("parser", "device")
-
-        def run():
-            return batched.allocations_packed(batched.pack_from_bodies(cpu_bodies, mem_bodies, 0, parser), **ref)
-
-        return await asyncio.to_thread(run)
+        return await asyncio.to_thread(batched.pack_from_bodies, cpu_bodies, mem_bodies, 0, parser)
     if loader == "grouped":
-        fleet = await fetch_grouped_fleet(runner, objects, settings, _options(runner).get("parser", "device"),
-                                          batched)
-        return await asyncio.to_thread(batched.allocations_packed, fleet, **ref)
+        return await fetch_grouped_fleet(runner, objects, settings, _options(runner).get("parser", "device"), batched)
 
     async def history(obj):  # runner.py:88-102, with the reference's own loaders
         lo = runner._get_prometheus_loader(obj.cluster)
@@ -129,8 +134,7 @@ async def gather_objects_recommendations(runner: Any, objects: Sequence[Any]) ->
         return {HipResourceType(rt.value): d for rt, d in zip(RefResourceType, data)}
 
     histories = await asyncio.gather(*[history(o) for o in objects])
-    # one fleet-wide kernel pass, off the event loop like the reference's to_thread (runner.py:106)
-    return await asyncio.to_thread(batched.allocations_packed, strategy.pack(histories), **ref)
+    return strategy.pack(histories)
 
 
 # ---- body-level loaders -------------------------------------------------------------------------
@@ -274,8 +278,23 @@ async def collect_result(runner: Any):
     clusters = await runner._k8s_loader.list_clusters()
     runner.debug(f'Using clusters: {clusters if clusters is not None else "inner cluster"}')
     objects = await runner._k8s_loader.list_scannable_objects(clusters)
-    recommendations = await runner._gather_objects_recommendations(objects)
     models = sys.modules[sys.modules[type(runner).__module__].Result.__module__]
+    strategy = hip_strategy(runner._strategy)
+    if strategy is not None and getattr(type(runner)._gather_objects_recommendations, _PATCHED_ATTR, False):
+        # the gather is this module's: its ResourceAllocations would only be read by the scan, so
+        # the rounded values go straight into it (fast_round.result_batch)
+        from krr_amd.core.fast_round import result_batch
+
+        batched = BatchedRunner(strategy, runner.config.cpu_min_value, runner.config.memory_min_value)
+        fleet = await packed_fleet(runner, objects, strategy, batched)
+
+        def run():
+            raw = strategy.settings.run_fleet(fleet)
+            return result_batch(objects, raw, strategy.settings, batched.cpu_min_value, batched.memory_min_value,
+                                models=models)
+
+        return await asyncio.to_thread(run)
+    recommendations = await runner._gather_objects_recommendations(objects)
     return fleet_collect(objects, recommendations, models)
 
 
@@ -303,6 +322,8 @@ def install(runner_cls: Any = None, *, loader: str = "reference", scan: str = "r
 
         async def _gather_objects_recommendations(self, objects):
             return await gather_objects_recommendations(self, objects)
+
+        setattr(_gather_objects_recommendations, _PATCHED_ATTR, True)
 
         runner_cls._gather_objects_recommendations = _gather_objects_recommendations
     if scan == "fleet" and getattr(runner_cls, _ORIGINAL_COLLECT_ATTR, None) is None:

@@ -80,9 +80,9 @@ class SimpleStrategySettings(StrategySettings):
         with decimal.localcontext(reference_context()):
             return Decimal(1 + self.memory_buffer_percentage / 100)
 
-    def run_fleet(self, fleet: PackedFleet) -> RawResults:
+    def run_fleet(self, fleet: PackedFleet, device: Optional[int] = None) -> RawResults:
         params = self.params()
-        raw = default_engine(self.device).run_packed(fleet, params)
+        raw = default_engine(self.device if device is None else device).run_packed(fleet, params)
         if fleet.cpu.exact is not None or fleet.mem.exact is not None:
             from krr_amd.core.exact import resolve
 

@@ -74,10 +74,24 @@ def gpu_local_cpus(device: int = 0, one_per_core: bool = False) -> Optional[set]
 
 
 def bind_local(device: int = 0, one_per_core: bool = False) -> Optional[set]:
-    """Restrict this process to the GPU-local CPUs (returns them), or leave it (None)."""
+    """Restrict this process to the GPU-local CPUs (returns them), or leave it (None).
+
+    sched_setaffinity(0, ...) moves the calling thread only (Linux affinity is per thread), so
+    every thread the process already runs — HIP / torch runtime threads, worker-pool threads of
+    an earlier parallel call — is moved too, through /proc/self/task; threads created later
+    inherit the mask from their creator."""
     cpus = gpu_local_cpus(device, one_per_core)
     if cpus:
         os.sched_setaffinity(0, cpus)
+        try:
+            tids = [int(t) for t in os.listdir("/proc/self/task")]
+        except OSError:
+            tids = []
+        for tid in tids:
+            try:
+                os.sched_setaffinity(tid, cpus)
+            except OSError:  # the thread ended meanwhile
+                pass
     return cpus
 
 

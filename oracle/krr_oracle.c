@@ -13,7 +13,9 @@
  *    (robusta_krr/core/integrations/prometheus.py:150-155);
  *  - n = present samples; empty -> NaN (robusta_krr/strategies/simple.py:26-27, 33-34);
  *  - REF_INDEX: data_[int((n-1) * p / 100)] on the UNSORTED concatenation
- *    (simple.py:31-36); p = p_num/p_den, index computed exactly;
+ *    (simple.py:31-36); p = p_num/p_den, index computed exactly — or, for p whose
+ *    28-digit Decimal product rounds, k = k_table[n] (oracle_percentile_ktab: the
+ *    caller's table of the reference's own expression);
  *  - SORTED_LOWER: the same index into sorted(data_) — Python's sorted() is a
  *    stable sort under Decimal '<' (so -0 and +0 keep their input order);
  *  - LINEAR: numpy 2.2.6 np.percentile(method="linear"):
@@ -120,9 +122,13 @@ static int64_t gather_present(const double* v, int64_t beg, int64_t end, int gap
     return n;
 }
 
+static int64_t rank_k(int64_t n, int64_t p_num, int64_t p_den, const int64_t* ktab) {
+    return ktab ? ktab[n] : oracle_exact_rank(n, p_num, p_den);
+}
+
 static void one_percentile(const double* values, int64_t beg, int64_t end, int mode, int gaps,
-                           int64_t p_num, int64_t p_den, double q, double* buf, double* tmp,
-                           double* ov, int64_t* on, uint32_t* of) {
+                           int64_t p_num, int64_t p_den, const int64_t* ktab, double q, double* buf,
+                           double* tmp, double* ov, int64_t* on, uint32_t* of) {
     int64_t nnan = 0;
     int64_t n = gather_present(values, beg, end, gaps, buf, &nnan);
     *on = n;
@@ -133,7 +139,7 @@ static void one_percentile(const double* values, int64_t beg, int64_t end, int m
         return;
     }
     if (mode == REF_INDEX) {
-        *ov = buf[oracle_exact_rank(n, p_num, p_den)];
+        *ov = buf[rank_k(n, p_num, p_den, ktab)];
         return;
     }
     if (nnan && !gaps) {
@@ -143,7 +149,7 @@ static void one_percentile(const double* values, int64_t beg, int64_t end, int m
     }
     if (mode == SORTED_LOWER) {
         merge_sort(buf, tmp, n);
-        *ov = buf[oracle_exact_rank(n, p_num, p_den)];
+        *ov = buf[rank_k(n, p_num, p_den, ktab)];
         return;
     }
     /* LINEAR, numpy: virtual index (n-1)*q, clip at n-1 with gamma vs index -1 */
@@ -170,15 +176,17 @@ static void one_percentile(const double* values, int64_t beg, int64_t end, int m
     *ov = np_lerp(a, b, gamma);
 }
 
-int oracle_percentile(const double* values, const int64_t* offsets, int64_t S, int mode, int gaps,
-                      int64_t p_num, int64_t p_den, double q, double* out_v, int64_t* out_n,
-                      uint32_t* out_f, int nthreads) {
+/* k_table (may be NULL): k(n) = k_table[n], k_table_len > every segment's slots. */
+int oracle_percentile_ktab(const double* values, const int64_t* offsets, int64_t S, int mode, int gaps,
+                           int64_t p_num, int64_t p_den, const int64_t* k_table, int64_t k_table_len, double q,
+                           double* out_v, int64_t* out_n, uint32_t* out_f, int nthreads) {
     if (mode < 0 || mode > 2 || p_den <= 0 || p_num <= 0) return -1;
     int64_t lmax = 0;
     for (int64_t s = 0; s < S; ++s) {
         int64_t L = offsets[s + 1] - offsets[s];
         if (L > lmax) lmax = L;
     }
+    if (k_table && lmax >= k_table_len) return -3;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
@@ -195,13 +203,20 @@ int oracle_percentile(const double* values, const int64_t* offsets, int64_t S, i
         } else {
 #pragma omp for schedule(dynamic, 8)
             for (int64_t s = 0; s < S; ++s)
-                one_percentile(values, offsets[s], offsets[s + 1], mode, gaps, p_num, p_den, q, buf, tmp,
-                               &out_v[s], &out_n[s], &out_f[s]);
+                one_percentile(values, offsets[s], offsets[s + 1], mode, gaps, p_num, p_den, k_table, q, buf,
+                               tmp, &out_v[s], &out_n[s], &out_f[s]);
         }
         free(buf);
         free(tmp);
     }
     return err ? -2 : 0;
+}
+
+int oracle_percentile(const double* values, const int64_t* offsets, int64_t S, int mode, int gaps,
+                      int64_t p_num, int64_t p_den, double q, double* out_v, int64_t* out_n,
+                      uint32_t* out_f, int nthreads) {
+    return oracle_percentile_ktab(values, offsets, S, mode, gaps, p_num, p_den, NULL, 0, q, out_v, out_n, out_f,
+                                  nthreads);
 }
 
 int oracle_max(const double* values, const int64_t* offsets, int64_t S, int gaps, double* out_v,

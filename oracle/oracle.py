@@ -40,6 +40,9 @@ def _load():
         lib.oracle_percentile.restype = ctypes.c_int
         lib.oracle_max.argtypes = [d, d, i64, u32, d, d, d, u32]
         lib.oracle_max.restype = ctypes.c_int
+        lib.oracle_percentile_ktab.argtypes = [d, d, i64, ctypes.c_int, ctypes.c_int, i64, i64, d, i64,
+                                               ctypes.c_double, d, d, d, ctypes.c_int]
+        lib.oracle_percentile_ktab.restype = ctypes.c_int
         lib.oracle_exact_rank.argtypes = [i64, i64, i64]
         lib.oracle_exact_rank.restype = i64
         _lib = lib
@@ -51,8 +54,10 @@ def _ptr(a: np.ndarray):
 
 
 def percentile(values: np.ndarray, offsets: np.ndarray, mode: int, p_num: int, p_den: int,
-               q: float, gaps: bool = False, nthreads: int = 0):
-    """Per-segment CPU proposal: returns (value f64[S], count i64[S], flags u32[S])."""
+               q: float, gaps: bool = False, nthreads: int = 0, k_table: np.ndarray = None):
+    """Per-segment CPU proposal: returns (value f64[S], count i64[S], flags u32[S]).
+    k_table (optional int64, longer than every segment): k(n) = k_table[n] instead of the
+    exact floor of p_num / p_den (the reference's rounded index rule for long p)."""
     lib = _load()
     values = np.ascontiguousarray(values, dtype=np.float64)
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
@@ -60,8 +65,13 @@ def percentile(values: np.ndarray, offsets: np.ndarray, mode: int, p_num: int, p
     ov = np.empty(S, np.float64)
     on = np.empty(S, np.int64)
     of = np.empty(S, np.uint32)
-    rc = lib.oracle_percentile(_ptr(values), _ptr(offsets), S, mode, int(bool(gaps)), p_num, p_den,
-                               q, _ptr(ov), _ptr(on), _ptr(of), nthreads)
+    if k_table is not None:
+        kt = np.ascontiguousarray(k_table, dtype=np.int64)
+        rc = lib.oracle_percentile_ktab(_ptr(values), _ptr(offsets), S, mode, int(bool(gaps)), p_num, p_den,
+                                        _ptr(kt), kt.size, q, _ptr(ov), _ptr(on), _ptr(of), nthreads)
+    else:
+        rc = lib.oracle_percentile(_ptr(values), _ptr(offsets), S, mode, int(bool(gaps)), p_num, p_den,
+                                   q, _ptr(ov), _ptr(on), _ptr(of), nthreads)
     if rc != 0:
         raise RuntimeError(f"oracle_percentile failed: {rc}")
     return ov, on, of

@@ -43,7 +43,7 @@ def _oracle_records(settings, fleet):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--compute", choices=("oracle", "gpu"), required=True)
-    ap.add_argument("--entry", choices=("packed", "loader", "bodies"), default="packed")
+    ap.add_argument("--entry", choices=("packed", "loader", "bodies", "exact"), default="packed")
     ap.add_argument("--path", default="cli_99_5")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
@@ -61,6 +61,11 @@ def main():
 
     if args.compute == "oracle":
         SimpleStrategySettings.run_fleet_records = lambda self, fleet, device=None: _oracle_records(self, fleet)
+        from _standin import oracle_run_packed
+        from krr_amd.core.engine import SimpleEngine
+
+        SimpleEngine.run_packed = oracle_run_packed  # the exact-HistoryData path (run_fleet + locate)
+        SimpleEngine.context = lambda self: None
     else:
         from krr_amd.core.distributed import local_device
 
@@ -71,7 +76,26 @@ def main():
     runner = BatchedRunner(SimpleStrategy(SimpleStrategySettings(**kw)))
     cpu, mem = config1.inputs()
     O, P, T = cpu.shape
-    if args.entry == "packed":
+    if args.entry == "exact":
+        # HistoryData outside Prometheus' strings (tests/golden/simple_strategy_exact.json):
+        # every rank packs the whole fleet and runs its shard; the sample objects resolved on
+        # each rank must reach rank 0 (the reference returns the objects themselves)
+        from decimal import Decimal
+
+        with open(os.path.join(HERE, "golden", "simple_strategy_exact.json")) as fh:
+            doc = json.load(fh)
+        cases = [c for c in doc["cases"] if "rounded" in c["results"][args.path]]
+
+        def hist(c):
+            return {ResourceType.CPU: {k: [Decimal(x) for x in v] for k, v in c["cpu"].items() if v},
+                    ResourceType.Memory: {k: [Decimal(x) for x in v] for k, v in c["mem"].items() if v}}
+
+        fleet = runner.strategy.pack([hist(c) for c in cases])
+        res = runner.recommend_packed_sharded(fleet)
+        rows = None if res is None else [
+            [str(r[ResourceType.CPU].request), str(r[ResourceType.Memory].request), str(r[ResourceType.Memory].limit)]
+            for r in res]
+    elif args.entry == "packed":
         offs = np.arange(0, O * P * T + 1, P * T, dtype=np.int64)
         fleet = PackedFleet(PackedSeries(cpu.reshape(-1).copy(), offs, P * T),
                             PackedSeries(mem.reshape(-1).copy(), offs.copy(), P * T))

@@ -316,5 +316,92 @@ def _variant(rng, x: float, i: int) -> str:
     return canon
 
 
+def pct_main():
+    """simple_strategy_pct.json: the reference's index rule and results for cpu_percentile values
+    whose Decimal product rounds, on both settings paths: the CLI's strings
+    (Config.other_args) and direct construction with a Decimal or a float (pydantic-validated)."""
+    import decimal
+
+    from pct_inputs import INDEX_NS, INDEX_SCAN, PERCENTILES, RUN_NS, cpu_values, mem_values, pods_of
+
+    ResourceType, Config, Runner, SimpleStrategy, SimpleStrategySettings = import_reference()
+    assert decimal.getcontext().prec == 28
+
+    def runner_for(cfg):
+        runner = Runner.__new__(Runner)
+        runner.config = cfg
+        return runner
+
+    base_cfg = Config(format="json", strategy="simple", log_to_stderr=True, other_args={})
+
+    def make(path, p):
+        if path == "cli":
+            cfg = Config(format="json", strategy="simple", log_to_stderr=True,
+                         other_args={"cpu_percentile": p, "memory_buffer_percentage": "5"})
+            return cfg.create_strategy(), runner_for(cfg)
+        value = Decimal(p) if path == "direct_decimal" else float(p)
+        return SimpleStrategy(SimpleStrategySettings(cpu_percentile=value)), runner_for(base_cfg)
+
+    paths = ["cli", "direct_decimal", "direct_float"]
+    index_rows = []
+    for path in paths:
+        for p in PERCENTILES:
+            strat, _ = make(path, p)
+            st = strat.settings
+            ns = sorted(set(INDEX_NS) | set(range(1, INDEX_SCAN + 1)))
+            ks = [int(st.calculate_cpu_proposal({"r": list(range(n))})) for n in ns]
+            index_rows.append({"path": path, "p": p, "setting": str(st.cpu_percentile),
+                               "setting_type": type(st.cpu_percentile).__name__, "n": ns, "k": ks})
+
+    inputs = {}
+    for n in RUN_NS:
+        c, m = cpu_values(n), mem_values(n)
+        cs = [prom_format(float(x)) for x in c]
+        ms = [prom_format(float(x)) for x in m]
+        pods, o = [], 0
+        for ln in pods_of(n):
+            pods.append((o, o + ln))
+            o += ln
+        inputs[n] = ({f"pod{i}": [Decimal(x) for x in cs[a:b]] for i, (a, b) in enumerate(pods)},
+                     {f"pod{i}": [Decimal(x) for x in ms[a:b]] for i, (a, b) in enumerate(pods)},
+                     np.array([float(x) for x in cs]))
+    runs = []
+    for path in paths:
+        for p in PERCENTILES:
+            strat, runner = make(path, p)
+            for n in RUN_NS:
+                cpu, mem, f = inputs[n]
+                raw = strat.run({ResourceType.CPU: cpu, ResourceType.Memory: mem}, None)
+                rr = runner._format_result(raw)
+                flat = [x for v in cpu.values() for x in v]
+                srt = strat.settings.calculate_cpu_proposal({"all": sorted(flat)})
+                lin = float(np.percentile(f, float(strat.settings.cpu_percentile)))
+                runs.append({"path": path, "p": p, "n": n,
+                             "raw": {"cpu_request": dstr(raw[ResourceType.CPU].request),
+                                     "mem_request": dstr(raw[ResourceType.Memory].request)},
+                             "rounded": {"cpu_request": dstr(rr[ResourceType.CPU].request),
+                                         "mem_request": dstr(rr[ResourceType.Memory].request),
+                                         "mem_limit": dstr(rr[ResourceType.Memory].limit)},
+                             "sorted": dstr(srt), "linear_hex": lin.hex()})
+    doc = {
+        "generator": "tests/golden/make_golden.py pct (inputs: tests/golden/pct_inputs.py)",
+        "reference": "yonahd/krr 1.0.0 @ /root/reference (imported, not copied)",
+        "paths": {"cli": "Config(other_args={'cpu_percentile': p, 'memory_buffer_percentage': '5'}).create_strategy()",
+                  "direct_decimal": "SimpleStrategy(SimpleStrategySettings(cpu_percentile=Decimal(p)))",
+                  "direct_float": "SimpleStrategy(SimpleStrategySettings(cpu_percentile=float(p)))"},
+        "index": index_rows,
+        "runs": runs,
+    }
+    path = os.path.join(HERE, "simple_strategy_pct.json")
+    with open(path, "w") as fh:
+        json.dump(doc, fh, indent=0, sort_keys=True)
+    print(f"wrote {path}: {len(index_rows)} index rows, {len(runs)} runs")
+
+
 if __name__ == "__main__":
-    main()
+    sys.path.insert(0, HERE)
+    if sys.argv[1:] == ["pct"]:
+        pct_main()
+    else:
+        main()
+        pct_main()

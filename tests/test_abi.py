@@ -56,7 +56,7 @@ def test_library_is_gfx950_code_object(lib):
 
 
 def test_abi_version_and_null_handling(lib):
-    assert lib.krr_abi_version() == 2
+    assert lib.krr_abi_version() == 3
     assert lib.krr_last_error(None) == b"null krr_ctx"
     assert lib.krr_segmented_percentile(None, None, None, None, None, None, None) == -1
     assert lib.krr_segmented_max(None, None, None, None, None, None) == -1
@@ -74,7 +74,7 @@ def test_struct_layouts_match_header():
     from krr_amd import _native
 
     assert ctypes.sizeof(_native.KrrSeries) == 8 * 5 + 4 * 2
-    assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 3
+    assert ctypes.sizeof(_native.KrrPercentileParams) == 4 * 2 + 8 * 5
     assert ctypes.sizeof(_native.KrrSketchLoc) == 8 * 5 + 4 * 4 and _native.LOC_WORDS == 7
     assert ctypes.sizeof(_native.KrrJsonBodies) == 8 * 4
 

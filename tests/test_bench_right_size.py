@@ -35,5 +35,5 @@ def test_right_size_leg_equals_per_object_path():
     # the pool puts (resource, selector) pairs in every bucket the reference scores
     assert {"GOOD", "OK", "WARNING", "CRITICAL", "UNKNOWN"} <= set(sev), sev
     split = out["config4_right_size_split_s"]
-    assert set(split) == {"unpack", "round", "decimal", "allocations_models", "scan_and_score"}
+    assert set(split) == {"unpack", "round", "decimal", "scan_and_score"}
     assert out["config4_scan_objects_per_s"] > 0

@@ -179,6 +179,19 @@ def test_sharded_runner_matches_reference_fixture(entry, path, tmp_path):
     assert run_sharded_workers(2, "oracle", entry, path, tmp_path) == expected_rows(path)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_runner_resolves_exact_history(world, tmp_path):
+    """HistoryData with non-canonical Decimals ('0.10', 25-digit values, float
+    collisions) through recommend_packed_sharded: the sample objects each rank resolves reach
+    rank 0, so N ranks answer as the reference (tests/golden/simple_strategy_exact.json)."""
+    with open(os.path.join(HERE, "golden", "simple_strategy_exact.json")) as fh:
+        doc = json.load(fh)
+    want = [[c["results"]["cli_99_5"]["rounded"][k] for k in ("cpu_request", "mem_request", "mem_limit")]
+            for c in doc["cases"] if "rounded" in c["results"]["cli_99_5"]]
+    got = run_sharded_workers(world, "oracle", "exact", "cli_99_5", tmp_path)
+    assert got == want
+
+
 def test_sharded_runner_three_ranks_equals_one(tmp_path):
     assert run_sharded_workers(3, "oracle", "packed", "cli_99_5", tmp_path) == \
         run_sharded_workers(1, "oracle", "packed", "cli_99_5", tmp_path)

@@ -86,8 +86,10 @@ def test_percentile_params_exact_rationals():
     assert p.q == 0.99 and p.mode == 2
     p = percentile_params(Decimal(99.9), "ref_index")  # binary float made exact: 2^-k denominator
     assert p.p_den <= 10**15
-    with pytest.raises(ValueError):
-        percentile_params(Decimal("99.12345678901234567"), "ref_index")
+    # more digits than the kernels' exact floor takes: an approximation that only sizes buffers,
+    # and the reference's own index rule (a table bound at launch; tests/test_index_rule.py)
+    p = percentile_params(Decimal("99.12345678901234567"), "ref_index")
+    assert p.p_den <= 10**15 and p.rule.needs_table(2) and not p.k_table
     with pytest.raises(ValueError):
         percentile_params(Decimal("0"), "ref_index")
     with pytest.raises(ValueError):
