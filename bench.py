@@ -100,6 +100,11 @@ def parse():
                     help="N > 1 records path: stream = RCCL send/recv through the C ABI on the launch stream "
                          "(gloo: torch); torch = torch.distributed.gather on its own stream, step k's gather "
                          "overlapping step k+1's kernel; blocking = torch gather + host copy after each kernel")
+    ap.add_argument("--comm", choices=("own", "torch"), default="own",
+                    help="N > 1, --gather stream: the RCCL communicator the C-ABI gather uses: own = the "
+                         "library's (krr_comm_unique_id on rank 0, the id broadcast over torch.distributed, "
+                         "krr_comm_init_timeout on every rank); torch = torch.distributed's own (a private "
+                         "ProcessGroupNCCL accessor)")
     ap.add_argument("--records", choices=("host", "device"), default="host",
                     help="N = 1: the fused launch writes the 32-B records straight into page-locked host "
                          "memory (host) or into HBM followed by a D2H copy (device)")
@@ -455,12 +460,11 @@ def main():
     gather_mode = args.gather if dist_on else None
     if gather_mode == "stream" and args.separate:
         gather_mode = "torch"
-    comm = None
-    if gather_mode == "stream":
-        # the RCCL communicator torch.distributed made (record_counts' all_gather created it)
-        comm = pg_comm(dev) if backend == "nccl" else None
-        if comm is None:
-            gather_mode = "torch"
+    comm, comm_src = None, None
+    if gather_mode == "stream" and backend == "nccl":
+        comm, comm_src = make_comm(args, ctx, dev, world, rank)
+    if gather_mode == "stream" and comm is None:
+        gather_mode = "torch"
     # N > 1 over RCCL, "stream" (default): the gather is enqueued on the launch stream through
     # the C ABI (krr_gather_results with torch's communicator), so a step is launch -> send/recv
     # with no cross-stream dependency in the launch queue (each cost 20-30 us of idle queue,
@@ -581,10 +585,10 @@ def main():
     if comm is not None:
         try:
             n_comm, r_comm = ctx.comm_info(comm)
-            rccl_info = {"ranks": n_comm, "rank0_rank": r_comm, "source": "ncclCommCount/ncclCommUserRank through "
-                         "krr_comm_info on torch.distributed's nccl communicator"}
+            rccl_info = {"ranks": n_comm, "rank0_rank": r_comm, "communicator": comm_src,
+                         "source": "ncclCommCount/ncclCommUserRank through krr_comm_info"}
         except _native.NativeError as e:
-            rccl_info = {"error": str(e)}
+            rccl_info = {"error": str(e), "communicator": comm_src}
     elif dist_on and backend == "nccl":
         rccl_info = {"ranks": None, "note": "torch.distributed's communicator not exposed: torch.distributed.gather"}
     if gather_mode == "stream":
@@ -825,6 +829,9 @@ def main():
         print(json.dumps(result), file=_JSON_OUT, flush=True)
     if dist_on:
         dist.barrier()
+        if comm is not None and args.comm == "own":
+            torch.cuda.synchronize()
+            ctx.comm_destroy(comm)
         dist.destroy_process_group()
     ctx.close()
 
@@ -917,18 +924,20 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         if parser == "hybrid":  # the host share settles on the rates both sides reach together
             for _ in range(5):
                 runner.recommend_from_bodies(cpu_b, mem_b, threads=threads, parser=parser)
-        best_e = float("inf")
-        for _ in range(2 if parser == "host" else 3):
+        runs_e = []
+        for _ in range(3 if parser == "host" else 7):
             t0 = time.perf_counter()
             res = runner.recommend_from_bodies(cpu_b, mem_b, threads=threads, parser=parser)
-            best_e = min(best_e, time.perf_counter() - t0)
+            runs_e.append(time.perf_counter() - t0)
             if parser != "host":
                 assert runner.last_pack_via == (parser, parser), runner.last_pack_via
         assert len(res) == objects
-        e2e[parser] = (best_e, [(str(r[k].request), str(r[k].limit)) for r in res for k in r])
+        e2e[parser] = (float(np.median(runs_e)), [(str(r[k].request), str(r[k].limit)) for r in res for k in r],
+                       sorted(runs_e))
     # e2e_objects_per_s: the hybrid parser (host packer on a share of the bodies while the
     # link carries the rest); the device-only and host-only figures beside it
     out["e2e_objects_per_s"] = objects / e2e["hybrid"][0]
+    out["e2e_objects_per_s_spread"] = [objects / e2e["hybrid"][2][-1], objects / e2e["hybrid"][2][0]]
     out["e2e_objects_per_s_device_parse"] = objects / e2e["device"][0]
     out["e2e_objects_per_s_host_parse"] = objects / e2e["host"][0]
     out["e2e_device_equals_host"] = e2e["device"][1] == e2e["host"][1]
@@ -978,16 +987,20 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     g_cpu, g_mem = grouped(cpu_vals, 0), grouped(mem_vals, 7)
     eg = {}
     for parser in ("host", "device"):
-        best_g = float("inf")
-        for _ in range(2):
+        runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)  # warm-up
+        runs_g = []
+        for _ in range(3 if parser == "host" else 7):
             t0 = time.perf_counter()
             res_g = runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)
-            best_g = min(best_g, time.perf_counter() - t0)
+            runs_g.append(time.perf_counter() - t0)
         assert len(res_g) == objects
-        eg[parser] = (best_g, [(str(r[k].request), str(r[k].limit)) for r in res_g[:64] for k in r])
+        eg[parser] = (float(np.median(runs_g)), [(str(r[k].request), str(r[k].limit)) for r in res_g for k in r],
+                      sorted(runs_g))
     assert runner.last_pack_via == ("device", "device"), runner.last_pack_via
     out["e2e_grouped_objects_per_s"] = objects / eg["device"][0]
+    out["e2e_grouped_objects_per_s_spread"] = [objects / eg["device"][2][-1], objects / eg["device"][2][0]]
     out["e2e_grouped_objects_per_s_host_parse"] = objects / eg["host"][0]
+    out["e2e_grouped_upload"] = _dp(dev.index or 0).last_upload
     out["e2e_grouped_device_equals_host"] = eg["device"][1] == eg["host"][1]
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",
@@ -995,6 +1008,8 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
                   f"{json_bytes / 1e9:.2f} GB of query_range JSON ({distinct} distinct pod series per resource, "
                   f"generated in {t_g:.1f} s)",
         "pack_s": best, "device_pack_s": best_d, "e2e_s": e2e["hybrid"][0], "e2e_device_parse_s": e2e["device"][0],
+        "e2e_runs_s": {p: [round(t, 5) for t in e2e[p][2]] for p in e2e},
+        "e2e_grouped_runs_s": {p: [round(t, 5) for t in eg[p][2]] for p in eg},
         "e2e_host_parse_s": e2e["host"][0],
         "grouped": f"{len(plan.groups)} grouped bodies per resource ({sum(len(b) for b in g_cpu) / 1e9:.2f} GB of "
                    f"CPU JSON), e2e {eg['device'][0]:.3f} s device parse, {eg['host'][0]:.3f} s host parse",
@@ -1006,7 +1021,10 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
                       "parser='hybrid' (the last share of the bodies parsed by the host packer while the rest "
                       "crosses PCIe raw and is parsed on the device; e2e_device_parse: parser='device'; "
                       "e2e_host_parse: parser='host'): pack -> fused kernel -> native exact-decimal rounding -> "
-                      "RunResults (best of 2-3; every object's strings compared across the three)"}
+                      "RunResults (the median of 7 runs, 3 for the host parser, each run's seconds in e2e_runs_s and "
+                      "the slowest / fastest rate in *_spread; every object's strings compared across the parsers); "
+                      "e2e_grouped: recommend_from_grouped, the same median rule, bodies staged with their "
+                      "timestamps cut as the per-pod ones (e2e_grouped_upload), every object compared"}
     return out
 
 
@@ -1218,6 +1236,45 @@ def host_path_sharded(args, dev, world, rank, coll_dev, objects: int = 2000, pod
                                f"pods x {SLOTS_7D} samples x 2 resources of query_range JSON per rank, packed on the "
                                f"rank's GPU with {threads} host threads, one kernel pass, records gathered to rank 0 "
                                f"and rounded there; {total} objects / max over ranks of the call (best of 3)")}
+
+
+def make_comm(args, ctx, dev, world: int, rank: int):
+    """The RCCL communicator of the C-ABI gather and where it came from, or (None, reason).
+
+    --comm own (default): the library's own — rank 0 makes the id (krr_comm_unique_id), every
+    rank receives it over torch.distributed (broadcast_object_list, a public API) and joins with
+    krr_comm_init_timeout, which gives up after 60 s instead of hanging when a peer never
+    arrives; every rank then agrees (one all_reduce) that all of them hold one, else none is used.
+    --comm torch: torch.distributed's own communicator (pg_comm, a private accessor)."""
+    import torch
+    import torch.distributed as dist
+
+    if args.comm == "torch":
+        c = pg_comm(dev)
+        return (c, "torch.distributed ProcessGroupNCCL._comm_ptr()") if c is not None else (None, "not exposed")
+    uid = [None]
+    err = None
+    if rank == 0:
+        try:
+            uid[0] = ctx.comm_unique_id()
+        except _native.NativeError as e:
+            err = str(e)
+    dist.broadcast_object_list(uid, src=0)
+    comm = None
+    if uid[0] is not None:
+        try:
+            comm = ctx.comm_init(world, uid[0], rank, timeout_s=60.0)
+        except _native.NativeError as e:
+            err = str(e)
+    ok = torch.tensor([1 if comm else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if comm:
+            ctx.comm_destroy(comm)
+        print(f"bench.py rank {rank}: own RCCL communicator unavailable ({err}); torch.distributed.gather",
+              file=sys.stderr)
+        return None, f"own communicator failed: {err}"
+    return comm, "krr_comm_unique_id + krr_comm_init_timeout (the id broadcast over torch.distributed)"
 
 
 def pg_comm(dev):

@@ -122,6 +122,21 @@ int krr_pack_concat_strip(const char* const* bodies, const int64_t* body_lens, i
                           const int64_t* dst_offsets, char* dst, int32_t threads, int32_t max_runs,
                           int64_t* new_lens, int64_t* run_first, int32_t* n_runs);
 
+/* The same stripped staging in PIECES that may split a large body (grouped `sum by (pod)` bodies
+ * of ~100 MB, which one thread would strip alone): bodies of fewer than 2P bytes (P = total /
+ * max_pieces) go in runs of whole bodies as above; a larger one is cut near every P bytes at a
+ * sample's '[' after a value string (`"],[` whose quote closes a string, found from the quote
+ * parity counted in parallel; a strippable body has no backslash), where no token spans the cut,
+ * so its pieces strip apart to exactly what the whole-body copy writes.  Piece j starts at byte
+ * piece_start[j] of the unstripped layout (dst_offsets coordinates; piece_start[n_pieces] = the
+ * end) and its piece_out[j] stripped bytes are written from dst[piece_start[j] - dst_offsets[0]]
+ * on; the pieces concatenated in order are the stripped bodies back to back.  new_lens[b] = the
+ * stripped bytes of body b.  A body with an unstrippable piece is copied unchanged.  piece_start
+ * needs 2 n_bodies + max_pieces + 1 entries, piece_out 2 n_bodies + max_pieces. */
+int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                                 const int64_t* dst_offsets, char* dst, int32_t threads, int32_t max_pieces,
+                                 int64_t* new_lens, int64_t* piece_start, int64_t* piece_out, int32_t* n_pieces);
+
 /* One body stripped as above into out (body_len bytes of room): the bytes written, or -1
  * when it is not strippable.  (Tests and probes.) */
 int64_t krr_pack_strip_body(const char* body, int64_t body_len, char* out);
@@ -141,6 +156,18 @@ int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int6
                            const int64_t* segments, int64_t n_segments, const int64_t* slot_body,
                            const char* slot_names, const int64_t* slot_name_offsets, int64_t n_slots,
                            int64_t* slot_src, int64_t* slot_count, int32_t* body_ok, int32_t threads);
+
+/* The same over a staged copy whose bytes do not sit at their device offsets: the staged
+ * pieces of krr_pack_concat_strip(_pieces) — piece j holds device positions [piece_dev[j],
+ * piece_dev[j + 1]) (ascending; the last one to the end), the byte at device position p of it
+ * at bodies[p + piece_shift[j]].  Pieces cut a body only inside values arrays, so the envelope,
+ * the bytes between series and every label sit inside one piece each. */
+int krr_pack_route_grouped_pieces(const char* bodies, const int64_t* body_offsets, int64_t n_bodies,
+                                  const int64_t* piece_dev, const int64_t* piece_shift, int64_t n_pieces,
+                                  const char* label, const int64_t* segments, int64_t n_segments,
+                                  const int64_t* slot_body, const char* slot_names,
+                                  const int64_t* slot_name_offsets, int64_t n_slots, int64_t* slot_src,
+                                  int64_t* slot_count, int32_t* body_ok, int32_t threads);
 
 #ifdef __cplusplus
 }

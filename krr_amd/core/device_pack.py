@@ -99,20 +99,22 @@ class DevicePacker:
 
         return torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
 
-    def _upload(self, flat, want_ts, st, launch, strip: bool = False):
+    def _upload(self, flat, want_ts, st, launch, strip: bool = False, pieces: bool = False):
         """``flat``: the bodies (bytes), or a body table (int64 buffer addresses, int64
-        lengths) from ``_body_table``."""
+        lengths) from ``_body_table``.  ``pieces``: stripped in pieces that may cut a large body
+        (``_upload_pieces``)."""
         if isinstance(flat, tuple):
-            return self._upload_table(int(flat[0].ctypes.data), flat[1], want_ts, st, launch, strip)
+            return self._upload_table(int(flat[0].ctypes.data), flat[1], want_ts, st, launch, strip, pieces)
         lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=len(flat))
         ptrs = (ctypes.c_char_p * len(flat))(*flat)  # alive while the staging below runs
-        return self._upload_table(ctypes.addressof(ptrs), lens, want_ts, st, launch, strip)
+        return self._upload_table(ctypes.addressof(ptrs), lens, want_ts, st, launch, strip, pieces)
 
-    def _upload_table(self, ptr_addr, lens, want_ts, st, launch, strip: bool = False):
+    def _upload_table(self, ptr_addr, lens, want_ts, st, launch, strip: bool = False, pieces: bool = False):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
         copy stream and call ``launch(jb, a, b, tmp_v, tmp_t, lo, hi)`` on ``st`` for bodies
         [a, b) = bytes [lo, hi) once the chunk is there.  ``strip``: the bodies' timestamps
-        are cut while staging (``_upload_stripped``; lo / hi are then meaningless)."""
+        are cut while staging (``_upload_stripped``; lo / hi are then the chunk's device positions,
+        and ``self._layout`` says where each body sits)."""
         import torch
 
         dev = self.device
@@ -121,8 +123,11 @@ class DevicePacker:
         np.cumsum(lens, out=boffs[1:])
         total = int(boffs[-1])
         stage = self._staging(total + 128)
+        self._layout = (boffs, None)  # device offsets, staging shift (none: same offsets)
         d_bodies = torch.empty(total + 128, dtype=torch.uint8, device=dev)
         if strip and not want_ts and nb:
+            if pieces:
+                return self._upload_pieces(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch)
             return self._upload_stripped(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch)
         d_boffs = torch.from_numpy(boffs).to(dev)
         slots = total // 8 + 1
@@ -160,7 +165,8 @@ class DevicePacker:
         bodies are stripped by the host threads in runs, run r back to back inside its own
         unstripped extent of the staging buffer; the runs go to HBM back to back, so the device
         offsets are the prefix sums of the stripped lengths (uploaded per chunk before its
-        parse).  The scratch is sized for the unstripped bytes (an upper bound)."""
+        parse).  The scratch is sized for the unstripped bytes (an upper bound).  ``launch``
+        gets the chunk's DEVICE byte range; ``self._layout`` keeps the device body offsets."""
         import os
 
         import torch
@@ -218,12 +224,85 @@ class DevicePacker:
                 ev = torch.cuda.Event()
                 ev.record(cs)
             st.wait_event(ev)
-            launch(jb, a, b, tmp_v, None, lo, int(boffs[b]))
+            launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
             a = b
         self._last = (d_bodies, stage, new_offs)
+        self._layout = (no.copy(), None)
         sent = int(no[nb])
         self.last_upload = {"bytes": total, "bytes_sent": sent, "bodies": nb,
                             "bodies_stripped": int((new_lens < lens).sum())}
+        return lens, boffs, total, jb, tmp_v, None
+
+    def _upload_pieces(self, ptr_addr, lens, boffs, total, stage, d_bodies, st, launch):
+        """_upload_stripped for a few large bodies (grouped `sum by (pod)` responses, ~100 MB each):
+        each chunk is stripped by krr_pack_concat_strip_pieces, which cuts a large body at sample
+        boundaries into pieces the host threads strip apart (one thread per body would bound the
+        staging at ~13 GB/s); the pieces go to HBM back to back.  ``self._layout`` = (device body
+        offsets, None, (piece device starts, piece staging shifts)) for the host's routing."""
+        import os
+
+        import torch
+
+        dev = self.device
+        nb = len(lens)
+        T = self.threads or len(os.sched_getaffinity(0))
+        max_pieces = max(2, 2 * T)
+        cap = 2 * nb + max_pieces
+        new_lens = np.empty(nb, dtype=np.int64)
+        p_start = np.empty(cap + 1, dtype=np.int64)
+        p_out = np.empty(cap, dtype=np.int64)
+        n_p = ctypes.c_int32(0)
+        new_offs = torch.zeros(nb + 1, dtype=torch.int64, pin_memory=True)
+        no = new_offs.numpy()
+        d_boffs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+        tmp_v = torch.empty(total // 8 + 1, dtype=torch.float64, device=dev)
+        jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
+        host = load_library()
+        cs = self._copy_stream
+        cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
+        o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
+        piece_dev, piece_shift = [], []
+        a = 0
+        step = min(self.chunk_bytes, 16 << 20)
+        while a < nb:
+            b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
+            step = min(step * 3 // 2, self.chunk_bytes)
+            b = min(max(b, a + 1), nb)
+            lo = int(boffs[a])
+            rc = host.krr_pack_concat_strip_pieces(ptr_addr + a * 8, lens[a:].ctypes.data, b - a,
+                                                   boffs[a:].ctypes.data, stage.data_ptr() + lo, self.threads,
+                                                   max_pieces, new_lens[a:].ctypes.data, p_start.ctypes.data,
+                                                   p_out.ctypes.data, ctypes.byref(n_p))
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_concat_strip_pieces failed")
+            np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
+            no[a + 1:b + 1] += no[a]
+            k = n_p.value
+            pd = no[a] + np.concatenate([[0], np.cumsum(p_out[:k])[:-1]]).astype(np.int64)
+            piece_dev.append(pd)
+            piece_shift.append(p_start[:k] - pd)
+            # every piece, then the chunk's body offsets: one native call of async copies
+            dst = np.empty(k + 1, dtype=np.int64)
+            src = np.empty(k + 1, dtype=np.int64)
+            nby = np.empty(k + 1, dtype=np.int64)
+            dst[:k], src[:k], nby[:k] = d_base + pd, s_base + p_start[:k], p_out[:k]
+            dst[k], src[k], nby[k] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
+            self.ctx.copy_h2d_batch(dst, src, nby, stream=cs)
+            with torch.cuda.stream(cs):
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            st.wait_event(ev)
+            launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
+            a = b
+        self._last = (d_bodies, stage, new_offs)
+        pdev = np.concatenate(piece_dev) if piece_dev else np.zeros(0, np.int64)
+        psh = np.concatenate(piece_shift) if piece_shift else np.zeros(0, np.int64)
+        # an empty piece shares its device start with the next: keep the last of such a group
+        keep = np.concatenate([np.diff(pdev) > 0, [True]]) if pdev.size else np.zeros(0, bool)
+        self._layout = (no.copy(), None, (np.ascontiguousarray(pdev[keep]), np.ascontiguousarray(psh[keep])))
+        self.last_upload = {"bytes": total, "bytes_sent": int(no[nb]), "bodies": nb,
+                            "bodies_stripped": int((new_lens < lens).sum()), "pieces": int(pdev.size)}
         return lens, boffs, total, jb, tmp_v, None
 
     def pack_grouped(self, plan, bodies: Sequence[bytes], *, want_timestamps: bool = False,
@@ -279,14 +358,19 @@ class DevicePacker:
             self.ctx.json_find_series(jb, cand, n_cand, begin=seen[0], end=end, limit=hi, stream=st)
             seen[0] = end
 
-        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch)
+        # timestamps cut while staging, as for per-pod bodies: the candidate search, the series
+        # parse and the host's chain walk read structure, labels and value strings only
+        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch, strip=self.strip,
+                                                            pieces=True)
+        dev_offs, shift = self._layout[:2]
+        pieces = self._layout[2] if len(self._layout) > 2 else None
         with torch.cuda.stream(st):
             nc = int(n_cand.item())  # sync
         if nc > cap:
             return [host_fallback(r, body0[r + 1] - body0[r]) for r in range(len(items))]
         starts = torch.sort(cand[:nc]).values
         starts_h = starts.cpu().numpy()
-        body_of = np.searchsorted(boffs, starts_h, side="right") - 1
+        body_of = np.searchsorted(dev_offs, starts_h, side="right") - 1
         segs = torch.empty((max(nc, 1), 7), dtype=torch.int64, device=dev)
         with torch.cuda.stream(st):
             self.ctx.json_parse_segments(jb, starts, torch.from_numpy(body_of).to(dev), label, want_ts, tmp_v, tmp_t,
@@ -300,12 +384,13 @@ class DevicePacker:
             slot_src = np.empty(ns, dtype=np.int64)
             slot_cnt = np.empty(ns, dtype=np.int64)
             body_ok = np.empty(max(nb, 1), dtype=np.int32)
-            b_offs = np.ascontiguousarray(boffs[body0[r]:body0[r + 1] + 1])
-            rc = host.krr_pack_route_grouped(stage.data_ptr(), b_offs.ctypes.data, nb, label.encode(),
-                                             segs_h.ctypes.data, nc, plan.slot_group.ctypes.data,
-                                             plan._names or b"\0", plan._name_offsets.ctypes.data, ns,
-                                             slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data,
-                                             self.threads)
+            b_offs = np.ascontiguousarray(dev_offs[body0[r]:body0[r + 1] + 1])
+            pdev, psh = pieces if pieces is not None else (np.zeros(0, np.int64), np.zeros(0, np.int64))
+            rc = host.krr_pack_route_grouped_pieces(
+                stage.data_ptr(), b_offs.ctypes.data, nb, pdev.ctypes.data, psh.ctypes.data, pdev.size,
+                label.encode(), segs_h.ctypes.data, nc, plan.slot_group.ctypes.data, plan._names or b"\0",
+                plan._name_offsets.ctypes.data, ns, slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data,
+                self.threads)
             if rc != KRR_PACK_OK:
                 raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
             if not body_ok[:nb].all():

@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = ("krr_pack_abi_version", "krr_pack_parse", "krr_pack_n_values
                     "krr_pack_copy", "krr_pack_error", "krr_pack_free", "krr_pack_parse_series", "krr_series_count",
                     "krr_series_label", "krr_series_len", "krr_series_copy", "krr_series_error", "krr_series_free",
                     "krr_pack_parse_grouped", "krr_round_simple", "krr_pack_concat", "krr_pack_route_grouped",
-                    "krr_pack_concat_strip", "krr_pack_strip_body")
+                    "krr_pack_concat_strip", "krr_pack_strip_body", "krr_pack_route_grouped_pieces",
+                    "krr_pack_concat_strip_pieces")
 
 
 class PackerUnavailable(RuntimeError):
@@ -108,6 +109,11 @@ def load_library() -> ctypes.CDLL:
         lib.krr_pack_route_grouped.argtypes = [vp, vp, i64, ctypes.c_char_p, vp, i64, vp, ctypes.c_char_p, vp, i64,
                                                vp, vp, vp, i32]
         lib.krr_pack_route_grouped.restype = ctypes.c_int
+        lib.krr_pack_route_grouped_pieces.argtypes = [vp, vp, i64, vp, vp, i64, ctypes.c_char_p, vp, i64, vp,
+                                                      ctypes.c_char_p, vp, i64, vp, vp, vp, i32]
+        lib.krr_pack_route_grouped_pieces.restype = ctypes.c_int
+        lib.krr_pack_concat_strip_pieces.argtypes = [vp, vp, i64, vp, vp, i32, i32, vp, vp, vp, ctypes.POINTER(i32)]
+        lib.krr_pack_concat_strip_pieces.restype = ctypes.c_int
         if lib.krr_pack_abi_version() != 1:
             raise PackerUnavailable("libkrr_host.so packer ABI version mismatch")
         _lib = lib

@@ -787,5 +787,48 @@ inline bool chain_grouped(const char* buf, int64_t ob, int64_t oe, const char* l
     }
 }
 
+// chain_grouped over a staged copy in pieces (krr_pack_route_grouped_pieces): M.at(pos) = the
+// byte at device position pos, M.end(pos) = one past the last position of pos's piece.  Pieces
+// cut a body only inside values arrays, so the head walk (to the first series), the bytes after
+// each series and the tail each lie inside one piece.
+template <class Map, class Find, class Emit>
+inline bool chain_grouped_mapped(const Map& M, int64_t ob, int64_t oe, const char* label, int64_t label_len,
+                                 const int64_t* seg, Find find, Emit emit) {
+    GroupedWalker W;
+    const char* h = M.at(ob);
+    const int64_t he = M.end(ob) < oe ? M.end(ob) : oe;
+    W.init(h, h + (he - ob), label, label_len);
+    W.stop_at_series = true;
+    int ev = W.step();
+    if (ev == W_DONE) return true;   // no series (empty result)
+    if (ev != W_AT_SERIES) return false;
+    int64_t pos = ob + (W.r.p - h);
+    for (;;) {
+        const int64_t j = find(pos);
+        if (j < 0 || !seg[7 * j + 6]) return false;
+        emit(j);
+        const int64_t qp = seg[7 * j + 1];  // one past the series' '}'
+        if (qp >= oe) return false;
+        const char* q0 = M.at(qp);
+        const int64_t qend = M.end(qp) < oe ? M.end(qp) : oe;
+        const char* qe = q0 + (qend - qp);
+        const char* q = q0;
+        skip_ws(q, qe, PlainLoad{});
+        if (q >= qe) return false;
+        if (*q == ',') {
+            const char* p = q + 1;
+            skip_ws(p, qe, PlainLoad{});
+            if (p >= qe || *p != '{') return false;
+            pos = qp + (p - q0);
+            continue;
+        }
+        if (*q != ']') return false;
+        W.r.e = qe;
+        W.resume(q, GroupedWalker::RESULT_NEXT);
+        W.stop_at_series = false;
+        return W.step() == W_DONE && qe == q0 + (oe - qp);  // the tail ends the body, in this piece
+    }
+}
+
 }  // namespace json
 }  // namespace krr

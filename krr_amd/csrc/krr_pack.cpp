@@ -870,6 +870,145 @@ int krr_pack_concat_strip(const char* const* bodies, const int64_t* body_lens, i
     return KRR_PACK_OK;
 }
 
+int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_lens, int64_t n_bodies,
+                                 const int64_t* dst_offsets, char* dst, int32_t threads, int32_t max_pieces,
+                                 int64_t* new_lens, int64_t* piece_start, int64_t* piece_out, int32_t* n_pieces) {
+    if (n_bodies < 0 || max_pieces < 1 || !piece_start || !piece_out || !n_pieces ||
+        (n_bodies > 0 && (!bodies || !body_lens || !dst_offsets || !dst || !new_lens)))
+        return KRR_PACK_E_INVALID;
+    for (int64_t b = 0; b < n_bodies; ++b)
+        if (body_lens[b] < 0 || (body_lens[b] > 0 && !bodies[b]) ||
+            dst_offsets[b + 1] - dst_offsets[b] != body_lens[b])
+            return KRR_PACK_E_INVALID;
+    const int64_t base = n_bodies > 0 ? dst_offsets[0] : 0;
+    const int64_t total = n_bodies > 0 ? dst_offsets[n_bodies] - base : 0;
+    const int64_t P = std::max<int64_t>(1, (total + max_pieces - 1) / max_pieces);
+    const bool simd = krr::strip::supported();
+    // nominal pieces: runs of whole bodies of ~P bytes; a body of >= 2P bytes on its own, cut at
+    // nominal offsets (moved to the next `"],[` below) into about len / P parts
+    struct Nom {
+        int64_t body, lo, hi;  // body (the first, for a run of whole bodies) and its bytes [lo, hi)
+        int64_t last;          // one past the run's last body (whole-body runs), or body + 1
+        int64_t quotes = 0;
+        const char* start = nullptr;  // the actual start after the split search
+    };
+    std::vector<Nom> nom;
+    try {
+        for (int64_t b = 0; b < n_bodies;) {
+            const int64_t n = body_lens[b];
+            if (n >= 2 * P && simd) {
+                const int64_t k = (n + P - 1) / P;  // <= max_pieces + 1 (n <= total)
+                for (int64_t i = 0; i < k; ++i) nom.push_back(Nom{b, n * i / k, n * (i + 1) / k, b + 1});
+                ++b;
+                continue;
+            }
+            int64_t e = b, bytes = 0;
+            while (e < n_bodies && (e == b || (bytes + body_lens[e] <= P && body_lens[e] < 2 * P))) bytes += body_lens[e++];
+            nom.push_back(Nom{b, 0, body_lens[b], e});
+            b = e;
+        }
+    } catch (...) {
+        return KRR_PACK_E_INVALID;
+    }
+    const int64_t N = (int64_t)nom.size();
+    // parity: quotes of every cut part (parallel), then each cut part's start moved to a split
+    parallel_for(N, threads, [&](int64_t i) {
+        Nom& u = nom[(size_t)i];
+        if (u.last == u.body + 1 && !(u.lo == 0 && u.hi == body_lens[u.body]))
+            u.quotes = krr::strip::count_quotes(bodies[u.body] + u.lo, bodies[u.body] + u.hi);
+    });
+    {
+        int64_t q = 0;
+        for (int64_t i = 0; i < N; ++i) {  // quotes before each cut part inside its body
+            Nom& u = nom[(size_t)i];
+            if (u.lo == 0) q = 0;
+            const int64_t mine = u.quotes;
+            u.quotes = q;
+            q += mine;
+        }
+    }
+    parallel_for(N, threads, [&](int64_t i) {
+        Nom& u = nom[(size_t)i];
+        const char* s0 = bodies[u.body];
+        if (u.lo == 0) {
+            u.start = s0;
+            return;
+        }
+        u.start = krr::strip::next_split(s0 + u.lo, s0 + u.hi, (u.quotes & 1) != 0);
+    });
+    // the pieces: cut parts without a split join the piece before them
+    std::vector<int64_t> ps_body, ps_first, ps_last;  // body, [start, end) byte offsets in that body
+    std::vector<const char*> ps_p, ps_e;
+    try {
+        for (int64_t i = 0; i < N; ++i) {
+            const Nom& u = nom[(size_t)i];
+            if (!u.start) continue;
+            if (u.last > u.body + 1 || (u.lo == 0 && u.hi == body_lens[u.body])) {  // whole bodies
+                ps_body.push_back(u.body);
+                ps_first.push_back(u.body);
+                ps_last.push_back(u.last);
+                ps_p.push_back(nullptr);
+                ps_e.push_back(nullptr);
+                continue;
+            }
+            if (!ps_p.empty() && ps_body.back() == u.body && ps_p.back()) ps_e.back() = u.start;
+            ps_body.push_back(u.body);
+            ps_first.push_back(u.body);
+            ps_last.push_back(u.body + 1);
+            ps_p.push_back(u.start);
+            ps_e.push_back(bodies[u.body] + body_lens[u.body]);
+        }
+    } catch (...) {
+        return KRR_PACK_E_INVALID;
+    }
+    const int64_t M = (int64_t)ps_body.size();
+    if (M > 2 * n_bodies + (int64_t)max_pieces) return KRR_PACK_E_INVALID;  // (the documented capacity)
+    std::vector<int64_t> out_len((size_t)M, 0);
+    std::vector<unsigned char> bad((size_t)n_bodies, 0);
+    parallel_for(M, threads, [&](int64_t j) {
+        if (!ps_p[(size_t)j]) {  // whole bodies back to back from the first one's extent
+            char* o = dst + (dst_offsets[ps_first[(size_t)j]] - base);
+            int64_t w_all = 0;
+            for (int64_t b = ps_first[(size_t)j]; b < ps_last[(size_t)j]; ++b) {
+                const int64_t n = body_lens[b];
+                int64_t w = n ? krr::strip::strip_body(bodies[b], n, o) : 0;
+                if (w < 0) {
+                    memmove(o, bodies[b], (size_t)n);
+                    w = n;
+                }
+                new_lens[b] = w;
+                o += w;
+                w_all += w;
+            }
+            out_len[(size_t)j] = w_all;
+            return;
+        }
+        const int64_t b = ps_body[(size_t)j];
+        const char* p = ps_p[(size_t)j];
+        char* o = dst + (dst_offsets[b] - base) + (p - bodies[b]);
+        out_len[(size_t)j] = krr::strip::strip_span(p, ps_e[(size_t)j], o);  // -1: not strippable
+    });
+    for (int64_t j = 0; j < M; ++j)
+        if (ps_p[(size_t)j] && out_len[(size_t)j] < 0) bad[(size_t)ps_body[(size_t)j]] = 1;
+    // a body with an unstrippable part is copied unchanged, part by part (its extents as they are)
+    parallel_for(M, threads, [&](int64_t j) {
+        if (!ps_p[(size_t)j] || !bad[(size_t)ps_body[(size_t)j]]) return;
+        const int64_t b = ps_body[(size_t)j];
+        const char* p = ps_p[(size_t)j];
+        memmove(dst + (dst_offsets[b] - base) + (p - bodies[b]), p, (size_t)(ps_e[(size_t)j] - p));
+        out_len[(size_t)j] = ps_e[(size_t)j] - p;
+    });
+    for (int64_t j = 0; j < M; ++j) {
+        const int64_t b = ps_body[(size_t)j];
+        piece_start[j] = ps_p[(size_t)j] ? dst_offsets[b] + (ps_p[(size_t)j] - bodies[b]) : dst_offsets[ps_first[(size_t)j]];
+        piece_out[j] = out_len[(size_t)j];
+        if (ps_p[(size_t)j]) new_lens[b] = (ps_p[(size_t)j] == bodies[b] ? 0 : new_lens[b]) + out_len[(size_t)j];
+    }
+    piece_start[M] = base + total;
+    *n_pieces = (int32_t)M;
+    return KRR_PACK_OK;
+}
+
 int64_t krr_pack_strip_body(const char* body, int64_t body_len, char* out) {
     if (body_len < 0 || (body_len > 0 && (!body || !out))) return -1;
     return krr::strip::strip_body(body, body_len, out);
@@ -879,16 +1018,46 @@ int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int6
                            const int64_t* segments, int64_t n_segments, const int64_t* slot_body,
                            const char* slot_names, const int64_t* slot_name_offsets, int64_t n_slots,
                            int64_t* slot_src, int64_t* slot_count, int32_t* body_ok, int32_t threads) {
-    if (n_bodies < 0 || n_segments < 0 || n_slots < 0 || !label || (n_bodies > 0 && (!bodies || !body_offsets ||
-                                                                                      !body_ok)) ||
+    return krr_pack_route_grouped_pieces(bodies, body_offsets, n_bodies, nullptr, nullptr, 0, label, segments,
+                                         n_segments, slot_body, slot_names, slot_name_offsets, n_slots, slot_src,
+                                         slot_count, body_ok, threads);
+}
+
+int krr_pack_route_grouped_pieces(const char* bodies, const int64_t* body_offsets, int64_t n_bodies,
+                                  const int64_t* piece_dev, const int64_t* piece_shift, int64_t n_pieces,
+                                  const char* label, const int64_t* segments, int64_t n_segments,
+                                  const int64_t* slot_body, const char* slot_names,
+                                  const int64_t* slot_name_offsets, int64_t n_slots, int64_t* slot_src,
+                                  int64_t* slot_count, int32_t* body_ok, int32_t threads) {
+    if (n_bodies < 0 || n_segments < 0 || n_slots < 0 || n_pieces < 0 || !label ||
+        (n_bodies > 0 && (!bodies || !body_offsets || !body_ok)) || (n_pieces > 0 && (!piece_dev || !piece_shift)) ||
         (n_segments > 0 && !segments) || (n_slots > 0 && (!slot_body || !slot_name_offsets || !slot_src ||
                                                           !slot_count)))
         return KRR_PACK_E_INVALID;
+    for (int64_t j = 1; j < n_pieces; ++j)
+        if (piece_dev[j] <= piece_dev[j - 1]) return KRR_PACK_E_INVALID;
     for (int64_t j = 1; j < n_segments; ++j)
         if (segments[7 * j] <= segments[7 * (j - 1)]) return KRR_PACK_E_INVALID;  // sorted, distinct starts
     for (int64_t s = 0; s < n_slots; ++s)
         if (slot_body[s] < 0 || slot_body[s] >= n_bodies || slot_name_offsets[s + 1] < slot_name_offsets[s])
             return KRR_PACK_E_INVALID;
+    struct Map {
+        const char* base;
+        const int64_t *dev, *shift;
+        int64_t n;
+        int64_t piece(int64_t pos) const {  // the last piece starting at or before pos
+            return (int64_t)(std::upper_bound(dev, dev + n, pos) - dev) - 1;
+        }
+        const char* at(int64_t pos) const {
+            const int64_t j = n ? piece(pos) : -1;
+            return base + pos + (j >= 0 ? shift[j] : 0);
+        }
+        int64_t end(int64_t pos) const {
+            if (!n) return std::numeric_limits<int64_t>::max();
+            const int64_t j = piece(pos);
+            return j + 1 < n ? dev[j + 1] : std::numeric_limits<int64_t>::max();
+        }
+    } map{bodies, piece_dev, piece_shift, n_pieces};
     const int64_t ll = (int64_t)strlen(label);
     std::vector<std::unordered_map<std::string_view, int64_t>> index;
     try {
@@ -907,12 +1076,12 @@ int krr_pack_route_grouped(const char* bodies, const int64_t* body_offsets, int6
     };
     parallel_for(n_bodies, threads, [&](int64_t b) {
         auto& ix = index[(size_t)b];
-        const bool ok = krr::json::chain_grouped(bodies, body_offsets[b], body_offsets[b + 1], label, ll, segments,
-                                                 find, [&](int64_t j) {
-                                                     const int64_t* R = segments + 7 * j;
-                                                     if (R[2] >= 0)  // the first series with the label wins
-                                                         ix.emplace(std::string_view(bodies + R[2], (size_t)R[3]), j);
-                                                 });
+        const bool ok = krr::json::chain_grouped_mapped(
+            map, body_offsets[b], body_offsets[b + 1], label, ll, segments, find, [&](int64_t j) {
+                const int64_t* R = segments + 7 * j;
+                if (R[2] >= 0)  // the first series with the label wins (a label never spans a piece cut)
+                    ix.emplace(std::string_view(map.at(R[2]), (size_t)R[3]), j);
+            });
         body_ok[b] = ok ? 1 : 0;
     });
     parallel_for(n_slots, threads, [&](int64_t s) {

@@ -141,5 +141,36 @@ inline int64_t strip_body(const char* s, int64_t n, char* out) {
     return strip_span(s, s + n, out);
 }
 
+// ---- one large body stripped by several threads (grouped `sum by (pod)` bodies, ~100 MB each) ----
+// A strippable body holds no backslash, so every quote delimits a string and the string state
+// at any byte is the parity of the quotes before it.  A piece may start at a sample's '[' that
+// follows a value string: `"],[` whose quote CLOSES a string (inside a values array, the only
+// place such bytes occur outside strings).  No token spans that point and the copy's state there
+// is empty (outside a string, no digit, '.', sign or exponent before), so stripping the pieces
+// apart writes what strip_span writes for the whole body, piece by piece.
+
+// quotes in [p, e)
+KRR_STRIP_TARGET inline int64_t count_quotes(const char* p, const char* e) {
+    const __m512i kq = _mm512_set1_epi8('"');
+    int64_t c = 0;
+    while (e - p >= 64) {
+        c += _mm_popcnt_u64(_mm512_cmpeq_epi8_mask(_mm512_loadu_si512(p), kq));
+        p += 64;
+    }
+    for (; p < e; ++p) c += *p == '"';
+    return c;
+}
+
+// The first piece start at or after p (string state in_str at p) before e, or nullptr.
+inline const char* next_split(const char* p, const char* e, bool in_str) {
+    for (; p + 3 < e; ++p) {
+        if (*p != '"') continue;
+        if (in_str && p[1] == ']' && p[2] == ',' && p[3] == '[') return p + 3;
+        in_str = !in_str;
+    }
+    return nullptr;
+}
+
+
 }  // namespace strip
 }  // namespace krr

@@ -14,6 +14,7 @@
 #                on the ab_variants.py workload ARGS, e.g. ab:--config,3,--percentile,50
 #   sq:ARGS      SQ issue / wait counters (two rocprofv3 --pmc passes) of the ab_variants.py workload
 #   script:NAME,ARGS  python scripts/NAME.py ARGS -> script_NAME_ARGS.log
+#   sqs:NAME,ARGS  the sq counter passes over python scripts/NAME.py LIB ARGS (e.g. kll_sparse_probe)
 #   diag:ARGS    per-segment phase breakdown with krr_amd/lib/variants/lib_diag.so (-DKRR_DIAG)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -u
@@ -104,6 +105,22 @@ EOF
           || { echo "sq pass $i $args failed"; tail -20 "$OUT/sq${n:+_$n}_$i.log"; exit 1; }
       done
       python3 scripts/pmc_summary.py "$OUT" > "$OUT/sq${n:+_$n}.txt" 2>&1 && cat "$OUT/sq${n:+_$n}.txt"
+      ;;
+    sqs)
+      # SQ counters of every kernel of scripts/NAME.py LIB ARGS (two passes of 8 SQ counters)
+      lib=${SQLIB:-krr_amd/lib/libkrr_amd.so}
+      sname=${args%% *}
+      sargs=""
+      [[ "$args" == *" "* ]] && sargs=${args#* }
+      i=0
+      for cs in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU" \
+                "SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_VMEM"; do
+        i=$((i + 1))
+        timeout -s KILL 150 rocprofv3 --pmc $cs --output-format csv -d "$OUT/sqs${n:+_$n}_$i" -o run -- \
+          python3 "scripts/$sname.py" $lib $sargs > "$OUT/sqs${n:+_$n}_$i.log" 2>&1 \
+          || { echo "sqs pass $i $args failed"; tail -20 "$OUT/sqs${n:+_$n}_$i.log"; exit 1; }
+      done
+      python3 scripts/pmc_summary.py "$OUT" > "$OUT/sqs${n:+_$n}.txt" 2>&1 && cat "$OUT/sqs${n:+_$n}.txt"
       ;;
     *)
       echo "unknown step $step"; exit 2 ;;

@@ -78,13 +78,15 @@ def test_bench_under_torchrun_like_the_driver():
     assert len(r["per_rank_kernel_ms"]) == 2
 
 
-@pytest.mark.parametrize("gather", ["stream", "torch", "blocking"])
-def test_bench_rccl_path_one_rank(gather):
+@pytest.mark.parametrize("gather,comm", [("stream", "own"), ("stream", "torch"), ("torch", "own"),
+                                        ("blocking", "own")])
+def test_bench_rccl_path_one_rank(gather, comm):
     """The N > 1 step over RCCL at one rank (`--force-dist`): the C-ABI gather on the launch
-    stream with torch's communicator (rank 0's launch writing into the rotating receive
-    buffers) or torch.distributed.gather from two alternating send buffers; the gathered
-    records go to the host on the second stream, and the host copy after the timed steps
-    equals the records of the last launch."""
+    stream with the library's own communicator (default: krr_comm_unique_id on rank 0, the id
+    broadcast over torch.distributed, krr_comm_init_timeout) or torch's (--comm torch), rank
+    0's launch writing into the rotating receive buffers; or torch.distributed.gather from two
+    alternating send buffers; the gathered records go to the host on the second stream, and
+    the host copy after the timed steps equals the records of the last launch."""
     import socket
 
     with socket.socket() as s:
@@ -94,12 +96,16 @@ def test_bench_rccl_path_one_rank(gather):
                MASTER_PORT=str(port), KRR_BENCH_BACKEND="nccl")
     p = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist",
                         "--containers", "400", "--steps", "5", "--warmup", "2", "--gather", gather,
-                        "--no-cpu-baseline"], capture_output=True, text=True, env=env, timeout=270)
+                        "--comm", comm, "--no-cpu-baseline"], capture_output=True, text=True, env=env, timeout=270)
     assert p.returncode == 0, p.stderr[-4000:]
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert r["n_gpus"] == 1 and r["config"]["records"] == "HBM + RCCL gather to rank 0"
     assert r["config"]["gather"].startswith("RCCL send/recv" if gather == "stream" else "torch.distributed")
     assert r["records_host_equal_device"] is True, r
+    if gather == "stream":  # the communicator the C-ABI gather ran on, and that RCCL saw this rank
+        assert r["rccl_comm"]["ranks"] == 1, r["rccl_comm"]
+        want = "krr_comm_unique_id" if comm == "own" else "torch.distributed"
+        assert r["rccl_comm"]["communicator"].startswith(want), r["rccl_comm"]
 
 
 @pytest.mark.parametrize("world,mode,pct,method", [(2, "linear", "99", "window"), (3, "sorted_lower", "50", "window"),

@@ -194,3 +194,124 @@ def test_body_table_matches_the_python_walk():
     assert [ctypes.string_at(int(p), int(n)) for p, n in zip(ptrs, lens)] == [b for b, _ in flat]
     assert _body_table([[[b"x", bytearray(b"y")]]]) is None
     assert _body_table([]) is not None and len(_body_table([])[0]) == 0
+
+
+# ---- pieces: one large body stripped by several threads (grouped bodies) ----------------------
+
+@pytest.fixture
+def lib():
+    return prom_native.load_library()
+
+
+def _grouped(rng, n_series, n_samples, pods=None, tricky=False):
+    """A `sum by (pod)` body: n_series series of n_samples each (label values may hold `"],[`-like
+    bytes, which must not be taken for a cut)."""
+    parts = []
+    for i in range(n_series):
+        pod = pods[i] if pods else f"pod-{i}"
+        if tricky and i % 3 == 0:
+            pod = f'x],[1,"{i}'  # no backslash: still strippable
+        ts = [f"{1.7e9 + 60 * j!r}" for j in range(n_samples)]
+        vals = [repr(float(v)) for v in rng.gamma(2.0, 0.05, n_samples)]
+        items = ",".join(f'[{t},"{v}"]' for t, v in zip(ts, vals))
+        parts.append(f'{{"metric":{{"pod":"{pod}"}},"values":[{items}]}}')
+    return (HEAD + ",".join(parts) + "]}}").encode()
+
+
+def _strip_pieces(lib, bodies, max_pieces, threads=4):
+    lens = np.array([len(b) for b in bodies], dtype=np.int64)
+    offs = np.zeros(len(bodies) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    dst = ctypes.create_string_buffer(int(offs[-1]) + 64)
+    new_lens = np.zeros(len(bodies), dtype=np.int64)
+    cap = 2 * len(bodies) + max_pieces
+    start = np.zeros(cap + 1, dtype=np.int64)
+    out = np.zeros(cap, dtype=np.int64)
+    n = ctypes.c_int32()
+    ptrs = (ctypes.c_char_p * len(bodies))(*bodies)
+    rc = lib.krr_pack_concat_strip_pieces(ctypes.addressof(ptrs), lens.ctypes.data, len(bodies), offs.ctypes.data,
+                                          ctypes.addressof(dst), threads, max_pieces, new_lens.ctypes.data,
+                                          start.ctypes.data, out.ctypes.data, ctypes.byref(n))
+    assert rc == 0
+    k = n.value
+    return dst.raw, offs, new_lens, start[:k + 1].copy(), out[:k].copy()
+
+
+def _whole(bodies):
+    w = [strip_body(b) if b else b"" for b in bodies]
+    return [b if s is None else s for b, s in zip(bodies, w)]
+
+
+@pytest.mark.parametrize("max_pieces", [1, 2, 5, 16, 64])
+def test_strip_pieces_equal_the_whole_body_copy(lib, max_pieces):
+    """krr_pack_concat_strip_pieces: large bodies cut at `"],[` inside values arrays and stripped
+    apart give, concatenated, exactly the whole-body stripped copy (or the original for a body
+    with an unstrippable part); small bodies go in runs."""
+    rng = np.random.default_rng(5)
+    bodies = [_grouped(rng, 30, 400), _body(["0.1", "0.2"]), _grouped(rng, 8, 900, tricky=True),
+              _grouped(rng, 40, 50), b"", _body(["1", "2"], ts=["1e9", "2"]),  # unstrippable: exponent
+              _grouped(rng, 20, 300).replace(b'"pod-3"', b'"po\\\\d"'),       # a backslash: unchanged
+              _grouped(rng, 1, 5000)]
+    raw, offs, new_lens, start, out = _strip_pieces(lib, bodies, max_pieces)
+    want = _whole(bodies)
+    assert new_lens.tolist() == [len(w) for w in want]
+    got = b"".join(raw[int(s - offs[0]):int(s - offs[0] + o)] for s, o in zip(start[:-1], out))
+    assert got == b"".join(want)
+    assert (np.diff(start) >= out).all() and start[-1] == offs[-1]
+    if max_pieces >= 16:
+        assert out.size > len(bodies)  # the large bodies were cut
+
+
+def _segments(stripped: bytes, body_offs):
+    """The device's series segments of a stripped concatenation (this generator's bodies only):
+    start, end (one past '}'), label offset / length, scratch slot, count, ok."""
+    segs = []
+    for m in re.finditer(rb'[\[,](\{"metric":\{"pod":")', stripped):
+        st = m.start(1)
+        lab = m.end(1)
+        lab_end = stripped.index(b'"}', lab)
+        end = stripped.index(b"]}", stripped.index(b'"values":[', lab_end)) + 2
+        cnt = stripped.count(b"],[", st, end) + 1
+        segs.append([st, end, lab, lab_end - lab, st // 8, cnt, 1])
+    return np.array(segs, dtype=np.int64).reshape(-1, 7)
+
+
+@pytest.mark.parametrize("max_pieces", [1, 7, 32])
+def test_route_over_pieces_equals_contiguous(lib, max_pieces):
+    """krr_pack_route_grouped_pieces over the piecewise staged copy routes every slot as
+    krr_pack_route_grouped does over the contiguous stripped bodies."""
+    rng = np.random.default_rng(9)
+    pods = [[f"pod-{b}-{i}" for i in range(n)] for b, n in enumerate((25, 6, 40))]
+    bodies = [_grouped(rng, len(p), m, pods=p) for p, m in zip(pods, (300, 2000, 120))]
+    raw, offs, new_lens, start, out = _strip_pieces(lib, bodies, max_pieces)
+    dev_offs = np.zeros(len(bodies) + 1, dtype=np.int64)
+    np.cumsum(new_lens, out=dev_offs[1:])
+    contiguous = b"".join(raw[int(s - offs[0]):int(s - offs[0] + o)] for s, o in zip(start[:-1], out))
+    segs = np.ascontiguousarray(_segments(contiguous, dev_offs))
+    piece_dev = np.concatenate([[0], np.cumsum(out)[:-1]]).astype(np.int64)
+    piece_shift = (start[:-1] - offs[0] - piece_dev).astype(np.int64)
+    names = [n.encode() for p in pods for n in p] + [b"absent"]
+    slot_body = np.array([b for b, p in enumerate(pods) for _ in p] + [1], dtype=np.int64)
+    name_offs = np.concatenate([[0], np.cumsum([len(n) for n in names])]).astype(np.int64)
+    blob = b"".join(names)
+    res = []
+    for pieces in (False, True):
+        src, cnt = np.zeros(len(names), np.int64), np.zeros(len(names), np.int64)
+        ok = np.zeros(len(bodies), np.int32)
+        if pieces:
+            buf = ctypes.create_string_buffer(raw, len(raw) + 128)
+            rc = lib.krr_pack_route_grouped_pieces(ctypes.addressof(buf), dev_offs.ctypes.data, len(bodies),
+                                                   piece_dev.ctypes.data, piece_shift.ctypes.data, len(out), b"pod",
+                                                   segs.ctypes.data, len(segs), slot_body.ctypes.data, blob,
+                                                   name_offs.ctypes.data, len(names), src.ctypes.data,
+                                                   cnt.ctypes.data, ok.ctypes.data, 2)
+        else:
+            buf = ctypes.create_string_buffer(contiguous, len(contiguous) + 128)
+            rc = lib.krr_pack_route_grouped(ctypes.addressof(buf), dev_offs.ctypes.data, len(bodies), b"pod",
+                                            segs.ctypes.data, len(segs), slot_body.ctypes.data, blob,
+                                            name_offs.ctypes.data, len(names), src.ctypes.data, cnt.ctypes.data,
+                                            ok.ctypes.data, 2)
+        assert rc == 0 and ok.all(), (pieces, ok)
+        res.append((src.tolist(), cnt.tolist()))
+    assert res[0] == res[1]
+    assert res[0][1][:-1] == [m for p, m in zip(pods, (300, 2000, 120)) for _ in p] and res[0][1][-1] == -1
