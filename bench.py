@@ -1001,6 +1001,8 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     out["e2e_grouped_objects_per_s_spread"] = [objects / eg["device"][2][-1], objects / eg["device"][2][0]]
     out["e2e_grouped_objects_per_s_host_parse"] = objects / eg["host"][0]
     out["e2e_grouped_upload"] = _dp(dev.index or 0).last_upload
+    out["e2e_grouped_phases_s"] = dict(getattr(runner, "grouped_last", {}),
+                                       **getattr(_dp(dev.index or 0), "last_grouped_phases", {}))
     out["e2e_grouped_device_equals_host"] = eg["device"][1] == eg["host"][1]
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",

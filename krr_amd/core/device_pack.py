@@ -263,19 +263,27 @@ class DevicePacker:
         d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
         o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
         piece_dev, piece_shift = [], []
+        import time
+
+        t_strip = 0.0
         a = 0
         step = min(self.chunk_bytes, 16 << 20)
         while a < nb:
+            left = total - int(boffs[a])
+            if left <= step + step // 2:  # the end: a small last chunk, whose search + parse is the tail
+                step = max(left * 3 // 4, 16 << 20)
             b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
             step = min(step * 3 // 2, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
             lo = int(boffs[a])
+            t_s = time.perf_counter()
             rc = host.krr_pack_concat_strip_pieces(ptr_addr + a * 8, lens[a:].ctypes.data, b - a,
                                                    boffs[a:].ctypes.data, stage.data_ptr() + lo, self.threads,
                                                    max_pieces, new_lens[a:].ctypes.data, p_start.ctypes.data,
                                                    p_out.ctypes.data, ctypes.byref(n_p))
             if rc != KRR_PACK_OK:
                 raise PrometheusResponseError(rc, "krr_pack_concat_strip_pieces failed")
+            t_strip += time.perf_counter() - t_s
             np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
             no[a + 1:b + 1] += no[a]
             k = n_p.value
@@ -302,7 +310,8 @@ class DevicePacker:
         keep = np.concatenate([np.diff(pdev) > 0, [True]]) if pdev.size else np.zeros(0, bool)
         self._layout = (no.copy(), None, (np.ascontiguousarray(pdev[keep]), np.ascontiguousarray(psh[keep])))
         self.last_upload = {"bytes": total, "bytes_sent": int(no[nb]), "bodies": nb,
-                            "bodies_stripped": int((new_lens < lens).sum()), "pieces": int(pdev.size)}
+                            "bodies_stripped": int((new_lens < lens).sum()), "pieces": int(pdev.size),
+                            "strip_s": round(t_strip, 5)}
         return lens, boffs, total, jb, tmp_v, None
 
     def pack_grouped(self, plan, bodies: Sequence[bytes], *, want_timestamps: bool = False,
@@ -346,36 +355,76 @@ class DevicePacker:
 
         if not flat or all(plan.n_slots == 0 for plan, _ in items):
             return [host_fallback(r, 0) for r in range(len(items))]
+        import time
+
+        clock = [time.perf_counter()]  # phase ends (host clock; only the existing synchronisations)
         total_bytes = sum(len(b) for b in flat)
         cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
+        segs = torch.empty((cap, 7), dtype=torch.int64, device=dev)
         seen = [0]  # positions below this were searched
+        # per chunk: the candidate counter after its search, copied to page-locked memory, and an
+        # event; the chunk's series are parsed one chunk later (its bytes are in HBM by then),
+        # so the parse runs beside the next chunks' staging and copies, not after the last one
+        LAG = 2  # chunks searched but not yet parsed: the host waits on an older chunk's event
+        snaps = torch.zeros(max(len(flat), 1) + 1, dtype=torch.int64, pin_memory=True)
+        snap_np = snaps.numpy()
+        pend: list = []         # (event, snap index, body end) of searched, unparsed chunks
+        waited = [0.0]
+        parsed = [0, False]     # candidates parsed so far, overflow
+
+        def parse_chunk(jb, tmp_v, tmp_t):
+            ev, k, b_end = pend.pop(0)
+            t_w = time.perf_counter()
+            ev.synchronize()  # that chunk's search only: later copies keep streaming
+            waited[0] += time.perf_counter() - t_w
+            n = int(snap_np[k])
+            lo = parsed[0]
+            if parsed[1] or n > cap:
+                parsed[1] = True
+                return
+            if n > lo:
+                with torch.cuda.stream(st):
+                    starts = torch.sort(cand[lo:n]).values
+                    # the chunk's bodies' device offsets are in HBM (copied with the chunk)
+                    body_of = torch.searchsorted(jb._keep[1][:b_end + 1], starts, right=True) - 1
+                    self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t, segs[lo:n],
+                                                 stream=st)
+            parsed[0] = n
 
         def launch(jb, a, b, tmp_v, tmp_t, lo, hi):  # search each chunk as it lands
             last = b == len(flat)
             end = hi if last else max(hi - 16, seen[0])
             self.ctx.json_find_series(jb, cand, n_cand, begin=seen[0], end=end, limit=hi, stream=st)
             seen[0] = end
+            k = len(done)  # this chunk's snapshot slot
+            with torch.cuda.stream(st):
+                snaps[k:k + 1].copy_(n_cand, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            pend.append((ev, k, b))
+            done.append(k)
+            if len(pend) > LAG:
+                parse_chunk(jb, tmp_v, tmp_t)
 
+        done: list = []
         # timestamps cut while staging, as for per-pod bodies: the candidate search, the series
         # parse and the host's chain walk read structure, labels and value strings only
         lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch, strip=self.strip,
                                                             pieces=True)
+        clock.append(time.perf_counter())
+        while pend:
+            parse_chunk(jb, tmp_v, tmp_t)
+        clock.append(time.perf_counter())
         dev_offs, shift = self._layout[:2]
         pieces = self._layout[2] if len(self._layout) > 2 else None
-        with torch.cuda.stream(st):
-            nc = int(n_cand.item())  # sync
-        if nc > cap:
+        nc = parsed[0]
+        if parsed[1]:
             return [host_fallback(r, body0[r + 1] - body0[r]) for r in range(len(items))]
-        starts = torch.sort(cand[:nc]).values
-        starts_h = starts.cpu().numpy()
-        body_of = np.searchsorted(dev_offs, starts_h, side="right") - 1
-        segs = torch.empty((max(nc, 1), 7), dtype=torch.int64, device=dev)
         with torch.cuda.stream(st):
-            self.ctx.json_parse_segments(jb, starts, torch.from_numpy(body_of).to(dev), label, want_ts, tmp_v, tmp_t,
-                                         segs, stream=st)
             segs_h = np.ascontiguousarray(segs[:nc].cpu().numpy())  # sync
+        clock.append(time.perf_counter())
         host = load_library()
         stage = self._last[1]
         out = []
@@ -415,6 +464,12 @@ class DevicePacker:
             series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
             out.append(DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
                                     ts[:n_vals] if ts is not None else None))
+        clock.append(time.perf_counter())
+        # seconds per phase: staging + copies + search (+ the parse of all chunks but the last),
+        # the last chunk's parse, the segments to the host, chain / route / gather enqueue
+        self.last_grouped_phases = dict(zip(("stage_copy_search", "last_parse", "segments_d2h", "route_gather"),
+                                            np.diff(clock).round(5).tolist()), parse_wait=round(waited[0], 5),
+                                        strip=(self.last_upload or {}).get("strip_s"))
         return out
 
     def pack_many(self, resources: Sequence[Sequence[Sequence[bytes]]], *, want_timestamps: bool = False,

@@ -424,7 +424,14 @@ class BatchedRunner:
         ``sum by (pod)`` query (one per (namespace, container), not one per pod).
         ``parser="device"``: the MI355X parses the bodies and the host routes series to
         pods by label (krr_amd.core.device_pack); ``"host"``: krr_pack_parse_grouped."""
-        return self.recommend_packed(self.pack_grouped(plan, cpu_bodies, mem_bodies, threads=threads, parser=parser))
+        import time
+
+        t0 = time.perf_counter()
+        fleet = self.pack_grouped(plan, cpu_bodies, mem_bodies, threads=threads, parser=parser)
+        t1 = time.perf_counter()
+        out = self.recommend_packed(fleet)
+        self.grouped_last = {"pack_s": t1 - t0, "kernel_round_s": time.perf_counter() - t1}
+        return out
 
     def pack_grouped(self, plan, cpu_bodies, mem_bodies, threads: int = 0, parser: str = "device"):
         from krr_amd.core.packing import PackedFleet

@@ -889,7 +889,6 @@ int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_
     struct Nom {
         int64_t body, lo, hi;  // body (the first, for a run of whole bodies) and its bytes [lo, hi)
         int64_t last;          // one past the run's last body (whole-body runs), or body + 1
-        int64_t quotes = 0;
         const char* start = nullptr;  // the actual start after the split search
     };
     std::vector<Nom> nom;
@@ -911,39 +910,21 @@ int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_
         return KRR_PACK_E_INVALID;
     }
     const int64_t N = (int64_t)nom.size();
-    // parity: quotes of every cut part (parallel), then each cut part's start moved to a split
-    parallel_for(N, threads, [&](int64_t i) {
-        Nom& u = nom[(size_t)i];
-        if (u.last == u.body + 1 && !(u.lo == 0 && u.hi == body_lens[u.body]))
-            u.quotes = krr::strip::count_quotes(bodies[u.body] + u.lo, bodies[u.body] + u.hi);
-    });
-    {
-        int64_t q = 0;
-        for (int64_t i = 0; i < N; ++i) {  // quotes before each cut part inside its body
-            Nom& u = nom[(size_t)i];
-            if (u.lo == 0) q = 0;
-            const int64_t mine = u.quotes;
-            u.quotes = q;
-            q += mine;
-        }
-    }
+    auto whole = [&](const Nom& u) { return u.last > u.body + 1 || (u.lo == 0 && u.hi == body_lens[u.body]); };
+    // each cut part's start moved to the first sample boundary inside it
     parallel_for(N, threads, [&](int64_t i) {
         Nom& u = nom[(size_t)i];
         const char* s0 = bodies[u.body];
-        if (u.lo == 0) {
-            u.start = s0;
-            return;
-        }
-        u.start = krr::strip::next_split(s0 + u.lo, s0 + u.hi, (u.quotes & 1) != 0);
+        u.start = (u.lo == 0) ? s0 : krr::strip::next_split(s0 + u.lo, s0 + u.hi);
     });
     // the pieces: cut parts without a split join the piece before them
-    std::vector<int64_t> ps_body, ps_first, ps_last;  // body, [start, end) byte offsets in that body
+    std::vector<int64_t> ps_body, ps_first, ps_last;
     std::vector<const char*> ps_p, ps_e;
     try {
         for (int64_t i = 0; i < N; ++i) {
             const Nom& u = nom[(size_t)i];
             if (!u.start) continue;
-            if (u.last > u.body + 1 || (u.lo == 0 && u.hi == body_lens[u.body])) {  // whole bodies
+            if (whole(u)) {
                 ps_body.push_back(u.body);
                 ps_first.push_back(u.body);
                 ps_last.push_back(u.last);
@@ -963,7 +944,7 @@ int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_
     }
     const int64_t M = (int64_t)ps_body.size();
     if (M > 2 * n_bodies + (int64_t)max_pieces) return KRR_PACK_E_INVALID;  // (the documented capacity)
-    std::vector<int64_t> out_len((size_t)M, 0);
+    std::vector<int64_t> out_len((size_t)M, 0), quotes((size_t)M, 0);
     std::vector<unsigned char> bad((size_t)n_bodies, 0);
     parallel_for(M, threads, [&](int64_t j) {
         if (!ps_p[(size_t)j]) {  // whole bodies back to back from the first one's extent
@@ -986,10 +967,20 @@ int krr_pack_concat_strip_pieces(const char* const* bodies, const int64_t* body_
         const int64_t b = ps_body[(size_t)j];
         const char* p = ps_p[(size_t)j];
         char* o = dst + (dst_offsets[b] - base) + (p - bodies[b]);
-        out_len[(size_t)j] = krr::strip::strip_span(p, ps_e[(size_t)j], o);  // -1: not strippable
+        // -1: not strippable; the quotes it saw check the cut (below)
+        out_len[(size_t)j] = krr::strip::strip_span(p, ps_e[(size_t)j], o, &quotes[(size_t)j]);
     });
-    for (int64_t j = 0; j < M; ++j)
-        if (ps_p[(size_t)j] && out_len[(size_t)j] < 0) bad[(size_t)ps_body[(size_t)j]] = 1;
+    {
+        int64_t q = 0;
+        for (int64_t j = 0; j < M; ++j) {
+            if (!ps_p[(size_t)j]) continue;
+            const int64_t b = ps_body[(size_t)j];
+            if (ps_p[(size_t)j] == bodies[b]) q = 0;
+            else if (q & 1) bad[(size_t)b] = 1;  // the cut was inside a string: not a sample boundary
+            if (out_len[(size_t)j] < 0) bad[(size_t)b] = 1;
+            q += quotes[(size_t)j];
+        }
+    }
     // a body with an unstrippable part is copied unchanged, part by part (its extents as they are)
     parallel_for(M, threads, [&](int64_t j) {
         if (!ps_p[(size_t)j] || !bad[(size_t)ps_body[(size_t)j]]) return;

@@ -62,13 +62,14 @@ struct StripState {
 // One block x (bytes `valid`): false when a run breaks the contract, else *keep = the bytes
 // the stripped copy keeps.
 KRR_STRIP_TARGET __attribute__((always_inline)) inline bool strip_block(StripState& st, __m512i x, uint64_t valid,
-                                                                        uint64_t* keep) {
+                                                                        uint64_t* keep, int64_t* quotes = nullptr) {
     const __m512i kq = _mm512_set1_epi8('"'), kbs = _mm512_set1_epi8('\\'), kdt = _mm512_set1_epi8('.');
     const __m512i k0 = _mm512_set1_epi8('0'), k9 = _mm512_set1_epi8(9);
     const __m512i k20 = _mm512_set1_epi8(0x20), ke = _mm512_set1_epi8('e');
     const __m512i k06 = _mm512_set1_epi8(0x06), k2f = _mm512_set1_epi8(0x2F);
     if (_mm512_mask_cmpeq_epi8_mask(valid, x, kbs)) return false;
     const uint64_t qt = _mm512_mask_cmpeq_epi8_mask(valid, x, kq);
+    if (quotes) *quotes += _mm_popcnt_u64(qt);
     const uint64_t dt = _mm512_mask_cmpeq_epi8_mask(valid, x, kdt);
     const uint64_t zr = _mm512_mask_cmpeq_epi8_mask(valid, x, k0);
     const uint64_t dg = _mm512_mask_cmple_epu8_mask(valid, _mm512_sub_epi8(x, k0), k9);
@@ -105,13 +106,18 @@ KRR_STRIP_TARGET __attribute__((always_inline)) inline bool strip_block(StripSta
 // stripped copy never runs ahead of the input, so a 64-byte store stays inside out); the
 // last partial block by a masked load and store (nothing read past e or written past the
 // stripped end).
-KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out) {
+// `quotes` (optional): the quotes of [p, e) counted on the way (a local sum, written once: a
+// pointer updated per block would alias the output stores and serialise the loop).
+template <bool COUNT>
+KRR_STRIP_TARGET inline int64_t strip_span_t(const char* p, const char* e, char* out, int64_t* quotes) {
     StripState st;
+    int64_t nq = 0;
+    int64_t* const qp = COUNT ? &nq : nullptr;
     char* o = out;
     while (e - p >= 64) {
         const __m512i x = _mm512_loadu_si512(p);
         uint64_t keep;
-        if (!strip_block(st, x, ~0ull, &keep)) return -1;
+        if (!strip_block(st, x, ~0ull, &keep, qp)) return -1;
 #if KRR_STRIP_MASKED_STORES
         const unsigned cnt = (unsigned)_mm_popcnt_u64(keep);
         _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), _mm512_maskz_compress_epi8(keep, x));
@@ -126,14 +132,22 @@ KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* o
         const uint64_t valid = _bzhi_u64(~0ull, (unsigned)(e - p));
         const __m512i x = _mm512_maskz_loadu_epi8(valid, p);
         uint64_t keep;
-        if (!strip_block(st, x, valid, &keep)) return -1;
+        if (!strip_block(st, x, valid, &keep, qp)) return -1;
         const unsigned cnt = (unsigned)_mm_popcnt_u64(keep);
         _mm512_mask_storeu_epi8(o, _bzhi_u64(~0ull, cnt), _mm512_maskz_compress_epi8(keep, x));
         o += cnt;
     } else if (st.cDt) {
         return -1;  // a '.' ends the body: nothing after it to look at
     }
+    if (COUNT) *quotes = nq;
     return o - out;
+}
+
+KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out) {
+    return strip_span_t<false>(p, e, out, nullptr);
+}
+KRR_STRIP_TARGET inline int64_t strip_span(const char* p, const char* e, char* out, int64_t* quotes) {
+    return strip_span_t<true>(p, e, out, quotes);
 }
 
 inline int64_t strip_body(const char* s, int64_t n, char* out) {
@@ -142,35 +156,36 @@ inline int64_t strip_body(const char* s, int64_t n, char* out) {
 }
 
 // ---- one large body stripped by several threads (grouped `sum by (pod)` bodies, ~100 MB each) ----
-// A strippable body holds no backslash, so every quote delimits a string and the string state
-// at any byte is the parity of the quotes before it.  A piece may start at a sample's '[' that
-// follows a value string: `"],[` whose quote CLOSES a string (inside a values array, the only
-// place such bytes occur outside strings).  No token spans that point and the copy's state there
-// is empty (outside a string, no digit, '.', sign or exponent before), so stripping the pieces
-// apart writes what strip_span writes for the whole body, piece by piece.
+// A piece may start at a sample's '[' in a values array: `"],[` + a number + `,"` + a value's first
+// byte ([0-9+-NI]).  In a valid body that quote CLOSES a string (were it an opening one, the quote
+// before the value would close a string and be followed by a value byte, which JSON forbids).
+// No token spans that point and the copy's state there is empty (outside a string, no digit,
+// '.', sign or exponent before), so the pieces strip apart to what strip_span writes for the
+// whole body.  The caller checks it anyway: a strippable body has no backslash, so every quote
+// delimits a string, and the quotes each piece's copy counted must be even before every cut;
+// when they are not the body is copied unchanged.
 
-// quotes in [p, e)
-KRR_STRIP_TARGET inline int64_t count_quotes(const char* p, const char* e) {
-    const __m512i kq = _mm512_set1_epi8('"');
-    int64_t c = 0;
-    while (e - p >= 64) {
-        c += _mm_popcnt_u64(_mm512_cmpeq_epi8_mask(_mm512_loadu_si512(p), kq));
-        p += 64;
-    }
-    for (; p < e; ++p) c += *p == '"';
-    return c;
+inline bool value_start(char c) {
+    return (c >= '0' && c <= '9') || c == '+' || c == '-' || c == 'N' || c == 'I';
 }
 
-// The first piece start at or after p (string state in_str at p) before e, or nullptr.
-inline const char* next_split(const char* p, const char* e, bool in_str) {
-    for (; p + 3 < e; ++p) {
-        if (*p != '"') continue;
-        if (in_str && p[1] == ']' && p[2] == ',' && p[3] == '[') return p + 3;
-        in_str = !in_str;
+// The first piece start in [p, e) (a pointer to a sample's '['), or nullptr.
+inline const char* next_split(const char* p, const char* e) {
+    for (; p + 8 < e; ++p) {
+        if (p[0] != '"' || p[1] != ']' || p[2] != ',' || p[3] != '[') continue;
+        const char* q = p + 4;
+        const char* d0 = q;
+        while (q < e && *q >= '0' && *q <= '9') ++q;
+        if (q == d0) continue;
+        if (q < e && *q == '.') {
+            const char* f0 = ++q;
+            while (q < e && *q >= '0' && *q <= '9') ++q;
+            if (q == f0) continue;
+        }
+        if (q + 2 < e && q[0] == ',' && q[1] == '"' && value_start(q[2])) return p + 3;
     }
     return nullptr;
 }
-
 
 }  // namespace strip
 }  // namespace krr
