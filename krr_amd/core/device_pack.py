@@ -76,6 +76,13 @@ class DevicePacker:
             self._stage = None
             self._last = None
 
+    def _parse_streams(self, n: int = 3):
+        import torch
+
+        if getattr(self, "_pstreams", None) is None:
+            self._pstreams = [torch.cuda.Stream(device=self.device) for _ in range(n)]
+        return self._pstreams
+
     def _staging(self, nbytes: int):
         import torch
 
@@ -367,7 +374,11 @@ class DevicePacker:
         # per chunk: the candidate counter after its search, copied to page-locked memory, and an
         # event; the chunk's series are parsed one chunk later (its bytes are in HBM by then),
         # so the parse runs beside the next chunks' staging and copies, not after the last one
-        LAG = 2  # chunks searched but not yet parsed: the host waits on an older chunk's event
+        LAG = 1  # chunks searched but not yet parsed: the host waits on the previous chunk's search
+        # the parses run on streams of their own (a chunk holds one or two bodies = a few hundred
+        # series = waves, far from filling the GPU): consecutive chunks' parses overlap each other
+        # and the copies, instead of queueing behind the next chunk's copy on the launch stream
+        pstreams = self._parse_streams()
         snaps = torch.zeros(max(len(flat), 1) + 1, dtype=torch.int64, pin_memory=True)
         snap_np = snaps.numpy()
         pend: list = []         # (event, snap index, body end) of searched, unparsed chunks
@@ -385,12 +396,14 @@ class DevicePacker:
                 parsed[1] = True
                 return
             if n > lo:
-                with torch.cuda.stream(st):
+                ps = pstreams[k % len(pstreams)]
+                ps.wait_event(ev)
+                with torch.cuda.stream(ps):
                     starts = torch.sort(cand[lo:n]).values
                     # the chunk's bodies' device offsets are in HBM (copied with the chunk)
                     body_of = torch.searchsorted(jb._keep[1][:b_end + 1], starts, right=True) - 1
                     self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t, segs[lo:n],
-                                                 stream=st)
+                                                 stream=ps)
             parsed[0] = n
 
         def launch(jb, a, b, tmp_v, tmp_t, lo, hi):  # search each chunk as it lands
@@ -416,6 +429,8 @@ class DevicePacker:
         clock.append(time.perf_counter())
         while pend:
             parse_chunk(jb, tmp_v, tmp_t)
+        for ps in pstreams:
+            st.wait_stream(ps)
         clock.append(time.perf_counter())
         dev_offs, shift = self._layout[:2]
         pieces = self._layout[2] if len(self._layout) > 2 else None
