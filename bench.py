@@ -986,8 +986,12 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
 
     g_cpu, g_mem = grouped(cpu_vals, 0), grouped(mem_vals, 7)
     eg = {}
-    for parser in ("host", "device"):
+    g_state = {}
+    for parser in ("host", "device", "hybrid"):
         runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)  # warm-up
+        if parser == "hybrid":  # the host share settles on the rates both sides reach together
+            for _ in range(4):
+                runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)
         runs_g = []
         for _ in range(3 if parser == "host" else 7):
             t0 = time.perf_counter()
@@ -996,13 +1000,22 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         assert len(res_g) == objects
         eg[parser] = (float(np.median(runs_g)), [(str(r[k].request), str(r[k].limit)) for r in res_g for k in r],
                       sorted(runs_g))
+        if parser == "device":  # its staging and phases are the ones reported
+            g_state = {"upload": _dp(dev.index or 0).last_upload,
+                       "phases": dict(getattr(runner, "grouped_last", {}),
+                                      **getattr(_dp(dev.index or 0), "last_grouped_phases", {}))}
     assert runner.last_pack_via == ("device", "device"), runner.last_pack_via
+    # e2e_grouped_objects_per_s: the device parser (a grouped body is ~100 MB: the host packer
+    # cannot split one across its threads, so the hybrid's host share only slows the staging
+    # threads it borrows — measured beside it); the host-only figure too
     out["e2e_grouped_objects_per_s"] = objects / eg["device"][0]
     out["e2e_grouped_objects_per_s_spread"] = [objects / eg["device"][2][-1], objects / eg["device"][2][0]]
+    out["e2e_grouped_objects_per_s_hybrid"] = objects / eg["hybrid"][0]
+    out["e2e_grouped_hybrid_equals_host"] = eg["hybrid"][1] == eg["host"][1]
+    out["e2e_grouped_hybrid_split"] = getattr(_dp(dev.index or 0), "last_grouped_hybrid", None)
     out["e2e_grouped_objects_per_s_host_parse"] = objects / eg["host"][0]
-    out["e2e_grouped_upload"] = _dp(dev.index or 0).last_upload
-    out["e2e_grouped_phases_s"] = dict(getattr(runner, "grouped_last", {}),
-                                       **getattr(_dp(dev.index or 0), "last_grouped_phases", {}))
+    out["e2e_grouped_upload"] = g_state["upload"]
+    out["e2e_grouped_phases_s"] = g_state["phases"]
     out["e2e_grouped_device_equals_host"] = eg["device"][1] == eg["host"][1]
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",
@@ -1025,8 +1038,10 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
                       "e2e_host_parse: parser='host'): pack -> fused kernel -> native exact-decimal rounding -> "
                       "RunResults (the median of 7 runs, 3 for the host parser, each run's seconds in e2e_runs_s and "
                       "the slowest / fastest rate in *_spread; every object's strings compared across the parsers); "
-                      "e2e_grouped: recommend_from_grouped, the same median rule, bodies staged with their "
-                      "timestamps cut as the per-pod ones (e2e_grouped_upload), every object compared"}
+                      "e2e_grouped: recommend_from_grouped with parser='device' (the same median rule, bodies "
+                      "staged with their timestamps cut as the per-pod ones, e2e_grouped_upload; chunks parsed "
+                      "and routed as they land, e2e_grouped_phases_s), parser='hybrid' and parser='host' beside "
+                      "it, every object compared"}
     return out
 
 

@@ -76,6 +76,30 @@ class DevicePacker:
             self._stage = None
             self._last = None
 
+    def _live_layout(self):
+        """(device body offsets, piece device starts, piece staging shifts) of the batch being
+        uploaded, as far as it has been staged: what the host routing of the chunks staged so far
+        needs (an empty piece shares its device start with the next: the last of such a run is
+        kept, so the starts increase strictly)."""
+        no, pd, ps = self._live
+        k = min(len(pd), len(ps))
+        if not k:
+            return no, np.zeros(0, np.int64), np.zeros(0, np.int64)
+        pdev, psh = np.concatenate(pd[:k]), np.concatenate(ps[:k])
+        keep = np.concatenate([np.diff(pdev) > 0, [True]])
+        return no, np.ascontiguousarray(pdev[keep]), np.ascontiguousarray(psh[keep])
+
+    def _host_rows(self, n: int):
+        """A page-locked int64 [>= n, 7] buffer for the grouped segments, kept and grown (a batch's
+        earlier chunks keep the buffer they were copied into alive through their views)."""
+        import torch
+
+        buf = getattr(self, "_seg_rows", None)
+        if buf is None or buf.shape[0] < n:
+            buf = self._seg_rows = torch.empty((max(n, 2 * (buf.shape[0] if buf is not None else 0), 1 << 14), 7),
+                                               dtype=torch.int64, pin_memory=True)
+        return buf
+
     def _parse_streams(self, n: int = 3):
         import torch
 
@@ -106,17 +130,19 @@ class DevicePacker:
 
         return torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device))
 
-    def _upload(self, flat, want_ts, st, launch, strip: bool = False, pieces: bool = False):
+    def _upload(self, flat, want_ts, st, launch, strip: bool = False, pieces: bool = False, extra_slots: int = 0):
         """``flat``: the bodies (bytes), or a body table (int64 buffer addresses, int64
         lengths) from ``_body_table``.  ``pieces``: stripped in pieces that may cut a large body
         (``_upload_pieces``)."""
         if isinstance(flat, tuple):
-            return self._upload_table(int(flat[0].ctypes.data), flat[1], want_ts, st, launch, strip, pieces)
+            return self._upload_table(int(flat[0].ctypes.data), flat[1], want_ts, st, launch, strip, pieces,
+                                      extra_slots)
         lens = np.fromiter((len(b) for b in flat), dtype=np.int64, count=len(flat))
         ptrs = (ctypes.c_char_p * len(flat))(*flat)  # alive while the staging below runs
-        return self._upload_table(ctypes.addressof(ptrs), lens, want_ts, st, launch, strip, pieces)
+        return self._upload_table(ctypes.addressof(ptrs), lens, want_ts, st, launch, strip, pieces, extra_slots)
 
-    def _upload_table(self, ptr_addr, lens, want_ts, st, launch, strip: bool = False, pieces: bool = False):
+    def _upload_table(self, ptr_addr, lens, want_ts, st, launch, strip: bool = False, pieces: bool = False,
+                      extra_slots: int = 0):
         """Stage ``flat`` bodies chunk by chunk (host threads), copy each chunk to HBM on the
         copy stream and call ``launch(jb, a, b, tmp_v, tmp_t, lo, hi)`` on ``st`` for bodies
         [a, b) = bytes [lo, hi) once the chunk is there.  ``strip``: the bodies' timestamps
@@ -131,13 +157,15 @@ class DevicePacker:
         total = int(boffs[-1])
         stage = self._staging(total + 128)
         self._layout = (boffs, None)  # device offsets, staging shift (none: same offsets)
+        self._live = (boffs, [], [])  # the same while the chunks stream (see _live_layout)
+        self._last_stage_ptr = stage.data_ptr()
         d_bodies = torch.empty(total + 128, dtype=torch.uint8, device=dev)
         if strip and not want_ts and nb:
             if pieces:
-                return self._upload_pieces(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch)
+                return self._upload_pieces(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch, extra_slots)
             return self._upload_stripped(ptr_addr, lens, boffs, total, stage, d_bodies, st, launch)
         d_boffs = torch.from_numpy(boffs).to(dev)
-        slots = total // 8 + 1
+        slots = total // 8 + 1 + int(extra_slots)
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
         tmp_t = torch.empty(slots, dtype=torch.float64, device=dev) if want_ts else None
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
@@ -240,7 +268,7 @@ class DevicePacker:
                             "bodies_stripped": int((new_lens < lens).sum())}
         return lens, boffs, total, jb, tmp_v, None
 
-    def _upload_pieces(self, ptr_addr, lens, boffs, total, stage, d_bodies, st, launch):
+    def _upload_pieces(self, ptr_addr, lens, boffs, total, stage, d_bodies, st, launch, extra_slots: int = 0):
         """_upload_stripped for a few large bodies (grouped `sum by (pod)` responses, ~100 MB each):
         each chunk is stripped by krr_pack_concat_strip_pieces, which cuts a large body at sample
         boundaries into pieces the host threads strip apart (one thread per body would bound the
@@ -262,7 +290,7 @@ class DevicePacker:
         new_offs = torch.zeros(nb + 1, dtype=torch.int64, pin_memory=True)
         no = new_offs.numpy()
         d_boffs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
-        tmp_v = torch.empty(total // 8 + 1, dtype=torch.float64, device=dev)
+        tmp_v = torch.empty(total // 8 + 1 + int(extra_slots), dtype=torch.float64, device=dev)
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
         host = load_library()
         cs = self._copy_stream
@@ -270,6 +298,7 @@ class DevicePacker:
         d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
         o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
         piece_dev, piece_shift = [], []
+        self._live = (no, piece_dev, piece_shift)  # grown chunk by chunk: the routing reads it
         import time
 
         t_strip = 0.0
@@ -332,13 +361,33 @@ class DevicePacker:
                                       return_pod_counts=return_pod_counts, stream=stream, label=label)[0]
 
     def pack_grouped_many(self, items, *, want_timestamps: bool = False, return_pod_counts: bool = False,
-                          stream=None, label: str = "pod") -> list:
+                          stream=None, label: str = "pod", hybrid: bool = False) -> list:
         """Several (plan, bodies) pairs (e.g. CPU and memory) through ONE staging / copy /
-        candidate-search pipeline; one DevicePacked per pair."""
+        candidate-search pipeline; one DevicePacked per pair.  ``hybrid``: the last bodies
+        (about ``grouped_share`` of the bytes) are parsed by the host packer on a worker thread
+        (``FleetQueryPlan.pack_group_slots``, a quarter of the threads) while the rest cross the
+        link; their slots' values join the device scratch and the same gather builds the CSR.
+        The share then moves toward r_host / (r_host + r_device)."""
         with self._lock, self._on(stream):
-            return self._pack_grouped_multi(items, want_timestamps, return_pod_counts, None, label)
+            return self._pack_grouped_multi(items, want_timestamps, return_pod_counts, None, label,
+                                            self.grouped_share if hybrid else 0.0)
 
-    def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label) -> list:
+    grouped_share = 0.06          # the hybrid grouped parser's host share of the bytes (adapted)
+    grouped_host_threads = 0      # 0: a quarter of the threads
+    grouped_route = "chunk"       # "chunk": segments to the host and routed per chunk; "end": once
+    _EMPTY_BODY = b'{"status":"success","data":{"resultType":"matrix","result":[]}}'
+
+    def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label, host_share: float = 0.0) -> list:
+        """The grouped pipeline, chunk by chunk (a chunk = whole bodies): stage (stripped, in
+        pieces) -> copy -> search the series starts (launch stream) -> one chunk later, parse the
+        chunk's series (a parse stream) and copy its segments to the host -> one chunk later
+        again, chain and route the chunk's bodies on the host (their slots only) — so after the
+        last copy only the last chunk's parse and route remain.  Then every slot's values are
+        gathered into the CSR."""
+        import os
+        import threading
+        import time
+
         import torch
 
         flat: list = []
@@ -362,31 +411,105 @@ class DevicePacker:
 
         if not flat or all(plan.n_slots == 0 for plan, _ in items):
             return [host_fallback(r, 0) for r in range(len(items))]
-        import time
-
         clock = [time.perf_counter()]  # phase ends (host clock; only the existing synchronisations)
-        total_bytes = sum(len(b) for b in flat)
+        # hybrid: the last bodies go to the host packer on a worker thread, the rest to the device
+        split = len(flat)
+        if host_share > 0 and not want_ts and len(flat) >= 2:
+            tail = np.cumsum(np.array([len(b) for b in flat[::-1]], dtype=np.int64))
+            k_host = int(np.searchsorted(tail, host_share * tail[-1], side="right"))
+            split = len(flat) - min(max(k_host, 1), len(flat) - 1)
+        host_res: dict = {}
+        host_thread = None
+        T_all = self.threads or len(os.sched_getaffinity(0))
+        t_host = max(1, int(self.grouped_host_threads or T_all // 4))
+        if split < len(flat):
+            from krr_amd.core.runner import _pinned_alloc_or_none
+
+            alloc = _pinned_alloc_or_none()
+
+            def host_part():
+                t0 = time.perf_counter()
+                try:
+                    for r, (plan, _) in enumerate(items):
+                        lo, hi = max(body0[r], split), body0[r + 1]
+                        if lo < hi:
+                            host_res[r] = plan.pack_group_slots(flat[lo:hi], lo - body0[r], hi - body0[r],
+                                                                threads=t_host, alloc=alloc)
+                except PrometheusResponseError as e:
+                    host_res["error"] = e
+                host_res["s"] = time.perf_counter() - t0
+
+            host_thread = threading.Thread(target=host_part, name="krr-grouped-host", daemon=True)
+            host_thread.start()
+        host_bytes = sum(len(b) for b in flat[split:])
+        dflat = flat[:split]
+        total_bytes = sum(len(b) for b in dflat)
         cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
         segs = torch.empty((cap, 7), dtype=torch.int64, device=dev)
         seen = [0]  # positions below this were searched
-        # per chunk: the candidate counter after its search, copied to page-locked memory, and an
-        # event; the chunk's series are parsed one chunk later (its bytes are in HBM by then),
-        # so the parse runs beside the next chunks' staging and copies, not after the last one
-        LAG = 1  # chunks searched but not yet parsed: the host waits on the previous chunk's search
         # the parses run on streams of their own (a chunk holds one or two bodies = a few hundred
         # series = waves, far from filling the GPU): consecutive chunks' parses overlap each other
         # and the copies, instead of queueing behind the next chunk's copy on the launch stream
         pstreams = self._parse_streams()
-        snaps = torch.zeros(max(len(flat), 1) + 1, dtype=torch.int64, pin_memory=True)
+        snaps = torch.zeros(max(len(dflat), 1) + 1, dtype=torch.int64, pin_memory=True)
         snap_np = snaps.numpy()
-        pend: list = []         # (event, snap index, body end) of searched, unparsed chunks
+        searched: list = []     # (event, snapshot slot, first body, body end) of chunks to parse
         waited = [0.0]
         parsed = [0, False]     # candidates parsed so far, overflow
+        host = load_library()
+        # per resource: routing outputs in the plan's group-sorted slot order (a chunk's bodies =
+        # whole groups = one contiguous range of it), and per body whether its series chained
+        rk = []
+        for plan, _ in items:
+            ns = plan.n_slots
+            rk.append({"sorted": plan.group_sorted_slots(), "src": np.full(max(ns, 1), -1, dtype=np.int64),
+                       "cnt": np.full(max(ns, 1), -1, dtype=np.int64),
+                       "ok": np.ones(max(len(plan.groups), 1), dtype=np.int32)})
+
+        def route(a, b, seg_rows, threads=2):
+            """Chain and route bodies [a, b) of dflat with their segments (int64 [k, 7] on the host)."""
+            n_seg = seg_rows.shape[0]
+            dev_offs, pdev, psh = self._live_layout()
+            for r, (plan, _) in enumerate(items):
+                g0, g1 = max(a, body0[r]) - body0[r], min(b, body0[r + 1]) - body0[r]
+                if g0 >= g1:
+                    continue
+                order, sgroup, blob, noffs, gstart = rk[r]["sorted"]
+                i0, i1 = int(gstart[g0]), int(gstart[g1])
+                b_offs = np.ascontiguousarray(dev_offs[body0[r] + g0:body0[r] + g1 + 1])
+                sb = np.ascontiguousarray(sgroup[i0:i1] - g0) if i1 > i0 else np.zeros(1, np.int64)
+                src = np.empty(max(i1 - i0, 1), dtype=np.int64)
+                cnt = np.empty(max(i1 - i0, 1), dtype=np.int64)
+                ok = np.empty(g1 - g0, dtype=np.int32)
+                rc = host.krr_pack_route_grouped_pieces(
+                    self._last_stage_ptr, b_offs.ctypes.data, g1 - g0, pdev.ctypes.data, psh.ctypes.data, pdev.size,
+                    label.encode(), seg_rows.ctypes.data, n_seg,
+                    sb.ctypes.data, blob or b"\0", noffs[i0:].ctypes.data, i1 - i0, src.ctypes.data,
+                    cnt.ctypes.data, ok.ctypes.data, threads)
+                if rc != KRR_PACK_OK:
+                    raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
+                rk[r]["src"][order[i0:i1]] = src[:i1 - i0]
+                rk[r]["cnt"][order[i0:i1]] = cnt[:i1 - i0]
+                rk[r]["ok"][g0:g1] = ok
+
+        per_chunk = self.grouped_route == "chunk"
+        to_route: list = []     # (event, first body, body end, segment range) of parsed chunks
+        route_wait = [0.0]
+
+        def route_ready(block=False):
+            """Route the parsed chunks whose parse and segment copy are done (the staging thread
+            does it between chunks, never waiting on the device; ``block``: all of them)."""
+            while to_route and (block or to_route[0][0].query()):
+                ev, a, b, rows = to_route.pop(0)
+                t_w = time.perf_counter()
+                ev.synchronize()
+                route_wait[0] += time.perf_counter() - t_w
+                route(a, b, rows.numpy())
 
         def parse_chunk(jb, tmp_v, tmp_t):
-            ev, k, b_end = pend.pop(0)
+            ev, k, a, b_end = searched.pop(0)
             t_w = time.perf_counter()
             ev.synchronize()  # that chunk's search only: later copies keep streaming
             waited[0] += time.perf_counter() - t_w
@@ -395,19 +518,27 @@ class DevicePacker:
             if parsed[1] or n > cap:
                 parsed[1] = True
                 return
-            if n > lo:
-                ps = pstreams[k % len(pstreams)]
-                ps.wait_event(ev)
-                with torch.cuda.stream(ps):
+            ps = pstreams[k % len(pstreams)]
+            ps.wait_event(ev)
+            rows = self._host_rows(n)[lo:n] if per_chunk else None
+            with torch.cuda.stream(ps):
+                if n > lo:
                     starts = torch.sort(cand[lo:n]).values
                     # the chunk's bodies' device offsets are in HBM (copied with the chunk)
                     body_of = torch.searchsorted(jb._keep[1][:b_end + 1], starts, right=True) - 1
                     self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t, segs[lo:n],
                                                  stream=ps)
+                    if per_chunk:
+                        rows.copy_(segs[lo:n], non_blocking=True)
+                if per_chunk:
+                    evp = torch.cuda.Event()
+                    evp.record(ps)
+            if per_chunk:
+                to_route.append((evp, a, b_end, rows))
             parsed[0] = n
 
         def launch(jb, a, b, tmp_v, tmp_t, lo, hi):  # search each chunk as it lands
-            last = b == len(flat)
+            last = b == len(dflat)
             end = hi if last else max(hi - 16, seen[0])
             self.ctx.json_find_series(jb, cand, n_cand, begin=seen[0], end=end, limit=hi, stream=st)
             seen[0] = end
@@ -416,74 +547,99 @@ class DevicePacker:
                 snaps[k:k + 1].copy_(n_cand, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(st)
-            pend.append((ev, k, b))
+            searched.append((ev, k, a, b))
             done.append(k)
-            if len(pend) > LAG:
+            if len(searched) > 1:  # parse the chunk searched before this one
                 parse_chunk(jb, tmp_v, tmp_t)
+            route_ready()
 
         done: list = []
-        # timestamps cut while staging, as for per-pod bodies: the candidate search, the series
-        # parse and the host's chain walk read structure, labels and value strings only
-        lens, boffs, total, jb, tmp_v, tmp_t = self._upload(flat, want_ts, st, launch, strip=self.strip,
-                                                            pieces=True)
-        clock.append(time.perf_counter())
-        while pend:
-            parse_chunk(jb, tmp_v, tmp_t)
+        threads_was = self.threads
+        if host_thread is not None:  # the staging threads: the rest
+            self.threads = max(1, T_all - t_host)
+        try:
+            # timestamps cut while staging, as for per-pod bodies: the candidate search, the series
+            # parse and the host's chain walk read structure, labels and value strings only
+            lens, boffs, total, jb, tmp_v, tmp_t = self._upload(dflat, want_ts, st, launch, strip=self.strip,
+                                                                pieces=True, extra_slots=host_bytes // 8 + 1)
+            clock.append(time.perf_counter())
+            while searched:
+                parse_chunk(jb, tmp_v, tmp_t)
+                route_ready()
+            clock.append(time.perf_counter())
+            if not parsed[1]:
+                route_ready(block=True)
+        finally:
+            self.threads = threads_was
         for ps in pstreams:
             st.wait_stream(ps)
+        if not per_chunk and not parsed[1]:  # every chunk's segments at once, then one route
+            nc = parsed[0]
+            rows = self._host_rows(nc)[:nc]
+            with torch.cuda.stream(st):
+                rows.copy_(segs[:nc])
+            route(0, len(dflat), rows.numpy(), self.threads)
+        t_dev = time.perf_counter() - clock[0]
+        if host_thread is not None:
+            host_thread.join()
         clock.append(time.perf_counter())
-        dev_offs, shift = self._layout[:2]
-        pieces = self._layout[2] if len(self._layout) > 2 else None
-        nc = parsed[0]
-        if parsed[1]:
+        if parsed[1] or "error" in host_res:  # candidates overflow / a body the host part rejects
             return [host_fallback(r, body0[r + 1] - body0[r]) for r in range(len(items))]
-        with torch.cuda.stream(st):
-            segs_h = np.ascontiguousarray(segs[:nc].cpu().numpy())  # sync
-        clock.append(time.perf_counter())
-        host = load_library()
-        stage = self._last[1]
+        if host_thread is not None:
+            # share toward r_host / (r_host + r_device) (bytes per second of each side)
+            r_h = host_bytes / max(host_res["s"], 1e-6)
+            r_d = total_bytes / max(t_dev, 1e-6)
+            self.grouped_share = min(max(0.5 * self.grouped_share + 0.5 * r_h / (r_h + r_d), 0.01), 0.5)
+            self.last_grouped_hybrid = {"share": host_bytes / (host_bytes + total_bytes), "host_bodies": len(flat) - split,
+                                        "host_s": round(host_res["s"], 5), "device_s": round(t_dev, 5),
+                                        "host_threads": t_host, "device_threads": max(1, T_all - t_host)}
         out = []
+        host_base = int(self._live_layout()[0][len(dflat)]) // 8 + 1  # scratch slots past the device bodies'
         for r, (plan, bodies) in enumerate(items):
-            ns, n_obj, nb = plan.n_slots, plan.n_objects, body0[r + 1] - body0[r]
-            slot_src = np.empty(ns, dtype=np.int64)
-            slot_cnt = np.empty(ns, dtype=np.int64)
-            body_ok = np.empty(max(nb, 1), dtype=np.int32)
-            b_offs = np.ascontiguousarray(dev_offs[body0[r]:body0[r + 1] + 1])
-            pdev, psh = pieces if pieces is not None else (np.zeros(0, np.int64), np.zeros(0, np.int64))
-            rc = host.krr_pack_route_grouped_pieces(
-                stage.data_ptr(), b_offs.ctypes.data, nb, pdev.ctypes.data, psh.ctypes.data, pdev.size,
-                label.encode(), segs_h.ctypes.data, nc, plan.slot_group.ctypes.data, plan._names or b"\0",
-                plan._name_offsets.ctypes.data, ns, slot_src.ctypes.data, slot_cnt.ctypes.data, body_ok.ctypes.data,
-                self.threads)
-            if rc != KRR_PACK_OK:
-                raise PrometheusResponseError(rc, "krr_pack_route_grouped failed")
-            if not body_ok[:nb].all():
-                out.append(host_fallback(r, int((body_ok[:nb] == 0).sum())))
+            ns, n_obj = plan.n_slots, plan.n_objects
+            n_dev_bodies = max(0, min(body0[r + 1], split) - body0[r])
+            slot_src, slot_cnt = rk[r]["src"][:ns].copy(), rk[r]["cnt"][:ns].copy()
+            if not rk[r]["ok"][:n_dev_bodies].all():
+                out.append(host_fallback(r, int((rk[r]["ok"][:n_dev_bodies] == 0).sum())))
                 continue
+            if r in host_res:  # the host-parsed groups' slots: their values after the device scratch
+                idx, hv, hoff, hcnt = host_res[r]
+                slot_src[idx] = host_base + hoff[:-1]
+                slot_cnt[idx] = hcnt
+                if hv.size:
+                    with torch.cuda.stream(st):
+                        tmp_v[host_base:host_base + hv.size].copy_(torch.from_numpy(hv), non_blocking=True)
+                host_base += hv.size
             kept = np.maximum(slot_cnt, 0)
             dst = np.zeros(ns, dtype=np.int64)
             if ns > 1:
                 np.cumsum(kept[:-1], out=dst[1:])
-            seg = np.zeros(n_obj, dtype=np.int64)
-            np.add.at(seg, plan.slot_obj, kept)
+            seg = np.bincount(plan.slot_obj, weights=kept, minlength=n_obj).astype(np.int64) if ns else \
+                np.zeros(n_obj, dtype=np.int64)
             offsets = np.zeros(n_obj + 1, dtype=np.int64)
             np.cumsum(seg, out=offsets[1:])
             n_vals = int(offsets[-1])
+            # the gather's three columns and the offsets in ONE page-locked buffer, one copy
+            cols = torch.empty(3 * ns + n_obj + 1, dtype=torch.int64, pin_memory=True)
+            cn = cols.numpy()
+            cn[:ns], cn[ns:2 * ns], cn[2 * ns:3 * ns], cn[3 * ns:] = np.maximum(slot_src, 0), kept, dst, offsets
             with torch.cuda.stream(st):
                 values = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev)
                 ts = torch.empty(max(n_vals, 1), dtype=torch.float64, device=dev) if want_ts else None
+                cols_d = cols.to(dev, non_blocking=True)
                 if ns:
-                    d = [torch.from_numpy(x).to(dev) for x in (np.maximum(slot_src, 0), kept, dst)]
-                    self.ctx.json_gather(d[0], d[1], d[2], tmp_v, tmp_t, values, ts, stream=st)
-                offs_d = torch.from_numpy(offsets).to(dev)
+                    self.ctx.json_gather(cols_d[:ns], cols_d[ns:2 * ns], cols_d[2 * ns:3 * ns], tmp_v, tmp_t, values,
+                                         ts, stream=st)
+                offs_d = cols_d[3 * ns:]
             series = PackedSeries(values[:n_vals], offs_d, int(seg.max()) if n_obj else 0)
             out.append(DevicePacked(series, "device", 0, slot_cnt if want_counts else None,
                                     ts[:n_vals] if ts is not None else None))
         clock.append(time.perf_counter())
-        # seconds per phase: staging + copies + search (+ the parse of all chunks but the last),
-        # the last chunk's parse, the segments to the host, chain / route / gather enqueue
-        self.last_grouped_phases = dict(zip(("stage_copy_search", "last_parse", "segments_d2h", "route_gather"),
+        # seconds per phase: staging + copies + search + the parse and route of all chunks but the
+        # last ones, the last chunks' parse, their route (+ the host part's join), the gather enqueue
+        self.last_grouped_phases = dict(zip(("stage_copy_search", "last_parse", "last_route", "gather"),
                                             np.diff(clock).round(5).tolist()), parse_wait=round(waited[0], 5),
+                                        route_wait=round(route_wait[0], 5),
                                         strip=(self.last_upload or {}).get("strip_s"))
         return out
 

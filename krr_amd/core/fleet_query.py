@@ -237,6 +237,65 @@ class FleetQueryPlan:
             out.append(counts[:ns])
         return out[0] if len(out) == 1 else tuple(out)
 
+    def group_sorted_slots(self):
+        """The slots ordered by group (stable): (order int64 [n_slots], slot_group[order], the pod
+        names blob in that order, its offsets int64 [n_slots + 1], group_start int64 [n_groups + 1]
+        = where each group's slots begin in that order).  A run of whole groups is then one
+        contiguous range — the device packer routes chunk by chunk over it.  Cached."""
+        cached = getattr(self, "_group_sorted", None)
+        if cached is not None:
+            return cached
+        order = np.argsort(self.slot_group, kind="stable").astype(np.int64)
+        sgroup = np.ascontiguousarray(self.slot_group[order])
+        names = [self.slot_pods[i].encode() for i in order.tolist()]
+        offs = np.zeros(len(names) + 1, dtype=np.int64)
+        if names:
+            np.cumsum([len(n) for n in names], out=offs[1:])
+        gstart = np.searchsorted(sgroup, np.arange(len(self.groups) + 1), side="left").astype(np.int64)
+        self._group_sorted = (order, sgroup, b"".join(names), offs, gstart)
+        return self._group_sorted
+
+    def pack_group_slots(self, bodies: Sequence[bytes], g0: int, g1: int, *, threads: int = 0, alloc=None):
+        """The slots of groups [g0, g1) alone, from their bodies (bodies[i] answers group g0 + i),
+        one segment per SLOT instead of per object: returns (slot indices int64 [k], values,
+        offsets int64 [k + 1], counts int64 [k], -1 = dropped) — the series ``pack`` would route
+        to each of those (object, pod) slots (krr_pack_parse_grouped, first series with the pod
+        label wins).  The hybrid grouped parser's host side (krr_amd.core.device_pack)."""
+        if len(bodies) != g1 - g0:
+            raise ValueError("one body per group of [g0, g1)")
+        idx = np.flatnonzero((self.slot_group >= g0) & (self.slot_group < g1)).astype(np.int64)
+        k = idx.size
+        lib = load_library()
+        flat = [b if isinstance(b, bytes) else bytes(b) for b in bodies]
+        ptrs = (ctypes.c_char_p * max(len(flat), 1))(*flat)
+        lens = np.array([len(b) for b in flat] or [0], dtype=np.int64)
+        names = [self.slot_pods[i].encode() for i in idx.tolist()]
+        blob = b"".join(names)
+        name_offs = np.zeros(k + 1, dtype=np.int64)
+        if k:
+            np.cumsum([len(n) for n in names], out=name_offs[1:])
+        sg = np.ascontiguousarray(self.slot_group[idx] - g0) if k else np.zeros(1, np.int64)
+        so = np.arange(max(k, 1), dtype=np.int64)
+        h = ctypes.c_void_p()
+        rc = lib.krr_pack_parse_grouped(ctypes.cast(ptrs, ctypes.c_void_p), _ptr(lens), len(flat), b"pod", _ptr(sg),
+                                        blob or b"\0", _ptr(name_offs), _ptr(so), k, k, 0, int(threads),
+                                        ctypes.byref(h))
+        try:
+            if rc != KRR_PACK_OK:
+                msg = lib.krr_pack_error(h) if h else b""
+                raise PrometheusResponseError(rc, (msg or b"invalid arguments").decode())
+            n = int(lib.krr_pack_n_values(h))
+            values = alloc(n) if alloc is not None else np.empty(n, dtype=np.float64)
+            offsets = np.empty(k + 1, dtype=np.int64)
+            counts = np.empty(max(k, 1), dtype=np.int64)
+            rc = lib.krr_pack_copy(h, _ptr(values), _ptr(offsets), None, _ptr(counts), int(threads))
+            if rc != KRR_PACK_OK:
+                raise PrometheusResponseError(rc, "krr_pack_copy failed")
+        finally:
+            if h:
+                lib.krr_pack_free(h)
+        return idx, values, offsets, counts[:k]
+
     def fetch(self, query_range: Callable[[str], bytes], *, max_workers: int = 16) -> dict:
         """Run every grouped query for both resources; ``query_range(query)``
         performs one /api/v1/query_range request (start, end and step — the

@@ -423,7 +423,9 @@ class BatchedRunner:
         krr_amd.core.fleet_query.FleetQueryPlan and bodies[g] answers its g-th grouped
         ``sum by (pod)`` query (one per (namespace, container), not one per pod).
         ``parser="device"``: the MI355X parses the bodies and the host routes series to
-        pods by label (krr_amd.core.device_pack); ``"host"``: krr_pack_parse_grouped."""
+        pods by label (krr_amd.core.device_pack); ``"host"``: krr_pack_parse_grouped;
+        ``"hybrid"``: the device, with the last groups' bodies parsed by the host packer
+        meanwhile (``DevicePacker.pack_grouped_many(hybrid=True)``)."""
         import time
 
         t0 = time.perf_counter()
@@ -436,12 +438,13 @@ class BatchedRunner:
     def pack_grouped(self, plan, cpu_bodies, mem_bodies, threads: int = 0, parser: str = "device"):
         from krr_amd.core.packing import PackedFleet
 
-        if parser not in ("device", "host"):
-            raise ValueError("parser must be 'device' or 'host'")
+        if parser not in ("device", "host", "hybrid"):
+            raise ValueError("parser must be 'device', 'host' or 'hybrid'")
         if parser == "host":
             return plan.pack_fleet(cpu_bodies, mem_bodies, threads=threads, alloc=_pinned_alloc_or_none())
         packer = self._device_packer(threads)
-        cpu, mem = packer.pack_grouped_many([(plan, cpu_bodies), (plan, mem_bodies)])
+        # hybrid: the last groups' bodies parsed by the host packer while the rest cross the link
+        cpu, mem = packer.pack_grouped_many([(plan, cpu_bodies), (plan, mem_bodies)], hybrid=parser == "hybrid")
         self.last_pack_via = (cpu.via, mem.via)
         return PackedFleet(cpu.series, mem.series)
 

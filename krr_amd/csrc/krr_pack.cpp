@@ -21,6 +21,8 @@
 #include <memory>
 #include <mutex>
 #include <pthread.h>
+#include <sched.h>
+#include <cstdlib>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -460,8 +462,24 @@ void parse_series_set(const char* s, int64_t n, const char* label, bool want_ts,
     if (!have_result) return fail(KRR_PACK_E_PARSE, "no data.result");
 }
 
+// threads = 0: the CPUs this process may run on (its affinity mask; hardware_concurrency counts
+// the whole machine's, many times a GPU box's lease), capped by OMP_NUM_THREADS when set
+int default_threads() {
+    static const int n = [] {
+        int c = (int)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) c = CPU_COUNT(&set);
+        if (const char* omp = std::getenv("OMP_NUM_THREADS")) {
+            const int o = std::atoi(omp);
+            if (o > 0 && o < c) c = o;
+        }
+        return c;
+    }();
+    return n;
+}
+
 int pool_size(int32_t threads, int64_t work) {
-    int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    int t = threads > 0 ? threads : default_threads();
     if (t < 1) t = 1;
     if ((int64_t)t > work) t = (int)std::max<int64_t>(work, 1);
     return t;

@@ -8,6 +8,8 @@
 // reference's result, digits and exponent included.
 #include "krr_round.h"
 
+#include <sched.h>
+#include <cstdlib>
 #include <algorithm>
 #include <atomic>
 #include <charconv>
@@ -484,9 +486,25 @@ bool fast_mem(double x, const Fast& F, char* out, int32_t width) {
     return true;
 }
 
+// threads = 0: the CPUs of this process's affinity mask, capped by OMP_NUM_THREADS when set
+// (hardware_concurrency counts the whole machine's CPUs, many times a GPU box's lease)
+inline int default_threads() {
+    static const int n = [] {
+        int c = (int)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) c = CPU_COUNT(&set);
+        if (const char* omp = std::getenv("OMP_NUM_THREADS")) {
+            const int o = std::atoi(omp);
+            if (o > 0 && o < c) c = o;
+        }
+        return c;
+    }();
+    return n;
+}
+
 template <class F>
 void parallel_for(int64_t n, int32_t threads, F f) {
-    int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    int t = threads > 0 ? threads : default_threads();
     if (t < 1) t = 1;
     if ((int64_t)t * 256 > n) t = (int)std::max<int64_t>(1, n / 256);
     if (t <= 1) {

@@ -211,7 +211,7 @@ async def fetch_grouped_fleet(runner: Any, objects: Sequence[Any], settings, par
         bodies = await asyncio.to_thread(plan.fetch, q)
         if parser in ("device", "hybrid") and batched is not None:  # parsed on the MI355X, routed by pod label
             fleet = await asyncio.to_thread(batched.pack_grouped, plan, bodies[HipResourceType.CPU],
-                                            bodies[HipResourceType.Memory], 0, "device")
+                                            bodies[HipResourceType.Memory], 0, parser)
         else:
             fleet = await asyncio.to_thread(plan.pack_fleet, bodies[HipResourceType.CPU],
                                             bodies[HipResourceType.Memory])

@@ -1,0 +1,82 @@
+"""Same-process A/B of the device packer's grouped pipeline variants on bench.py's grouped
+workload (2,000 objects x 3 pods x 10,080 samples as 20-namespace `sum by (pod)` bodies).
+
+    python scripts/grouped_probe.py [--rounds R]
+
+Prints per variant the median seconds of pack_grouped_many (both resources, to a synchronised
+CSR in HBM) and the packer's last phase split.  Variants: grouped_route "chunk" / "end"."""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from krr_amd.core.device_pack import default_packer  # noqa: E402
+from krr_amd.core.fleet_query import FleetQueryPlan  # noqa: E402
+from krr_amd.strategies.simple import SimpleStrategySettings  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--objects", type=int, default=2000)
+    args = ap.parse_args()
+    objects, pods, distinct = args.objects, 3, 48
+    from krr_amd.utils.numa import bind_local
+
+    bind_local(0)  # as bench.py: the GPU's NUMA node
+    threads = bench.cpu_lease()["threads"]
+    cpu_vals, mem_vals, _, _ = bench.body_fleet(0, objects, pods, distinct)
+
+    class _Obj:
+        def __init__(self, o):
+            self.namespace, self.container = f"ns{o % 20}", "main"
+            self.pods = [f"pod-{o}-{i}" for i in range(pods)]
+
+    plan = FleetQueryPlan.for_settings([_Obj(o) for o in range(objects)], SimpleStrategySettings())
+
+    def grouped(vals, shift):
+        out_b = []
+        for gq in plan.groups:
+            parts = [f'{{"metric":{{"pod":"{pod}"}},"values":[{vals[(i + shift) % distinct]}]}}'
+                     for i, pod in enumerate(reversed(gq.pods))]
+            out_b.append((bench.BODY_HEAD + ",".join(parts) + ']}}').encode())
+        return out_b
+
+    g_cpu, g_mem = grouped(cpu_vals, 0), grouped(mem_vals, 7)
+    print(f"{len(plan.groups)} bodies per resource, {sum(map(len, g_cpu)) / 1e9:.2f} GB CPU JSON", flush=True)
+    packer = default_packer(0)
+    packer.threads = threads
+    want = [(plan.pack(g_cpu).values, plan.pack(g_mem).values)]
+    variants = ["chunk", "end", "hybrid", "chunk_after_hybrid"]
+    times = {v: [] for v in variants}
+    phases = {}
+    for r in range(args.rounds + 1):
+        for v in variants:
+            packer.grouped_route = "end" if v == "end" else "chunk"
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)], hybrid=v == "hybrid")
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if r == 0:
+                got = (out[0].series.values.cpu().numpy(), out[1].series.values.cpu().numpy())
+                assert all(np.array_equal(a, b) for a, b in zip(got, want[0])), v
+                continue
+            times[v].append(dt)
+            phases[v] = packer.last_grouped_phases
+        print(f"round {r} done", flush=True)
+    for v in variants:
+        print(f"{v}: median {np.median(times[v]) * 1e3:.2f} ms  runs {[round(t * 1e3, 2) for t in sorted(times[v])]}")
+        print(f"   phases {phases[v]}")
+
+
+if __name__ == "__main__":
+    main()

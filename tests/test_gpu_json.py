@@ -409,3 +409,82 @@ def test_stripped_staging_error_and_host_batches(packer):
     with pytest.raises(PrometheusResponseError) as host_err:
         _host(bad)
     assert str(dev_err.value) == str(host_err.value) and dev_err.value.code == host_err.value.code
+
+
+@pytest.mark.parametrize("share", [0.05, 0.3, 0.9])
+def test_grouped_hybrid_equals_host_plan(packer, share):
+    """The hybrid grouped parser (round 6): the last groups' bodies parsed by the host packer
+    (FleetQueryPlan.pack_group_slots) while the rest are staged in pieces, parsed on the device
+    and routed; the host slots' values join the device scratch and one gather builds the CSR —
+    plan.pack's CSR and pod counts bit for bit, at any share; a body the host part rejects, or
+    the device part, gives the host packer's error for the batch."""
+    from test_fleet_query import make_fleet
+
+    from krr_amd.core.device_pack import DevicePacker
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.core.models.allocations import ResourceType
+    from krr_amd.core.prom_native import PrometheusResponseError
+
+    objects, prom = make_fleet(seed=5, n_obj=60)
+    plan = FleetQueryPlan(objects, max_query_chars=300)
+    bc = [_recompact(prom.query_range(q)) for q in plan.queries(ResourceType.CPU)]
+    bm = [_recompact(prom.query_range(q)) for q in plan.queries(ResourceType.Memory)]
+    assert len(plan.groups) >= 4
+    for p in (packer, DevicePacker(packer.ctx, chunk_bytes=8192)):
+        p.grouped_share = share
+        a, b = p.pack_grouped_many([(plan, bc), (plan, bm)], return_pod_counts=True, hybrid=True)
+        assert getattr(p, "last_grouped_hybrid", None) and p.last_grouped_hybrid["host_bodies"] >= 1
+        for dp, bodies in ((a, bc), (b, bm)):
+            want, want_counts = plan.pack(bodies, return_pod_counts=True)
+            assert dp.via == "device"
+            assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+            assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+            assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+            assert dp.series.max_len == want.max_len
+    err = b'{"status":"error","errorType":"bad_data","error":"boom"}'
+    for at in (0, len(bm) - 1):  # the device part / the host part
+        bad = list(bm)
+        bad[at] = err
+        with pytest.raises(PrometheusResponseError) as e_h:
+            plan.pack(bad)
+        packer.grouped_share = share
+        with pytest.raises(PrometheusResponseError) as e_y:
+            packer.pack_grouped_many([(plan, bc), (plan, bad)], hybrid=True)
+        assert str(e_y.value) == str(e_h.value)
+
+
+def test_grouped_large_bodies_in_pieces_and_hybrid(packer):
+    """~2.5 MB grouped bodies staged in pieces cut inside the bodies (`"],[`), parsed one chunk
+    behind the search on the parse streams, with and without the host share: plan.pack's CSR."""
+    from krr_amd.core.device_pack import DevicePacker
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.utils.prom_decimal import prom_format
+
+    class Obj:
+        def __init__(self, ns, c, pods):
+            self.namespace, self.container, self.pods = ns, c, pods
+
+    rng = np.random.default_rng(31)
+    objects = [Obj(f"ns{g % 6}", "app", [f"pod-{g}-{k}" for k in range(int(rng.integers(1, 4)))]) for g in range(60)]
+    plan = FleetQueryPlan(objects, max_query_chars=2000)
+    bodies = []
+    for grp in plan.groups:
+        res = []
+        for pod in reversed(grp.pods):
+            xs = rng.gamma(2.0, 0.05, int(rng.integers(3000, 10081)))
+            res.append({"metric": {"pod": pod, "note": "],[1,2"},  # cut-like bytes inside a string
+                        "values": [[1700000000 + 60 * k + 0.25 * (k % 3), prom_format(float(x))]
+                                   for k, x in enumerate(xs)]})
+        bodies.append(_compact({"status": "success", "data": {"resultType": "matrix", "result": res}}))
+    want, want_counts = plan.pack(bodies, return_pod_counts=True)
+    for p in (packer, DevicePacker(packer.ctx, chunk_bytes=1 << 20, threads=5)):
+        for hybrid in (False, True):
+            p.grouped_share = 0.25
+            dp = p.pack_grouped_many([(plan, bodies)], return_pod_counts=True, hybrid=hybrid)[0]
+            assert dp.via == "device"
+            n_dev = len(bodies) - (p.last_grouped_hybrid["host_bodies"] if hybrid else 0)
+            if p is packer:  # its pieces (2 per staging thread) are smaller than a body: the bodies were cut
+                assert p.last_upload["pieces"] > n_dev, (p.last_upload, n_dev)
+            assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+            assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+            assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
