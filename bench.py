@@ -36,6 +36,7 @@ gathered to rank 0) against the oracle on a sample regenerated from every shard.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -239,6 +240,59 @@ def fleet_chunks(offs_np: np.ndarray, chunk_gib: float) -> list[tuple[int, int]]
         return [(0, S)]
     n = int(np.ceil(nbytes / limit))
     return [(lo, hi) for lo, hi in shard_bounds(np.diff(offs_np), n) if hi > lo]
+
+
+class _gc_timer:
+    """Python garbage-collector passes (per generation) and their seconds until stop()."""
+
+    def __init__(self):
+        import gc
+
+        self.t = {}
+        self.n = {}
+        self._t0 = None
+
+        def cb(phase, info):
+            if phase == "start":
+                self._t0 = time.perf_counter()
+            elif self._t0 is not None:
+                g = info.get("generation", -1)
+                self.t[g] = self.t.get(g, 0.0) + time.perf_counter() - self._t0
+                self.n[g] = self.n.get(g, 0) + 1
+                self._t0 = None
+
+        self._cb = cb
+        gc.callbacks.append(cb)
+
+    def stop(self) -> dict:
+        import gc
+
+        gc.callbacks.remove(self._cb)
+        return {f"gen{g}": [self.n[g], round(self.t[g], 5)] for g in sorted(self.t)}
+
+
+def cgroup_cpu() -> dict:
+    """The CPU controller's quota and throttling counters of this process's cgroup (v2 or v1
+    files; {} where absent): a host phase that runs more busy threads than the quota allows is
+    stopped for the rest of each period, which shows up as nr_throttled / throttled_usec."""
+    out = {}
+    for base in ("/sys/fs/cgroup", "/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+        try:
+            with open(os.path.join(base, "cpu.stat")) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k in ("nr_periods", "nr_throttled", "throttled_usec", "throttled_time", "usage_usec"):
+                        out[k] = int(v)
+        except (OSError, ValueError):
+            continue
+        for name in ("cpu.max", "cpu.cfs_quota_us"):
+            try:
+                with open(os.path.join(base, name)) as fh:
+                    out[name] = fh.read().strip()
+            except OSError:
+                pass
+        break
+    return out
 
 
 def cpu_lease() -> dict:
@@ -993,6 +1047,8 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
             for _ in range(4):
                 runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)
         runs_g = []
+        cg0 = cgroup_cpu()
+        gc_t = _gc_timer()
         for _ in range(3 if parser == "host" else 7):
             t0 = time.perf_counter()
             res_g = runner.recommend_from_grouped(plan, g_cpu, g_mem, threads=threads, parser=parser)
@@ -1000,10 +1056,16 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
         assert len(res_g) == objects
         eg[parser] = (float(np.median(runs_g)), [(str(r[k].request), str(r[k].limit)) for r in res_g for k in r],
                       sorted(runs_g))
-        if parser == "device":  # its staging and phases are the ones reported
-            g_state = {"upload": _dp(dev.index or 0).last_upload,
-                       "phases": dict(getattr(runner, "grouped_last", {}),
-                                      **getattr(_dp(dev.index or 0), "last_grouped_phases", {}))}
+        cg1 = cgroup_cpu()
+        g_state.setdefault("cgroup", {})[parser] = {k: cg1[k] - cg0.get(k, 0) for k in cg1 if isinstance(cg1[k], int)}
+        g_state["cgroup"][parser]["gc"] = gc_t.stop()
+        g_state["cgroup"]["quota"] = cg1.get("cpu.max") or cg1.get("cpu.cfs_quota_us")
+        if parser != "host":  # the last run's staging and phases
+            g_state[parser] = {"upload": dict(_dp(dev.index or 0).last_upload or {},
+                                              stage_nodes=getattr(_dp(dev.index or 0), "stage_nodes", None),
+                                              stage_mapping=getattr(_dp(dev.index or 0), "stage_mapping", None)),
+                               "phases": dict(getattr(runner, "grouped_last", {}),
+                                              **getattr(_dp(dev.index or 0), "last_grouped_phases", {}))}
     assert runner.last_pack_via == ("device", "device"), runner.last_pack_via
     # e2e_grouped_objects_per_s: the device parser (a grouped body is ~100 MB: the host packer
     # cannot split one across its threads, so the hybrid's host share only slows the staging
@@ -1014,8 +1076,17 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
     out["e2e_grouped_hybrid_equals_host"] = eg["hybrid"][1] == eg["host"][1]
     out["e2e_grouped_hybrid_split"] = getattr(_dp(dev.index or 0), "last_grouped_hybrid", None)
     out["e2e_grouped_objects_per_s_host_parse"] = objects / eg["host"][0]
-    out["e2e_grouped_upload"] = g_state["upload"]
-    out["e2e_grouped_phases_s"] = g_state["phases"]
+    out["e2e_grouped_upload"] = g_state["device"]["upload"]
+    out["e2e_grouped_phases_s"] = g_state["device"]["phases"]
+    out["e2e_grouped_hybrid_phases_s"] = g_state["hybrid"]["phases"]
+    out["e2e_grouped_cgroup_cpu"] = g_state["cgroup"]
+    from krr_amd.utils.numa import page_nodes
+
+    from krr_amd.utils.numa import mapping_info
+
+    b_addr = ctypes.cast(ctypes.c_char_p(g_cpu[0]), ctypes.c_void_p).value
+    out["e2e_grouped_body_nodes"] = page_nodes(b_addr, len(g_cpu[0]), 16)
+    out["e2e_grouped_body_mapping"] = mapping_info(b_addr, len(g_cpu[0]))
     out["e2e_grouped_device_equals_host"] = eg["device"][1] == eg["host"][1]
     out["host_path"] = {
         "h2d": f"{n * 8 >> 20} MiB of this run's CPU series, page-locked, {chunk * 8 >> 20}-MiB copies, {reps} reps",

@@ -816,7 +816,7 @@ class Context:
         n = starts.numel()
         _check_tensor(starts, "int64", n)
         _check_tensor(body_of, "int64", n)
-        _check_tensor(segments, "int64", 7 * n)
+        _check_tensor(segments, "int64", 7 * n, host_pinned_ok=True)  # pinned: written through the mapping
         _check_tensor(scratch_values, "float64", jb.total_bytes // 8 + 1)
         if want_timestamps:
             _check_tensor(scratch_ts, "float64", jb.total_bytes // 8 + 1)

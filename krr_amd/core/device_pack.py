@@ -24,6 +24,7 @@ either way (``DevicePacked.via`` says which ran).
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from dataclasses import dataclass
 from typing import Optional, Sequence
@@ -62,6 +63,9 @@ class DevicePacker:
         self.strip = (os.environ.get("KRR_PACK_STRIP", "1") != "0") if strip is None else bool(strip)
         self.last_upload: Optional[dict] = None
         self.strip_runs_per_thread = 1  # runs per staging thread (each run = one H2D copy)
+        # grouped bodies: strip pieces per staging thread and chunk (each piece is one H2D copy: 4 per
+        # thread cost 6 ms of 57 on the bench fleet against 1, which still balances the strip)
+        self.pieces_per_thread = 1
         self.device = torch.device("cuda", ctx.device)
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
@@ -111,7 +115,18 @@ class DevicePacker:
         import torch
 
         if self._stage is None or self._stage.numel() < nbytes:
+            from krr_amd.utils.numa import page_nodes
+
+            if self._stage is not None:  # the old buffer goes back to the system first
+                self._stage = self._last = None
+                empty = getattr(torch._C, "_host_emptyCache", None)
+                if empty is not None:
+                    empty()
             self._stage = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            self.stage_nodes = page_nodes(self._stage.data_ptr(), self._stage.numel())
+            from krr_amd.utils.numa import mapping_info
+
+            self.stage_mapping = mapping_info(self._stage.data_ptr(), self._stage.numel())
         return self._stage
 
     def pack(self, per_object_bodies: Sequence[Sequence[bytes]], *, want_timestamps: bool = False,
@@ -281,7 +296,7 @@ class DevicePacker:
         dev = self.device
         nb = len(lens)
         T = self.threads or len(os.sched_getaffinity(0))
-        max_pieces = max(2, 2 * T)
+        max_pieces = max(2, int(self.pieces_per_thread * T))
         cap = 2 * nb + max_pieces
         new_lens = np.empty(nb, dtype=np.int64)
         p_start = np.empty(cap + 1, dtype=np.int64)
@@ -374,7 +389,8 @@ class DevicePacker:
 
     grouped_share = 0.06          # the hybrid grouped parser's host share of the bytes (adapted)
     grouped_host_threads = 0      # 0: a quarter of the threads
-    grouped_route = "chunk"       # "chunk": segments to the host and routed per chunk; "end": once
+    # "chunk": segments to the host and routed per chunk; "end": once, after the last parse
+    grouped_route = os.environ.get("KRR_GROUPED_ROUTE", "chunk")
     _EMPTY_BODY = b'{"status":"success","data":{"resultType":"matrix","result":[]}}'
 
     def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label, host_share: float = 0.0) -> list:
@@ -447,7 +463,8 @@ class DevicePacker:
         cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
-        segs = torch.empty((cap, 7), dtype=torch.int64, device=dev)
+        per_chunk = self.grouped_route == "chunk"
+        segs = None if per_chunk else torch.empty((cap, 7), dtype=torch.int64, device=dev)
         seen = [0]  # positions below this were searched
         # the parses run on streams of their own (a chunk holds one or two bodies = a few hundred
         # series = waves, far from filling the GPU): consecutive chunks' parses overlap each other
@@ -457,6 +474,7 @@ class DevicePacker:
         snap_np = snaps.numpy()
         searched: list = []     # (event, snapshot slot, first body, body end) of chunks to parse
         waited = [0.0]
+        enq = [0.0]             # host seconds enqueueing the parses
         parsed = [0, False]     # candidates parsed so far, overflow
         host = load_library()
         # per resource: routing outputs in the plan's group-sorted slot order (a chunk's bodies =
@@ -494,9 +512,9 @@ class DevicePacker:
                 rk[r]["cnt"][order[i0:i1]] = cnt[:i1 - i0]
                 rk[r]["ok"][g0:g1] = ok
 
-        per_chunk = self.grouped_route == "chunk"
         to_route: list = []     # (event, first body, body end, segment range) of parsed chunks
-        route_wait = [0.0]
+        route_wait = [0.0, 0.0]  # waiting for parsed chunks, routing them
+        route_threads = [2]      # while staging: 2 (the staging keeps the pool)
 
         def route_ready(block=False):
             """Route the parsed chunks whose parse and segment copy are done (the staging thread
@@ -505,8 +523,10 @@ class DevicePacker:
                 ev, a, b, rows = to_route.pop(0)
                 t_w = time.perf_counter()
                 ev.synchronize()
-                route_wait[0] += time.perf_counter() - t_w
-                route(a, b, rows.numpy())
+                t_r = time.perf_counter()
+                route_wait[0] += t_r - t_w
+                route(a, b, rows.numpy(), route_threads[0])
+                route_wait[1] += time.perf_counter() - t_r
 
         def parse_chunk(jb, tmp_v, tmp_t):
             ev, k, a, b_end = searched.pop(0)
@@ -518,6 +538,7 @@ class DevicePacker:
             if parsed[1] or n > cap:
                 parsed[1] = True
                 return
+            t_e = time.perf_counter()
             ps = pstreams[k % len(pstreams)]
             ps.wait_event(ev)
             rows = self._host_rows(n)[lo:n] if per_chunk else None
@@ -526,16 +547,18 @@ class DevicePacker:
                     starts = torch.sort(cand[lo:n]).values
                     # the chunk's bodies' device offsets are in HBM (copied with the chunk)
                     body_of = torch.searchsorted(jb._keep[1][:b_end + 1], starts, right=True) - 1
-                    self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t, segs[lo:n],
-                                                 stream=ps)
-                    if per_chunk:
-                        rows.copy_(segs[lo:n], non_blocking=True)
+                    # per chunk: the kernel writes the segments straight into page-locked host
+                    # memory (no device-to-host DMA: on the copy engines it queued behind, and
+                    # slowed, the chunks' host-to-device copies)
+                    self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t,
+                                                 rows if per_chunk else segs[lo:n], stream=ps)
                 if per_chunk:
                     evp = torch.cuda.Event()
                     evp.record(ps)
             if per_chunk:
                 to_route.append((evp, a, b_end, rows))
             parsed[0] = n
+            enq[0] += time.perf_counter() - t_e
 
         def launch(jb, a, b, tmp_v, tmp_t, lo, hi):  # search each chunk as it lands
             last = b == len(dflat)
@@ -567,7 +590,8 @@ class DevicePacker:
                 parse_chunk(jb, tmp_v, tmp_t)
                 route_ready()
             clock.append(time.perf_counter())
-            if not parsed[1]:
+            if not parsed[1]:  # the staging is over: the last chunks' routing gets every thread
+                route_threads[0] = self.threads
                 route_ready(block=True)
         finally:
             self.threads = threads_was
@@ -639,7 +663,8 @@ class DevicePacker:
         # last ones, the last chunks' parse, their route (+ the host part's join), the gather enqueue
         self.last_grouped_phases = dict(zip(("stage_copy_search", "last_parse", "last_route", "gather"),
                                             np.diff(clock).round(5).tolist()), parse_wait=round(waited[0], 5),
-                                        route_wait=round(route_wait[0], 5),
+                                        route_wait=round(route_wait[0], 5), route_s=round(route_wait[1], 5),
+                                        parse_enqueue_s=round(enq[0], 5),
                                         strip=(self.last_upload or {}).get("strip_s"))
         return out
 

@@ -312,7 +312,9 @@ struct SegArgs {
     int64_t n;
     int32_t want_ts;
     int32_t label_len;
-    const char* label;         // device copy of the routing label key
+    // the routing label key, by value in the kernel arguments (no per-launch copy into a
+    // device buffer shared by the launches of several streams); NUL-padded to kMaxLabel
+    uint64_t label_w[kMaxLabel / 8];
     double* tmp_v;
     double* tmp_t;
     int64_t* seg;              // [n][kSegWords]
@@ -320,13 +322,20 @@ struct SegArgs {
 
 __global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
+    __shared__ uint64_t label_lds[kMaxLabel / 8];
     const int lane = threadIdx.x;
+    if (lane == 0) {
+#pragma unroll
+        for (int w = 0; w < kMaxLabel / 8; ++w) label_lds[w] = A.label_w[w];
+    }
+    __syncthreads();
+    const char* label = reinterpret_cast<const char*>(label_lds);
     for (int64_t j = blockIdx.x; j < A.n; j += gridDim.x) {
         const int64_t x = A.start[j], bi = A.body[j];
         const char* e = A.bodies + A.offs[bi + 1];
         GroupedWalker W;
         if (lane == 0) {
-            W.init(A.bodies + x, e, A.label, A.label_len);
+            W.init(A.bodies + x, e, label, A.label_len);
             W.resume(A.bodies + x, GroupedWalker::SERIES_OPEN);
         }
         int ok = 0;

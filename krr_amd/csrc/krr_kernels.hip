@@ -3340,7 +3340,6 @@ struct krr_ctx {
     hipEvent_t fail_ev;
     hipStream_t fail_stream;
     bool fail_ev_valid;
-    char* d_label;                // krr_json_parse_segments: the routing label key (device copy)
     char err[512];
 };
 
@@ -3537,7 +3536,6 @@ int krr_create(int device, krr_ctx** out_ctx) {
     c->fail_ev = nullptr;
     c->fail_stream = nullptr;
     c->fail_ev_valid = false;
-    c->d_label = nullptr;
     if (hipEventCreateWithFlags(&c->fail_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return KRR_E_HIP;
@@ -3578,7 +3576,6 @@ int krr_destroy(krr_ctx* ctx) {
     if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
     if (ctx->d_fail_count) (void)hipFree(ctx->d_fail_count);
     if (ctx->d_fail_list) (void)hipFree(ctx->d_fail_list);
-    if (ctx->d_label) (void)hipFree(ctx->d_label);
     if (ctx->fail_ev) (void)hipEventDestroy(ctx->fail_ev);
     delete ctx;
     return KRR_OK;
@@ -4475,10 +4472,11 @@ int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_
         return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
-    if (!ctx->d_label) KRR_HIP(ctx, hipMalloc(&ctx->d_label, json::kMaxLabel));
-    KRR_HIP(ctx, hipMemcpyAsync(ctx->d_label, label, ll + 1, hipMemcpyHostToDevice, (hipStream_t)stream));
+    // the label travels in the kernel arguments: a pageable hipMemcpyAsync here stalled the
+    // calling thread behind the stream's earlier work (and raced across parse streams)
     json::SegArgs A{b->bodies, b->body_offsets, starts, body_of, n, want_timestamps ? 1 : 0, (int32_t)ll,
-                    ctx->d_label, scratch_values, want_timestamps ? scratch_ts : nullptr, segments};
+                    {}, scratch_values, want_timestamps ? scratch_ts : nullptr, segments};
+    memcpy(A.label_w, label, ll);
     hipLaunchKernelGGL(json::k_json_segments, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
     KRR_HIP(ctx, hipGetLastError());
     return KRR_OK;

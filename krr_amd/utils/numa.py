@@ -95,4 +95,54 @@ def bind_local(device: int = 0, one_per_core: bool = False) -> Optional[set]:
     return cpus
 
 
-__all__ = ["bind_local", "gpu_local_cpus", "gpu_numa_node"]
+def page_nodes(addr: int, nbytes: int, samples: int = 64) -> Optional[dict]:
+    """{NUMA node: pages} over ``samples`` pages spread across [addr, addr + nbytes) (the
+    move_pages query form: no page moves), or None where the kernel does not say.  Where a
+    page-locked staging buffer landed decides whether the H2D DMA and the staging threads
+    cross the socket link."""
+    import ctypes
+    import platform
+
+    if nbytes <= 0 or platform.machine() != "x86_64":
+        return None
+    page = os.sysconf("SC_PAGE_SIZE")
+    first = addr // page * page
+    n = max(1, min(samples, nbytes // page))
+    step = max(page, (nbytes // n) // page * page)
+    pages = (ctypes.c_void_p * n)(*[first + i * step for i in range(n)])
+    status = (ctypes.c_int * n)()
+    libc = ctypes.CDLL(None, use_errno=True)
+    SYS_move_pages = 279
+    if libc.syscall(SYS_move_pages, 0, ctypes.c_ulong(n), pages, None, status, 0) != 0:
+        return None
+    out: dict = {}
+    for s in status:
+        out[int(s)] = out.get(int(s), 0) + 1  # a negative entry: -errno (e.g. -14 not mapped)
+    return out
+
+
+def mapping_info(addr: int, nbytes: int = 1) -> Optional[dict]:
+    """The /proc/self/smaps entries overlapping [addr, addr + nbytes), summed: Size, Rss and
+    how much is backed by transparent huge pages (kB), and the mappings' count, or None.  A
+    DMA source on 4-KiB pages costs the IOMMU one translation per 4 KiB; on 2-MiB pages, one per
+    2 MiB."""
+    keys = ("Size:", "Rss:", "AnonHugePages:", "Locked:")
+    out: dict = {}
+    try:
+        with open("/proc/self/smaps") as fh:
+            take = False
+            for line in fh:
+                head = line.split(None, 1)[0]
+                if not head.endswith(":"):
+                    lo, hi = (int(x, 16) for x in head.split("-"))
+                    take = lo < addr + max(nbytes, 1) and hi > addr
+                    if take:
+                        out["mappings"] = out.get("mappings", 0) + 1
+                elif take and head in keys:
+                    out[head[:-1]] = out.get(head[:-1], 0) + int(line.split()[1])
+    except (OSError, ValueError):
+        return None
+    return out or None
+
+
+__all__ = ["bind_local", "gpu_local_cpus", "gpu_numa_node", "mapping_info", "page_nodes"]

@@ -52,30 +52,33 @@ def main():
 
     g_cpu, g_mem = grouped(cpu_vals, 0), grouped(mem_vals, 7)
     print(f"{len(plan.groups)} bodies per resource, {sum(map(len, g_cpu)) / 1e9:.2f} GB CPU JSON", flush=True)
-    packer = default_packer(0)
-    packer.threads = threads
-    want = [(plan.pack(g_cpu).values, plan.pack(g_mem).values)]
-    variants = ["chunk", "end", "hybrid", "chunk_after_hybrid"]
-    times = {v: [] for v in variants}
-    phases = {}
-    for r in range(args.rounds + 1):
-        for v in variants:
-            packer.grouped_route = "end" if v == "end" else "chunk"
+    from krr_amd.core.device_pack import DevicePacker
+
+    base = default_packer(0)
+    want = (plan.pack(g_cpu).values, plan.pack(g_mem).values)
+    # the packer's streams (copy stream at construction, 3 parse streams at the first grouped
+    # call) come from torch's stream pool in order: k dummy streams first shift which hardware
+    # queues (GPU_MAX_HW_QUEUES) they land on
+    res = {}
+    variants = [(2, 256), (1, 256), (2, 512), (1, 512), (4, 256)]
+    for ppt, mb in variants:
+        packer = DevicePacker(base.ctx, threads=threads, chunk_bytes=mb << 20)
+        packer.pieces_per_thread = ppt
+        out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
+        torch.cuda.synchronize()
+        assert all(np.array_equal(o.series.values.cpu().numpy(), w) for o, w in zip(out, want))
+        ts = []
+        for r in range(args.rounds):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)], hybrid=v == "hybrid")
+            packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
             torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            if r == 0:
-                got = (out[0].series.values.cpu().numpy(), out[1].series.values.cpu().numpy())
-                assert all(np.array_equal(a, b) for a, b in zip(got, want[0])), v
-                continue
-            times[v].append(dt)
-            phases[v] = packer.last_grouped_phases
-        print(f"round {r} done", flush=True)
-    for v in variants:
-        print(f"{v}: median {np.median(times[v]) * 1e3:.2f} ms  runs {[round(t * 1e3, 2) for t in sorted(times[v])]}")
-        print(f"   phases {phases[v]}")
+            ts.append(time.perf_counter() - t0)
+        print(f"pieces/thread {ppt} chunk {mb} MiB: median {np.median(ts) * 1e3:.2f} ms "
+              f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} pieces {packer.last_upload.get('pieces')}", flush=True)
+        print(f"   phases {packer.last_grouped_phases}", flush=True)
+        packer.release()
+        del packer
 
 
 if __name__ == "__main__":

@@ -237,9 +237,19 @@ def _recompact(b: bytes) -> bytes:
     return json.dumps(json.loads(b), separators=(",", ":")).encode()
 
 
+@pytest.fixture(params=["chunk", "end"])
+def route_mode(request, packer):
+    """Both routings: chunk by chunk (segments written into page-locked host memory by the
+    parse kernel) and once after the last parse (one device-to-host copy)."""
+    was = packer.grouped_route
+    packer.grouped_route = request.param
+    yield request.param
+    packer.grouped_route = was
+
+
 @pytest.mark.parametrize("max_chars", [6000, 40, 1])
 @pytest.mark.parametrize("resource", ["cpu", "memory"])
-def test_grouped_bodies_on_device_equal_host_plan(packer, resource, max_chars):
+def test_grouped_bodies_on_device_equal_host_plan(packer, resource, max_chars, route_mode):
     """tests/test_fleet_query.py's fleet (regex-metacharacter pod names, restarts summed per
     pod, decoy series, shuffled series order, duplicated and ghost pods): the device parse
     routed by pod label gives plan.pack's CSR, timestamps and pod counts bit for bit."""
@@ -321,7 +331,7 @@ def test_pack_many_equals_separate(packer):
     _same(b, mem_bad)
 
 
-def test_grouped_many_and_small_chunks(packer):
+def test_grouped_many_and_small_chunks(packer, route_mode):
     """CPU and memory grouped bodies through one pipeline, with 1-MiB chunks: candidates
     near chunk ends are searched with the next chunk (the 16-byte carry)."""
     from test_fleet_query import make_fleet
@@ -453,7 +463,7 @@ def test_grouped_hybrid_equals_host_plan(packer, share):
         assert str(e_y.value) == str(e_h.value)
 
 
-def test_grouped_large_bodies_in_pieces_and_hybrid(packer):
+def test_grouped_large_bodies_in_pieces_and_hybrid(packer, route_mode):
     """~2.5 MB grouped bodies staged in pieces cut inside the bodies (`"],[`), parsed one chunk
     behind the search on the parse streams, with and without the host share: plan.pack's CSR."""
     from krr_amd.core.device_pack import DevicePacker
