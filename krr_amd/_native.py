@@ -138,7 +138,9 @@ def bind_index_table(params: KrrPercentileParams, max_n: Optional[int], device: 
     if rule is None or params.k_table or params.mode == KRR_PCT_LINEAR:
         return params
     if max_n is None:
-        if not rule.needs_table(1 << 62):
+        # unknown counts: bounded by what a device holds (2^40 float64 = 8 TiB, past any HBM);
+        # the int default's float rule is exact to 2^46 and a <= 15-digit Decimal's to >= 10^13
+        if not rule.needs_table(1 << 40):
             return params
         raise ValueError(f"cpu_percentile {rule.percentile!r} needs the reference's index table here: "
                          "pass the largest present count (max_n)")

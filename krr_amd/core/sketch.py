@@ -150,7 +150,7 @@ def _needs_table(params) -> bool:
     Only then do the queries below size one from their merged counts (a synchronisation)."""
     rule = getattr(params, "rule", None)
     return (rule is not None and params.mode != _native.KRR_PCT_LINEAR and not params.k_table
-            and rule.needs_table(1 << 62))
+            and rule.needs_table(1 << 40))  # counts past 2^40 cannot be held (see _native.bind_index_table)
 
 
 def query(ctx: _native.Context, merged: dict, cfg: SketchConfig, params: _native.KrrPercentileParams,
