@@ -273,3 +273,50 @@ def test_plan_for_settings_counts_points():
     # without settings the plan still bounds samples, at the reference's default settings
     default = FleetQueryPlan(big, max_query_chars=10**9)
     assert default.points_per_series == 1345 and max(len(g.pods) for g in default.groups) == max(pods_per_group)
+
+
+@pytest.mark.parametrize("max_chars", [6000, 40])
+def test_group_sorted_slots_are_contiguous_per_group(max_chars):
+    """The device packer routes a chunk of whole bodies over one range of this order."""
+    objects, _ = make_fleet()
+    plan = FleetQueryPlan(objects, max_query_chars=max_chars)
+    order, sgroup, blob, offs, gstart = plan.group_sorted_slots()
+    assert sorted(order.tolist()) == list(range(plan.n_slots))
+    np.testing.assert_array_equal(sgroup, plan.slot_group[order])
+    assert np.all(np.diff(sgroup) >= 0)
+    for g in range(len(plan.groups)):
+        idx = order[gstart[g]:gstart[g + 1]]
+        np.testing.assert_array_equal(idx, np.flatnonzero(plan.slot_group == g))  # stable: plan order
+    assert gstart[0] == 0 and gstart[-1] == plan.n_slots
+    names = [blob[offs[i]:offs[i + 1]].decode() for i in range(plan.n_slots)]
+    assert names == [plan.slot_pods[i] for i in order.tolist()]
+    assert plan.group_sorted_slots() is plan.group_sorted_slots()  # cached
+
+
+@pytest.mark.parametrize("resource", list(ResourceType))
+def test_pack_group_slots_equals_the_plan_pack(resource):
+    """The hybrid grouped parser's host side: groups [g0, g1) alone, one segment per slot, give
+    each slot the series plan.pack routes to it (values and per-slot counts)."""
+    objects, prom = make_fleet(seed=5)
+    plan = FleetQueryPlan(objects, max_query_chars=40)
+    bodies = [prom.query_range(q) for q in plan.queries(resource)]
+    full, counts = plan.pack(bodies, return_pod_counts=True)
+    ng = len(plan.groups)
+    # the full plan's per-slot values: walk objects' segments in slot order (kept slots only)
+    per_slot, pos = {}, 0
+    for s in range(plan.n_slots):
+        if counts[s] > 0:
+            per_slot[s] = full.values[pos:pos + counts[s]]
+            pos += counts[s]
+    for g0, g1 in ((0, ng), (ng // 2, ng), (ng - 1, ng), (0, 1)):
+        idx, values, offsets, cnt = plan.pack_group_slots(bodies[g0:g1], g0, g1)
+        np.testing.assert_array_equal(idx, np.flatnonzero((plan.slot_group >= g0) & (plan.slot_group < g1)))
+        np.testing.assert_array_equal(cnt, counts[idx])
+        for j, s in enumerate(idx.tolist()):
+            got = values[offsets[j]:offsets[j + 1]]
+            if counts[s] > 0:
+                assert got.tobytes() == per_slot[s].tobytes()
+            else:
+                assert got.size == 0
+    with pytest.raises(ValueError):
+        plan.pack_group_slots(bodies[:1], 0, 2)
