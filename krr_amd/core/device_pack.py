@@ -72,6 +72,9 @@ class DevicePacker:
         self._stage = None
         self._last = None  # (device bodies, staging buffer) of the last batch
         self._copy_stream = torch.cuda.Stream(device=self.device)
+        # a second copy stream: the grouped pieces (~10 MB each) alternate between the two, so one
+        # copy's setup overlaps the other's transfer (54 -> 57 GB/s for 10-MiB copies on the box)
+        self._copy_stream2 = torch.cuda.Stream(device=self.device)
         self._lock = threading.Lock()
 
     def release(self) -> None:
@@ -308,8 +311,9 @@ class DevicePacker:
         tmp_v = torch.empty(total // 8 + 1 + int(extra_slots), dtype=torch.float64, device=dev)
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
         host = load_library()
-        cs = self._copy_stream
+        cs, cs2 = self._copy_stream, self._copy_stream2
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        cs2.wait_stream(st)
         d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
         o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
         piece_dev, piece_shift = [], []
@@ -347,11 +351,16 @@ class DevicePacker:
             nby = np.empty(k + 1, dtype=np.int64)
             dst[:k], src[:k], nby[:k] = d_base + pd, s_base + p_start[:k], p_out[:k]
             dst[k], src[k], nby[k] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
-            self.ctx.copy_h2d_batch(dst, src, nby, stream=cs)
-            with torch.cuda.stream(cs):
-                ev = torch.cuda.Event()
-                ev.record(cs)
-            st.wait_event(ev)
+            # even pieces (and the offsets) on one copy stream, odd pieces on the other
+            ev_idx = np.concatenate([np.arange(0, k, 2), [k]])
+            self.ctx.copy_h2d_batch(dst[ev_idx], src[ev_idx], nby[ev_idx], stream=cs)
+            if k > 1:
+                self.ctx.copy_h2d_batch(dst[1:k:2], src[1:k:2], nby[1:k:2], stream=cs2)
+            for c in (cs, cs2):
+                with torch.cuda.stream(c):
+                    ev = torch.cuda.Event()
+                    ev.record(c)
+                st.wait_event(ev)
             launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
             a = b
         self._last = (d_bodies, stage, new_offs)

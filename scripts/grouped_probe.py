@@ -59,8 +59,40 @@ def main():
     # the packer's streams (copy stream at construction, 3 parse streams at the first grouped
     # call) come from torch's stream pool in order: k dummy streams first shift which hardware
     # queues (GPU_MAX_HW_QUEUES) they land on
+    # the link alone: the bench's pinned->HBM rate with copies of several sizes, one stream
+    n = 1 << 28
+    src = torch.empty(n * 10, dtype=torch.uint8, pin_memory=True)
+    src.fill_(1)
+    dst = torch.empty(n * 10, dtype=torch.uint8, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    for piece in (4 << 20, 10 << 20, 32 << 20, 128 << 20):
+        for ns in (1, 2, 4):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i, a in enumerate(range(0, src.numel(), piece)):
+                with torch.cuda.stream(streams[i % ns]):
+                    dst[a:a + piece].copy_(src[a:a + piece], non_blocking=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"H2D {piece >> 20} MiB pieces on {ns} streams: {src.numel() / dt / 1e9:.1f} GB/s", flush=True)
+    # the library's batch call (one hipMemcpyAsync per piece, as the packer issues them)
+    from krr_amd.core.device_pack import default_packer as _dp
+
+    ctx = _dp(0).ctx
+    for piece in (10 << 20, 128 << 20):
+        k = src.numel() // piece
+        d = np.array([dst.data_ptr() + i * piece for i in range(k)], dtype=np.int64)
+        s_ = np.array([src.data_ptr() + i * piece for i in range(k)], dtype=np.int64)
+        b = np.full(k, piece, dtype=np.int64)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.copy_h2d_batch(d, s_, b, stream=streams[0])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"copy_h2d_batch {piece >> 20} MiB pieces: {k * piece / dt / 1e9:.1f} GB/s", flush=True)
+    del src, dst
     res = {}
-    variants = [(2, 256), (1, 256), (2, 512), (1, 512), (4, 256)]
+    variants = [(1, 256)]
     for ppt, mb in variants:
         packer = DevicePacker(base.ctx, threads=threads, chunk_bytes=mb << 20)
         packer.pieces_per_thread = ppt
