@@ -36,6 +36,20 @@ from krr_amd.core.packing import PackedSeries
 from krr_amd.core.prom_native import KRR_PACK_OK, PrometheusResponseError, load_library, pack_query_range_bodies
 
 
+def default_threads() -> int:
+    """Host threads when the caller gives none: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS when set (a GPU box leases 16 CPUs per GPU but its affinity mask shows the
+    node's) — what the native pool uses for threads = 0 (krr_pack.cpp default_threads)."""
+    import os
+
+    n = len(os.sched_getaffinity(0)) or 1
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    return min(n, omp) if omp > 0 else n
+
+
 @dataclass
 class DevicePacked:
     series: PackedSeries            # values / offsets: torch tensors in HBM (via == "device") or numpy (host)
@@ -82,6 +96,7 @@ class DevicePacker:
         with self._lock:
             self._stage = None
             self._last = None
+            self._seg_rows = None
 
     def _live_layout(self):
         """(device body offsets, piece device starts, piece staging shifts) of the batch being
@@ -226,7 +241,7 @@ class DevicePacker:
 
         dev = self.device
         nb = len(lens)
-        T = self.threads or len(os.sched_getaffinity(0))
+        T = self.threads or default_threads()
         max_runs = max(1, self.strip_runs_per_thread * T)
         new_lens = np.empty(nb, dtype=np.int64)
         runs = np.empty(max_runs + 1, dtype=np.int64)
@@ -298,7 +313,7 @@ class DevicePacker:
 
         dev = self.device
         nb = len(lens)
-        T = self.threads or len(os.sched_getaffinity(0))
+        T = self.threads or default_threads()
         max_pieces = max(2, int(self.pieces_per_thread * T))
         cap = 2 * nb + max_pieces
         new_lens = np.empty(nb, dtype=np.int64)
@@ -445,7 +460,7 @@ class DevicePacker:
             split = len(flat) - min(max(k_host, 1), len(flat) - 1)
         host_res: dict = {}
         host_thread = None
-        T_all = self.threads or len(os.sched_getaffinity(0))
+        T_all = self.threads or default_threads()
         t_host = max(1, int(self.grouped_host_threads or T_all // 4))
         if split < len(flat):
             from krr_amd.core.runner import _pinned_alloc_or_none
@@ -460,9 +475,10 @@ class DevicePacker:
                         if lo < hi:
                             host_res[r] = plan.pack_group_slots(flat[lo:hi], lo - body0[r], hi - body0[r],
                                                                 threads=t_host, alloc=alloc)
-                except PrometheusResponseError as e:
+                except BaseException as e:  # noqa: BLE001 — handed to the caller after the join
                     host_res["error"] = e
-                host_res["s"] = time.perf_counter() - t0
+                finally:
+                    host_res["s"] = time.perf_counter() - t0
 
             host_thread = threading.Thread(target=host_part, name="krr-grouped-host", daemon=True)
             host_thread.start()
@@ -616,7 +632,10 @@ class DevicePacker:
         if host_thread is not None:
             host_thread.join()
         clock.append(time.perf_counter())
-        if parsed[1] or "error" in host_res:  # candidates overflow / a body the host part rejects
+        err = host_res.get("error")
+        if err is not None and not isinstance(err, PrometheusResponseError):
+            raise err  # not a body the host packer rejects: the host part itself failed
+        if parsed[1] or err is not None:  # candidates overflow / a body the host part rejects
             return [host_fallback(r, body0[r + 1] - body0[r]) for r in range(len(items))]
         if host_thread is not None:
             # share toward r_host / (r_host + r_device) (bytes per second of each side)
