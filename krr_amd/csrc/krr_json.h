@@ -47,6 +47,16 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 // positions are >= 0 (INT64_MAX: none)
 __device__ __forceinline__ int64_t wave_min_pos(int64_t x) { return (int64_t)wave_min_u64((uint64_t)x); }
 
+// The json kernels run one wave per workgroup (__launch_bounds__(64)): a wave's LDS accesses
+// complete in order, so lanes only need the compiler to keep the stores before the loads.  A
+// workgroup barrier's release fence would also wait for every outstanding global load — the
+// prefetched next block included.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Element bytes come from the wave's LDS copy of [blk, blk + kStageBytes) — an element
 // starting in the block's first 2 KiB and shorter than 2 KiB lies inside it — and from
 // global memory past it (long value strings only).
@@ -71,22 +81,26 @@ __device__ bool values_array(const char* const buf, bool want_ts, const char* vs
     const int64_t lo_abs = vs - buf, hi_abs = e - buf;
     int64_t blk = lo_abs & ~(int64_t)(kLaneBytes - 1);
     int64_t cnt = 0;
+    // lane l's 32 bytes of the current block (x) and of the next one (y) stay in registers from
+    // one block to the next: each block is read from memory once, and the block after next (z)
+    // is requested before the current one is parsed, so its load overlaps the parse (a grouped
+    // chunk's series give one wave each — too few waves per SIMD to hide a load otherwise)
+    auto load32 = [&](int64_t at, v4u32& a, v4u32& b) {
+        if (at < hi_abs) {
+            const v4u32* q = reinterpret_cast<const v4u32*>(buf + at);
+            a = q[0];
+            b = q[1];
+        }
+    };
+    const v4u32 zero = {0, 0, 0, 0};
+    v4u32 x0 = zero, x1 = zero, y0 = zero, y1 = zero;
+    load32(blk + (int64_t)lane * kLaneBytes, x0, x1);
+    load32(blk + (int64_t)lane * kLaneBytes + kBlockBytes, y0, y1);
     for (; blk < hi_abs; blk += kBlockBytes) {
         // stage [blk, blk + 4 KiB): lane l's 32 bytes at 32 l and at 2 KiB + 32 l
         const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
         uint32_t mine_w[8];
         {
-            v4u32 x0 = {0, 0, 0, 0}, x1 = x0, y0 = x0, y1 = x0;
-            if (r0 < hi_abs) {
-                const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0);
-                x0 = q[0];
-                x1 = q[1];
-            }
-            if (r0 + kBlockBytes < hi_abs) {
-                const v4u32* q = reinterpret_cast<const v4u32*>(buf + r0 + kBlockBytes);
-                y0 = q[0];
-                y1 = q[1];
-            }
             v4u32* d = reinterpret_cast<v4u32*>(lds + lane * kLaneBytes);
             d[0] = x0;
             d[1] = x1;
@@ -96,7 +110,9 @@ __device__ bool values_array(const char* const buf, bool want_ts, const char* vs
             mine_w[0] = x0[0], mine_w[1] = x0[1], mine_w[2] = x0[2], mine_w[3] = x0[3];
             mine_w[4] = x1[0], mine_w[5] = x1[1], mine_w[6] = x1[2], mine_w[7] = x1[3];
         }
-        __syncthreads();
+        v4u32 z0 = zero, z1 = zero;
+        load32(r0 + 2 * kBlockBytes, z0, z1);
+        wave_lds_sync();
         // '[' in this lane's 32 bytes that lie inside the array's span
         uint32_t starts = 0;
 #pragma unroll
@@ -159,7 +175,8 @@ __device__ bool values_array(const char* const buf, bool want_ts, const char* vs
             *count = cnt;
             return true;
         }
-        __syncthreads();  // every lane is done with the staged bytes
+        wave_lds_sync();  // every lane is done with the staged bytes
+        x0 = y0, x1 = y1, y0 = z0, y1 = z1;
     }
     return false;  // no closing ']'
 }
