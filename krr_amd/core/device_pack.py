@@ -488,6 +488,8 @@ class DevicePacker:
         cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
+        if self.grouped_route not in ("chunk", "end"):
+            raise ValueError(f"grouped_route must be 'chunk' or 'end', got {self.grouped_route!r}")
         per_chunk = self.grouped_route == "chunk"
         segs = None if per_chunk else torch.empty((cap, 7), dtype=torch.int64, device=dev)
         seen = [0]  # positions below this were searched
