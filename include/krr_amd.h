@@ -558,6 +558,17 @@ int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t begin, 
 int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
                             int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
                             double* scratch_ts, int64_t* segments, void* stream);
+/* krr_json_parse_segments with each series' values array parsed by several waves (round 6):
+ * the series' wave finds the array's end and cuts it into 16-KiB parts, then one wave per part
+ * parses its elements (same segments, scratch values and validation).  workspace: device
+ * int64 [workspace_words] = 1 (part counter) + n (array ends) + 6 per part; a series whose
+ * parts find no room is reported not ok (its body goes to the host packer), so
+ * (bytes of the candidates' bodies) / 16384 + 2 n parts always suffice.  Replaces nothing in
+ * the reference: the host-side equivalent is krr_pack_parse_grouped (include/krr_pack.h). */
+int krr_json_parse_segments_split(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts,
+                                  const int64_t* body_of, int64_t n, const char* label, int32_t want_timestamps,
+                                  double* scratch_values, double* scratch_ts, int64_t* segments, int64_t* workspace,
+                                  int64_t workspace_words, void* stream);
 /* values[dst[j] ..) = scratch_values[src[j] ..), count[j] values (count < 0: none); the same
  * for timestamps when both pointers are given. */
 int krr_json_gather(krr_ctx* ctx, int64_t n_items, const int64_t* src, const int64_t* count, const int64_t* dst,

@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "krr_copy_h2d_batch",
     "krr_json_find_series",
     "krr_json_parse_segments",
+    "krr_json_parse_segments_split",
     "krr_json_gather",
     "krr_create",
     "krr_destroy",
@@ -356,6 +357,9 @@ def load_library(require_torch: bool = True) -> ctypes.CDLL:
         lib.krr_json_find_series.restype = ctypes.c_int
         lib.krr_json_parse_segments.argtypes = [vp, jb, vp, vp, i64, ctypes.c_char_p, i32, vp, vp, vp, vp]
         lib.krr_json_parse_segments.restype = ctypes.c_int
+        lib.krr_json_parse_segments_split.argtypes = [vp, jb, vp, vp, i64, ctypes.c_char_p, i32, vp, vp, vp, vp, i64,
+                                                      vp]
+        lib.krr_json_parse_segments_split.restype = ctypes.c_int
         lib.krr_json_gather.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.krr_json_gather.restype = ctypes.c_int
         if lib.krr_abi_version() != 3:
@@ -814,7 +818,9 @@ class Context:
                                                    self._stream(stream)))
 
     def json_parse_segments(self, jb: KrrJsonBodies, starts, body_of, label: str, want_timestamps: bool,
-                            scratch_values, scratch_ts, segments, stream=None) -> None:
+                            scratch_values, scratch_ts, segments, stream=None, workspace=None) -> None:
+        """``workspace``: an int64 device tensor for the split values parse
+        (krr_json_parse_segments_split: 1 + n + 6 per 16-KiB part), or None (one wave per series)."""
         n = starts.numel()
         _check_tensor(starts, "int64", n)
         _check_tensor(body_of, "int64", n)
@@ -822,10 +828,15 @@ class Context:
         _check_tensor(scratch_values, "float64", jb.total_bytes // 8 + 1)
         if want_timestamps:
             _check_tensor(scratch_ts, "float64", jb.total_bytes // 8 + 1)
-        self._check(self._lib.krr_json_parse_segments(
-            self._h, ctypes.byref(jb), starts.data_ptr(), body_of.data_ptr(), n, label.encode(),
-            int(bool(want_timestamps)), scratch_values.data_ptr(), scratch_ts.data_ptr() if want_timestamps else None,
-            segments.data_ptr(), self._stream(stream)))
+        args = (self._h, ctypes.byref(jb), starts.data_ptr(), body_of.data_ptr(), n, label.encode(),
+                int(bool(want_timestamps)), scratch_values.data_ptr(),
+                scratch_ts.data_ptr() if want_timestamps else None, segments.data_ptr())
+        if workspace is None:
+            self._check(self._lib.krr_json_parse_segments(*args, self._stream(stream)))
+            return
+        _check_tensor(workspace, "int64", n + 1 + 6)
+        self._check(self._lib.krr_json_parse_segments_split(*args, workspace.data_ptr(), workspace.numel(),
+                                                            self._stream(stream)))
 
     def json_gather(self, src, count, dst, scratch_values, scratch_ts, values, timestamps=None, stream=None) -> None:
         n = src.numel()

@@ -413,6 +413,9 @@ class DevicePacker:
 
     grouped_share = 0.06          # the hybrid grouped parser's host share of the bytes (adapted)
     grouped_host_threads = 0      # 0: a quarter of the threads
+    # a grouped chunk's values arrays parsed in 16-KiB parts, one wave each
+    # (krr_json_parse_segments_split), instead of one wave per series
+    grouped_split_parse = os.environ.get("KRR_GROUPED_SPLIT", "1") != "0"
     # "chunk": segments to the host and routed per chunk; "end": once, after the last parse
     grouped_route = os.environ.get("KRR_GROUPED_ROUTE", "chunk")
     _EMPTY_BODY = b'{"status":"success","data":{"resultType":"matrix","result":[]}}'
@@ -570,6 +573,14 @@ class DevicePacker:
             ps.wait_event(ev)
             rows = self._host_rows(n)[lo:n] if per_chunk else None
             with torch.cuda.stream(ps):
+                ws = None
+                if n > lo and self.grouped_split_parse:
+                    # the split values parse's workspace: 1 + n + 6 words per 16-KiB part, parts
+                    # <= the chunk's bytes / 16 KiB + 2 per series (include/krr_amd.h)
+                    no_ = self._live_layout()[0]
+                    span = int(no_[b_end]) - int(no_[max(a - 1, 0)])
+                    ws = torch.empty(1 + (n - lo) + 6 * (span // 16384 + 2 * (n - lo) + 8), dtype=torch.int64,
+                                     device=dev)
                 if n > lo:
                     starts = torch.sort(cand[lo:n]).values
                     # the chunk's bodies' device offsets are in HBM (copied with the chunk)
@@ -578,7 +589,7 @@ class DevicePacker:
                     # memory (no device-to-host DMA: on the copy engines it queued behind, and
                     # slowed, the chunks' host-to-device copies)
                     self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t,
-                                                 rows if per_chunk else segs[lo:n], stream=ps)
+                                                 rows if per_chunk else segs[lo:n], stream=ps, workspace=ws)
                 if per_chunk:
                     evp = torch.cuda.Event()
                     evp.record(ps)

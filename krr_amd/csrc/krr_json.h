@@ -335,7 +335,195 @@ struct SegArgs {
     double* tmp_v;
     double* tmp_t;
     int64_t* seg;              // [n][kSegWords]
+    // split values parse (null: each series' values parsed by its own wave, values_array):
+    // phase 1 (here) finds each values array's end and cuts it into parts, phase 2
+    // (k_json_value_parts) parses the parts, one wave each
+    int64_t* parts;                 // [parts_cap][kPartWords]
+    int64_t parts_cap;
+    unsigned long long* n_parts;    // device counter (zeroed by the caller)
+    int64_t* series_vend;           // [n]: one past each split array's ']'
 };
+
+// ---- split values parse (round 6): a grouped chunk holds a few hundred series of ~10^4
+// samples, one wave each — too few waves to hide a wave's serial element parse, so the
+// last chunk's parse was the pipeline's tail.  Phase 1 scans each series' values array for
+// its end (the last element's ']' followed by the array's ']') and counts the element
+// starts ('[') per kPartBytes part; phase 2 parses every part with a wave of its own and
+// writes its values at the series' slot + the elements before the part — the same slots,
+// values and validation values_array gives (every element parsed by sample_element; the
+// array's last element is the one followed by ']', at the end phase 1 found).
+constexpr int kPartBytes = 8 * kBlockBytes;  // 16 KiB of a values array per phase-2 wave
+constexpr int kPartWords = 6;                // series, first start, starts end, vend, slot, count
+
+// Phase 1 scan over [vs, e) (vs = the first element's '['): *vend = one past the first "]]"
+// at or after vs; per part [blk0 + k kPartBytes, +kPartBytes) the '[' count below the end.
+// Returns the number of parts (lane-uniform) or -1: no "]]" below e (the caller falls back
+// to values_array, which also accepts whitespace between the two brackets).  emit(k, lo,
+// hi, base, count) runs on every lane with uniform arguments.
+template <class Emit>
+__device__ int64_t values_scan(const char* const buf, const char* vs, const char* e, int lane, int64_t* vend_out,
+                               Emit emit) {
+    const int64_t lo_abs = vs - buf, hi_abs = e - buf;
+    const int64_t blk0 = lo_abs & ~(int64_t)(kLaneBytes - 1);
+    auto load32 = [&](int64_t at, v4u32& a, v4u32& b) {
+        if (at < hi_abs) {
+            const v4u32* q = reinterpret_cast<const v4u32*>(buf + at);
+            a = q[0];
+            b = q[1];
+        }
+    };
+    const v4u32 zero = {0, 0, 0, 0};
+    v4u32 x0 = zero, x1 = zero;
+    load32(blk0 + (int64_t)lane * kLaneBytes, x0, x1);
+    bool prev_rb = false;      // the byte before this block is ']' (lane 63's last byte)
+    int64_t base = 0, part_cnt = 0, part = 0;
+    for (int64_t blk = blk0; blk < hi_abs; blk += kBlockBytes) {
+        const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
+        v4u32 y0 = zero, y1 = zero;
+        load32(r0 + kBlockBytes, y0, y1);  // the next block, requested before this one is scanned
+        uint32_t w[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        uint32_t lb = 0, rb = 0;
+#pragma unroll
+        for (int k = 0; k < kLaneBytes; ++k) {
+            const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFF;
+            lb |= (c == '[' ? 1u : 0u) << k;
+            rb |= (c == ']' ? 1u : 0u) << k;
+        }
+        // bytes outside [lo_abs, hi_abs)
+        uint32_t valid = 0xFFFFFFFFu;
+        if (r0 < lo_abs) {
+            const int64_t d = lo_abs - r0;
+            valid = d >= kLaneBytes ? 0u : (valid >> d) << d;
+        }
+        if (r0 + kLaneBytes > hi_abs) {
+            const int64_t d = hi_abs - r0;
+            valid = d <= 0 ? 0u : valid & (0xFFFFFFFFu >> (kLaneBytes - d));
+        }
+        lb &= valid;
+        rb &= valid;
+        // "]]": a ']' whose next byte is ']' (the next lane's first byte for bit 31); the
+        // previous block's last ']' pairs with this block's first byte
+        const uint32_t next_first = (uint32_t)__shfl_down((int)(rb & 1u), 1);
+        const uint32_t nxt = (rb >> 1) | ((lane < kWave - 1 ? next_first : 0u) << 31);
+        uint32_t pair = rb & nxt;
+        int64_t my_end = INT64_MAX;  // position of the first ']' of the pair
+        if (pair) my_end = r0 + __builtin_ctz(pair);
+        if (lane == 0 && prev_rb && (rb & 1u)) my_end = r0 - 1;
+        const int64_t end = wave_min_pos(my_end);
+        prev_rb = (lane_bcast32(rb, kWave - 1) >> 31) & 1u;
+        // element starts below the end
+        uint32_t mine = lb;
+        if (end != INT64_MAX) {
+            const int64_t d = end - r0;
+            mine = d <= 0 ? 0u : (d >= kLaneBytes ? mine : mine & (0xFFFFFFFFu >> (kLaneBytes - d)));
+        }
+        part_cnt += (int64_t)wave_sum_u32((uint32_t)__builtin_popcount(mine));
+        const bool part_full = blk + kBlockBytes >= blk0 + (part + 1) * (int64_t)kPartBytes;
+        if (end != INT64_MAX) {
+            *vend_out = end + 2;
+            const int64_t plo = part == 0 ? lo_abs : blk0 + part * (int64_t)kPartBytes;
+            emit(part, plo, end + 2, base, part_cnt);
+            return part + 1;
+        }
+        if (part_full) {
+            const int64_t plo = part == 0 ? lo_abs : blk0 + part * (int64_t)kPartBytes;
+            emit(part, plo, blk0 + (part + 1) * (int64_t)kPartBytes, base, part_cnt);
+            base += part_cnt;
+            part_cnt = 0;
+            ++part;
+        }
+        x0 = y0, x1 = y1;
+    }
+    return -1;
+}
+
+// Phase 2: the elements starting in [plo, phi) of one values array ending at vend (one past
+// its ']'): parsed, checked (an element followed by ']' must end the array at vend, every
+// other one must be followed by the next element before vend) and written at tv[0 ..) in
+// order; true when all parse and their number is `expect`.
+__device__ bool values_part(const char* const buf, bool want_ts, int64_t plo, int64_t phi, int64_t vend,
+                            double* tv, double* tt, int64_t expect, int lane, unsigned char* lds) {
+    const int64_t hi_abs = vend;  // nothing an element reads lies past the array
+    const char* const e = buf + vend;
+    auto load32 = [&](int64_t at, v4u32& a, v4u32& b) {
+        if (at < hi_abs) {
+            const v4u32* q = reinterpret_cast<const v4u32*>(buf + at);
+            a = q[0];
+            b = q[1];
+        }
+    };
+    const v4u32 zero = {0, 0, 0, 0};
+    int64_t blk = plo & ~(int64_t)(kLaneBytes - 1);
+    v4u32 x0 = zero, x1 = zero, y0 = zero, y1 = zero;
+    load32(blk + (int64_t)lane * kLaneBytes, x0, x1);
+    load32(blk + (int64_t)lane * kLaneBytes + kBlockBytes, y0, y1);
+    int64_t cnt = 0;
+    bool bad = false;
+    for (; blk < phi; blk += kBlockBytes) {
+        const int64_t r0 = blk + (int64_t)lane * kLaneBytes;
+        uint32_t mine_w[8];
+        {
+            v4u32* d = reinterpret_cast<v4u32*>(lds + lane * kLaneBytes);
+            d[0] = x0;
+            d[1] = x1;
+            v4u32* d2 = reinterpret_cast<v4u32*>(lds + kBlockBytes + lane * kLaneBytes);
+            d2[0] = y0;
+            d2[1] = y1;
+            mine_w[0] = x0[0], mine_w[1] = x0[1], mine_w[2] = x0[2], mine_w[3] = x0[3];
+            mine_w[4] = x1[0], mine_w[5] = x1[1], mine_w[6] = x1[2], mine_w[7] = x1[3];
+        }
+        v4u32 z0 = zero, z1 = zero;
+        load32(r0 + 2 * kBlockBytes, z0, z1);
+        wave_lds_sync();
+        uint32_t starts = 0;
+#pragma unroll
+        for (int k = 0; k < kLaneBytes; ++k)
+            starts |= (((mine_w[k >> 2] >> (8 * (k & 3))) & 0xFF) == '[' ? 1u : 0u) << k;
+        if (r0 < plo) {
+            const int64_t d = plo - r0;
+            starts = d >= kLaneBytes ? 0u : (starts >> d) << d;
+        }
+        if (r0 + kLaneBytes > phi) {
+            const int64_t d = phi - r0;
+            starts = d <= 0 ? 0u : starts & (0xFFFFFFFFu >> (kLaneBytes - d));
+        }
+        double v[kMaxPerLane], t[kMaxPerLane];
+        int nok = 0;
+        bool lane_bad = false;
+        const StagedLoad ld{buf, lds, blk};
+        while (starts) {
+            const int k = __builtin_ctz(starts);
+            starts &= starts - 1;
+            double vv = 0.0, tt2 = 0.0;
+            const char* next = nullptr;
+            bool last = false;
+            if (nok == kMaxPerLane || !sample_element(buf + r0 + k, e, want_ts, &vv, &tt2, &next, &last, ld) ||
+                (last ? next != e : next >= e)) {
+                lane_bad = true;
+                continue;
+            }
+            v[nok] = vv;
+            t[nok] = tt2;
+            ++nok;
+        }
+        bad |= ballot(lane_bad) != 0;
+        const uint32_t incl = wave_scan32((uint32_t)nok, 0u, OpAdd32{});
+        const int64_t at = cnt + (int64_t)(incl - (uint32_t)nok);
+        if (!bad && cnt + (int64_t)lane_bcast32(incl, kWave - 1) <= expect) {
+#pragma unroll
+            for (int j = 0; j < kMaxPerLane; ++j) {
+                if (j < nok) {
+                    tv[at + j] = v[j];
+                    if (want_ts) tt[at + j] = t[j];
+                }
+            }
+        }
+        cnt += (int64_t)lane_bcast32(incl, kWave - 1);
+        wave_lds_sync();  // every lane is done with the staged bytes
+        x0 = y0, x1 = y1, y0 = z0, y1 = z1;
+    }
+    return !bad && cnt == expect;
+}
 
 __global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
@@ -378,8 +566,42 @@ __global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
                 vok = true;
                 vend = vs + 1;
             } else if (vs < e && *vs == '[') {
-                vok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (at >> 3),
-                                   A.tmp_t ? A.tmp_t + (at >> 3) : nullptr, lane, lds, &count, &vend);
+                int64_t np = -1;
+                if (A.parts) {
+                    // phase 1: the array's end and its parts (phase 2 parses them); a part that
+                    // finds no room in the workspace fails the series (its batch goes to the host)
+                    int64_t vend_abs = 0, total = 0;
+                    bool room = true;
+                    np = values_scan(A.bodies, vs, e, lane, &vend_abs,
+                                     [&](int64_t k, int64_t plo, int64_t phi, int64_t base, int64_t c) {
+                                         (void)k;
+                                         total = base + c;
+                                         if (lane == 0) {
+                                             const unsigned long long q = atomicAdd(A.n_parts, 1ull);
+                                             if ((int64_t)q < A.parts_cap) {
+                                                 int64_t* P = A.parts + (int64_t)q * kPartWords;
+                                                 P[0] = j;
+                                                 P[1] = plo;
+                                                 P[2] = phi;
+                                                 P[3] = 0;
+                                                 P[4] = (at >> 3) + base;
+                                                 P[5] = c;
+                                             } else {
+                                                 room = false;
+                                             }
+                                         }
+                                     });
+                    room = __builtin_amdgcn_readfirstlane(room ? 1 : 0) != 0;
+                    if (np >= 0 && lane == 0) A.series_vend[j] = vend_abs;
+                    if (np >= 0) {
+                        vok = room;
+                        count = total;
+                        vend = A.bodies + vend_abs;
+                    }
+                }
+                if (np < 0)
+                    vok = values_array(A.bodies, A.want_ts != 0, vs, e, A.tmp_v + (at >> 3),
+                                       A.tmp_t ? A.tmp_t + (at >> 3) : nullptr, lane, lds, &count, &vend);
             }
             if (!vok) break;
             if (lane == 0) W.values_done(vend, count);
@@ -393,6 +615,38 @@ __global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
             r[4] = ok ? (int64_t)((W.values_at - A.bodies) >> 3) : 0;
             r[5] = ok ? W.count : 0;
             r[6] = ok;
+        }
+    }
+}
+
+struct PartArgs {
+    const char* bodies;
+    const int64_t* parts;              // [*n_parts][kPartWords] (phase 1)
+    const unsigned long long* n_parts;
+    const int64_t* series_vend;        // phase 1's array ends, by series
+    int64_t parts_cap;
+    int32_t want_ts;
+    double* tmp_v;
+    double* tmp_t;
+    int64_t* seg;                      // a failed part clears its series' ok word
+};
+
+// Phase 2 of the split values parse: one part per wave (grid-stride over the parts phase 1
+// recorded; the array's end from phase 1's series_vend).
+__global__ __launch_bounds__(64) void k_json_value_parts(PartArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes];
+    const int lane = threadIdx.x;
+    const unsigned long long np_ = *A.n_parts;
+    const int64_t np = (int64_t)np_ < A.parts_cap ? (int64_t)np_ : A.parts_cap;
+    for (int64_t q = blockIdx.x; q < np; q += gridDim.x) {
+        const int64_t* P = A.parts + q * kPartWords;
+        const int64_t j = P[0], plo = P[1], phi = P[2], slot = P[4], c = P[5];
+        const int64_t vend = A.series_vend[j];
+        const bool ok = values_part(A.bodies, A.want_ts != 0, plo, phi, vend, A.tmp_v + slot,
+                                    A.tmp_t ? A.tmp_t + slot : nullptr, c, lane, lds);
+        if (!ok && lane == 0) {
+            A.seg[j * kSegWords + 1] = -1;
+            A.seg[j * kSegWords + 6] = 0;
         }
     }
 }

@@ -4458,9 +4458,10 @@ int krr_json_find_series(krr_ctx* ctx, const krr_json_bodies* b, int64_t begin, 
     return KRR_OK;
 }
 
-int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
-                            int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
-                            double* scratch_ts, int64_t* segments, void* stream) {
+static int json_segments_launch(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts,
+                                const int64_t* body_of, int64_t n, const char* label, int32_t want_timestamps,
+                                double* scratch_values, double* scratch_ts, int64_t* segments, int64_t* workspace,
+                                int64_t workspace_words, void* stream) {
     if (!ctx) return KRR_E_INVALID;
     if (!b || n < 0) return set_err(ctx, KRR_E_INVALID, "json: bad arguments%s", "");
     if (!label) return set_err(ctx, KRR_E_INVALID, "json: null label%s", "");
@@ -4470,16 +4471,55 @@ int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_
     if (!b->bodies || !b->body_offsets || !starts || !body_of || !scratch_values || !segments ||
         (want_timestamps && !scratch_ts))
         return set_err(ctx, KRR_E_INVALID, "json: null buffer%s", "");
+    int64_t parts_cap = 0;
+    if (workspace) {
+        parts_cap = (workspace_words - 1 - n) / json::kPartWords;
+        if (parts_cap < 1)
+            return set_err(ctx, KRR_E_INVALID, "json: workspace of %s%lld words holds no part", "",
+                           (long long)workspace_words);
+    }
     DeviceGuard g(ctx->device);
     if (!g.ok) return set_err(ctx, KRR_E_HIP, "cannot select device%s", "");
+    hipStream_t st = (hipStream_t)stream;
     // the label travels in the kernel arguments: a pageable hipMemcpyAsync here stalled the
     // calling thread behind the stream's earlier work (and raced across parse streams)
     json::SegArgs A{b->bodies, b->body_offsets, starts, body_of, n, want_timestamps ? 1 : 0, (int32_t)ll,
-                    {}, scratch_values, want_timestamps ? scratch_ts : nullptr, segments};
+                    {}, scratch_values, want_timestamps ? scratch_ts : nullptr, segments,
+                    nullptr, 0, nullptr, nullptr};
     memcpy(A.label_w, label, ll);
-    hipLaunchKernelGGL(json::k_json_segments, dim3(grid_for(n)), dim3(64), 0, (hipStream_t)stream, A);
+    if (workspace) {
+        A.n_parts = (unsigned long long*)workspace;
+        A.series_vend = workspace + 1;
+        A.parts = workspace + 1 + n;
+        A.parts_cap = parts_cap;
+        KRR_HIP(ctx, hipMemsetAsync(workspace, 0, sizeof(int64_t), st));
+    }
+    hipLaunchKernelGGL(json::k_json_segments, dim3(grid_for(n)), dim3(64), 0, st, A);
     KRR_HIP(ctx, hipGetLastError());
+    if (workspace) {
+        json::PartArgs P{b->bodies, A.parts, A.n_parts, A.series_vend, parts_cap, want_timestamps ? 1 : 0,
+                         scratch_values, want_timestamps ? scratch_ts : nullptr, segments};
+        const int64_t grid = parts_cap < 8192 ? parts_cap : 8192;  // grid-stride past that
+        hipLaunchKernelGGL(json::k_json_value_parts, dim3((unsigned)grid), dim3(64), 0, st, P);
+        KRR_HIP(ctx, hipGetLastError());
+    }
     return KRR_OK;
+}
+
+int krr_json_parse_segments(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts, const int64_t* body_of,
+                            int64_t n, const char* label, int32_t want_timestamps, double* scratch_values,
+                            double* scratch_ts, int64_t* segments, void* stream) {
+    return json_segments_launch(ctx, b, starts, body_of, n, label, want_timestamps, scratch_values, scratch_ts,
+                                segments, nullptr, 0, stream);
+}
+
+int krr_json_parse_segments_split(krr_ctx* ctx, const krr_json_bodies* b, const int64_t* starts,
+                                  const int64_t* body_of, int64_t n, const char* label, int32_t want_timestamps,
+                                  double* scratch_values, double* scratch_ts, int64_t* segments, int64_t* workspace,
+                                  int64_t workspace_words, void* stream) {
+    if (ctx && !workspace) return set_err(ctx, KRR_E_INVALID, "json: null workspace%s", "");
+    return json_segments_launch(ctx, b, starts, body_of, n, label, want_timestamps, scratch_values, scratch_ts,
+                                segments, workspace, workspace_words, stream);
 }
 
 int krr_json_gather(krr_ctx* ctx, int64_t n_items, const int64_t* src, const int64_t* count, const int64_t* dst,

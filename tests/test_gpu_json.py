@@ -237,14 +237,16 @@ def _recompact(b: bytes) -> bytes:
     return json.dumps(json.loads(b), separators=(",", ":")).encode()
 
 
-@pytest.fixture(params=["chunk", "end"])
+@pytest.fixture(params=[("chunk", True), ("end", True), ("chunk", False)], ids=["chunk-split", "end-split",
+                                                                                   "chunk-wave"])
 def route_mode(request, packer):
     """Both routings: chunk by chunk (segments written into page-locked host memory by the
-    parse kernel) and once after the last parse (one device-to-host copy)."""
-    was = packer.grouped_route
-    packer.grouped_route = request.param
+    parse kernel) and once after the last parse (one device-to-host copy); the values arrays
+    parsed in 16-KiB parts (krr_json_parse_segments_split) or one wave per series."""
+    was = packer.grouped_route, packer.grouped_split_parse
+    packer.grouped_route, packer.grouped_split_parse = request.param
     yield request.param
-    packer.grouped_route = was
+    packer.grouped_route, packer.grouped_split_parse = was
 
 
 @pytest.mark.parametrize("max_chars", [6000, 40, 1])
@@ -311,6 +313,61 @@ def test_grouped_large_bodies(packer):
     assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
     assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
     assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_grouped_split_parse_at_part_boundaries(packer, split):
+    """Values arrays ending at every offset around the 16-KiB parts of the split parse (1 to
+    4,000 samples, value strings of several lengths, NaN / Inf / signs), json.dumps spacing,
+    and end brackets the split scan cannot pair (`] ]`, an indented body): the CSR is the
+    host plan's either way; canonical and json.dumps bodies stay on the device."""
+    from krr_amd.core.fleet_query import FleetQueryPlan
+
+    class Obj:
+        def __init__(self, ns, c, pods):
+            self.namespace, self.container, self.pods = ns, c, pods
+
+    rng = np.random.default_rng(31)
+    lens = [1, 2, 3, 511, 512, 513, 700, 701, 1023, 1024, 1025, 1400, 2047, 2048, 2049, 4000]
+    objects = [Obj("ns", "app", [f"pod-{k}" for k in range(len(lens))])]
+    plan = FleetQueryPlan(objects, max_query_chars=10_000)
+    assert len(plan.groups) == 1
+    specials = ["NaN", "+Inf", "-Inf", "-0", "0", "1e-300", "123456789012345678"]
+
+    def body(shift, dumps_kw):
+        res = []
+        for k, pod in enumerate(plan.groups[0].pods):
+            n = lens[(k + shift) % len(lens)]
+            vals = [specials[i % len(specials)] if i % 97 == 5 else repr(float(rng.gamma(2.0, 10.0 ** (i % 7 - 3))))
+                    for i in range(n)]
+            res.append({"metric": {"pod": pod, "container": "app"},
+                        "values": [[1700000000 + 15 * i, v] for i, v in enumerate(vals)]})
+        return json.dumps({"status": "success", "data": {"resultType": "matrix", "result": res}},
+                          **dumps_kw).encode()
+
+    p = packer
+    was = p.grouped_split_parse
+    p.grouped_split_parse = split
+    try:
+        for shift in range(0, len(lens), 5):
+            cases = {"compact": ([body(shift, {"separators": (",", ":")})], True),
+                     "dumps": ([body(shift, {})], True),
+                     "indent": ([body(shift, {"indent": 1})], False)}
+            b = cases["compact"][0][0]
+            cut = b.index(b'"]]}') + 2  # the first series' "]]" -> "] ]"
+            cases["spaced_end"] = ([b[:cut - 1] + b" " + b[cut - 1:]], False)
+            for name, (bodies, on_device) in cases.items():
+                want, want_counts = plan.pack(bodies, return_pod_counts=True)
+                dp = p.pack_grouped(plan, bodies, return_pod_counts=True)
+                if on_device:
+                    assert dp.via == "device", name
+                got = dp.series.values.cpu().numpy() if dp.via == "device" else dp.series.values
+                offs = dp.series.offsets.cpu().numpy() if dp.via == "device" else dp.series.offsets
+                assert np.array_equal(offs, want.offsets), name
+                assert np.array_equal(np.asarray(got).view(np.uint64), want.values.view(np.uint64)), name
+                assert np.array_equal(np.asarray(dp.pod_counts), want_counts), name
+    finally:
+        p.grouped_split_parse = was
 
 
 def test_pack_many_equals_separate(packer):
