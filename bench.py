@@ -1111,7 +1111,8 @@ def host_path(args, dev, c_host_sample, objects: int = 2000, pods: int = 3, dist
                       "the slowest / fastest rate in *_spread; every object's strings compared across the parsers); "
                       "e2e_grouped: recommend_from_grouped with parser='device' (the same median rule, bodies "
                       "staged with their timestamps cut as the per-pod ones, e2e_grouped_upload; chunks parsed "
-                      "and routed as they land, e2e_grouped_phases_s), parser='hybrid' and parser='host' beside "
+                      "(values arrays in 16-KiB parts, one wave each) and routed as they land, "
+                      "e2e_grouped_phases_s), parser='hybrid' and parser='host' beside "
                       "it, every object compared"}
     return out
 
