@@ -92,22 +92,25 @@ def main():
         print(f"copy_h2d_batch {piece >> 20} MiB pieces: {k * piece / dt / 1e9:.1f} GB/s", flush=True)
     del src, dst
     res = {}
-    variants = [(1, 256)]
-    for ppt, mb in variants:
-        packer = DevicePacker(base.ctx, threads=threads, chunk_bytes=mb << 20)
-        packer.pieces_per_thread = ppt
+    variants = [True, False, True, False]
+    for pipe in variants:
+        packer = DevicePacker(base.ctx, threads=threads)
+        packer.grouped_pipeline_thread = pipe
         out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
         torch.cuda.synchronize()
         assert all(np.array_equal(o.series.values.cpu().numpy(), w) for o, w in zip(out, want))
         ts = []
+        cg0 = bench.cgroup_cpu()
         for r in range(args.rounds):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        print(f"pieces/thread {ppt} chunk {mb} MiB: median {np.median(ts) * 1e3:.2f} ms "
-              f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} pieces {packer.last_upload.get('pieces')}", flush=True)
+        cg1 = bench.cgroup_cpu()
+        print(f"pipeline thread {pipe}: median {np.median(ts) * 1e3:.2f} ms "
+              f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} throttled periods "
+              f"{cg1.get('nr_throttled', 0) - cg0.get('nr_throttled', 0)}", flush=True)
         print(f"   phases {packer.last_grouped_phases}", flush=True)
         packer.release()
         del packer
