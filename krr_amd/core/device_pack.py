@@ -658,8 +658,10 @@ class DevicePacker:
                                                                     pieces=True, extra_slots=host_bytes // 8 + 1)
             finally:
                 if pipe is not None:
+                    t_j = time.perf_counter()
                     pipe["jobs"].put(None)
                     pipe["thread"].join()
+                    pipe["join_s"] = time.perf_counter() - t_j
             if pipe is not None and pipe["err"]:
                 raise pipe["err"][0]
             clock.append(time.perf_counter())
@@ -745,6 +747,7 @@ class DevicePacker:
                                             np.diff(clock).round(5).tolist()), parse_wait=round(waited[0], 5),
                                         route_wait=round(route_wait[0], 5), route_s=round(route_wait[1], 5),
                                         parse_enqueue_s=round(enq[0], 5),
+                                        pipeline_join_s=round(pipe["join_s"], 5) if pipe else None,
                                         strip=(self.last_upload or {}).get("strip_s"))
         return out
 
