@@ -1,10 +1,13 @@
-"""Same-process A/B of the device packer's grouped pipeline variants on bench.py's grouped
-workload (2,000 objects x 3 pods x 10,080 samples as 20-namespace `sum by (pod)` bodies).
+"""Same-process probes of the device packer's grouped pipeline on bench.py's grouped workload
+(2,000 objects x 3 pods x 10,080 samples as 20-namespace `sum by (pod)` bodies).
 
     python scripts/grouped_probe.py [--rounds R]
 
-Prints per variant the median seconds of pack_grouped_many (both resources, to a synchronised
-CSR in HBM) and the packer's last phase split.  Variants: grouped_route "chunk" / "end"."""
+Prints the pinned->HBM copy rate for several copy sizes and stream counts (torch copies and
+the library's krr_copy_h2d_batch), then, per packer variant (edit `variants`: round 6 compared
+pieces per thread, chunk sizes, routing modes and the pipeline thread this way), the median
+seconds of pack_grouped_many (both resources, to a synchronised CSR in HBM, checked against the
+host plan once) with the packer's last phase split and the cgroup's throttled periods."""
 from __future__ import annotations
 
 import argparse
