@@ -80,6 +80,8 @@ class DevicePacker:
         # grouped bodies: strip pieces per staging thread and chunk (each piece is one H2D copy: 4 per
         # thread cost 6 ms of 57 on the bench fleet against 1, which still balances the strip)
         self.pieces_per_thread = 1
+        # grouped staging: chunks stripped by a thread of their own, one chunk ahead of the copies
+        self.strip_ahead = os.environ.get("KRR_STRIP_AHEAD", "1") != "0"
         self.device = torch.device("cuda", ctx.device)
         self.chunk_bytes = int(chunk_bytes)
         self.threads = int(threads)
@@ -315,11 +317,7 @@ class DevicePacker:
         nb = len(lens)
         T = self.threads or default_threads()
         max_pieces = max(2, int(self.pieces_per_thread * T))
-        cap = 2 * nb + max_pieces
         new_lens = np.empty(nb, dtype=np.int64)
-        p_start = np.empty(cap + 1, dtype=np.int64)
-        p_out = np.empty(cap, dtype=np.int64)
-        n_p = ctypes.c_int32(0)
         new_offs = torch.zeros(nb + 1, dtype=torch.int64, pin_memory=True)
         no = new_offs.numpy()
         d_boffs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
@@ -335,7 +333,8 @@ class DevicePacker:
         self._live = (no, piece_dev, piece_shift)  # grown chunk by chunk: the routing reads it
         import time
 
-        t_strip = 0.0
+        # the chunks (whole bodies): they depend on the body sizes only
+        chunks = []
         a = 0
         step = min(self.chunk_bytes, 16 << 20)
         while a < nb:
@@ -345,39 +344,82 @@ class DevicePacker:
             b = int(np.searchsorted(boffs, boffs[a] + step, side="left"))
             step = min(step * 3 // 2, self.chunk_bytes)
             b = min(max(b, a + 1), nb)
-            lo = int(boffs[a])
+            chunks.append((a, b))
+            a = b
+
+        def strip_chunk(a, b):
+            cap = 2 * (b - a) + max_pieces
+            p_start, p_out, n_p = np.empty(cap + 1, dtype=np.int64), np.empty(cap, dtype=np.int64), ctypes.c_int32(0)
             t_s = time.perf_counter()
             rc = host.krr_pack_concat_strip_pieces(ptr_addr + a * 8, lens[a:].ctypes.data, b - a,
-                                                   boffs[a:].ctypes.data, stage.data_ptr() + lo, self.threads,
-                                                   max_pieces, new_lens[a:].ctypes.data, p_start.ctypes.data,
-                                                   p_out.ctypes.data, ctypes.byref(n_p))
-            if rc != KRR_PACK_OK:
-                raise PrometheusResponseError(rc, "krr_pack_concat_strip_pieces failed")
-            t_strip += time.perf_counter() - t_s
-            np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
-            no[a + 1:b + 1] += no[a]
-            k = n_p.value
-            pd = no[a] + np.concatenate([[0], np.cumsum(p_out[:k])[:-1]]).astype(np.int64)
-            piece_dev.append(pd)
-            piece_shift.append(p_start[:k] - pd)
-            # every piece, then the chunk's body offsets: one native call of async copies
-            dst = np.empty(k + 1, dtype=np.int64)
-            src = np.empty(k + 1, dtype=np.int64)
-            nby = np.empty(k + 1, dtype=np.int64)
-            dst[:k], src[:k], nby[:k] = d_base + pd, s_base + p_start[:k], p_out[:k]
-            dst[k], src[k], nby[k] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
-            # even pieces (and the offsets) on one copy stream, odd pieces on the other
-            ev_idx = np.concatenate([np.arange(0, k, 2), [k]])
-            self.ctx.copy_h2d_batch(dst[ev_idx], src[ev_idx], nby[ev_idx], stream=cs)
-            if k > 1:
-                self.ctx.copy_h2d_batch(dst[1:k:2], src[1:k:2], nby[1:k:2], stream=cs2)
-            for c in (cs, cs2):
-                with torch.cuda.stream(c):
-                    ev = torch.cuda.Event()
-                    ev.record(c)
-                st.wait_event(ev)
-            launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
-            a = b
+                                                   boffs[a:].ctypes.data, stage.data_ptr() + int(boffs[a]),
+                                                   self.threads, max_pieces, new_lens[a:].ctypes.data,
+                                                   p_start.ctypes.data, p_out.ctypes.data, ctypes.byref(n_p))
+            return a, b, rc, p_start, p_out, n_p.value, time.perf_counter() - t_s
+
+        # strip_ahead: a thread strips the chunks one after the other while this one enqueues each
+        # stripped chunk's copies and search (on a slow host the staging thread's own work per
+        # chunk, ~0.4 ms, otherwise sits between two strips with the worker pool idle)
+        import queue
+        import threading
+
+        done_q: "queue.Queue" = queue.Queue()
+        stop = [False]
+
+        def producer():
+            try:
+                for a, b in chunks:
+                    if stop[0]:
+                        break
+                    item = strip_chunk(a, b)
+                    done_q.put(item)
+                    if item[2] != KRR_PACK_OK:
+                        break
+            except BaseException as e:  # noqa: BLE001 — re-raised by the consumer
+                done_q.put(e)
+            finally:
+                done_q.put(None)
+
+        ahead = self.strip_ahead and len(chunks) > 1
+        if ahead:
+            prod = threading.Thread(target=producer, name="krr-strip-ahead", daemon=True)
+            prod.start()
+        items = iter(done_q.get, None) if ahead else (strip_chunk(a, b) for a, b in chunks)
+        t_strip = 0.0
+        try:
+            for item in items:
+                if isinstance(item, BaseException):
+                    raise item
+                a, b, rc, p_start, p_out, k, dt = item
+                if rc != KRR_PACK_OK:
+                    raise PrometheusResponseError(rc, "krr_pack_concat_strip_pieces failed")
+                t_strip += dt
+                np.cumsum(new_lens[a:b], out=no[a + 1:b + 1])
+                no[a + 1:b + 1] += no[a]
+                pd = no[a] + np.concatenate([[0], np.cumsum(p_out[:k])[:-1]]).astype(np.int64)
+                piece_dev.append(pd)
+                piece_shift.append(p_start[:k] - pd)
+                # every piece, then the chunk's body offsets: one native call of async copies
+                dst = np.empty(k + 1, dtype=np.int64)
+                src = np.empty(k + 1, dtype=np.int64)
+                nby = np.empty(k + 1, dtype=np.int64)
+                dst[:k], src[:k], nby[:k] = d_base + pd, s_base + p_start[:k], p_out[:k]
+                dst[k], src[k], nby[k] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
+                # even pieces (and the offsets) on one copy stream, odd pieces on the other
+                ev_idx = np.concatenate([np.arange(0, k, 2), [k]])
+                self.ctx.copy_h2d_batch(dst[ev_idx], src[ev_idx], nby[ev_idx], stream=cs)
+                if k > 1:
+                    self.ctx.copy_h2d_batch(dst[1:k:2], src[1:k:2], nby[1:k:2], stream=cs2)
+                for c in (cs, cs2):
+                    with torch.cuda.stream(c):
+                        ev = torch.cuda.Event()
+                        ev.record(c)
+                    st.wait_event(ev)
+                launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
+        finally:
+            if ahead:
+                stop[0] = True
+                prod.join()
         self._last = (d_bodies, stage, new_offs)
         pdev = np.concatenate(piece_dev) if piece_dev else np.zeros(0, np.int64)
         psh = np.concatenate(piece_shift) if piece_shift else np.zeros(0, np.int64)

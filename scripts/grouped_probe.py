@@ -95,10 +95,10 @@ def main():
         print(f"copy_h2d_batch {piece >> 20} MiB pieces: {k * piece / dt / 1e9:.1f} GB/s", flush=True)
     del src, dst
     res = {}
-    variants = [True, True]
+    variants = [True, False, True, False]
     for pipe in variants:
         packer = DevicePacker(base.ctx, threads=threads)
-        packer.grouped_pipeline_thread = pipe
+        packer.strip_ahead = pipe
         out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
         torch.cuda.synchronize()
         assert all(np.array_equal(o.series.values.cpu().numpy(), w) for o, w in zip(out, want))
@@ -111,7 +111,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         cg1 = bench.cgroup_cpu()
-        print(f"pipeline thread {pipe}: median {np.median(ts) * 1e3:.2f} ms "
+        print(f"strip ahead {pipe}: median {np.median(ts) * 1e3:.2f} ms "
               f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} throttled periods "
               f"{cg1.get('nr_throttled', 0) - cg0.get('nr_throttled', 0)}", flush=True)
         print(f"   phases {packer.last_grouped_phases}", flush=True)
