@@ -465,13 +465,17 @@ class DevicePacker:
     _EMPTY_BODY = b'{"status":"success","data":{"resultType":"matrix","result":[]}}'
 
     def _pack_grouped_multi(self, items, want_ts, want_counts, stream, label, host_share: float = 0.0) -> list:
-        """The grouped pipeline, chunk by chunk (a chunk = whole bodies): stage (stripped, in
-        pieces) -> copy -> search the series starts (launch stream) -> one chunk later, parse the
-        chunk's series (a parse stream) and copy its segments to the host -> one chunk later
-        again, chain and route the chunk's bodies on the host (their slots only) — so after the
-        last copy only the last chunk's parse and route remain.  Then every slot's values are
-        gathered into the CSR."""
-        import os
+        """The grouped pipeline, chunk by chunk (a chunk = whole bodies):
+          strip thread:     strip the chunk's bodies in pieces into the staging buffer;
+          staging thread:   enqueue the pieces' copies (two copy streams) and the search of the
+                            chunk's series starts (launch stream);
+          pipeline thread:  wait for the search, enqueue the chunk's parse on a parse stream (the
+                            values arrays in 16-KiB parts, segment rows written into page-locked
+                            host memory), and chain and route every parsed chunk's bodies on the
+                            host (their groups' slots only);
+        so after the last copy only the last chunk's search, parse and route remain.  Then every
+        slot's values are gathered into the CSR.  grouped_route = "end" (or no pipeline thread)
+        runs the parse one chunk behind on the staging thread instead, and "end" routes once."""
         import threading
         import time
 
