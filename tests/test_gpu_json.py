@@ -555,3 +555,79 @@ def test_grouped_large_bodies_in_pieces_and_hybrid(packer, route_mode):
             assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
             assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
             assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+def _fuzz_grouped_bodies(rng, plan):
+    """One body per group of `plan`, each with random variations of what a query_range answer
+    may hold: separators (compact, json.dumps, indented), key orders, extra keys, empty and long
+    values arrays, value spellings (shortest reprs, integers, exponents, NaN / +Inf / -Inf, 19
+    and 21 significant digits), a label value with an escape, and `] ]` at an array's end."""
+    spellings = [lambda x: repr(x), lambda x: str(int(x * 1000)), lambda x: f"{x:.6e}", lambda x: "NaN",
+                 lambda x: "+Inf", lambda x: "-Inf", lambda x: "1234567890123456789",
+                 lambda x: "123456789012345678901", lambda x: f"{-x!r}"]
+    bodies = []
+    for grp in plan.groups:
+        res = []
+        for pod in rng.permutation(grp.pods).tolist():
+            n = int(rng.choice([0, 1, 2, 3, 100, 2047, 2048, 5000]))
+            xs = rng.gamma(2.0, 0.05, n)
+            vals = [spellings[int(rng.integers(0, len(spellings)))](float(x)) if rng.random() < 0.05 else repr(float(x))
+                    for x in xs]
+            metric = {"pod": pod, "container": "app"}
+            if rng.random() < 0.2:
+                metric = dict(reversed(list(metric.items())))
+            if rng.random() < 0.05:
+                metric["note"] = 'a"b'  # an escape: this body is the host's
+            series = {"metric": metric, "values": [[1700000000 + 15 * i, v] for i, v in enumerate(vals)]}
+            if rng.random() < 0.2:
+                series = {"values": series["values"], "metric": series["metric"]}
+            if rng.random() < 0.1:
+                series["extra"] = [1, {"k": "v"}]
+            if n or rng.random() < 0.5:  # a series without samples now and then
+                res.append(series)
+        doc = {"status": "success", "data": {"resultType": "matrix", "result": res}}
+        form = rng.random()
+        if form < 0.6:
+            b = json.dumps(doc, separators=(",", ":")).encode()
+        elif form < 0.85:
+            b = json.dumps(doc).encode()
+        else:
+            b = json.dumps(doc, indent=int(rng.integers(0, 3))).encode()
+        if rng.random() < 0.1 and b'"]]' in b:
+            i = b.index(b'"]]') + 2
+            b = b[:i] + b" " + b[i:]
+        bodies.append(b)
+    return bodies
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_grouped_fuzz_equals_host(packer, route_mode, seed):
+    """Randomly varied grouped bodies through the device pipeline (every routing / parse form of
+    route_mode) give exactly the host plan's CSR and pod counts, or the host plan's error —
+    whichever parser ends up deciding."""
+    from krr_amd.core.fleet_query import FleetQueryPlan
+    from krr_amd.core.prom_native import PrometheusResponseError
+
+    class Obj:
+        def __init__(self, ns, c, pods):
+            self.namespace, self.container, self.pods = ns, c, pods
+
+    rng = np.random.default_rng(1000 + seed)
+    n_ns = int(rng.integers(2, 7))
+    objects = [Obj(f"ns{g % n_ns}", f"c{g % 2}", [f"pod-{g}-{k}" for k in range(int(rng.integers(1, 5)))])
+               for g in range(int(rng.integers(4, 16)))]
+    plan = FleetQueryPlan(objects, max_query_chars=int(rng.choice([40, 200, 10_000])))
+    bodies = _fuzz_grouped_bodies(rng, plan)
+    try:
+        want, want_counts = plan.pack(bodies, return_pod_counts=True)
+    except PrometheusResponseError as e:
+        with pytest.raises(PrometheusResponseError) as got:
+            packer.pack_grouped(plan, bodies, return_pod_counts=True)
+        assert got.value.code == e.code
+        return
+    dp = packer.pack_grouped(plan, bodies, return_pod_counts=True)
+    vals = dp.series.values.cpu().numpy() if dp.via == "device" else np.asarray(dp.series.values)
+    offs = dp.series.offsets.cpu().numpy() if dp.via == "device" else np.asarray(dp.series.offsets)
+    assert np.array_equal(offs, want.offsets)
+    assert np.array_equal(vals.view(np.uint64), want.values.view(np.uint64))
+    assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
