@@ -255,8 +255,9 @@ class DevicePacker:
         tmp_v = torch.empty(slots, dtype=torch.float64, device=dev)
         jb = self.ctx.json_bodies(d_bodies, d_boffs, total)
         host = load_library()
-        cs = self._copy_stream
+        cs, cs2 = self._copy_stream, self._copy_stream2
         cs.wait_stream(st)  # d_bodies / d_boffs were allocated on st
+        cs2.wait_stream(st)
         d_base, s_base = d_bodies.data_ptr(), stage.data_ptr()
         o_base, n_base = d_boffs.data_ptr(), new_offs.data_ptr()
         a = 0
@@ -289,11 +290,17 @@ class DevicePacker:
             src[:nr] = s_base + boffs[b0]
             nby[:nr] = no[a + runs[1:nr + 1]] - no[b0]
             dst[nr], src[nr], nby[nr] = o_base + 8 * a, n_base + 8 * a, 8 * (b - a + 1)
-            self.ctx.copy_h2d_batch(dst, src, nby, stream=cs)
-            with torch.cuda.stream(cs):
-                ev = torch.cuda.Event()
-                ev.record(cs)
-            st.wait_event(ev)
+            # even runs (and the offsets) on one copy stream, odd runs on the other (as the
+            # grouped pieces: one copy's setup overlaps the other's transfer)
+            ev_idx = np.concatenate([np.arange(0, nr, 2), [nr]])
+            self.ctx.copy_h2d_batch(dst[ev_idx], src[ev_idx], nby[ev_idx], stream=cs)
+            if nr > 1:
+                self.ctx.copy_h2d_batch(dst[1:nr:2], src[1:nr:2], nby[1:nr:2], stream=cs2)
+            for c in (cs, cs2):
+                with torch.cuda.stream(c):
+                    ev = torch.cuda.Event()
+                    ev.record(c)
+                st.wait_event(ev)
             launch(jb, a, b, tmp_v, None, int(no[a]), int(no[b]))
             a = b
         self._last = (d_bodies, stage, new_offs)
