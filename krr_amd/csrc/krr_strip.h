@@ -108,13 +108,17 @@ KRR_STRIP_TARGET __attribute__((always_inline)) inline bool strip_block(StripSta
 // stripped end).
 // `quotes` (optional): the quotes of [p, e) counted on the way (a local sum, written once: a
 // pointer updated per block would alias the output stores and serialise the loop).
-template <bool COUNT>
+#ifndef KRR_STRIP_PREFETCH
+#define KRR_STRIP_PREFETCH 0  // bytes ahead of the block to prefetch (0: none)
+#endif
+template <bool COUNT, int PF = KRR_STRIP_PREFETCH>
 KRR_STRIP_TARGET inline int64_t strip_span_t(const char* p, const char* e, char* out, int64_t* quotes) {
     StripState st;
     int64_t nq = 0;
     int64_t* const qp = COUNT ? &nq : nullptr;
     char* o = out;
     while (e - p >= 64) {
+        if (PF) _mm_prefetch(p + PF, _MM_HINT_T0);  // past a 4-KiB page the hardware prefetchers stop
         const __m512i x = _mm512_loadu_si512(p);
         uint64_t keep;
         if (!strip_block(st, x, ~0ull, &keep, qp)) return -1;
