@@ -80,6 +80,7 @@ class DevicePacker:
         # grouped bodies: strip pieces per staging thread and chunk (each piece is one H2D copy: 4 per
         # thread cost 6 ms of 57 on the bench fleet against 1, which still balances the strip)
         self.pieces_per_thread = 1
+        self.strip_threads = 0          # grouped strip threads (0: one fewer than self.threads)
         # grouped staging: chunks stripped by a thread of their own, one chunk ahead of the copies
         self.strip_ahead = os.environ.get("KRR_STRIP_AHEAD", "1") != "0"
         self.device = torch.device("cuda", ctx.device)
@@ -322,7 +323,10 @@ class DevicePacker:
 
         dev = self.device
         nb = len(lens)
-        T = self.threads or default_threads()
+        T = self.strip_threads
+        if not T:  # one thread fewer than the lease: the staging and pipeline threads keep a core
+            T = self.threads or default_threads()
+            T = T - 1 if T >= 4 else T
         max_pieces = max(2, int(self.pieces_per_thread * T))
         new_lens = np.empty(nb, dtype=np.int64)
         new_offs = torch.zeros(nb + 1, dtype=torch.int64, pin_memory=True)
@@ -360,7 +364,7 @@ class DevicePacker:
             t_s = time.perf_counter()
             rc = host.krr_pack_concat_strip_pieces(ptr_addr + a * 8, lens[a:].ctypes.data, b - a,
                                                    boffs[a:].ctypes.data, stage.data_ptr() + int(boffs[a]),
-                                                   self.threads, max_pieces, new_lens[a:].ctypes.data,
+                                                   T, max_pieces, new_lens[a:].ctypes.data,
                                                    p_start.ctypes.data, p_out.ctypes.data, ctypes.byref(n_p))
             return a, b, rc, p_start, p_out, n_p.value, time.perf_counter() - t_s
 

@@ -95,26 +95,24 @@ def main():
         print(f"copy_h2d_batch {piece >> 20} MiB pieces: {k * piece / dt / 1e9:.1f} GB/s", flush=True)
     del src, dst
     res = {}
-    variants = [True, False, True, False]
-    for pipe in variants:
+    variants = [(16, 1), (15, 1), (16, 2), (14, 1), (16, 1), (15, 1), (16, 2), (14, 1)]
+    for st_, ppt in variants:
         packer = DevicePacker(base.ctx, threads=threads)
-        packer.strip_ahead = pipe
+        packer.strip_threads, packer.pieces_per_thread = st_, ppt
         out = packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
         torch.cuda.synchronize()
         assert all(np.array_equal(o.series.values.cpu().numpy(), w) for o, w in zip(out, want))
         ts = []
-        cg0 = bench.cgroup_cpu()
         for r in range(args.rounds):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             packer.pack_grouped_many([(plan, g_cpu), (plan, g_mem)])
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        cg1 = bench.cgroup_cpu()
-        print(f"strip ahead {pipe}: median {np.median(ts) * 1e3:.2f} ms "
-              f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} throttled periods "
-              f"{cg1.get('nr_throttled', 0) - cg0.get('nr_throttled', 0)}", flush=True)
-        print(f"   phases {packer.last_grouped_phases}", flush=True)
+        ph = packer.last_grouped_phases
+        print(f"strip threads {st_} pieces/thread {ppt}: median {np.median(ts) * 1e3:.2f} ms "
+              f"runs {[round(t * 1e3, 2) for t in sorted(ts)]} strip {ph.get('strip')} "
+              f"join {ph.get('pipeline_join_s')}", flush=True)
         packer.release()
         del packer
 
