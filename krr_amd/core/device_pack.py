@@ -547,13 +547,15 @@ class DevicePacker:
         host_bytes = sum(len(b) for b in flat[split:])
         dflat = flat[:split]
         total_bytes = sum(len(b) for b in dflat)
-        cap = max(4096, total_bytes // 256)  # a series object with a few samples takes > 256 bytes
+        # candidates: a series object takes >= 48 bytes (`{"metric":{"pod":"…"},"values":[[1,"1"]]}`);
+        # more than that (a body of empty label sets) overflows to the host packer
+        cap = max(4096, total_bytes // 48)
         cand = torch.empty(cap, dtype=torch.int64, device=dev)
         n_cand = torch.zeros(1, dtype=torch.int64, device=dev)
         if self.grouped_route not in ("chunk", "end"):
             raise ValueError(f"grouped_route must be 'chunk' or 'end', got {self.grouped_route!r}")
         per_chunk = self.grouped_route == "chunk"
-        segs = None if per_chunk else torch.empty((cap, 7), dtype=torch.int64, device=dev)
+        seg_parts: list = []  # "end": each chunk's segments on the device, copied once at the end
         seen = [0]  # positions below this were searched
         # the parses run on streams of their own (a chunk holds one or two bodies = a few hundred
         # series = waves, far from filling the GPU): consecutive chunks' parses overlap each other
@@ -650,8 +652,10 @@ class DevicePacker:
                     # per chunk: the kernel writes the segments straight into page-locked host
                     # memory (no device-to-host DMA: on the copy engines it queued behind, and
                     # slowed, the chunks' host-to-device copies)
+                    if not per_chunk:
+                        seg_parts.append(torch.empty((n - lo, 7), dtype=torch.int64, device=dev))
                     self.ctx.json_parse_segments(jb, starts, body_of, label, want_ts, tmp_v, tmp_t,
-                                                 rows if per_chunk else segs[lo:n], stream=ps, workspace=ws)
+                                                 rows if per_chunk else seg_parts[-1], stream=ps, workspace=ws)
                 if per_chunk:
                     evp = torch.cuda.Event(blocking=pipe is not None)
                     evp.record(ps)
@@ -736,8 +740,9 @@ class DevicePacker:
         if not per_chunk and not parsed[1]:  # every chunk's segments at once, then one route
             nc = parsed[0]
             rows = self._host_rows(nc)[:nc]
-            with torch.cuda.stream(st):
-                rows.copy_(segs[:nc])
+            if nc:
+                with torch.cuda.stream(st):
+                    rows.copy_(torch.cat(seg_parts) if len(seg_parts) > 1 else seg_parts[0])
             route(0, len(dflat), rows.numpy(), self.threads)
         t_dev = time.perf_counter() - clock[0]
         if host_thread is not None:

@@ -631,3 +631,34 @@ def test_grouped_fuzz_equals_host(packer, route_mode, seed):
     assert np.array_equal(offs, want.offsets)
     assert np.array_equal(vals.view(np.uint64), want.values.view(np.uint64))
     assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+def test_grouped_segment_rows_grow_mid_batch(packer):
+    """More series than the page-locked segment-row buffer holds at first (16,384 rows): the
+    buffer grows while earlier chunks' rows are still being parsed into and routed from the old
+    one (their views keep it alive); the CSR is still the host plan's."""
+    from krr_amd.core.device_pack import DevicePacker
+    from krr_amd.core.fleet_query import FleetQueryPlan
+
+    class Obj:
+        def __init__(self, ns, c, pods):
+            self.namespace, self.container, self.pods = ns, c, pods
+
+    rng = np.random.default_rng(77)
+    objects = [Obj(f"ns{o % 4}", "app", [f"p{o}-{k}" for k in range(100)]) for o in range(220)]
+    plan = FleetQueryPlan(objects, max_query_chars=20_000)
+    bodies = []
+    for grp in plan.groups:
+        res = [{"metric": {"pod": pod}, "values": [[1700000000 + 15 * i, repr(float(x))]
+                                                   for i, x in enumerate(rng.gamma(2.0, 0.05, int(rng.integers(1, 4))))]}
+               for pod in grp.pods]
+        bodies.append(_compact({"status": "success", "data": {"resultType": "matrix", "result": res}}))
+    want, want_counts = plan.pack(bodies, return_pod_counts=True)
+    assert plan.n_slots > 16384
+    p = DevicePacker(packer.ctx, chunk_bytes=64 << 10)
+    dp = p.pack_grouped(plan, bodies, return_pod_counts=True)
+    assert dp.via == "device"
+    assert p._seg_rows.shape[0] > 16384  # grew during the batch
+    assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
+    assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
+    assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
