@@ -382,12 +382,13 @@ __device__ int64_t values_scan(const char* const buf, const char* vs, const char
         v4u32 y0 = zero, y1 = zero;
         load32(r0 + kBlockBytes, y0, y1);  // the next block, requested before this one is scanned
         uint32_t w[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-        uint32_t lb = 0, rb = 0;
+        uint32_t lb = 0, rb = 0, sb = 0;
 #pragma unroll
         for (int k = 0; k < kLaneBytes; ++k) {
             const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFF;
             lb |= (c == '[' ? 1u : 0u) << k;
             rb |= (c == ']' ? 1u : 0u) << k;
+            sb |= (c == '{' || c == '}' || c == ':' ? 1u : 0u) << k;  // never inside a values array
         }
         // bytes outside [lo_abs, hi_abs)
         uint32_t valid = 0xFFFFFFFFu;
@@ -401,6 +402,7 @@ __device__ int64_t values_scan(const char* const buf, const char* vs, const char
         }
         lb &= valid;
         rb &= valid;
+        sb &= valid;
         // "]]": a ']' whose next byte is ']' (the next lane's first byte for bit 31); the
         // previous block's last ']' pairs with this block's first byte
         const uint32_t next_first = (uint32_t)__shfl_down((int)(rb & 1u), 1);
@@ -410,6 +412,11 @@ __device__ int64_t values_scan(const char* const buf, const char* vs, const char
         if (pair) my_end = r0 + __builtin_ctz(pair);
         if (lane == 0 && prev_rb && (rb & 1u)) my_end = r0 - 1;
         const int64_t end = wave_min_pos(my_end);
+        // a byte no values array holds before any "]]": the array ends otherwise (whitespace
+        // between its brackets) — values_array takes it, the scan stops here instead of
+        // running on through the rest of the body
+        const int64_t stop = wave_min_pos(sb ? r0 + __builtin_ctz(sb) : INT64_MAX);
+        if (stop != INT64_MAX && (end == INT64_MAX || stop < end)) return -1;
         prev_rb = (lane_bcast32(rb, kWave - 1) >> 31) & 1u;
         // element starts below the end
         uint32_t mine = lb;
@@ -592,7 +599,9 @@ __global__ __launch_bounds__(64) void k_json_segments(SegArgs A) {
                                          }
                                      });
                     room = __builtin_amdgcn_readfirstlane(room ? 1 : 0) != 0;
-                    if (np >= 0 && lane == 0) A.series_vend[j] = vend_abs;
+                    // the parts phase 2 may parse: only those of a finished scan (-1: the scan
+                    // stopped — its parts so far are skipped, values_array below parses it all)
+                    if (lane == 0) A.series_vend[j] = np >= 0 ? vend_abs : -1;
                     if (np >= 0) {
                         vok = room;
                         count = total;
@@ -642,6 +651,7 @@ __global__ __launch_bounds__(64) void k_json_value_parts(PartArgs A) {
         const int64_t* P = A.parts + q * kPartWords;
         const int64_t j = P[0], plo = P[1], phi = P[2], slot = P[4], c = P[5];
         const int64_t vend = A.series_vend[j];
+        if (vend < 0) continue;  // the series' scan stopped: its own wave parsed it
         const bool ok = values_part(A.bodies, A.want_ts != 0, plo, phi, vend, A.tmp_v + slot,
                                     A.tmp_t ? A.tmp_t + slot : nullptr, c, lane, lds);
         if (!ok && lane == 0) {

@@ -319,8 +319,9 @@ def test_grouped_large_bodies(packer):
 def test_grouped_split_parse_at_part_boundaries(packer, split):
     """Values arrays ending at every offset around the 16-KiB parts of the split parse (1 to
     4,000 samples, value strings of several lengths, NaN / Inf / signs), json.dumps spacing,
-    and end brackets the split scan cannot pair (`] ]`, an indented body): the CSR is the
-    host plan's either way; canonical and json.dumps bodies stay on the device."""
+    end brackets the split scan cannot pair (`] ]` in the first or the last series: the scan
+    stops at the series' `}` and the series' own wave parses it — on the device), and an
+    indented body (the host's): the CSR is the host plan's."""
     from krr_amd.core.fleet_query import FleetQueryPlan
 
     class Obj:
@@ -352,10 +353,13 @@ def test_grouped_split_parse_at_part_boundaries(packer, split):
         for shift in range(0, len(lens), 5):
             cases = {"compact": ([body(shift, {"separators": (",", ":")})], True),
                      "dumps": ([body(shift, {})], True),
+                     # (indented: `,\n  {"metric"` is no series candidate — the host's batch)
                      "indent": ([body(shift, {"indent": 1})], False)}
             b = cases["compact"][0][0]
             cut = b.index(b'"]]}') + 2  # the first series' "]]" -> "] ]"
-            cases["spaced_end"] = ([b[:cut - 1] + b" " + b[cut - 1:]], False)
+            cases["spaced_end"] = ([b[:cut - 1] + b" " + b[cut - 1:]], True)
+            last = b.rindex(b'"]]}') + 2  # and the last one's (no "]]" after it in the body)
+            cases["spaced_last_end"] = ([b[:last - 1] + b" " + b[last - 1:]], True)
             for name, (bodies, on_device) in cases.items():
                 want, want_counts = plan.pack(bodies, return_pod_counts=True)
                 dp = p.pack_grouped(plan, bodies, return_pod_counts=True)
