@@ -666,3 +666,44 @@ def test_grouped_segment_rows_grow_mid_batch(packer):
     assert np.array_equal(dp.series.offsets.cpu().numpy(), want.offsets)
     assert np.array_equal(dp.series.values.cpu().numpy().view(np.uint64), want.values.view(np.uint64))
     assert np.array_equal(np.asarray(dp.pod_counts), want_counts)
+
+
+def test_split_parse_workspace_is_checked(packer):
+    """krr_json_parse_segments_split refuses a workspace with no room for a part (the Python
+    binding before the call, the C ABI for a raw call)."""
+    import ctypes
+
+    import torch
+
+    from krr_amd import _native
+
+    ctx = packer.ctx
+    body = _compact({"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {"pod": "a"}, "values": [[1, "0.5"], [2, "0.25"]]}]}})
+    dev = torch.device("cuda", ctx.device)
+    d_bodies = torch.zeros(len(body) + 128, dtype=torch.uint8, device=dev)
+    d_bodies[:len(body)] = torch.frombuffer(bytearray(body), dtype=torch.uint8).to(dev)
+    offs = torch.tensor([0, len(body)], dtype=torch.int64, device=dev)
+    jb = ctx.json_bodies(d_bodies, offs, len(body))
+    starts = torch.tensor([body.index(b'{"metric"')], dtype=torch.int64, device=dev)
+    body_of = torch.zeros(1, dtype=torch.int64, device=dev)
+    tmp_v = torch.zeros(len(body) // 8 + 1, dtype=torch.float64, device=dev)
+    segs = torch.zeros(7, dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError):
+        ctx.json_parse_segments(jb, starts, body_of, "pod", False, tmp_v, None, segs,
+                                workspace=torch.zeros(4, dtype=torch.int64, device=dev))
+    small = torch.zeros(1 + 1 + 5, dtype=torch.int64, device=dev)  # 1 + n + < 6: no part fits
+    rc = ctx._lib.krr_json_parse_segments_split(ctx._h, ctypes.byref(jb), starts.data_ptr(), body_of.data_ptr(), 1,
+                                                 b"pod", 0, tmp_v.data_ptr(), None, segs.data_ptr(),
+                                                 small.data_ptr(), small.numel(), None)
+    assert rc == _native.KRR_E_INVALID
+    rc = ctx._lib.krr_json_parse_segments_split(ctx._h, ctypes.byref(jb), starts.data_ptr(), body_of.data_ptr(), 1,
+                                                 b"pod", 0, tmp_v.data_ptr(), None, segs.data_ptr(), None, 0, None)
+    assert rc == _native.KRR_E_INVALID
+    # with room: the segment and its values, as the one-wave parse gives them
+    ws = torch.zeros(1 + 1 + 6 * 4, dtype=torch.int64, device=dev)
+    ctx.json_parse_segments(jb, starts, body_of, "pod", False, tmp_v, None, segs, workspace=ws)
+    torch.cuda.synchronize()
+    seg = segs.cpu().numpy()
+    assert seg[6] == 1 and seg[5] == 2
+    assert tmp_v.cpu().numpy()[seg[4]:seg[4] + 2].tolist() == [0.5, 0.25]
